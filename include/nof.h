@@ -1,0 +1,219 @@
+/*
+ * nof.h — C ABI of the MI355X-native ScratchNerf hot path ("nerf-or-nothing_amd").
+ *
+ * This is the drop-in boundary for the reference's C++/CLI host API
+ * (namespace AcceleratedNeRFUtils, the headers in /root/reference/ScratchNerf/AcceleratedNeRFUtils/),
+ * consumed by ScratchNerf/Program.cs:24-26,42,51-60.  Each entry point below names the
+ * reference member it replaces.  Conventions:
+ *   - every call returns nof_status; nof_last_error() gives a thread-local message;
+ *     nothing aborts the process;
+ *   - device pointers returned by the library are BORROWED: valid until the next call
+ *     on the same object or its destruction (MLPcpp:254,315-320);
+ *   - host inputs are only read during the call; host outputs are caller-provided;
+ *   - all device work is enqueued on cfg->stream (NULL = default stream), asynchronously,
+ *     except where a host result is returned (layer sizes, retrieve_output, loss);
+ *   - float3 / System.Numerics.Vector3 arrays are packed float[n][3] (12 B per element).
+ * No torch / HIP types appear in these signatures.
+ */
+#ifndef NOF_H
+#define NOF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum nof_status {
+  NOF_OK = 0,
+  NOF_ERR_INVALID_ARG = 1,
+  NOF_ERR_HIP = 2,
+  NOF_ERR_RCCL = 3,
+  NOF_ERR_OOM = 4,
+  NOF_ERR_UNSUPPORTED = 5
+} nof_status;
+
+#define NOF_MAX_LEVELS 4
+
+/* One POD replacing the reference's compile-time constants (helpers.h:16-20,
+ * AcceleratedMLP.h:10-19, AF:15-16,183-184,243-245,345-346) and static C# Config
+ * (TrainState.cs:45-72).  nof_config_default() fills the reference values. */
+typedef struct nof_config {
+  int32_t device;                         /* HIP device ordinal (reference: cudaSetDevice(0), MNcpp:10) */
+  int32_t max_rays;                       /* capacity in rays per call (reference: 1024, helpers.h:18) */
+  int32_t num_levels;                     /* 2 (helpers.h:16) */
+  int32_t num_samples[NOF_MAX_LEVELS];    /* per level; 128, 128 (helpers.h:17); GPU: multiple of 64, <= 512 */
+  int32_t net_depth, net_width;           /* 8, 256 */
+  int32_t net_depth_condition, net_width_condition; /* 1, 128 */
+  int32_t skip_layer;                     /* 4 */
+  int32_t min_deg_point, max_deg_point;   /* 0, 16 */
+  int32_t deg_view;                       /* 4 */
+  int32_t randomized;                     /* 1 (TrainState.cs:66) */
+  int32_t white_bkgd;                     /* 1 (TrainState.cs:71) */
+  float resample_padding;                 /* 0.01 (MNcs:12, AF:243) */
+  float coarse_loss_mult;                 /* 0.1 (TrainState.cs:69, AF:345) */
+  uint64_t seed;                          /* Philox key (reference: time(nullptr), MNcpp:44) */
+  void* stream;                           /* hipStream_t, NULL = default stream */
+} nof_config;
+
+void nof_config_default(nof_config* cfg);
+const char* nof_last_error(void);
+const char* nof_version(void);
+
+typedef struct nof_mipnerf nof_mipnerf;
+typedef struct nof_mlp nof_mlp;
+typedef struct nof_adam nof_adam;
+typedef struct nof_gradcalc nof_gradcalc;
+
+/* Func<uint64_t, int, float, uint64_t, uint64_t> getOutputGradient (AcceleratedMipNeRF.h:14-16):
+ * (device compRgb [n][3], level, lossMultSum, device lossMults [n]) -> device dL/dCompRgb [n][3].
+ * Invoked synchronously on the calling thread once per level in order 0..L-1 (MNcpp:125-127);
+ * it may re-enter the library and must enqueue its work on the same stream. */
+typedef uint64_t (*nof_output_grad_fn)(void* user, uint64_t dev_comp_rgb, int32_t level, float loss_mult_sum,
+                                       uint64_t dev_loss_mults);
+
+/* ---- AcceleratedMipNeRF (AcceleratedMipNeRF.h:10-41) --------------------------------------- */
+/* ctor MNcpp:7-50 (which also builds AcceleratedMLP(16, 4), AcceleratedMipNeRF.h:18) */
+nof_status nof_mipnerf_create(const nof_config* cfg, nof_mipnerf** out);
+/* dtor MNcpp:151-176 */
+nof_status nof_mipnerf_destroy(nof_mipnerf* h);
+/* GetGradient MNcpp:52-144: host ray SoA (origins/dirs [n][3]; radii, nears, fars, loss_mults [n])
+ * + loss-gradient callback -> 22 borrowed device gradient pointers [W0..W10, b0..b10]. */
+nof_status nof_mipnerf_get_gradient(nof_mipnerf* h, int32_t n, const float* origins, const float* directions,
+                                    const float* radii, const float* nears, const float* fars,
+                                    const float* loss_mults, nof_output_grad_fn cb, void* cb_user,
+                                    float* const** out_dev_grads);
+/* Same step with every input already resident in device memory and the loss gradient
+ * (AF:347-361 / Program.LossFn, D14-D15 fixed) fused into the integrator adjoint:
+ * dev_pixels [n][3]; loss_mult_sum = the GLOBAL sum over all data-parallel shards. */
+nof_status nof_mipnerf_get_gradient_device(nof_mipnerf* h, int32_t n, const float* dev_origins,
+                                           const float* dev_directions, const float* dev_radii,
+                                           const float* dev_nears, const float* dev_fars,
+                                           const float* dev_loss_mults, const float* dev_pixels,
+                                           float loss_mult_sum, float* const** out_dev_grads);
+/* GetLayerSizes MNcpp:146-149 -> get_layer_sizes MLPcpp:131-154 */
+nof_status nof_mipnerf_layer_sizes(nof_mipnerf* h, int32_t* out, int32_t cap, int32_t* count);
+/* public field `mlp` (AcceleratedMipNeRF.h:18), borrowed */
+nof_status nof_mipnerf_mlp(nof_mipnerf* h, nof_mlp** out);
+/* Philox stream position: key = seed, counter = (step, level, global ray id, k); ray_base = global
+ * id of this shard's first ray.  `step` auto-increments after every get_gradient call. */
+nof_status nof_mipnerf_set_rng(nof_mipnerf* h, uint64_t seed, uint32_t step, uint32_t ray_base);
+nof_status nof_mipnerf_get_rng(nof_mipnerf* h, uint64_t* seed, uint32_t* step, uint32_t* ray_base);
+
+/* Device views of one level's buffers from the last call (borrowed; for tests / tooling). */
+typedef struct nof_level_view {
+  int32_t n, samples;
+  const float* t;          /* [n][S+1] */
+  const float* weights;    /* [n][S] */
+  const float* comp_rgb;   /* [n][3] */
+  const float* density;    /* [n][S]   (post softplus) */
+  const float* rgb;        /* [n][S][3] (post sigmoid/padding) */
+  const float* density_grad; /* [n][S] */
+  const float* rgb_grad;   /* [n][S][3] */
+} nof_level_view;
+nof_status nof_mipnerf_level_view(nof_mipnerf* h, int32_t level, nof_level_view* out);
+/* sum over rays and levels of lambda_l * m_r |C - p|^2 / sum m (fused path only; synchronises) */
+nof_status nof_mipnerf_loss(nof_mipnerf* h, float* out);
+
+/* ---- AcceleratedMLP (AcceleratedMLP.h:7-45) -------------------------------------------------- */
+/* get_output MLPcpp:214-255: encoded inputs in device memory (enc_pos [n*S][96] in the reference's
+ * feature order, enc_dir [n][27] per ray, D5) -> (density [n*S], rgb [n*S][3]) borrowed.  The
+ * reference returns (density, rgb) but its caller binds them swapped (D9): here they are named. */
+nof_status nof_mlp_get_output(nof_mlp* m, const float* dev_enc_pos, const float* dev_enc_dir, int32_t level,
+                              int32_t n_rays, int32_t samples, uint64_t* dev_density, uint64_t* dev_rgb);
+/* get_gradient MLPcpp:256-321: dL/d rgb [n*S][3] and dL/d density [n*S] of `level`'s last forward.
+ * level 0 overwrites the gradient arena, level > 0 accumulates (sum over levels, D10). */
+nof_status nof_mlp_get_gradient(nof_mlp* m, const float* dev_color_grad, const float* dev_density_grad,
+                                int32_t level, float* const** out_dev_grads);
+/* allParams / allGradients (AcceleratedMLP.h:24-25): 22 views into one flat arena */
+nof_status nof_mlp_params(nof_mlp* m, float* const** out);
+nof_status nof_mlp_grads(nof_mlp* m, float* const** out);
+nof_status nof_mlp_flat_params(nof_mlp* m, float** out, int64_t* count);
+nof_status nof_mlp_flat_grads(nof_mlp* m, float** out, int64_t* count);
+nof_status nof_mlp_layer_sizes(nof_mlp* m, int32_t* out, int32_t cap, int32_t* count);
+/* Internal per-level buffers of the last forward/backward (borrowed; tests and tooling).  Block
+ * layout: element (feature f, sample m) of an [F]-feature tensor lives at
+ * (m/32)*F*32 + f*32 + ((m%32) ^ (f%32)).  masks: [M/32][9][64][4] uint32 ReLU bits. */
+typedef struct nof_mlp_debug {
+  int32_t M;              /* samples of this level's last forward */
+  const float* act_in;    /* [128]-feature blocks: IPE 0..95 | view PE 96..122 | 0 */
+  const float* act_h;     /* 8 consecutive [256]-feature tensors h0..h7 (stride M*256) */
+  const float* act_h9;    /* [128]-feature blocks */
+  const uint32_t* masks;
+  const float* zhead;     /* [M][4]: z_density, z_rgb[3] (pre-activation heads) */
+  const float* delta;     /* 8 consecutive [256]-feature dL/dz tensors (last get_gradient) */
+  const float* delta9x;   /* [160]-feature blocks: dL/dz9 | dz_density | dz_rgb | 0 */
+} nof_mlp_debug;
+nof_status nof_mlp_debug_view(nof_mlp* m, int32_t level, nof_mlp_debug* out);
+
+/* ---- AcceleratedAdamOptimizer (AcceleratedAdamOptimizer.h:5-20) ------------------------------ */
+/* ctor AcceleratedAdamOptimizer.cpp:6-21 (m, v zero-initialised: D18); cfg supplies device/stream */
+nof_status nof_adam_create(const int32_t* layer_sizes, int32_t num_layers, const nof_config* cfg, nof_adam** out);
+/* step AcceleratedAdamOptimizer.cpp:23-41: one fused launch when params/grads are views of flat arenas */
+nof_status nof_adam_step(nof_adam* a, float* const* params, float* const* grads, float learning_rate);
+nof_status nof_adam_iteration(nof_adam* a, int32_t* iteration);
+nof_status nof_adam_destroy(nof_adam* a);
+
+/* ---- AcceleratedGradientCalculator (AcceleratedGradientCalculator.h:8-17) -------------------- */
+nof_status nof_gradcalc_create(int32_t batch_size, const nof_config* cfg, nof_gradcalc** out);
+/* get_output_gradient AcceleratedGradientCalculator.cpp:18-30: one output buffer per level (D15) */
+nof_status nof_gradcalc_output_gradient(nof_gradcalc* g, uint64_t dev_comp_rgb, const float* host_pixels,
+                                        int32_t n, uint64_t dev_loss_mults, float loss_mult_sum, int32_t level,
+                                        uint64_t* out_dev_grad);
+nof_status nof_gradcalc_destroy(nof_gradcalc* g);
+
+/* ---- OutputRetriever::RetrieveOutput (OutputRetriever.cpp:6-14) ----------------------------- */
+nof_status nof_retrieve_output(uint64_t dev_output, int32_t n, float* host_out /* [n][3] */);
+
+/* ---- LearningRateDecay (MipHelpers.cs:758-773) ---------------------------------------------- */
+float nof_lr_decay(int32_t step, float lr_init, float lr_final, int32_t max_steps, int32_t delay_steps,
+                   float delay_mult);
+
+/* ---- device memory / stream utilities (tooling and tests) ----------------------------------- */
+nof_status nof_device_count(int32_t* count);
+nof_status nof_set_device(int32_t device);
+nof_status nof_malloc(void** ptr, size_t bytes);
+nof_status nof_free(void* ptr);
+nof_status nof_memcpy_h2d(void* dst, const void* src, size_t bytes);
+nof_status nof_memcpy_d2h(void* dst, const void* src, size_t bytes);
+nof_status nof_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
+nof_status nof_memset(void* dst, int value, size_t bytes);
+nof_status nof_stream_sync(void* stream);
+
+/* ---- individual hot-path kernels (parity tests; all device pointers, async on `stream`) -----
+ * get_sample_t_vals AF:222-242, get_resampled_t_vals AF:246-291, cast_rays AF:292-317,
+ * encode_input_data AF:187-221, volumetric_rendering AF:318-344, volumetric_rendering_gradient
+ * AF:362-402 (g = dL/dC given, or fused from pixels when dev_g == NULL). */
+nof_status nof_kernel_sample_stratified(int32_t n, int32_t samples, const float* nears, const float* fars,
+                                        int32_t randomized, uint64_t seed, uint32_t step, uint32_t level,
+                                        uint32_t ray_base, float* t_out, void* stream);
+nof_status nof_kernel_sample_pdf(int32_t n, int32_t samples_in, const float* t_in, const float* weights,
+                                 int32_t samples_out, float padding, int32_t randomized, uint64_t seed,
+                                 uint32_t step, uint32_t level, uint32_t ray_base, float* t_out, int32_t* idx_out,
+                                 void* stream);
+nof_status nof_kernel_cast(int32_t n, int32_t samples, const float* t, const float* origins, const float* dirs,
+                           const float* radii, float* means, float* covs, void* stream);
+nof_status nof_kernel_encode(int32_t n, int32_t samples, const float* means, const float* covs, const float* dirs,
+                             float* enc_pos, float* enc_dir, void* stream);
+nof_status nof_kernel_render(int32_t n, int32_t samples, const float* density, const float* rgb, const float* t,
+                             const float* dirs, int32_t white_bkgd, float* comp_rgb, float* weights, void* stream);
+nof_status nof_kernel_render_grad(int32_t n, int32_t samples, const float* density, const float* rgb,
+                                  const float* t, const float* dirs, int32_t white_bkgd, const float* comp_rgb,
+                                  const float* dev_g, const float* pixels, const float* loss_mults,
+                                  float loss_mult_sum, float lambda, float* density_grad, float* rgb_grad,
+                                  void* stream);
+nof_status nof_kernel_adam(int64_t n, float* params, const float* grads, float* m, float* v, float lr,
+                           int32_t iteration, void* stream);
+
+/* ---- per-kernel timing (hipEvents on the object's stream) ----------------------------------- */
+#define NOF_NUM_TIMERS 8
+/* timer ids: 0 pack, 1 sample, 2 mlp_fwd, 3 render_fwd, 4 render_bwd, 5 mlp_bwd, 6 wgrad, 7 wgrad_reduce */
+nof_status nof_mipnerf_enable_timing(nof_mipnerf* h, int32_t enable);
+/* synchronises; returns summed milliseconds and launch counts per timer id since the last read */
+nof_status nof_mipnerf_read_timing(nof_mipnerf* h, float* ms, int32_t* launches, int32_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NOF_H */

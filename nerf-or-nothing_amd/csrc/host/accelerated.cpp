@@ -1,0 +1,539 @@
+// Host implementation of the AcceleratedNeRFUtils classes for MI355X (see accelerated.h).
+#include "accelerated.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "../kernels/common.h"
+#include "../kernels/mlp_common.h"
+
+namespace AcceleratedNeRFUtils {
+
+using nof::kBlk;
+
+// ------------------------------------------------------------------------------------------------
+// KernelTimer
+// ------------------------------------------------------------------------------------------------
+void KernelTimer::enable(bool on, hipStream_t st) {
+  on_ = on;
+  st_ = st;
+  used_ = 0;
+  recs_.clear();
+}
+hipEvent_t KernelTimer::get() {
+  if (used_ == pool_.size()) {
+    hipEvent_t e;
+    NOF_HIP(hipEventCreate(&e));
+    pool_.push_back(e);
+  }
+  return pool_[used_++];
+}
+void KernelTimer::begin(int id) {
+  if (!on_) return;
+  open_[id] = get();
+  NOF_HIP(hipEventRecord(open_[id], st_));
+}
+void KernelTimer::end(int id) {
+  if (!on_ || !open_[id]) return;
+  hipEvent_t b = get();
+  NOF_HIP(hipEventRecord(b, st_));
+  recs_.push_back({id, open_[id], b});
+  open_[id] = nullptr;
+}
+void KernelTimer::read(float* ms, int* launches, int cap) {
+  for (int i = 0; i < cap; ++i) { ms[i] = 0.0f; launches[i] = 0; }
+  if (!recs_.empty()) NOF_HIP(hipEventSynchronize(recs_.back().b));
+  for (const Rec& r : recs_) {
+    float t = 0.0f;
+    NOF_HIP(hipEventElapsedTime(&t, r.a, r.b));
+    if (r.id < cap) { ms[r.id] += t; launches[r.id] += 1; }
+  }
+  recs_.clear();
+  used_ = 0;
+}
+KernelTimer::~KernelTimer() {
+  for (hipEvent_t e : pool_) (void)hipEventDestroy(e);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Philox-based Glorot init (MLPcs:78-85 C# semantics, D6): W = sqrt(6/(in+out)) * (2u - 1), b = 0.
+// ------------------------------------------------------------------------------------------------
+static void glorot_host(float* P, const int* out, const int* in, const int* woff, int L, uint64_t seed) {
+#pragma clang fp contract(off)
+  for (int l = 0; l < L; ++l) {
+    const float g = std::sqrt(6.0f / (float)(in[l] + out[l]));
+    const size_t cnt = (size_t)out[l] * in[l];
+    for (size_t e = 0; e < cnt; ++e) {
+      const float u = nof::philox_uniform(seed, 0, (uint32_t)l, nof::kStreamInit, (uint32_t)(e >> 32), (uint32_t)e);
+      P[woff[l] + e] = g * (u * 2.0f - 1.0f);
+    }
+  }
+}
+
+static void check_cfg(const nof_config& c) {
+  NOF_REQUIRE(c.max_rays > 0, "max_rays must be > 0");
+  NOF_REQUIRE(c.num_levels >= 1 && c.num_levels <= NOF_MAX_LEVELS, "num_levels out of range");
+  for (int l = 0; l < c.num_levels; ++l) {
+    const int S = c.num_samples[l];
+    if (!(S == 64 || S == 128 || S == 256 || S == 512))
+      throw Error(NOF_ERR_UNSUPPORTED, "GPU path supports 64/128/256/512 samples per level");
+  }
+  if (c.net_depth != 8 || c.net_width != 256 || c.net_depth_condition != 1 || c.net_width_condition != 128 ||
+      c.skip_layer != 4 || c.min_deg_point != 0 || c.max_deg_point != 16 || c.deg_view != 4)
+    throw Error(NOF_ERR_UNSUPPORTED, "GPU path implements the reference network (8x256, 1x128, skip 4, PE 16/4)");
+}
+
+// ------------------------------------------------------------------------------------------------
+// AcceleratedMLP
+// ------------------------------------------------------------------------------------------------
+AcceleratedMLP::AcceleratedMLP(int deg_point, int deg_view, const nof_config& cfg) : cfg_(cfg) {
+  check_cfg(cfg);
+  NOF_REQUIRE(deg_point == cfg.max_deg_point - cfg.min_deg_point && deg_view == cfg.deg_view,
+              "AcceleratedMLP(deg_point, deg_view) must match the config");
+  NOF_HIP(hipSetDevice(cfg.device));
+  st_ = (hipStream_t)cfg.stream;
+  hipDeviceProp_t prop;
+  NOF_HIP(hipGetDeviceProperties(&prop, cfg.device));
+  num_cu_ = prop.multiProcessorCount;
+
+  // layer dims (get_layer_sizes MLPcpp:131-154)
+  const int W = 256, Wc = 128, pos = 96, dir = 27;
+  for (int l = 0; l < 8; ++l) { out_[l] = W; in_[l] = l == 0 ? pos : (l == 4 ? W + pos : W); }
+  out_[8] = 1; in_[8] = W;
+  out_[9] = Wc; in_[9] = W + dir;
+  out_[10] = 3; in_[10] = Wc;
+  size_t o = 0;
+  for (int l = 0; l < kLayers; ++l) { woff_[l] = (int)o; o += (size_t)out_[l] * in_[l]; }
+  for (int l = 0; l < kLayers; ++l) { boff_[l] = (int)o; o += out_[l]; }
+  P_ = o;
+
+  params_.alloc(P_);
+  grads_.alloc(P_);
+  NOF_HIP(hipMemset(grads_.p, 0, P_ * sizeof(float)));
+  std::vector<float> h(P_, 0.0f);
+  glorot_host(h.data(), out_.data(), in_.data(), woff_.data(), kLayers, cfg.seed);
+  NOF_HIP(hipMemcpy(params_.p, h.data(), P_ * sizeof(float), hipMemcpyHostToDevice));
+  for (int l = 0; l < kLayers; ++l) { param_views_.push_back(params_.p + woff_[l]); grad_views_.push_back(grads_.p + woff_[l]); }
+  for (int l = 0; l < kLayers; ++l) { param_views_.push_back(params_.p + boff_[l]); grad_views_.push_back(grads_.p + boff_[l]); }
+
+  wimg_f_.alloc(nof::kFwdImageFloats);
+  wimg_b_.alloc(nof::kBwdImageFloats);
+
+  lv_.resize(cfg.num_levels);
+  for (int l = 0; l < cfg.num_levels; ++l) {
+    Level& L = lv_[l];
+    L.cap = cfg.max_rays * cfg.num_samples[l];
+    const size_t nb = (size_t)L.cap / kBlk;
+    L.act_in.alloc(nb * nof::kInF * kBlk);
+    L.act_h.alloc(8 * nb * 256 * kBlk);
+    L.act_h9.alloc(nb * 128 * kBlk);
+    L.masks.alloc(nb * nof::kMaskSlots * 256);
+    L.zhead.alloc((size_t)L.cap * 4);
+    L.sigma.alloc(L.cap);
+    L.rgb.alloc((size_t)L.cap * 3);
+    max_M_ = std::max(max_M_, L.cap);
+  }
+  const size_t nbm = (size_t)max_M_ / kBlk;
+  delta_.alloc(8 * nbm * 256 * kBlk);
+  delta9x_.alloc(nbm * nof::kD9F * kBlk);
+  NOF_HIP(hipMemset(delta9x_.p, 0, delta9x_.n * sizeof(float)));  // rows 132..159 stay zero
+  slab_cap_ = (size_t)(num_cu_ + 64) * 65536;
+  slabs_.alloc(slab_cap_);
+  bias_slabs_.alloc((size_t)(num_cu_ + 64) * 256);
+}
+
+std::vector<int> AcceleratedMLP::get_layer_sizes() const {
+  std::vector<int> s(2 * kLayers);
+  for (int l = 0; l < kLayers; ++l) { s[l] = out_[l] * in_[l]; s[kLayers + l] = out_[l]; }
+  return s;
+}
+
+void AcceleratedMLP::pack_weights() {
+  nof::PackArgs pa;
+  for (int l = 0; l < kLayers; ++l) { pa.woff[l] = woff_[l]; pa.boff[l] = boff_[l]; }
+  tb(kTPack);
+  NOF_HIP(nof::launch_pack_weights(params_.p, pa, wimg_f_.p, wimg_b_.p, st_));
+  te(kTPack);
+}
+
+void AcceleratedMLP::run_forward(int level, const nof::FwdArgs& a0) {
+  Level& L = lv_[level];
+  nof::FwdArgs a = a0;
+  a.wimg = wimg_f_.p;
+  a.act_in = L.act_in.p;
+  a.act_h = L.act_h.p;
+  a.act_h9 = L.act_h9.p;
+  a.masks = L.masks.p;
+  a.zhead = L.zhead.p;
+  a.sigma = L.sigma.p;
+  a.rgb = L.rgb.p;
+  tb(kTMlpFwd);
+  NOF_HIP(nof::launch_mlp_fwd(a, st_));
+  te(kTMlpFwd);
+}
+
+void AcceleratedMLP::forward_fused(int level, int n, int samples, const float* t, const float* origins,
+                                   const float* dirs, const float* radii) {
+  NOF_REQUIRE(level >= 0 && level < (int)lv_.size(), "level out of range");
+  const int M = n * samples;
+  NOF_REQUIRE(n > 0 && samples % kBlk == 0 && M <= lv_[level].cap, "batch exceeds the level's capacity");
+  lv_[level].M = M; lv_[level].n = n; lv_[level].S = samples;
+  nof::FwdArgs a{};
+  a.M = M; a.S = samples; a.encoded = 0;
+  a.t = t; a.origins = origins; a.dirs = dirs; a.radii = radii;
+  run_forward(level, a);
+}
+
+std::pair<float*, float*> AcceleratedMLP::get_output(const float* enc_pos, const float* enc_dir, int level,
+                                                     int n_rays, int samples) {
+  NOF_REQUIRE(level >= 0 && level < (int)lv_.size(), "level out of range");
+  NOF_REQUIRE(enc_pos && enc_dir, "null encoded inputs");
+  const int M = n_rays * samples;
+  NOF_REQUIRE(n_rays > 0 && samples > 0 && samples % kBlk == 0 && M <= lv_[level].cap,
+              "n_rays * samples must be a multiple of 32 within the level's capacity");
+  pack_weights();
+  lv_[level].M = M; lv_[level].n = n_rays; lv_[level].S = samples;
+  nof::FwdArgs a{};
+  a.M = M; a.S = samples; a.encoded = 1;
+  a.enc_pos = enc_pos; a.enc_dir = enc_dir;
+  run_forward(level, a);
+  return {lv_[level].sigma.p, lv_[level].rgb.p};
+}
+
+nof_mlp_debug AcceleratedMLP::debug_view(int level) const {
+  NOF_REQUIRE(level >= 0 && level < (int)lv_.size(), "level out of range");
+  const Level& L = lv_[level];
+  nof_mlp_debug d;
+  d.M = L.M;
+  d.act_in = L.act_in.p; d.act_h = L.act_h.p; d.act_h9 = L.act_h9.p; d.masks = L.masks.p; d.zhead = L.zhead.p;
+  d.delta = delta_.p; d.delta9x = delta9x_.p;
+  return d;
+}
+
+AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M) {
+  Level& L = lv_[level];
+  auto it = L.sched.find(M);
+  if (it != L.sched.end()) return it->second;
+  const int nblk = M / kBlk;
+  const size_t ls = (size_t)nblk * 256 * kBlk;
+  std::vector<nof::WgProblem> P;
+  auto prob = [&](const float* A, int FA, int a0, int ntr, const float* B, int FB, int b0, int ntc) {
+    nof::WgProblem p;
+    p.A = A; p.FA = FA; p.a_row0 = a0; p.ntr = ntr; p.B = B; p.FB = FB; p.b_col0 = b0; p.ntc = ntc;
+    P.push_back(p);
+    return (int)P.size() - 1;
+  };
+  struct OutSpec { int prob, row_off, nrows, col_off, ncols; float* dst; int ld, dst_col; float* bias; };
+  std::vector<OutSpec> os;
+  float* G = grads_.p;
+  auto Wg = [&](int l) { return G + woff_[l]; };
+  auto Bg = [&](int l) { return G + boff_[l]; };
+  int p;
+  p = prob(delta_.p, 256, 0, 8, L.act_in.p, nof::kInF, 0, 3);
+  os.push_back({p, 0, 256, 0, 96, Wg(0), 96, 0, Bg(0)});
+  for (int l = 1; l < 8; ++l) {
+    p = prob(delta_.p + l * ls, 256, 0, 8, L.act_h.p + (l - 1) * ls, 256, 0, 8);
+    os.push_back({p, 0, 256, 0, 256, Wg(l), in_[l], 0, Bg(l)});
+    if (l == 4) {
+      p = prob(delta_.p + l * ls, 256, 0, 8, L.act_in.p, nof::kInF, 0, 3);
+      os.push_back({p, 0, 256, 0, 96, Wg(4), in_[4], 256, nullptr});
+    }
+  }
+  p = prob(delta9x_.p, nof::kD9F, 0, 5, L.act_h.p + 7 * ls, 256, 0, 8);
+  os.push_back({p, 0, 128, 0, 256, Wg(9), in_[9], 0, Bg(9)});
+  os.push_back({p, 128, 1, 0, 256, Wg(8), in_[8], 0, Bg(8)});
+  p = prob(delta9x_.p, nof::kD9F, 0, 4, L.act_in.p, nof::kInF, 96, 1);
+  os.push_back({p, 0, 128, 0, 27, Wg(9), in_[9], 256, nullptr});
+  p = prob(delta9x_.p, nof::kD9F, 128, 1, L.act_h9.p, 128, 0, 4);
+  os.push_back({p, 1, 3, 0, 128, Wg(10), in_[10], 0, Bg(10)});
+
+  // cost per k-block: MFMA rounds of the 8-wave tile split vs staging bytes (4 KB per 32-row operand block)
+  std::vector<int64_t> cost(P.size());
+  int64_t total = 0;
+  for (size_t i = 0; i < P.size(); ++i) {
+    const int tiles = P[i].ntr * P[i].ntc;
+    cost[i] = std::max((tiles + 7) / 8, (P[i].ntr + P[i].ntc + 3) / 4);
+    total += cost[i] * nblk;
+  }
+  const int G_wg = num_cu_;
+  const int64_t per = (total + G_wg - 1) / G_wg;
+  std::vector<nof::WgItem> items;
+  std::vector<int> item_wg;
+  std::vector<int> first_item(P.size()), nitems(P.size());
+  int wg = 0;
+  int64_t used = 0;
+  for (size_t pi = 0; pi < P.size(); ++pi) {
+    first_item[pi] = (int)items.size();
+    int kb = 0;
+    while (kb < nblk) {
+      int64_t take;
+      if (wg == G_wg - 1) {
+        take = nblk - kb;
+      } else {
+        take = std::min<int64_t>(nblk - kb, (per - used) / cost[pi]);
+        if (take == 0) {
+          if (used > 0) { ++wg; used = 0; continue; }  // finish this workgroup instead of a 1-block sliver
+          take = 1;
+        }
+      }
+      nof::WgItem itm;
+      itm.prob = (int)pi; itm.kb0 = kb; itm.kb1 = kb + (int)take; itm.slab = (int)items.size();
+      items.push_back(itm);
+      item_wg.push_back(wg);
+      used += take * cost[pi];
+      kb += (int)take;
+      if (used >= per && wg < G_wg - 1) { ++wg; used = 0; }
+    }
+    nitems[pi] = (int)items.size() - first_item[pi];
+  }
+  const int nwg = std::min(G_wg, item_wg.empty() ? 0 : item_wg.back() + 1);
+  std::vector<int> item_ptr(nwg + 1, 0);
+  for (int w : item_wg) item_ptr[w + 1]++;
+  for (int w = 0; w < nwg; ++w) item_ptr[w + 1] += item_ptr[w];
+  std::vector<int64_t> slab_off(items.size());
+  int64_t so = 0;
+  for (size_t i = 0; i < items.size(); ++i) {
+    slab_off[i] = so;
+    so += (int64_t)P[items[i].prob].ntr * 32 * P[items[i].prob].ntc * 32;
+  }
+  if ((size_t)so > slab_cap_ || items.size() * 256 > bias_slabs_.n) {  // grow (schedules are built once per M)
+    NOF_HIP(hipStreamSynchronize(st_));
+    slab_cap_ = std::max((size_t)so, slab_cap_);
+    slabs_.alloc(slab_cap_);
+    bias_slabs_.alloc(std::max(items.size() * 256, bias_slabs_.n));
+  }
+  std::vector<nof::WgOut> outs;
+  int max_elems = 0;
+  for (const OutSpec& s : os) {
+    nof::WgOut o;
+    o.item0 = first_item[s.prob]; o.nitems = nitems[s.prob];
+    o.row_off = s.row_off; o.nrows = s.nrows; o.col_off = s.col_off; o.ncols = s.ncols;
+    o.dst = s.dst; o.ld = s.ld; o.dst_col = s.dst_col; o.bias_dst = s.bias; o.prob = s.prob;
+    outs.push_back(o);
+    max_elems = std::max(max_elems, s.nrows * s.ncols);
+  }
+  Schedule& sc = L.sched[M];
+  sc.probs.alloc(P.size());
+  sc.items.alloc(items.size());
+  sc.item_ptr.alloc(item_ptr.size());
+  sc.slab_off.alloc(slab_off.size());
+  sc.outs.alloc(outs.size());
+  NOF_HIP(hipMemcpy(sc.probs.p, P.data(), P.size() * sizeof(P[0]), hipMemcpyHostToDevice));
+  NOF_HIP(hipMemcpy(sc.items.p, items.data(), items.size() * sizeof(items[0]), hipMemcpyHostToDevice));
+  NOF_HIP(hipMemcpy(sc.item_ptr.p, item_ptr.data(), item_ptr.size() * sizeof(int), hipMemcpyHostToDevice));
+  NOF_HIP(hipMemcpy(sc.slab_off.p, slab_off.data(), slab_off.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  NOF_HIP(hipMemcpy(sc.outs.p, outs.data(), outs.size() * sizeof(outs[0]), hipMemcpyHostToDevice));
+  sc.nouts = (int)outs.size();
+  sc.max_elems = max_elems;
+  sc.num_wg = nwg;
+  return sc;
+}
+
+float* const* AcceleratedMLP::get_gradient(const float* color_grad, const float* density_grad, int level) {
+  NOF_REQUIRE(level >= 0 && level < (int)lv_.size(), "level out of range");
+  Level& L = lv_[level];
+  NOF_REQUIRE(L.M > 0, "get_gradient before get_output for this level");
+  NOF_REQUIRE(color_grad && density_grad, "null output gradients");
+  Schedule& sc = schedule(level, L.M);
+  nof::BwdArgs b{};
+  b.M = L.M;
+  b.dsigma = density_grad; b.drgb = color_grad; b.zhead = L.zhead.p;
+  b.masks = L.masks.p;
+  b.wimg_b = wimg_b_.p;
+  b.delta = delta_.p; b.delta9x = delta9x_.p;
+  tb(kTMlpBwd);
+  NOF_HIP(nof::launch_mlp_bwd(b, st_));
+  te(kTMlpBwd);
+  tb(kTWgrad);
+  NOF_HIP(nof::launch_wgrad(sc.probs.p, sc.items.p, sc.item_ptr.p, sc.num_wg, sc.slab_off.p, slabs_.p,
+                            bias_slabs_.p, st_));
+  te(kTWgrad);
+  tb(kTWgradReduce);
+  NOF_HIP(nof::launch_wgrad_reduce(sc.outs.p, sc.nouts, sc.max_elems, sc.items.p, sc.probs.p, sc.slab_off.p,
+                                   slabs_.p, bias_slabs_.p, level > 0 ? 1 : 0, st_));
+  te(kTWgradReduce);
+  return grad_views_.data();
+}
+
+// ------------------------------------------------------------------------------------------------
+// AcceleratedMipNeRF
+// ------------------------------------------------------------------------------------------------
+AcceleratedMipNeRF::AcceleratedMipNeRF(const nof_config& cfg) : mlp(nullptr), cfg_(cfg) {
+  check_cfg(cfg);
+  NOF_HIP(hipSetDevice(cfg.device));
+  st_ = (hipStream_t)cfg.stream;
+  seed_ = cfg.seed;
+  mlp = new AcceleratedMLP(cfg.max_deg_point - cfg.min_deg_point, cfg.deg_view, cfg);
+  mlp->timer = &timer;
+  const size_t N = cfg.max_rays;
+  o_.alloc(3 * N); d_.alloc(3 * N); radii_.alloc(N); nears_.alloc(N); fars_.alloc(N); lm_.alloc(N); pix_.alloc(3 * N);
+  const int L = cfg.num_levels;
+  t_.resize(L); w_.resize(L); C_.resize(L); dsig_.resize(L); drgb_.resize(L); loss_rays_.resize(L);
+  for (int l = 0; l < L; ++l) {
+    const size_t S = cfg.num_samples[l];
+    t_[l].alloc(N * (S + 1)); w_[l].alloc(N * S); C_[l].alloc(3 * N);
+    dsig_[l].alloc(N * S); drgb_[l].alloc(3 * N * S); loss_rays_[l].alloc(N);
+  }
+}
+
+AcceleratedMipNeRF::~AcceleratedMipNeRF() { delete mlp; }
+
+float* const* AcceleratedMipNeRF::GetGradient(int n, const float* origins, const float* directions,
+                                              const float* radii, const float* nears, const float* fars,
+                                              const float* loss_mults, nof_output_grad_fn cb, void* user) {
+  NOF_REQUIRE(n > 0 && n <= cfg_.max_rays, "ray count out of range");
+  NOF_REQUIRE(origins && directions && radii && nears && fars && loss_mults && cb, "null argument");
+  // loss-mult sum as float (D14: the reference truncates it into an int, MNcpp:61-65)
+  float msum = 0.0f;
+  for (int i = 0; i < n; ++i) msum += loss_mults[i];
+  NOF_HIP(hipMemcpyAsync(o_.p, origins, 3 * n * sizeof(float), hipMemcpyHostToDevice, st_));
+  NOF_HIP(hipMemcpyAsync(d_.p, directions, 3 * n * sizeof(float), hipMemcpyHostToDevice, st_));
+  NOF_HIP(hipMemcpyAsync(radii_.p, radii, n * sizeof(float), hipMemcpyHostToDevice, st_));
+  NOF_HIP(hipMemcpyAsync(nears_.p, nears, n * sizeof(float), hipMemcpyHostToDevice, st_));
+  NOF_HIP(hipMemcpyAsync(fars_.p, fars, n * sizeof(float), hipMemcpyHostToDevice, st_));
+  NOF_HIP(hipMemcpyAsync(lm_.p, loss_mults, n * sizeof(float), hipMemcpyHostToDevice, st_));
+  return run(n, o_.p, d_.p, radii_.p, nears_.p, fars_.p, lm_.p, nullptr, msum, cb, user);
+}
+
+float* const* AcceleratedMipNeRF::GetGradientDevice(int n, const float* o, const float* d, const float* radii,
+                                                    const float* nears, const float* fars, const float* loss_mults,
+                                                    const float* pixels, float msum) {
+  NOF_REQUIRE(n > 0 && n <= cfg_.max_rays, "ray count out of range");
+  NOF_REQUIRE(o && d && radii && nears && fars && loss_mults && pixels, "null argument");
+  NOF_REQUIRE(msum > 0.0f, "loss_mult_sum must be > 0");
+  return run(n, o, d, radii, nears, fars, loss_mults, pixels, msum, nullptr, nullptr);
+}
+
+float* const* AcceleratedMipNeRF::run(int n, const float* o, const float* d, const float* radii, const float* nears,
+                                      const float* fars, const float* lm, const float* pix, float msum,
+                                      nof_output_grad_fn cb, void* user) {
+  const int L = cfg_.num_levels;
+  mlp->pack_weights();
+  for (int lv = 0; lv < L; ++lv) {  // MNcpp:85-123
+    const int S = cfg_.num_samples[lv];
+    timer.begin(kTSample);
+    if (lv == 0) {
+      NOF_HIP(nof::launch_sample_stratified(n, S, nears, fars, cfg_.randomized, seed_, step_, 0, ray_base_,
+                                            t_[0].p, st_));
+    } else {
+      NOF_HIP(nof::launch_sample_pdf(n, cfg_.num_samples[lv - 1], t_[lv - 1].p, w_[lv - 1].p, S,
+                                     cfg_.resample_padding, cfg_.randomized, seed_, step_, (uint32_t)lv, ray_base_,
+                                     t_[lv].p, nullptr, st_));
+    }
+    timer.end(kTSample);
+    mlp->forward_fused(lv, n, S, t_[lv].p, o, d, radii);
+    timer.begin(kTRenderFwd);
+    NOF_HIP(nof::launch_render_fwd(n, S, mlp->density(lv), mlp->rgb(lv), t_[lv].p, d, cfg_.white_bkgd, C_[lv].p,
+                                   w_[lv].p, st_));
+    timer.end(kTRenderFwd);
+  }
+  for (int lv = 0; lv < L; ++lv) {  // MNcpp:125-134
+    const int S = cfg_.num_samples[lv];
+    const float lam = lv < L - 1 ? cfg_.coarse_loss_mult : 1.0f;
+    const float* g = nullptr;
+    if (cb) {
+      g = reinterpret_cast<const float*>(cb(user, (uint64_t)(uintptr_t)C_[lv].p, lv, msum, (uint64_t)(uintptr_t)lm));
+      NOF_REQUIRE(g != nullptr, "output-gradient callback returned null");
+    }
+    timer.begin(kTRenderBwd);
+    NOF_HIP(nof::launch_render_bwd(n, S, mlp->density(lv), mlp->rgb(lv), t_[lv].p, d, cfg_.white_bkgd, C_[lv].p, g,
+                                   pix, lm, msum, lam, dsig_[lv].p, drgb_[lv].p, cb ? nullptr : loss_rays_[lv].p,
+                                   st_));
+    timer.end(kTRenderBwd);
+  }
+  float* const* grads = nullptr;
+  for (int lv = 0; lv < L; ++lv) grads = mlp->get_gradient(drgb_[lv].p, dsig_[lv].p, lv);  // MNcpp:135-142
+  last_n_ = n;
+  last_fused_ = cb == nullptr;
+  ++step_;
+  return grads;
+}
+
+nof_level_view AcceleratedMipNeRF::level_view(int level) const {
+  NOF_REQUIRE(level >= 0 && level < cfg_.num_levels, "level out of range");
+  nof_level_view v;
+  v.n = last_n_;
+  v.samples = cfg_.num_samples[level];
+  v.t = t_[level].p; v.weights = w_[level].p; v.comp_rgb = C_[level].p;
+  v.density = mlp->density(level); v.rgb = mlp->rgb(level);
+  v.density_grad = dsig_[level].p; v.rgb_grad = drgb_[level].p;
+  return v;
+}
+
+float AcceleratedMipNeRF::loss() {
+  NOF_REQUIRE(last_fused_ && last_n_ > 0, "loss is available after get_gradient_device");
+  std::vector<float> h(last_n_);
+  double s = 0.0;
+  for (int l = 0; l < cfg_.num_levels; ++l) {
+    NOF_HIP(hipMemcpyAsync(h.data(), loss_rays_[l].p, last_n_ * sizeof(float), hipMemcpyDeviceToHost, st_));
+    NOF_HIP(hipStreamSynchronize(st_));
+    for (float x : h) s += x;
+  }
+  return (float)s;
+}
+
+// ------------------------------------------------------------------------------------------------
+// AcceleratedAdamOptimizer
+// ------------------------------------------------------------------------------------------------
+AcceleratedAdamOptimizer::AcceleratedAdamOptimizer(const std::vector<int>& layer_sizes, const nof_config& cfg)
+    : sizes_(layer_sizes) {
+  NOF_REQUIRE(!layer_sizes.empty(), "empty layer sizes");
+  NOF_HIP(hipSetDevice(cfg.device));
+  st_ = (hipStream_t)cfg.stream;
+  for (int s : sizes_) {
+    NOF_REQUIRE(s >= 0, "negative layer size");
+    off_.push_back(total_);
+    total_ += s;
+  }
+  m_.alloc(total_);
+  v_.alloc(total_);
+  NOF_HIP(hipMemset(m_.p, 0, total_ * sizeof(float)));  // D18: the reference never zeroes m, v
+  NOF_HIP(hipMemset(v_.p, 0, total_ * sizeof(float)));
+}
+
+void AcceleratedAdamOptimizer::step(float* const* params, float* const* grads, float lr) {
+  NOF_REQUIRE(params && grads, "null params/grads");
+  ++iteration_;
+  // host-side bias corrections exactly as AcceleratedAdamOptimizer.cpp:26-28
+  const float inv1 = 1.0f / (1.0f - std::pow(0.9f, (float)iteration_));
+  const float inv2 = 1.0f / (1.0f - std::pow(0.999f, (float)iteration_));
+  bool flat = true;
+  for (size_t i = 0; i < sizes_.size(); ++i)
+    flat = flat && params[i] == params[0] + off_[i] && grads[i] == grads[0] + off_[i];
+  if (flat) {
+    NOF_HIP(nof::launch_adam(total_, params[0], grads[0], m_.p, v_.p, lr, inv1, inv2, st_));
+  } else {
+    for (size_t i = 0; i < sizes_.size(); ++i)
+      NOF_HIP(nof::launch_adam(sizes_[i], params[i], grads[i], m_.p + off_[i], v_.p + off_[i], lr, inv1, inv2, st_));
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// AcceleratedGradientCalculator
+// ------------------------------------------------------------------------------------------------
+AcceleratedGradientCalculator::AcceleratedGradientCalculator(int batch_size, const nof_config& cfg)
+    : batch_(batch_size), cfg_(cfg) {
+  NOF_REQUIRE(batch_size > 0, "batch_size must be > 0");
+  NOF_HIP(hipSetDevice(cfg.device));
+  st_ = (hipStream_t)cfg.stream;
+  pixels_.alloc(3 * (size_t)batch_size);
+  grad_.resize(NOF_MAX_LEVELS);
+  for (auto& g : grad_) g.alloc(3 * (size_t)batch_size);
+}
+
+uint64_t AcceleratedGradientCalculator::get_output_gradient(uint64_t input, const float* host_pixels, int n,
+                                                            uint64_t loss_mults, float loss_mult_sum, int level) {
+  NOF_REQUIRE(n > 0 && n <= batch_, "n exceeds batch size");
+  NOF_REQUIRE(level >= 0 && level < cfg_.num_levels, "level out of range");
+  NOF_REQUIRE(input && host_pixels && loss_mults, "null argument");
+  // D15: upload host -> device (the reference's memcpy has src/dst swapped) and keep one buffer per level
+  NOF_HIP(hipMemcpyAsync(pixels_.p, host_pixels, 3 * (size_t)n * sizeof(float), hipMemcpyHostToDevice, st_));
+  const float lam = level < cfg_.num_levels - 1 ? cfg_.coarse_loss_mult : 1.0f;
+  NOF_HIP(nof::launch_output_gradient(n, reinterpret_cast<const float*>(input), pixels_.p,
+                                      reinterpret_cast<const float*>(loss_mults), loss_mult_sum, lam,
+                                      grad_[level].p, st_));
+  return (uint64_t)(uintptr_t)grad_[level].p;
+}
+
+}  // namespace AcceleratedNeRFUtils

@@ -1,0 +1,226 @@
+// C++ host classes of the MI355X hot path, mirroring the reference's C++/CLI API surface
+// (namespace AcceleratedNeRFUtils, /root/reference/ScratchNerf/AcceleratedNeRFUtils/*.h) with
+// plain C++ types: device pointers instead of array<float*>^, std::function-free callbacks,
+// an explicit device/stream instead of cudaSetDevice(0) and cudaDeviceSynchronize() after
+// every launch.  The extern "C" shim in capi.cpp exposes them as include/nof.h.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../../include/nof.h"
+#include "../kernels/launch.h"
+
+namespace AcceleratedNeRFUtils {
+
+struct Error : std::runtime_error {
+  nof_status code;
+  Error(nof_status c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define NOF_HIP(expr)                                                                                    \
+  do {                                                                                                   \
+    hipError_t _e = (expr);                                                                              \
+    if (_e != hipSuccess)                                                                                \
+      throw ::AcceleratedNeRFUtils::Error(_e == hipErrorOutOfMemory ? NOF_ERR_OOM : NOF_ERR_HIP,         \
+                                          std::string(#expr) + ": " + hipGetErrorString(_e));            \
+  } while (0)
+
+#define NOF_REQUIRE(cond, msg)                                                   \
+  do {                                                                           \
+    if (!(cond)) throw ::AcceleratedNeRFUtils::Error(NOF_ERR_INVALID_ARG, msg);  \
+  } while (0)
+
+// RAII device buffer
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  DevBuf() = default;
+  explicit DevBuf(size_t count) { alloc(count); }
+  void alloc(size_t count) {
+    release();
+    n = count;
+    if (count) NOF_HIP(hipMalloc(&p, count * sizeof(T)));
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  ~DevBuf() { release(); }
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    if (this != &o) { release(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; }
+    return *this;
+  }
+};
+
+// Per-kernel-class hipEvent timing on one stream.
+class KernelTimer {
+ public:
+  void enable(bool on, hipStream_t st);
+  bool on() const { return on_; }
+  void begin(int id);
+  void end(int id);
+  void read(float* ms, int* launches, int cap);  // synchronises
+  ~KernelTimer();
+
+ private:
+  hipEvent_t get();
+  bool on_ = false;
+  hipStream_t st_ = nullptr;
+  std::vector<hipEvent_t> pool_;
+  size_t used_ = 0;
+  struct Rec { int id; hipEvent_t a, b; };
+  std::vector<Rec> recs_;
+  hipEvent_t open_[NOF_NUM_TIMERS] = {};
+};
+
+enum TimerId { kTPack = 0, kTSample, kTMlpFwd, kTRenderFwd, kTRenderBwd, kTMlpBwd, kTWgrad, kTWgradReduce };
+
+// ---------------------------------------------------------------------------------------------
+// AcceleratedMLP (AcceleratedMLP.h:7-45; MLPcpp:7-339)
+// ---------------------------------------------------------------------------------------------
+class AcceleratedMLP {
+ public:
+  static constexpr int kLayers = 11;   // net_depth + net_depth_condition + 2
+  static constexpr int kTensors = 22;  // [W0..W10, b0..b10]
+
+  AcceleratedMLP(int deg_point, int deg_view, const nof_config& cfg);  // MLPcpp:168-213
+  ~AcceleratedMLP() = default;
+
+  std::vector<int> get_layer_sizes() const;  // MLPcpp:131-154
+  // get_output (MLPcpp:214-255), encoded inputs.  Returns {density, rgb}.
+  std::pair<float*, float*> get_output(const float* enc_pos, const float* enc_dir, int level, int n_rays,
+                                       int samples);
+  // get_gradient (MLPcpp:256-321); level 0 overwrites, level > 0 accumulates.
+  float* const* get_gradient(const float* color_grad, const float* density_grad, int level);
+
+  float* const* allParams() const { return param_views_.data(); }
+  float* const* allGradients() const { return grad_views_.data(); }
+  float* flat_params() const { return params_.p; }
+  float* flat_grads() const { return grads_.p; }
+  int64_t num_params() const { return (int64_t)P_; }
+
+  // fused path (AcceleratedMipNeRF): frustum + IPE computed inside the forward kernel
+  void forward_fused(int level, int n, int samples, const float* t, const float* origins, const float* dirs,
+                     const float* radii);
+  void pack_weights();  // rebuild the packed weight images from the canonical arena
+  const float* density(int level) const { return lv_[level].sigma.p; }
+  const float* rgb(int level) const { return lv_[level].rgb.p; }
+  KernelTimer* timer = nullptr;
+  hipStream_t stream() const { return st_; }
+  nof_mlp_debug debug_view(int level) const;
+
+ private:
+  struct Schedule {
+    DevBuf<nof::WgProblem> probs;
+    DevBuf<nof::WgItem> items;
+    DevBuf<int> item_ptr;
+    DevBuf<int64_t> slab_off;
+    DevBuf<nof::WgOut> outs;
+    int nouts = 0, max_elems = 0, num_wg = 0;
+  };
+  struct Level {
+    int cap = 0, M = 0, n = 0, S = 0;
+    DevBuf<float> act_in, act_h, act_h9, zhead, sigma, rgb;
+    DevBuf<uint32_t> masks;
+    std::map<int, Schedule> sched;  // by M
+  };
+  void run_forward(int level, const nof::FwdArgs& a);
+  Schedule& schedule(int level, int M);
+  void tb(int id) { if (timer) timer->begin(id); }
+  void te(int id) { if (timer) timer->end(id); }
+
+  nof_config cfg_;
+  hipStream_t st_;
+  int num_cu_ = 256;
+  size_t P_ = 0;
+  std::array<int, kLayers> out_{}, in_{}, woff_{}, boff_{};
+  DevBuf<float> params_, grads_, wimg_f_, wimg_b_;
+  std::vector<float*> param_views_, grad_views_;
+  std::vector<Level> lv_;
+  int max_M_ = 0;
+  DevBuf<float> delta_, delta9x_, slabs_, bias_slabs_;
+  size_t slab_cap_ = 0;
+};
+
+// ---------------------------------------------------------------------------------------------
+// AcceleratedMipNeRF (AcceleratedMipNeRF.h:10-41; MNcpp:7-176)
+// ---------------------------------------------------------------------------------------------
+class AcceleratedMipNeRF {
+ public:
+  explicit AcceleratedMipNeRF(const nof_config& cfg);
+  ~AcceleratedMipNeRF();
+  AcceleratedMLP* mlp;  // public field, as AcceleratedMipNeRF.h:18
+
+  float* const* GetGradient(int n, const float* origins, const float* directions, const float* radii,
+                            const float* nears, const float* fars, const float* loss_mults, nof_output_grad_fn cb,
+                            void* user);
+  float* const* GetGradientDevice(int n, const float* o, const float* d, const float* radii, const float* nears,
+                                  const float* fars, const float* loss_mults, const float* pixels, float msum);
+  std::vector<int> GetLayerSizes() const { return mlp->get_layer_sizes(); }
+
+  void set_rng(uint64_t seed, uint32_t step, uint32_t ray_base) { seed_ = seed; step_ = step; ray_base_ = ray_base; }
+  void get_rng(uint64_t* seed, uint32_t* step, uint32_t* ray_base) const { *seed = seed_; *step = step_; *ray_base = ray_base_; }
+  nof_level_view level_view(int level) const;
+  float loss();
+  KernelTimer timer;
+
+ private:
+  float* const* run(int n, const float* o, const float* d, const float* radii, const float* nears,
+                    const float* fars, const float* lm, const float* pix, float msum, nof_output_grad_fn cb,
+                    void* user);
+  nof_config cfg_;
+  hipStream_t st_;
+  uint64_t seed_;
+  uint32_t step_ = 0, ray_base_ = 0;
+  int last_n_ = 0;
+  bool last_fused_ = false;
+  DevBuf<float> o_, d_, radii_, nears_, fars_, lm_, pix_;
+  std::vector<DevBuf<float>> t_, w_, C_, dsig_, drgb_, loss_rays_;
+};
+
+// ---------------------------------------------------------------------------------------------
+// AcceleratedAdamOptimizer (AcceleratedAdamOptimizer.h:5-20)
+// ---------------------------------------------------------------------------------------------
+class AcceleratedAdamOptimizer {
+ public:
+  AcceleratedAdamOptimizer(const std::vector<int>& layer_sizes, const nof_config& cfg);
+  void step(float* const* params, float* const* grads, float learning_rate);
+  int iteration() const { return iteration_; }
+
+ private:
+  std::vector<int> sizes_;
+  std::vector<int64_t> off_;
+  int64_t total_ = 0;
+  int iteration_ = 0;
+  hipStream_t st_;
+  DevBuf<float> m_, v_;
+};
+
+// ---------------------------------------------------------------------------------------------
+// AcceleratedGradientCalculator (AcceleratedGradientCalculator.h:8-17)
+// ---------------------------------------------------------------------------------------------
+class AcceleratedGradientCalculator {
+ public:
+  AcceleratedGradientCalculator(int batch_size, const nof_config& cfg);
+  uint64_t get_output_gradient(uint64_t input, const float* host_pixels, int n, uint64_t loss_mults,
+                               float loss_mult_sum, int level);
+
+ private:
+  int batch_;
+  nof_config cfg_;
+  hipStream_t st_;
+  DevBuf<float> pixels_;
+  std::vector<DevBuf<float>> grad_;  // one per level (D15)
+};
+
+}  // namespace AcceleratedNeRFUtils

@@ -1,0 +1,118 @@
+// Fused Adam over the flat parameter arena, and the per-step weight-image packer.
+//
+// Adam replaces the 22 per-tensor launches of AcceleratedAdamOptimizer::step
+// (AcceleratedAdamOptimizer.cpp:23-41) with one launch; formula = the CUDA kernel's
+// (adam_optimizer_step AF:403-416, D18): eps inside 1/sqrt, fp32, contraction off, so the
+// result is bit-identical to oracle/oracle.cpp::orc_adam_step.
+#include "common.h"
+#include "launch.h"
+#include "mlp_common.h"
+
+#pragma clang fp contract(off)
+
+namespace nof {
+
+__global__ void k_adam(int64_t n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                       float* __restrict__ v, float lr, float inv1, float inv2) {
+  const float b1 = 0.9f, b2 = 0.999f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = g[i];
+    const float mi = b1 * m[i] + (1.0f - b1) * gi;
+    const float vi = b2 * v[i] + (1.0f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float mh = mi * inv1, vh = vi * inv2;
+    p[i] = p[i] - lr * mh * (1.0f / sqrtf(vh + 1e-8f));
+  }
+}
+
+hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v, float lr, float inv1, float inv2,
+                       hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(256), 0, st, n, p, g, m, v, lr, inv1, inv2);
+  return hipGetLastError();
+}
+
+// layer dims of the fixed 8x256 / 128 network (MLPcpp:131-154)
+__device__ inline int layer_out(int l) { return l < 8 ? 256 : (l == 8 ? 1 : (l == 9 ? 128 : 3)); }
+__device__ inline int layer_in(int l) {
+  return l == 0 ? 96 : (l == 4 ? 352 : (l < 8 ? 256 : (l == 8 ? 256 : (l == 9 ? 283 : 128))));
+}
+
+// forward schedule slice -> (layer, first input column)
+__device__ inline void fwd_slice(int s, int& l, int& col) {
+  if (s < 3) { l = 0; col = 32 * s; }
+  else if (s < 27) { l = 1 + (s - 3) / 8; col = 32 * ((s - 3) % 8); }
+  else if (s < 38) { l = 4; col = 32 * (s - 27); }
+  else if (s < 62) { l = 5 + (s - 38) / 8; col = 32 * ((s - 38) % 8); }
+  else { l = 9; col = 32 * (s - 62); }
+}
+// backward schedule slice -> (layer, first output row used as k)
+__device__ inline void bwd_slice(int s, int& l, int& o) {
+  if (s < 4) { l = 9; o = 32 * s; }
+  else { l = 7 - (s - 4) / 8; o = 32 * ((s - 4) % 8); }
+}
+
+// One thread per image float.  Forward slice element (row r, col c) = W_l[r][col + c];
+// backward slice element (row i, col c) = W_l[o + c][i]; both stored at slice_off(r, c).
+__global__ void k_pack_weights(const float* __restrict__ P, PackArgs pa, float* __restrict__ wf,
+                               float* __restrict__ wb) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nf = (int64_t)kFwdImageFloats, nb = (int64_t)kBwdImageFloats;
+  if (gid < nf) {
+    const int64_t slices = (int64_t)kFwdSlices * kSliceFloats;
+    float v = 0.0f;
+    if (gid < slices) {
+      const int s = (int)(gid / kSliceFloats);
+      const int e = (int)(gid - (int64_t)s * kSliceFloats);
+      const int r = e >> 5, pc = e & 31;
+      const int c = ((((pc >> 2) ^ ((r >> 1) & 7)) << 2) | (pc & 3));  // inverse of slice_off's swizzle
+      int l, col;
+      fwd_slice(s, l, col);
+      const int in = layer_in(l);
+      if (r < layer_out(l) && col + c < in) v = P[pa.woff[l] + (int64_t)r * in + col + c];
+    } else {
+      const int t = (int)(gid - slices);
+      if (t < kFwdTailW8) {
+        const int l = t / 256, x = t % 256;
+        v = x < layer_out(l) ? P[pa.boff[l] + x] : 0.0f;
+      } else if (t < kFwdTailW10) {
+        v = P[pa.woff[8] + (t - kFwdTailW8)];
+      } else if (t < kFwdTailW9d) {
+        v = P[pa.woff[10] + (t - kFwdTailW10)];
+      } else {
+        const int o = (t - kFwdTailW9d) / 32, k = (t - kFwdTailW9d) % 32;
+        v = k < kDirIn ? P[pa.woff[9] + (int64_t)o * 283 + 256 + k] : 0.0f;
+      }
+    }
+    wf[gid] = v;
+  } else if (gid < nf + nb) {
+    const int64_t b = gid - nf;
+    const int64_t slices = (int64_t)kBwdSlices * kSliceFloats;
+    float v = 0.0f;
+    if (b < slices) {
+      const int s = (int)(b / kSliceFloats);
+      const int e = (int)(b - (int64_t)s * kSliceFloats);
+      const int i = e >> 5, pc = e & 31;
+      const int c = ((((pc >> 2) ^ ((i >> 1) & 7)) << 2) | (pc & 3));
+      int l, o;
+      bwd_slice(s, l, o);
+      v = P[pa.woff[l] + (int64_t)(o + c) * layer_in(l) + i];
+    } else {
+      const int t = (int)(b - slices);
+      v = t < kBwdTailW10 ? P[pa.woff[8] + t] : P[pa.woff[10] + (t - kBwdTailW10)];
+    }
+    wb[b] = v;
+  }
+}
+
+hipError_t launch_pack_weights(const float* params, const PackArgs& pa, float* wimg_f, float* wimg_b, hipStream_t st) {
+  const int64_t total = (int64_t)kFwdImageFloats + (int64_t)kBwdImageFloats;
+  hipLaunchKernelGGL(k_pack_weights, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, params, pa, wimg_f,
+                     wimg_b);
+  return hipGetLastError();
+}
+
+}  // namespace nof

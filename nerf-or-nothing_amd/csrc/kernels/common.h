@@ -1,0 +1,93 @@
+// Shared device-side definitions for the gfx950 kernels of the ScratchNerf hot path.
+// Written for CDNA4 only: wave64, v_mfma_f32_32x32x2_f32, XOR-swizzled LDS / HBM images.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nof {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------
+// Fixed network shape of the reference (AcceleratedMLP.h:10-19, MipNerfModel ctor
+// AcceleratedMLP(16, 4) at AcceleratedMipNeRF.h:18).
+// ---------------------------------------------------------------------------
+constexpr int kDepth = 8;        // trunk layers
+constexpr int kWidth = 256;      // trunk width
+constexpr int kWidthCond = 128;  // view-branch width
+constexpr int kSkip = 4;         // [h3, IPE] feeds layer 4
+constexpr int kPosIn = 96;       // 3 * 2 * 16 IPE features
+constexpr int kDirIn = 27;       // 3 * (2 * 4 + 1) view PE features
+constexpr int kInF = 128;        // act_in rows: IPE 0..95 | view PE 96..122 | zero 123..127
+constexpr int kNumLayers = kDepth + 1 + 2;   // 11 (0..7 trunk, 8 density, 9 view, 10 rgb)
+constexpr int kD9F = 160;        // delta9x rows: delta9 0..127 | dz_sigma 128 | dz_rgb 129..131 | 0
+constexpr int kBlk = 32;         // samples per activation block (= MFMA N/M tile)
+constexpr int kSliceFloats = 8192;  // one packed weight slice: 256 rows x 32 cols fp32 (32 KB)
+constexpr int kFwdSlices = 3 + 8 * 3 + 11 + 8 * 3 + 8;   // 70: L0 | L1-3 | L4 | L5-7 | L9
+constexpr int kBwdSlices = 4 + 8 * 7;                      // 60: L9 | L7..L1
+
+// Element (f, s) of a [F][32] activation block: sample index XOR-swizzled by the
+// feature row so that 32 lanes reading one sample of 32 consecutive features hit
+// 32 distinct LDS banks (ds_read_b32 bank = dword % 32), while 32 lanes writing one
+// feature for 32 consecutive samples still fill one whole 128-B line.
+__host__ __device__ inline int blk_off(int f, int s) { return f * kBlk + (s ^ (f & 31)); }
+
+// Packed weight slice [rows][32]: logical 16-B chunk c of row r stored at c ^ ((r >> 1) & 7),
+// making the ds_read_b128 operand fetches of the MFMA A operand bank-conflict-free.
+__host__ __device__ inline int slice_off(int r, int c /*0..31*/) {
+  return r * 32 + ((((c >> 2) ^ ((r >> 1) & 7)) << 2) | (c & 3));
+}
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Random123 constants) — replaces cuRAND XORWOW (D2).
+// ---------------------------------------------------------------------------
+enum : uint32_t { kStreamStratified = 1, kStreamPdf = 2, kStreamInit = 3 };
+
+__host__ __device__ inline void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0;
+    const uint32_t n1 = (uint32_t)p1;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    const uint32_t n3 = (uint32_t)p0;
+    c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+}
+
+// uniform in [0,1) for counter (k, ray, level|stream, step), key = seed.
+__host__ __device__ inline float philox_uniform(uint64_t seed, uint32_t step, uint32_t level, uint32_t stream,
+                                                uint32_t ray, uint32_t k) {
+  uint32_t c[4] = {k >> 2, ray, (level & 0xFFFFu) | (stream << 16), step};
+  philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const uint32_t x = c[k & 3];
+  return (float)(x >> 8) * (1.0f / 16777216.0f);
+}
+
+// ---------------------------------------------------------------------------
+// wave64 helpers
+// ---------------------------------------------------------------------------
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// fp32 MFMA 32x32x2: lane l supplies A[l&31][l>>5], B[l>>5][l&31]; D lane l reg r =
+// D[(r&3) + 8*(r>>2) + 4*(l>>5)][l&31]  (verified on gfx950, tools/probe/mfma_probe.hip).
+__device__ inline f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ inline float softplus_f(float x) { return x > 20.0f ? x : log1pf(expf(x)); }  // D28
+__device__ inline float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+constexpr float kRgbPadding = 0.001f;
+constexpr float kRgbScale = 1.0f + 2.0f * 0.001f;  // (1 + 2*RgbPadding), MNcs:308
+constexpr float kDensityBias = -1.0f;              // MNcs:20
+constexpr float kHalfPi = 3.14159274f * 0.5f;      // MathF.PI * 0.5f, MH:446
+
+}  // namespace nof

@@ -1,0 +1,86 @@
+// Host-side launchers of the gfx950 kernels (one definition per .hip file).
+// All launches are asynchronous on the given stream; none allocates or synchronises,
+// so a caller may capture any sequence of them into a hipGraph.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nof {
+
+// ---- sampling.hip (get_sample_t_vals AF:222-242, get_resampled_t_vals AF:246-291) ----------
+hipError_t launch_sample_stratified(int n, int S, const float* nears, const float* fars, int randomized,
+                                    uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base, float* t,
+                                    hipStream_t st);
+hipError_t launch_sample_pdf(int n, int S_in, const float* t_in, const float* w, int S_out, float padding,
+                             int randomized, uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base,
+                             float* t_out, int32_t* idx_out, hipStream_t st);
+hipError_t launch_cast(int n, int S, const float* t, const float* o, const float* d, const float* radius,
+                       float* mean, float* cov, hipStream_t st);
+hipError_t launch_encode(int n, int S, const float* mean, const float* cov, const float* d, float* enc_pos,
+                         float* enc_dir, hipStream_t st);
+
+// ---- render.hip (volumetric_rendering AF:318-344, get_output_gradient AF:347-361,
+//      volumetric_rendering_gradient AF:362-402) -------------------------------------------------
+hipError_t launch_render_fwd(int n, int S, const float* sigma, const float* rgb, const float* t, const float* d,
+                             int white, float* C, float* w, hipStream_t st);
+// g_ext != null: dL/dC supplied by the caller (callback path); else fused loss gradient from pix.
+hipError_t launch_render_bwd(int n, int S, const float* sigma, const float* rgb, const float* t, const float* d,
+                             int white, const float* C, const float* g_ext, const float* pix,
+                             const float* lossmult, float loss_mult_sum, float lam, float* dsigma, float* drgb,
+                             float* loss_rays, hipStream_t st);
+hipError_t launch_output_gradient(int n, const float* C, const float* pix, const float* lossmult,
+                                  float loss_mult_sum, float lam, float* g, hipStream_t st);
+
+// ---- mlp_fwd.hip / mlp_bwd.hip -----------------------------------------------------------------
+struct FwdArgs {
+  int M, S, encoded;
+  const float *t, *origins, *dirs, *radii;  // fused-encoding inputs
+  const float *enc_pos, *enc_dir;          // encoded inputs (API path): [M][96], [n][27]
+  const float* wimg;                       // packed forward image (slices + tail)
+  float* act_in;   // [M/32][128][32]
+  float* act_h;    // [8][M/32][256][32]
+  float* act_h9;   // [M/32][128][32]
+  uint32_t* masks; // [M/32][9][64][4]
+  float* zhead;    // [M][4]
+  float* sigma;    // [M]
+  float* rgb;      // [M][3]
+};
+hipError_t launch_mlp_fwd(const FwdArgs& a, hipStream_t st);
+
+struct BwdArgs {
+  int M;
+  const float *dsigma, *drgb, *zhead;
+  const uint32_t* masks;
+  const float* wimg_b;                     // packed backward image (slices + tail)
+  float* delta;    // [8][M/32][256][32]
+  float* delta9x;  // [M/32][160][32]
+};
+hipError_t launch_mlp_bwd(const BwdArgs& a, hipStream_t st);
+
+// ---- wgrad.hip: weight/bias gradients as one scheduled split-K launch + ordered reduce ------
+struct WgProblem {
+  const float* A; const float* B;
+  int FA, a_row0, ntr;   // A rows [a_row0, a_row0 + 32*ntr) of an [FA][32]-block buffer
+  int FB, b_col0, ntc;   // B rows (= output columns) [b_col0, b_col0 + 32*ntc)
+};
+struct WgItem { int prob, kb0, kb1; int slab; };  // slab = index into slab_off[]
+struct WgOut {
+  int item0, nitems;        // contiguous items of the problem
+  int row_off, nrows, col_off, ncols;
+  float* dst; int ld, dst_col;
+  float* bias_dst;          // null: no bias
+  int prob;
+};
+hipError_t launch_wgrad(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,
+                        const int64_t* slab_off, float* slabs, float* bias_slabs, hipStream_t st);
+hipError_t launch_wgrad_reduce(const WgOut* outs, int nouts, int max_elems, const WgItem* items,
+                               const WgProblem* probs, const int64_t* slab_off, const float* slabs,
+                               const float* bias_slabs, int accumulate, hipStream_t st);
+
+// ---- adam.hip ----------------------------------------------------------------------------------
+hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v, float lr, float inv1, float inv2,
+                       hipStream_t st);
+struct PackArgs { int woff[11]; int boff[11]; };
+hipError_t launch_pack_weights(const float* params, const PackArgs& pa, float* wimg_f, float* wimg_b, hipStream_t st);
+
+}  // namespace nof

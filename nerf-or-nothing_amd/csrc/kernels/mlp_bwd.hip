@@ -1,0 +1,124 @@
+// Fused MLP backward (input-gradient chain) on gfx950: heads -> layer 9 -> layers 7..1.
+//
+// Replaces the 11 backpropagate_neuron* launches of AcceleratedMLP::get_gradient
+// (MLPcpp:256-321; AF:91-182), whose ~17 G global atomicAdds per 256x256 layer (AF:101-110)
+// are the reference's dominant cost.  Here the chain dh_{l-1} = W_l^T delta_l runs as fp32
+// MFMAs with delta resident in registers (same register layout trick as the forward), ReLU
+// masks come from the forward's packed bits, and every delta_l is written once in the
+// block-swizzled [F][32] layout for the deterministic weight-gradient GEMMs (wgrad.hip).
+// Gradient routing per D11: dh7 = W8^T dz_s + W9[:, :256]^T delta9 ; dh3 = W4[:, :256]^T delta4.
+// Heads per MNcs:410-415 with the sigmoid' written as s(1-s) (overflow-safe, D28).
+#include "common.h"
+#include "launch.h"
+#include "mlp_common.h"
+
+namespace nof {
+
+// delta = mask ? acc (+ w8 * dzs) : 0 -> B operand + delta block.
+template <bool kDensity>
+__device__ __forceinline__ void bwd_epilogue(const f32x16 (&acc)[8], float (&bin)[8][16], const float* w8, float dzs,
+                                             const uint4 mk, float* __restrict__ dst_blk, int lane) {
+  int lv = lane;
+  asm volatile("" : "+v"(lv));  // keep per-store offsets out of the layer loop (see fwd_epilogue)
+  const int h = lv >> 5, j = lv & 31;
+#pragma unroll
+  for (int ot = 0; ot < 8; ++ot) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int fb = ot * 32 + 8 * q + 4 * h;
+      f32x4 w4 = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (kDensity) w4 = *reinterpret_cast<const f32x4*>(w8 + fb);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int r = 4 * q + jj;
+        float v = acc[ot][r];
+        if (kDensity) v += w4[jj] * dzs;
+        v = mask_bit(mk, ot, r) ? v : 0.0f;
+        bin[ot][r] = v;
+        dst_blk[blk_off(fb + jj, j)] = v;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[2 * kSliceFloats];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
+  const int nblk = a.M / kBlk;
+  const int blk_raw = blockIdx.x * 4 + wave;
+  const int blk = blk_raw < nblk ? blk_raw : nblk - 1;  // tail waves duplicate the last block
+  const int m = blk * kBlk + j;
+  const float* tail = a.wimg_b + (size_t)kBwdSlices * kSliceFloats;
+  const size_t layer_stride = (size_t)nblk * kWidth * kBlk;
+
+  slice_dma(a.wimg_b, lds, tid);
+
+  // ---- heads (MNcs:410-415) ------------------------------------------------------------
+  const f32x4 zh = reinterpret_cast<const f32x4*>(a.zhead)[m];
+  const float dzs = a.dsigma[m] * sigmoid_f(zh[0] + kDensityBias);
+  float dzc[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float s = sigmoid_f(zh[1 + c]);
+    dzc[c] = a.drgb[(size_t)m * 3 + c] * (s * (1.0f - s)) * kRgbScale;
+  }
+  float* d9 = a.delta9x + (size_t)blk * kD9F * kBlk;
+  if (h == 0) {
+    d9[blk_off(128, j)] = dzs;
+    d9[blk_off(129, j)] = dzc[0];
+    d9[blk_off(130, j)] = dzc[1];
+    d9[blk_off(131, j)] = dzc[2];
+  }
+  // ---- delta9 = (W10^T dz_rgb) * relu'(layer 9) ------------------------------------------
+  float bin[8][16];
+  {
+    const uint4 mk = reinterpret_cast<const uint4*>(mask_ptr(const_cast<uint32_t*>(a.masks), blk, 8))[lane];
+    const float* w10 = tail + kBwdTailW10;
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int fb = ot * 32 + 8 * q + 4 * h;
+        const f32x4 wa = *reinterpret_cast<const f32x4*>(w10 + fb);
+        const f32x4 wb = *reinterpret_cast<const f32x4*>(w10 + 128 + fb);
+        const f32x4 wc = *reinterpret_cast<const f32x4*>(w10 + 256 + fb);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int r = 4 * q + jj;
+          float v = (wa[jj] * dzc[0] + wb[jj] * dzc[1]) + wc[jj] * dzc[2];
+          v = mask_bit(mk, ot, r) ? v : 0.0f;
+          bin[ot][r] = v;
+          d9[blk_off(fb + jj, j)] = v;
+        }
+      }
+  }
+  __syncthreads();
+
+  int cur = 0;
+  const float* wsrc = a.wimg_b;
+  f32x16 acc[8];
+  // ---- dh7 = W9[:, :256]^T delta9 + w8 dz_s ; delta7 ---------------------------------------
+  mlp_layer<4, 0, 8>(bin, nullptr, acc, lds, cur, wsrc, false, tid, lane);
+  {
+    const uint4 mk = reinterpret_cast<const uint4*>(mask_ptr(const_cast<uint32_t*>(a.masks), blk, 7))[lane];
+    bwd_epilogue<true>(acc, bin, tail + kBwdTailW8, dzs, mk, a.delta + 7 * layer_stride + (size_t)blk * kWidth * kBlk,
+                       lane);
+  }
+  // ---- dh_{l-1} = W_l[:, :256]^T delta_l ; delta_{l-1}, l = 7..1 --------------------------
+  for (int l = kDepth - 1; l >= 1; --l) {
+    mlp_layer<8, 0, 8>(bin, nullptr, acc, lds, cur, wsrc, l == 1, tid, lane);
+    const uint4 mk = reinterpret_cast<const uint4*>(mask_ptr(const_cast<uint32_t*>(a.masks), blk, l - 1))[lane];
+    bwd_epilogue<false>(acc, bin, nullptr, 0.0f, mk, a.delta + (l - 1) * layer_stride + (size_t)blk * kWidth * kBlk,
+                        lane);
+  }
+}
+
+hipError_t launch_mlp_bwd(const BwdArgs& a, hipStream_t st) {
+  if (a.M <= 0) return hipSuccess;
+  if (a.M % kBlk != 0) return hipErrorInvalidValue;
+  const int nblk = a.M / kBlk;
+  hipLaunchKernelGGL(k_mlp_bwd, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace nof

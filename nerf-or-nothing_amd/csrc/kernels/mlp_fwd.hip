@@ -1,0 +1,197 @@
+// Fused conical-frustum + IPE + 8x256 MLP + density/RGB heads forward on gfx950 (fp32 MFMA).
+//
+// Replaces cast_rays (AF:292-317), encode_input_data (AF:187-221) and the 11 per-layer
+// launches of AcceleratedMLP::get_output (MLPcpp:214-255: get_neuron_output*, AF:36-90) with
+// one launch per level.  Semantics per MLP.CallCached (MLPcs:112-136) and the C# heads
+// (MNcs:307-309, D23): sigma = softplus(z_s - 1), rgb = sigmoid(z_c) * 1.002 - 0.001.
+//
+// Per wave (32 samples of one ray): encodings computed in registers (48 IPE features per
+// lane, B-operand layout), then 11 layers with activations resident in registers (see
+// mlp_common.h).  Side outputs for the backward pass: every layer's activations in the
+// block-swizzled [F][32] layout (for the weight-gradient GEMMs), packed ReLU masks (for the
+// dX chain), and raw head values.
+#include "common.h"
+#include "geometry.h"
+#include "launch.h"
+#include "mlp_common.h"
+
+namespace nof {
+
+// bias + ReLU epilogue on OT accumulator tiles -> next layer's B operand, act block, mask.
+// No per-lane guards: a tail wave past the last block is clamped onto that block and
+// recomputes bit-identical values, so its duplicate stores are benign.
+template <int OT>
+__device__ __forceinline__ void fwd_epilogue(const f32x16 (&acc)[8], float (&bin)[8][16], const float* bias,
+                                             float* __restrict__ act_blk, uint32_t* __restrict__ mask_dst, int lane) {
+  // opaque copy of the lane index: keeps the 128 per-store offsets from being hoisted out of the
+  // layer loop (they would pin 256 VGPRs of addresses); recomputing them is a few VALU ops each
+  int lv = lane;
+  asm volatile("" : "+v"(lv));
+  const int h = lv >> 5, j = lv & 31;
+  uint32_t mw[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int ot = 0; ot < OT; ++ot) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int fb = ot * 32 + 8 * q + 4 * h;
+      const f32x4 b4 = *reinterpret_cast<const f32x4*>(bias + fb);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int r = 4 * q + jj;
+        const float z = acc[ot][r] + b4[jj];
+        const float hv = z > 0.0f ? z : 0.0f;
+        bin[ot][r] = hv;
+        // shift-accumulate: bit of (ot, r) ends at position 31 - ((ot & 1) * 16 + r) of word ot >> 1
+        mw[ot >> 1] = (mw[ot >> 1] << 1) | (hv > 0.0f ? 1u : 0u);
+        act_blk[blk_off(fb + jj, j)] = hv;
+      }
+    }
+  }
+  uint4 mv;
+  mv.x = mw[0]; mv.y = mw[1]; mv.z = mw[2]; mv.w = mw[3];
+  reinterpret_cast<uint4*>(mask_dst)[lv] = mv;
+}
+
+__global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[2 * kSliceFloats + 4 * kIpeLdsFloats + 4 * 128];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
+  const int nblk = a.M / kBlk;
+  const int blk_raw = blockIdx.x * 4 + wave;
+  const int blk = blk_raw < nblk ? blk_raw : nblk - 1;  // tail waves duplicate the last block
+  const int m0 = blk * kBlk;
+  const int ray = m0 / a.S;
+  const int s0 = m0 - ray * a.S;
+  const int m = m0 + j;
+  const float* tail = a.wimg + (size_t)kFwdSlices * kSliceFloats;
+
+  slice_dma(a.wimg, lds, tid);  // first slice in flight while the encodings are computed
+
+  // ---- encodings: 48 IPE features per lane in B-operand order ----------------------------
+  float ipe[3][16];
+  float d3[3];
+  if (!a.encoded) {
+    d3[0] = a.dirs[3 * ray]; d3[1] = a.dirs[3 * ray + 1]; d3[2] = a.dirs[3 * ray + 2];
+    const float o3[3] = {a.origins[3 * ray], a.origins[3 * ray + 1], a.origins[3 * ray + 2]};
+    const float* tr = a.t + (size_t)ray * (a.S + 1) + s0 + j;
+    float mean[3], cov[3];
+    frustum_gaussian(tr[0], tr[1], o3, d3, a.radii[ray], mean, cov);
+#pragma unroll
+    for (int tp = 0; tp < 3; ++tp)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ipe[tp][r] = ipe_feature(tile_feature(tp, r, h), mean, cov);
+  } else {
+#pragma unroll
+    for (int tp = 0; tp < 3; ++tp)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ipe[tp][r] = a.enc_pos[(size_t)m * kPosIn + tile_feature(tp, r, h)];
+  }
+  float pe[kDirIn];
+#pragma unroll
+  for (int k = 0; k < kDirIn; ++k) pe[k] = a.encoded ? a.enc_dir[(size_t)ray * kDirIn + k] : dir_feature(k, d3);
+
+  float* act_in_blk = a.act_in + (size_t)blk * kInF * kBlk;
+  {
+#pragma unroll
+    for (int tp = 0; tp < 3; ++tp)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) act_in_blk[blk_off(tile_feature(tp, r, h), j)] = ipe[tp][r];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {  // view PE rows 96..122, zero rows 123..127
+      const int k = 16 * h + i;
+      float v = 0.0f;
+#pragma unroll
+      for (int kk = 0; kk < kDirIn; ++kk) v = (kk == k) ? pe[kk] : v;
+      act_in_blk[blk_off(kPosIn + k, j)] = v;
+    }
+  }
+  // view-direction part of layer 9 folded into a per-ray bias: b9 + W9[:, 256:283] . PE(d)
+  float* ipe_lds = lds + 2 * kSliceFloats + wave * kIpeLdsFloats;
+#pragma unroll
+  for (int tp = 0; tp < 3; ++tp)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 v;
+      v[0] = ipe[tp][4 * q]; v[1] = ipe[tp][4 * q + 1]; v[2] = ipe[tp][4 * q + 2]; v[3] = ipe[tp][4 * q + 3];
+      *reinterpret_cast<f32x4*>(ipe_lds + ((tp * 4 + q) * 64 + lane) * 4) = v;
+    }
+  float* dirb = lds + 2 * kSliceFloats + 4 * kIpeLdsFloats + wave * 128;
+#pragma unroll
+  for (int rep = 0; rep < 2; ++rep) {
+    const int o = lane + 64 * rep;
+    float s = tail[kFwdTailBias + 9 * 256 + o];
+    const float* w9 = tail + kFwdTailW9d + o * 32;
+#pragma unroll
+    for (int k = 0; k < kDirIn; ++k) s += w9[k] * pe[k];
+    dirb[o] = s;
+  }
+  __syncthreads();
+
+  int cur = 0;
+  const float* wsrc = a.wimg;
+  f32x16 acc[8];
+  float bin[8][16];
+  const size_t layer_stride = (size_t)nblk * kWidth * kBlk;
+
+  // ---- trunk ----------------------------------------------------------------------------
+  mlp_layer<0, 3, 8>(bin, ipe_lds, acc, lds, cur, wsrc, false, tid, lane);
+  fwd_epilogue<8>(acc, bin, tail + kFwdTailBias, a.act_h + (size_t)blk * kWidth * kBlk, mask_ptr(a.masks, blk, 0),
+                  lane);
+  for (int l = 1; l < kDepth; ++l) {
+    if (l == kSkip) mlp_layer<8, 3, 8>(bin, ipe_lds, acc, lds, cur, wsrc, false, tid, lane);
+    else mlp_layer<8, 0, 8>(bin, ipe_lds, acc, lds, cur, wsrc, false, tid, lane);
+    fwd_epilogue<8>(acc, bin, tail + kFwdTailBias + l * 256,
+                    a.act_h + l * layer_stride + (size_t)blk * kWidth * kBlk, mask_ptr(a.masks, blk, l), lane);
+  }
+
+  // ---- density head (layer 8): z_s = w8 . h7 + b8 ---------------------------------------
+  float zs = 0.0f;
+#pragma unroll
+  for (int ot = 0; ot < 8; ++ot)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 w4 = *reinterpret_cast<const f32x4*>(tail + kFwdTailW8 + ot * 32 + 8 * q + 4 * h);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) zs += w4[jj] * bin[ot][4 * q + jj];
+    }
+  zs += __shfl_xor(zs, 32, 64);
+  zs += tail[kFwdTailBias + 8 * 256];
+
+  // ---- view layer 9: relu(W9[:, :256] h7 + dirbias) --------------------------------------
+  mlp_layer<8, 0, 4>(bin, ipe_lds, acc, lds, cur, wsrc, true, tid, lane);
+  fwd_epilogue<4>(acc, bin, dirb, a.act_h9 + (size_t)blk * kWidthCond * kBlk, mask_ptr(a.masks, blk, 8), lane);
+
+  // ---- RGB head (layer 10) ------------------------------------------------------------
+  float zc[3] = {0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 w4 = *reinterpret_cast<const f32x4*>(tail + kFwdTailW10 + c * 128 + ot * 32 + 8 * q + 4 * h);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) zc[c] += w4[jj] * bin[ot][4 * q + jj];
+      }
+    zc[c] += __shfl_xor(zc[c], 32, 64);
+    zc[c] += tail[kFwdTailBias + 10 * 256 + c];
+  }
+
+  if (h == 0) {
+    a.sigma[m] = softplus_f(zs + kDensityBias);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) a.rgb[(size_t)m * 3 + c] = sigmoid_f(zc[c]) * kRgbScale - kRgbPadding;
+    f32x4 zh;
+    zh[0] = zs; zh[1] = zc[0]; zh[2] = zc[1]; zh[3] = zc[2];
+    reinterpret_cast<f32x4*>(a.zhead)[m] = zh;
+  }
+}
+
+hipError_t launch_mlp_fwd(const FwdArgs& a, hipStream_t st) {
+  if (a.M <= 0) return hipSuccess;
+  if (a.M % kBlk != 0 || a.S % kBlk != 0) return hipErrorInvalidValue;
+  const int nblk = a.M / kBlk;
+  hipLaunchKernelGGL(k_mlp_fwd, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace nof

@@ -1,0 +1,182 @@
+// Volumetric alpha-compositing integrator and its adjoint for gfx950.
+// One wave64 per ray, S/64 consecutive samples per lane; the transmittance product and
+// the adjoint's suffix sum are wave-level scans (__shfl_up/__shfl_down), so a ray of any
+// S in {64,128,256,512} is one pass over coalesced SoA loads — HBM-bound by design.
+//
+// Replaces volumetric_rendering (AF:318-344), get_output_gradient (AF:347-361, folded in
+// with D14/D15 fixed) and volumetric_rendering_gradient (AF:362-402, D12: every sample);
+// math per CachedVolumetricRendering / VolumetricRenderingGradient (MH:494-610).
+#include "common.h"
+#include "launch.h"
+
+namespace nof {
+
+template <int PER>
+struct RayState {
+  float a[PER];      // alpha_k
+  float T[PER];      // T_k (exclusive transmittance)
+  float delta[PER];  // t_{k+1} - t_k
+  float dl;          // |d|
+};
+
+// alpha_k = 1 - exp(-sigma_k * delta_k * |d|); T_k = prod_{j<k} (1 - alpha_j).
+template <int PER>
+__device__ inline void ray_alpha_T(int S, int r, int lane, const float* __restrict__ sigma, const float* __restrict__ t,
+                                   const float* __restrict__ d, RayState<PER>& rs) {
+  const float dx = d[3 * r], dy = d[3 * r + 1], dz = d[3 * r + 2];
+  rs.dl = sqrtf((dx * dx + dy * dy) + dz * dz);
+  const int k0 = lane * PER;
+  const float* tr = t + (size_t)r * (S + 1) + k0;
+  const float* sr = sigma + (size_t)r * S + k0;
+  float lp = 1.0f;
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    rs.delta[p] = tr[p + 1] - tr[p];
+    rs.a[p] = 1.0f - expf(-sr[p] * rs.delta[p] * rs.dl);
+    lp *= (1.0f - rs.a[p]);
+  }
+  float inc = lp;  // inclusive product scan over lanes
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc *= y;
+  }
+  float T = __shfl_up(inc, 1, 64);
+  if (lane == 0) T = 1.0f;
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    rs.T[p] = T;
+    T *= (1.0f - rs.a[p]);
+  }
+}
+
+template <int PER>
+__global__ __launch_bounds__(256) void k_render_fwd(int n, int S, const float* __restrict__ sigma,
+                                                    const float* __restrict__ rgb, const float* __restrict__ t,
+                                                    const float* __restrict__ d, int white, float* __restrict__ C,
+                                                    float* __restrict__ w) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;  // wave-uniform; no block barriers below
+  RayState<PER> rs;
+  ray_alpha_T<PER>(S, r, lane, sigma, t, d, rs);
+  const int k0 = lane * PER;
+  const float* cr = rgb + ((size_t)r * S + k0) * 3;
+  float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, acc = 0.0f;
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const float wk = rs.a[p] * rs.T[p];
+    w[(size_t)r * S + k0 + p] = wk;
+    c0 += wk * cr[3 * p];
+    c1 += wk * cr[3 * p + 1];
+    c2 += wk * cr[3 * p + 2];
+    acc += wk;
+  }
+  c0 = wave_sum(c0); c1 = wave_sum(c1); c2 = wave_sum(c2); acc = wave_sum(acc);
+  if (lane == 0) {
+    const float bg = white ? (1.0f - acc) : 0.0f;
+    C[3 * r] = c0 + bg; C[3 * r + 1] = c1 + bg; C[3 * r + 2] = c2 + bg;
+  }
+}
+
+// dL/dc_k = g w_k ;  dL/dsigma_k = delta_k |d| [T_{k+1} e_k - sum_{j>k} w_j e_j],  e_k = g.c_k - G
+// (the C# recursion MH:565-596 in closed form; G = g.1 under a white background).
+template <int PER>
+__global__ __launch_bounds__(256) void k_render_bwd(int n, int S, const float* __restrict__ sigma,
+                                                    const float* __restrict__ rgb, const float* __restrict__ t,
+                                                    const float* __restrict__ d, int white,
+                                                    const float* __restrict__ C, const float* __restrict__ g_ext,
+                                                    const float* __restrict__ pix, const float* __restrict__ lossmult,
+                                                    float msum, float lam, float* __restrict__ dsigma,
+                                                    float* __restrict__ drgb, float* __restrict__ loss_rays) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;
+  RayState<PER> rs;
+  ray_alpha_T<PER>(S, r, lane, sigma, t, d, rs);
+  float g0, g1, g2;
+  if (g_ext) {
+    g0 = g_ext[3 * r]; g1 = g_ext[3 * r + 1]; g2 = g_ext[3 * r + 2];
+  } else {  // AF:356-358 order: 2*m/sum*(C-p)*lambda
+    const float m = lossmult[r];
+    const float s = 2.0f * m / msum;
+    const float e0 = C[3 * r] - pix[3 * r], e1 = C[3 * r + 1] - pix[3 * r + 1], e2 = C[3 * r + 2] - pix[3 * r + 2];
+    g0 = s * e0 * lam; g1 = s * e1 * lam; g2 = s * e2 * lam;
+    if (loss_rays && lane == 0) loss_rays[r] = lam * m * ((e0 * e0 + e1 * e1) + e2 * e2) / msum;
+  }
+  const float G = white ? (g0 + g1 + g2) : 0.0f;
+  const int k0 = lane * PER;
+  const float* cr = rgb + ((size_t)r * S + k0) * 3;
+  float* dcr = drgb + ((size_t)r * S + k0) * 3;
+  float wk[PER], ek[PER];
+  float ls = 0.0f;
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    wk[p] = rs.a[p] * rs.T[p];
+    ek[p] = (g0 * cr[3 * p] + g1 * cr[3 * p + 1]) + g2 * cr[3 * p + 2] - G;
+    dcr[3 * p] = g0 * wk[p]; dcr[3 * p + 1] = g1 * wk[p]; dcr[3 * p + 2] = g2 * wk[p];
+    ls += wk[p] * ek[p];
+  }
+  float inc = ls;  // inclusive suffix sum over lanes
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float y = __shfl_down(inc, o, 64);
+    if (lane + o < 64) inc += y;
+  }
+  float after = __shfl_down(inc, 1, 64);  // sum over lanes > lane
+  if (lane == 63) after = 0.0f;
+  float* dsr = dsigma + (size_t)r * S + k0;
+#pragma unroll
+  for (int p = PER - 1; p >= 0; --p) {
+    const float Tn = rs.T[p] * (1.0f - rs.a[p]);
+    dsr[p] = (Tn * ek[p] - after) * rs.delta[p] * rs.dl;
+    after += wk[p] * ek[p];
+  }
+}
+
+__global__ void k_output_gradient(int n, const float* __restrict__ C, const float* __restrict__ pix,
+                                  const float* __restrict__ lossmult, float msum, float lam, float* __restrict__ g) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const float s = 2.0f * lossmult[r] / msum;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) g[3 * r + j] = s * (C[3 * r + j] - pix[3 * r + j]) * lam;
+}
+
+#define NOF_RENDER_DISPATCH(S, BODY)            \
+  switch (S) {                                   \
+    case 64: { constexpr int PER = 1; BODY; } break;  \
+    case 128: { constexpr int PER = 2; BODY; } break; \
+    case 256: { constexpr int PER = 4; BODY; } break; \
+    case 512: { constexpr int PER = 8; BODY; } break; \
+    default: return hipErrorInvalidValue;        \
+  }
+
+hipError_t launch_render_fwd(int n, int S, const float* sigma, const float* rgb, const float* t, const float* d,
+                             int white, float* C, float* w, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const dim3 grid((n + 3) / 4), block(256);
+  NOF_RENDER_DISPATCH(S, hipLaunchKernelGGL(k_render_fwd<PER>, grid, block, 0, st, n, S, sigma, rgb, t, d, white, C, w));
+  return hipGetLastError();
+}
+
+hipError_t launch_render_bwd(int n, int S, const float* sigma, const float* rgb, const float* t, const float* d,
+                             int white, const float* C, const float* g_ext, const float* pix,
+                             const float* lossmult, float loss_mult_sum, float lam, float* dsigma, float* drgb,
+                             float* loss_rays, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const dim3 grid((n + 3) / 4), block(256);
+  NOF_RENDER_DISPATCH(S, hipLaunchKernelGGL(k_render_bwd<PER>, grid, block, 0, st, n, S, sigma, rgb, t, d, white, C,
+                                            g_ext, pix, lossmult, loss_mult_sum, lam, dsigma, drgb, loss_rays));
+  return hipGetLastError();
+}
+
+hipError_t launch_output_gradient(int n, const float* C, const float* pix, const float* lossmult,
+                                  float loss_mult_sum, float lam, float* g, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_output_gradient, dim3((n + 255) / 256), dim3(256), 0, st, n, C, pix, lossmult, loss_mult_sum,
+                     lam, g);
+  return hipGetLastError();
+}
+
+}  // namespace nof

@@ -1,0 +1,189 @@
+// Ray sampling for gfx950: stratified t-values (level 0) and hierarchical resampling
+// (levels >= 1).  Bit-exact contract with oracle/oracle.cpp: identical fp32 op sequence,
+// contraction off (this file is also built with -ffp-contract=off), correctly rounded
+// division, a sequential per-ray cdf and idx = max{i : cdf_i <= u}.
+//
+// Replaces get_sample_t_vals (AF:222-242; launched 1-D in the reference, D1) and
+// get_resampled_t_vals (AF:246-291; broken per D4) with the C# semantics
+// SampleAlongRay (MH:611-631) / ResampleAlongRay + SortedPiecewiseConstantPDF (MH:634-666, 774-851).
+#include "common.h"
+#include "geometry.h"
+#include "launch.h"
+
+#pragma clang fp contract(off)
+
+namespace nof {
+
+__device__ inline float lin_t(int k, int S, float nr, float fr) {
+  const float tv = (float)k / (float)S;
+  return nr * (1.0f - tv) + fr * tv;
+}
+
+// One thread per t-value: t_i = lower_i + (upper_i - lower_i) * u_i, lower=[t0,mids], upper=[mids,tS] (D3).
+__global__ void k_sample_stratified(int n, int S, const float* __restrict__ nears, const float* __restrict__ fars,
+                                    int randomized, uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base,
+                                    float* __restrict__ t) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n * (S + 1)) return;
+  const int r = gid / (S + 1);
+  const int i = gid - r * (S + 1);
+  const float nr = nears[r], fr = fars[r];
+  float ti;
+  if (!randomized) {
+    ti = lin_t(i, S, nr, fr);
+  } else {
+    const float li = lin_t(i, S, nr, fr);
+    const float lower = i == 0 ? li : 0.5f * (lin_t(i - 1, S, nr, fr) + li);
+    const float upper = i == S ? li : 0.5f * (li + lin_t(i + 1, S, nr, fr));
+    const float u = philox_uniform(seed, step, level, kStreamStratified, ray_base + (uint32_t)r, (uint32_t)i);
+    ti = lower + (upper - lower) * u;
+  }
+  t[gid] = ti;
+}
+
+// One 64-lane workgroup per ray.  LDS: wb[B] then cdf[B+1].
+__global__ __launch_bounds__(64) void k_sample_pdf(int n, int B, const float* __restrict__ t_in,
+                                                   const float* __restrict__ w, int S_out, float padding,
+                                                   int randomized, uint64_t seed, uint32_t step, uint32_t level,
+                                                   uint32_t ray_base, float* __restrict__ t_out,
+                                                   int32_t* __restrict__ idx_out) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* wb = smem;           // [B]   blurred weights, then pdf
+  float* cdf = smem + B;      // [B+1]
+  __shared__ float s_wsum;
+  const int r = blockIdx.x;
+  const int lane = threadIdx.x;
+  const float* wr = w + (size_t)r * B;
+  // blur-pool: wmax[i] = max(pad[i], pad[i+1]); wb[i] = .5(wmax[i] + wmax[i+1]) + padding (MH:646-661)
+  for (int i = lane; i < B; i += 64) {
+    const float w0 = wr[i];
+    const float wl = i == 0 ? w0 : wr[i - 1];
+    const float wh = i == B - 1 ? w0 : wr[i + 1];
+    const float m0 = fmaxf(wl, w0);
+    const float m1 = fmaxf(w0, wh);
+    wb[i] = 0.5f * (m0 + m1) + padding;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    double acc = 0.0;  // LINQ Sum over float accumulates in double (MH:785)
+    for (int i = 0; i < B; ++i) acc += (double)wb[i];
+    float wsum = (float)acc;
+    const float pad = fmaxf(0.0f, 1e-5f - wsum);
+    if (pad > 0.0f) {
+      const float per = pad / (float)B;
+      for (int i = 0; i < B; ++i) wb[i] = wb[i] + per;
+      wsum = wsum + pad;
+    }
+    s_wsum = wsum;
+  }
+  __syncthreads();
+  const float wsum = s_wsum;
+  for (int i = lane; i < B; i += 64) wb[i] = wb[i] / wsum;   // pdf
+  __syncthreads();
+  if (lane == 0) {  // sequential fp32 cumsum: a parallel scan would change the rounding
+    cdf[0] = 0.0f;
+    float run = 0.0f;
+    for (int i = 0; i < B - 1; ++i) {
+      run = run + wb[i];
+      cdf[i + 1] = fminf(1.0f, run);
+    }
+    cdf[B] = 1.0f;
+  }
+  __syncthreads();
+  const int ns = S_out + 1;
+  const float s1 = 1.0f / (float)ns;
+  const float* tr = t_in + (size_t)r * (B + 1);
+  for (int s = lane; s < ns; s += 64) {
+    float u;
+    if (randomized) {
+      const float rr = philox_uniform(seed, step, level, kStreamPdf, ray_base + (uint32_t)r, (uint32_t)s);
+      u = fminf((float)s * s1 + rr * (s1 - 1e-7f), 1.0f - 1e-7f);
+    } else {
+      u = (float)s * ((1.0f - 1e-7f) / (float)(ns - 1));
+    }
+    int lo = 0, hi = B - 1;  // largest i in [0, B-1] with cdf[i] <= u (cdf[0] = 0 <= u)
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (cdf[mid] <= u) lo = mid; else hi = mid - 1;
+    }
+    const float b0 = tr[lo], b1 = tr[lo + 1], c0 = cdf[lo], c1 = cdf[lo + 1];
+    const float denom = c1 - c0;
+    float tt = denom > 0.0f ? (u - c0) / denom : 0.0f;
+    tt = fminf(fmaxf(tt, 0.0f), 1.0f);
+    t_out[(size_t)r * ns + s] = b0 + tt * (b1 - b0);
+    if (idx_out) idx_out[(size_t)r * ns + s] = lo;
+  }
+}
+
+// cast_rays (AF:292-317) as a standalone kernel for the encoded-input API path / parity tests.
+__global__ void k_cast(int n, int S, const float* __restrict__ t, const float* __restrict__ o,
+                       const float* __restrict__ d, const float* __restrict__ radius, float* __restrict__ mean,
+                       float* __restrict__ cov) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n * S) return;
+  const int r = gid / S;
+  const int k = gid - r * S;
+  const float oo[3] = {o[3 * r], o[3 * r + 1], o[3 * r + 2]};
+  const float dd[3] = {d[3 * r], d[3 * r + 1], d[3 * r + 2]};
+  float mu[3], cv[3];
+  frustum_gaussian(t[(size_t)r * (S + 1) + k], t[(size_t)r * (S + 1) + k + 1], oo, dd, radius[r], mu, cv);
+  for (int j = 0; j < 3; ++j) { mean[(size_t)gid * 3 + j] = mu[j]; cov[(size_t)gid * 3 + j] = cv[j]; }
+}
+
+// encode_input_data (AF:187-221, D5 fixed): enc_pos [n*S][96] (reference feature order), enc_dir [n][27].
+__global__ void k_encode(int n, int S, const float* __restrict__ mean, const float* __restrict__ cov,
+                         const float* __restrict__ d, float* __restrict__ enc_pos, float* __restrict__ enc_dir) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int total = n * S * kPosIn;
+  if (gid < total) {
+    const int m = gid / kPosIn;
+    const int F = gid - m * kPosIn;
+    const float mu[3] = {mean[3 * m], mean[3 * m + 1], mean[3 * m + 2]};
+    const float cv[3] = {cov[3 * m], cov[3 * m + 1], cov[3 * m + 2]};
+    enc_pos[gid] = ipe_feature(F, mu, cv);
+  }
+  if (gid < n * kDirIn) {
+    const int r = gid / kDirIn;
+    const int k = gid - r * kDirIn;
+    const float dd[3] = {d[3 * r], d[3 * r + 1], d[3 * r + 2]};
+    enc_dir[gid] = dir_feature(k, dd);
+  }
+}
+
+hipError_t launch_sample_stratified(int n, int S, const float* nears, const float* fars, int randomized,
+                                    uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base, float* t,
+                                    hipStream_t st) {
+  const int total = n * (S + 1);
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sample_stratified, dim3((total + 255) / 256), dim3(256), 0, st, n, S, nears, fars, randomized,
+                     seed, step, level, ray_base, t);
+  return hipGetLastError();
+}
+
+hipError_t launch_sample_pdf(int n, int S_in, const float* t_in, const float* w, int S_out, float padding,
+                             int randomized, uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base,
+                             float* t_out, int32_t* idx_out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const size_t shm = sizeof(float) * (2 * S_in + 1);
+  hipLaunchKernelGGL(k_sample_pdf, dim3(n), dim3(64), shm, st, n, S_in, t_in, w, S_out, padding, randomized, seed,
+                     step, level, ray_base, t_out, idx_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_cast(int n, int S, const float* t, const float* o, const float* d, const float* radius,
+                       float* mean, float* cov, hipStream_t st) {
+  const int total = n * S;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_cast, dim3((total + 255) / 256), dim3(256), 0, st, n, S, t, o, d, radius, mean, cov);
+  return hipGetLastError();
+}
+
+hipError_t launch_encode(int n, int S, const float* mean, const float* cov, const float* d, float* enc_pos,
+                         float* enc_dir, hipStream_t st) {
+  const int total = n * S * kPosIn;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_encode, dim3((total + 255) / 256), dim3(256), 0, st, n, S, mean, cov, d, enc_pos, enc_dir);
+  return hipGetLastError();
+}
+
+}  // namespace nof

@@ -1,0 +1,304 @@
+"""Python mirror of the reference's host API (namespace AcceleratedNeRFUtils) over the C ABI.
+
+Same class and method names as the C++/CLI classes the C# driver binds
+(Program.cs:24-26,42,51-60): ``AcceleratedMipNeRF``, ``AcceleratedMLP``,
+``AcceleratedAdamOptimizer``, ``AcceleratedGradientCalculator``, ``OutputRetriever``.
+Device pointers cross this boundary as Python ints (the reference's uint64_t / float*),
+exactly as they cross it in the reference; ``device_tensor`` wraps one in a torch view
+(torch is used only for device memory and streams).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+from ._lib import call, lib
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _ptr(x) -> int:
+    """int device pointer from an int or a torch tensor."""
+    if x is None:
+        return 0
+    if isinstance(x, int):
+        return x
+    return int(x.data_ptr())
+
+
+def device_tensor(ptr: int, shape, dtype="float32", device=None):
+    """Zero-copy torch view of library-owned device memory (borrowed: do not keep past the owner)."""
+    import torch
+
+    typestr = {"float32": "<f4", "int32": "<i4"}[dtype]
+    n = int(np.prod(shape))
+
+    class _View:
+        __cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (int(ptr), False), "version": 3}
+
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    return torch.as_tensor(_View(), device=dev).view(*shape)
+
+
+def to_numpy(ptr: int, shape, dtype=np.float32) -> np.ndarray:
+    out = np.empty(shape, dtype)
+    call("nof_memcpy_d2h", out.ctypes.data, C.c_void_p(ptr), out.nbytes)
+    return out
+
+
+def _ptr_list(pp, count) -> list[int]:
+    return [C.cast(pp[i], C.c_void_p).value or 0 for i in range(count)]
+
+
+class AcceleratedMLP:
+    """Borrowed view of the MLP owned by an AcceleratedMipNeRF (AcceleratedMLP.h:7-45)."""
+
+    NUM_TENSORS = 22
+
+    def __init__(self, handle, owner):
+        self._h = handle
+        self._owner = owner  # keeps the owning AcceleratedMipNeRF alive
+
+    def get_layer_sizes(self) -> list[int]:
+        out = (C.c_int32 * 64)()
+        cnt = C.c_int32()
+        call("nof_mlp_layer_sizes", self._h, out, 64, C.byref(cnt))
+        return list(out[: cnt.value])
+
+    def get_output(self, enc_pos, enc_dir, level: int, n_rays: int, samples: int):
+        """MLPcpp:214-255 -> (density_ptr, rgb_ptr)."""
+        d, r = C.c_uint64(), C.c_uint64()
+        call("nof_mlp_get_output", self._h, _ptr(enc_pos), _ptr(enc_dir), level, n_rays, samples, C.byref(d),
+             C.byref(r))
+        return d.value, r.value
+
+    def get_gradient(self, color_gradient, density_gradient, level: int) -> list[int]:
+        """MLPcpp:256-321 -> 22 device gradient pointers."""
+        pp = L.PP()
+        call("nof_mlp_get_gradient", self._h, _ptr(color_gradient), _ptr(density_gradient), level, C.byref(pp))
+        return _ptr_list(pp, self.NUM_TENSORS)
+
+    @property
+    def allParams(self) -> list[int]:
+        pp = L.PP()
+        call("nof_mlp_params", self._h, C.byref(pp))
+        return _ptr_list(pp, self.NUM_TENSORS)
+
+    @property
+    def allGradients(self) -> list[int]:
+        pp = L.PP()
+        call("nof_mlp_grads", self._h, C.byref(pp))
+        return _ptr_list(pp, self.NUM_TENSORS)
+
+    def debug_view(self, level: int) -> dict:
+        d = L.nof_mlp_debug()
+        call("nof_mlp_debug_view", self._h, level, C.byref(d))
+        return {k: getattr(d, k) for k in ("M", "act_in", "act_h", "act_h9", "masks", "zhead", "delta", "delta9x")}
+
+    def relu_masks(self, level: int) -> np.ndarray:
+        """Decode the forward's packed ReLU bits -> uint8 [M, 8*256 + 128] (h0..h7, h9)."""
+        dv = self.debug_view(level)
+        M = dv["M"]
+        nb = M // 32
+        raw = to_numpy(dv["masks"], (nb, 9, 64, 4), np.uint32)
+        lane = np.arange(64)
+        j, h = lane & 31, lane >> 5
+        out = np.zeros((M, 8 * 256 + 128), np.uint8)
+        for slot in range(9):
+            ntile = 8 if slot < 8 else 4
+            base = slot * 256
+            for ot in range(ntile):
+                for r in range(16):
+                    f = ot * 32 + 8 * (r >> 2) + 4 * h + (r & 3)  # [64]
+                    bit = (raw[:, slot, :, ot >> 1] >> np.uint32(31 - ((ot & 1) * 16 + r))) & np.uint32(1)  # [nb, 64]
+                    rows = (np.arange(nb)[:, None] * 32 + j[None, :])
+                    out[rows, base + f[None, :]] = bit.astype(np.uint8)
+        return out
+
+    def flat_params(self):
+        p, n = C.c_void_p(), C.c_int64()
+        call("nof_mlp_flat_params", self._h, C.byref(p), C.byref(n))
+        return p.value, n.value
+
+    def flat_grads(self):
+        p, n = C.c_void_p(), C.c_int64()
+        call("nof_mlp_flat_grads", self._h, C.byref(p), C.byref(n))
+        return p.value, n.value
+
+
+class AcceleratedMipNeRF:
+    """AcceleratedMipNeRF.h:10-41 (ctor MNcpp:7-50, GetGradient MNcpp:52-144)."""
+
+    def __init__(self, config: L.nof_config | None = None, **overrides):
+        self.config = config if config is not None else L.default_config(**overrides)
+        h = C.c_void_p()
+        call("nof_mipnerf_create", C.byref(self.config), C.byref(h))
+        self._h = h
+        m = C.c_void_p()
+        call("nof_mipnerf_mlp", self._h, C.byref(m))
+        self.mlp = AcceleratedMLP(m, self)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().nof_mipnerf_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def GetGradient(self, origins, directions, radii, nears, fars, loss_multipliers, get_output_gradient):
+        """Host arrays + callback(dev_comp_rgb, level, loss_mult_sum, dev_loss_mults) -> dev dL/dC ptr."""
+        arrs = [_f32(a) for a in (origins, directions, radii, nears, fars, loss_multipliers)]
+        n = arrs[2].shape[0]
+        err = []
+
+        def tramp(user, comp, level, msum, lm):
+            try:
+                return int(get_output_gradient(comp, level, msum, lm))
+            except Exception as e:  # never unwind through C
+                err.append(e)
+                return 0
+
+        cb = L.OUTPUT_GRAD_FN(tramp)
+        pp = L.PP()
+        st = lib().nof_mipnerf_get_gradient(self._h, n, *[a.ctypes.data for a in arrs], cb, None, C.byref(pp))
+        if err:
+            raise err[0]
+        L.check(st, "nof_mipnerf_get_gradient")
+        return _ptr_list(pp, AcceleratedMLP.NUM_TENSORS)
+
+    def get_gradient_device(self, n, origins, directions, radii, nears, fars, loss_mults, pixels, loss_mult_sum):
+        """All inputs device-resident (ints or torch tensors); loss gradient fused into the integrator."""
+        pp = L.PP()
+        call("nof_mipnerf_get_gradient_device", self._h, n, _ptr(origins), _ptr(directions), _ptr(radii),
+             _ptr(nears), _ptr(fars), _ptr(loss_mults), _ptr(pixels), float(loss_mult_sum), C.byref(pp))
+        return _ptr_list(pp, AcceleratedMLP.NUM_TENSORS)
+
+    def GetLayerSizes(self) -> list[int]:
+        out = (C.c_int32 * 64)()
+        cnt = C.c_int32()
+        call("nof_mipnerf_layer_sizes", self._h, out, 64, C.byref(cnt))
+        return list(out[: cnt.value])
+
+    def set_rng(self, seed: int, step: int, ray_base: int = 0):
+        call("nof_mipnerf_set_rng", self._h, seed, step, ray_base)
+
+    def get_rng(self):
+        s, st, rb = C.c_uint64(), C.c_uint32(), C.c_uint32()
+        call("nof_mipnerf_get_rng", self._h, C.byref(s), C.byref(st), C.byref(rb))
+        return s.value, st.value, rb.value
+
+    def level_view(self, level: int) -> dict:
+        v = L.nof_level_view()
+        call("nof_mipnerf_level_view", self._h, level, C.byref(v))
+        n, S = v.n, v.samples
+        shapes = {"t": (n, S + 1), "weights": (n, S), "comp_rgb": (n, 3), "density": (n, S), "rgb": (n, S, 3),
+                  "density_grad": (n, S), "rgb_grad": (n, S, 3)}
+        return {k: (getattr(v, k), shp) for k, shp in shapes.items()}
+
+    def level_numpy(self, level: int) -> dict:
+        return {k: to_numpy(p, shp) for k, (p, shp) in self.level_view(level).items()}
+
+    def loss(self) -> float:
+        out = C.c_float()
+        call("nof_mipnerf_loss", self._h, C.byref(out))
+        return out.value
+
+    def enable_timing(self, on: bool = True):
+        call("nof_mipnerf_enable_timing", self._h, int(on))
+
+    def read_timing(self) -> dict:
+        ms = (C.c_float * L.NOF_NUM_TIMERS)()
+        cnt = (C.c_int32 * L.NOF_NUM_TIMERS)()
+        call("nof_mipnerf_read_timing", self._h, ms, cnt, L.NOF_NUM_TIMERS)
+        return {name: (ms[i], cnt[i]) for i, name in enumerate(L.TIMER_NAMES)}
+
+
+class AcceleratedAdamOptimizer:
+    """AcceleratedAdamOptimizer.h:5-20; step = one fused launch over flat arenas."""
+
+    def __init__(self, layer_sizes, config: L.nof_config | None = None):
+        self.config = config if config is not None else L.default_config()
+        arr = (C.c_int32 * len(layer_sizes))(*layer_sizes)
+        self.n = len(layer_sizes)
+        h = C.c_void_p()
+        call("nof_adam_create", arr, len(layer_sizes), C.byref(self.config), C.byref(h))
+        self._h = h
+
+    def step(self, params, grads, learning_rate: float):
+        pa = (C.POINTER(C.c_float) * self.n)(*[C.cast(C.c_void_p(p), C.POINTER(C.c_float)) for p in params])
+        ga = (C.POINTER(C.c_float) * self.n)(*[C.cast(C.c_void_p(g), C.POINTER(C.c_float)) for g in grads])
+        call("nof_adam_step", self._h, pa, ga, float(learning_rate))
+
+    @property
+    def iteration(self) -> int:
+        it = C.c_int32()
+        call("nof_adam_iteration", self._h, C.byref(it))
+        return it.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().nof_adam_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class AcceleratedGradientCalculator:
+    """AcceleratedGradientCalculator.h:8-17 (D15 fixed: pixels uploaded, one buffer per level)."""
+
+    def __init__(self, batch_size: int, config: L.nof_config | None = None):
+        self.config = config if config is not None else L.default_config()
+        h = C.c_void_p()
+        call("nof_gradcalc_create", batch_size, C.byref(self.config), C.byref(h))
+        self._h = h
+
+    def get_output_gradient(self, input_ptr, pixels, loss_mults, loss_mult_sum: float, level: int) -> int:
+        px = _f32(pixels)
+        out = C.c_uint64()
+        call("nof_gradcalc_output_gradient", self._h, _ptr(input_ptr), px.ctypes.data, px.shape[0], _ptr(loss_mults),
+             float(loss_mult_sum), level, C.byref(out))
+        return out.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().nof_gradcalc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class OutputRetriever:
+    @staticmethod
+    def RetrieveOutput(dev_output: int, size: int) -> np.ndarray:
+        """OutputRetriever.cpp:6-14 -> float32 [size, 3]."""
+        out = np.empty((size, 3), np.float32)
+        call("nof_retrieve_output", C.c_uint64(dev_output), size, out.ctypes.data)
+        return out
+
+
+def learning_rate_decay(step, lr_init=5e-4, lr_final=5e-6, max_steps=1000000, lr_delay_steps=2500,
+                        lr_delay_mult=0.01) -> float:
+    """MathHelpers.LearningRateDecay (MipHelpers.cs:758-773); defaults = TrainState.cs:54-58."""
+    return float(lib().nof_lr_decay(step, lr_init, lr_final, max_steps, lr_delay_steps, lr_delay_mult))
+
+
+def device_count() -> int:
+    c = C.c_int32()
+    call("nof_device_count", C.byref(c))
+    return c.value

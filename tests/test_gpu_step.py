@@ -1,0 +1,150 @@
+"""GPU parity of the whole training step (AcceleratedMipNeRF.GetGradient) vs the fp64 oracle.
+
+Level-1 t-values are resampled on the GPU from the GPU's level-0 weights; they are checked
+bit-exactly against the oracle's resampler fed those same weights, and then injected into the
+oracle step (t_override) so that every other tensor is compared on identical samples.
+"""
+import numpy as np
+import pytest
+
+from conftest import rel_l2
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+def _device_rays(r, dev):
+    import torch
+
+    return {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in r.items()}
+
+
+def _run_gpu(model, r, dev, msum=None):
+    d = _device_rays(r, dev)
+    n = r["o"].shape[0]
+    msum = float(np.sum(r["lossmult"], dtype=np.float32)) if msum is None else msum
+    return model.get_gradient_device(n, d["o"], d["d"], d["radius"], d["near"], d["far"], d["lossmult"], d["pix"], msum)
+
+
+@pytest.mark.parametrize("n,samples", [(16, (64, 64)), (8, (128, 128)), (6, (64, 128))])
+def test_step_parity(gpu, oracle, n, samples):
+    import torch
+    import nof
+    from nof import synth
+
+    seed, step, ray_base = 0x1234, 3, 500
+    model = nof.AcceleratedMipNeRF(seed=seed, max_rays=n, num_samples=samples)
+    model.set_rng(seed, step, ray_base)
+    r = synth.blender_rays(n, seed=11)
+    grads = _run_gpu(model, r, gpu)
+    torch.cuda.synchronize()
+    lv = [model.level_numpy(l) for l in range(len(samples))]
+    pptr, P = model.mlp.flat_params()
+    params = nof.to_numpy(pptr, (P,))
+    gptr, _ = model.mlp.flat_grads()
+    G = nof.to_numpy(gptr, (P,))
+    assert grads[0] == gptr
+
+    # level-0 samples: bit-exact; level-1 resampling: bit-exact given the GPU's level-0 weights
+    t0 = oracle.sample_stratified(r["near"], r["far"], samples[0], True, seed, step, 0, ray_base)
+    assert np.array_equal(lv[0]["t"], t0)
+    t1, _ = oracle.sample_pdf(lv[0]["t"], lv[0]["weights"], samples[1], 0.01, True, seed, step, 1, ray_base)
+    assert np.array_equal(lv[1]["t"], t1)
+
+    # The oracle adopts the GPU's ReLU decisions: a pre-activation at ~0 may round to opposite
+    # signs in fp32 and fp64, which would shift every gradient below that unit (measure-zero tie).
+    masks = {l: model.mlp.relu_masks(l).reshape(n, samples[l], -1) for l in range(len(samples))}
+    ref = oracle.step(oracle.Spec(), params, r, samples=samples, seed=seed, step_idx=step, ray_base=ray_base,
+                      t_override={1: lv[1]["t"]}, relu_mask=masks, nthreads=16)
+    ref_free = oracle.step(oracle.Spec(), params, r, samples=samples, seed=seed, step_idx=step, ray_base=ray_base,
+                           t_override={1: lv[1]["t"]}, nthreads=16, want=("sigma",))
+    for l in range(len(samples)):  # the masks only differ at ties: forward outputs agree either way
+        assert rel_l2(lv[l]["density"], ref_free["sigma"][l]) < TOL
+    for l in range(len(samples)):
+        assert rel_l2(lv[l]["density"], ref["sigma"][l]) < TOL, f"density level {l}"
+        assert rel_l2(lv[l]["rgb"], ref["rgb"][l]) < TOL, f"rgb level {l}"
+        assert rel_l2(lv[l]["weights"], ref["w"][l]) < TOL, f"weights level {l}"
+        assert rel_l2(lv[l]["comp_rgb"], ref["C"][l]) < TOL, f"comp_rgb level {l}"
+        assert rel_l2(lv[l]["density_grad"], ref["dsigma"][l]) < TOL, f"dsigma level {l}"
+        assert rel_l2(lv[l]["rgb_grad"], ref["drgb"][l]) < TOL, f"drgb level {l}"
+    sizes = oracle.layer_sizes(oracle.Spec())
+    off = 0
+    for i, s in enumerate(sizes):
+        e = rel_l2(G[off:off + s], ref["grads"][off:off + s])
+        assert e < TOL, f"gradient tensor {i}: rel L2 {e:.3g}"
+        off += s
+    assert abs(model.loss() - ref["loss"]) <= 1e-5 * abs(ref["loss"])
+    model.close()
+
+
+def test_callback_path_equals_fused(gpu):
+    """GetGradient(host arrays + AcceleratedGradientCalculator callback) == fused device path, bitwise."""
+    import torch
+    import nof
+    from nof import synth
+
+    n = 32
+    r = synth.blender_rays(n, seed=5)
+    a = nof.AcceleratedMipNeRF(seed=7, max_rays=n)
+    b = nof.AcceleratedMipNeRF(seed=7, max_rays=n)
+    gc = nof.AcceleratedGradientCalculator(n, b.config)
+    _run_gpu(a, r, gpu)
+    seen = []
+
+    def cb(comp, level, msum, lm):
+        seen.append(level)
+        return gc.get_output_gradient(comp, r["pix"], lm, msum, level)
+
+    b.GetGradient(r["o"], r["d"], r["radius"], r["near"], r["far"], r["lossmult"], cb)
+    torch.cuda.synchronize()
+    assert seen == [0, 1]
+    ga = nof.to_numpy(a.mlp.flat_grads()[0], (546948,))
+    gb = nof.to_numpy(b.mlp.flat_grads()[0], (546948,))
+    assert np.array_equal(ga, gb)
+    out = nof.OutputRetriever.RetrieveOutput(b.level_view(1)["comp_rgb"][0], n)
+    assert np.array_equal(out, a.level_numpy(1)["comp_rgb"])
+
+
+def test_encoded_get_output_equals_fused(gpu):
+    """AcceleratedMLP.get_output on cast+encode kernels == the fused frustum/IPE forward, bitwise."""
+    import torch
+    import nof
+    from nof import synth
+
+    n, S = 8, 128
+    r = synth.blender_rays(n, seed=9)
+    model = nof.AcceleratedMipNeRF(seed=3, max_rays=n)
+    _run_gpu(model, r, gpu)
+    torch.cuda.synchronize()
+    v0 = model.level_numpy(0)
+    dev = _device_rays(r, gpu)
+    t = torch.from_numpy(v0["t"]).to(gpu)
+    mean = torch.zeros((n, S, 3), device=gpu)
+    cov = torch.zeros((n, S, 3), device=gpu)
+    nof._lib.call("nof_kernel_cast", n, S, t.data_ptr(), dev["o"].data_ptr(), dev["d"].data_ptr(),
+                  dev["radius"].data_ptr(), mean.data_ptr(), cov.data_ptr(), None)
+    ep = torch.zeros((n * S, 96), device=gpu)
+    ed = torch.zeros((n, 27), device=gpu)
+    nof._lib.call("nof_kernel_encode", n, S, mean.data_ptr(), cov.data_ptr(), dev["d"].data_ptr(), ep.data_ptr(),
+                  ed.data_ptr(), None)
+    dptr, rptr = model.mlp.get_output(ep, ed, 0, n, S)
+    torch.cuda.synchronize()
+    assert np.array_equal(nof.to_numpy(dptr, (n, S)), v0["density"])
+    assert np.array_equal(nof.to_numpy(rptr, (n, S, 3)), v0["rgb"])
+
+
+def test_gradients_deterministic(gpu):
+    import torch
+    import nof
+    from nof import synth
+
+    n = 64
+    r = synth.blender_rays(n, seed=2)
+    outs = []
+    for _ in range(2):
+        m = nof.AcceleratedMipNeRF(seed=5, max_rays=n)
+        _run_gpu(m, r, gpu)
+        torch.cuda.synchronize()
+        outs.append(nof.to_numpy(m.mlp.flat_grads()[0], (546948,)))
+        m.close()
+    assert np.array_equal(outs[0], outs[1])

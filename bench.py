@@ -1,0 +1,254 @@
+"""Benchmark: train rays/s of the ScratchNerf mip-NeRF step on MI355X (BASELINE.json `metric`).
+
+One step = both levels forward (stratified + hierarchical sampling, fused frustum/IPE/8x256 MLP,
+integrator) + fused loss gradient + both levels backward (integrator adjoint, MLP dX chain,
+weight-gradient GEMMs) + (N>1) RCCL all-reduce of the flat gradient arena + fused Adam.
+Workload = BASELINE.json configs[1]: Lego-shaped synthetic 800x800 batches, 1024 rays per GPU,
+128 + 128 samples, 8x256 MLP, fp32.  Inputs are pre-staged in HBM before the timed region.
+
+    python bench.py [--gpus N --steps K --warmup W]                      (N = 1)
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  `roofline` covers the dominant kernel, timed live with hipEvents
+on the library's stream inside the timed region; `cpu_baseline` times the oracle's faithful
+C++ restatement of MipNerfModel.GetGradient on the host (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "nerf-or-nothing_amd"))
+
+METRIC = "train rays/sec (128 samples/ray, 8×256 MLP) at 1/2/4/8 MI355X; PSNR vs ref"
+# algorithmic work per sample per level (SURVEY.md §8d / BASELINE.md §3)
+MACS_FWD = 544768
+MACS_DX = 492160
+MACS_DW = 544768
+PEAK_F32_TFLOPS = 157.3   # MI355X fp32 MFMA dense (= packed-fp32 VALU), MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+INTEGRATOR_FWD_B = lambda S: S * (12 + 4 + 4) + (S + 1) * 4 + 12 + 12  # rgb, sigma, w | t | d | C  (3100 @128)
+INTEGRATOR_BWD_B = lambda S: 12 + S * (12 + 4) + (S + 1) * 4 + 12 + S * (12 + 4)  # 4636 @128
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--rays", type=int, default=1024, help="rays per GPU per step")
+    p.add_argument("--samples", type=int, nargs="+", default=[128, 128])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-integrator", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work")
+    return p.parse_args()
+
+
+def cpu_baseline(samples, target_s):
+    """Oracle = faithful scalar C++ restatement of MipNerfModel.GetGradient (MNcs:99-200), float,
+    OpenMP over rays on this host; bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from nof import synth
+
+    cores = min(16, os.cpu_count() or 1)
+    spec = O.Spec()
+    P = O.glorot_init(spec, 0x5EED0002)
+    probe_n = cores
+    r = synth.blender_rays(probe_n, seed=99)
+    t0 = time.perf_counter()
+    O.step(spec, P, r, samples=tuple(samples), seed=1, nthreads=cores, dtype=np.float32, want=("grads",))
+    dt = time.perf_counter() - t0
+    n = max(cores, int(probe_n * max(1.0, (target_s - dt) / max(dt, 1e-3))) // cores * cores)
+    r = synth.blender_rays(n, seed=100)
+    t0 = time.perf_counter()
+    O.step(spec, P, r, samples=tuple(samples), seed=2, nthreads=cores, dtype=np.float32, want=("grads",))
+    dt = time.perf_counter() - t0
+    import platform
+    model = platform.processor()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": n / dt, "unit": "rays/s", "cores": cores, "kind": "port",
+            "sample": f"{n} rays x ({samples[0]}+{samples[1]}) samples, one full step (fwd+loss+bwd), float, "
+                      f"OpenMP over rays, {dt:.1f} s on {model}"}
+
+
+def integrator_roofline(torch, nof, dev, n=1 << 20, S=128, reps=5):
+    """HBM roofline of the integrator fwd/bwd on an integrator-only 2^20 x 128 batch."""
+    g = torch.Generator(device=dev).manual_seed(3)
+    sigma = torch.rand((n, S), device=dev, generator=g) * 5
+    rgb = torch.rand((n, S, 3), device=dev, generator=g)
+    t = torch.sort(torch.rand((n, S + 1), device=dev, generator=g) * 4 + 2, dim=1).values
+    d = torch.randn((n, 3), device=dev, generator=g)
+    C = torch.empty((n, 3), device=dev)
+    w = torch.empty((n, S), device=dev)
+    gr = torch.randn((n, 3), device=dev, generator=g)
+    ds = torch.empty((n, S), device=dev)
+    dc = torch.empty((n, S, 3), device=dev)
+    call = nof._lib.call
+    fwd = lambda: call("nof_kernel_render", n, S, sigma.data_ptr(), rgb.data_ptr(), t.data_ptr(), d.data_ptr(), 1,
+                       C.data_ptr(), w.data_ptr(), None)
+    bwd = lambda: call("nof_kernel_render_grad", n, S, sigma.data_ptr(), rgb.data_ptr(), t.data_ptr(), d.data_ptr(),
+                       1, C.data_ptr(), gr.data_ptr(), None, None, 0.0, 1.0, ds.data_ptr(), dc.data_ptr(), None)
+    out = {}
+    for name, fn, b in (("render_fwd", fwd, INTEGRATOR_FWD_B(S)), ("render_bwd", bwd, INTEGRATOR_BWD_B(S))):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        gbs = b * n / (ms * 1e-3) / 1e9
+        out[name] = {"ms": ms, "bytes_per_ray": b, "achieved": gbs, "frac": gbs / PEAK_HBM_GBS}
+    tot_b = (INTEGRATOR_FWD_B(S) + INTEGRATOR_BWD_B(S)) * n
+    tot_ms = out["render_fwd"]["ms"] + out["render_bwd"]["ms"]
+    ach = tot_b / (tot_ms * 1e-3) / 1e9
+    del sigma, rgb, t, d, C, w, gr, ds, dc
+    torch.cuda.empty_cache()
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
+            "workload": f"{n} rays x {S} samples, render fwd+bwd", "kernels": out}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    import nof
+    from nof import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 via torch.distributed.run")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    n = a.rays
+    samples = a.samples
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    seed = 0x5EED0002
+    model = nof.AcceleratedMipNeRF(device=local, max_rays=n, num_samples=samples, seed=seed,
+                                   stream=stream)
+    model.set_rng(seed, 0, rank * n)  # global ray ids: sharding never changes a sample
+    opt = nof.AcceleratedAdamOptimizer(model.GetLayerSizes(), model.config)
+    params = model.mlp.allParams
+    gptr, P = model.mlp.flat_grads()
+    grad_view = nof.device_tensor(gptr, (P,), device=dev)
+
+    # pre-staged synthetic batches (views of a 100-pose Lego-shaped scene; shard = disjoint views)
+    pool = []
+    for i in range(4):
+        r = synth.blender_rays(n, seed=1000 * rank + i)
+        pool.append({k: torch.from_numpy(v).to(dev) for k, v in r.items()})
+    msum_global = float(n * world)  # lossmult = 1 everywhere: sum over all shards (D14, DP-global)
+
+    def step(k):
+        b = pool[k % len(pool)]
+        grads = model.get_gradient_device(n, b["o"], b["d"], b["radius"], b["near"], b["far"], b["lossmult"],
+                                          b["pix"], msum_global)
+        if world > 1:
+            dist.all_reduce(grad_view)  # sum of per-shard gradient sums (no averaging: L is a sum)
+        opt.step(params, grads, nof.learning_rate_decay(k + 1))
+
+    for k in range(a.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    model.enable_timing(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(a.warmup, a.warmup + a.steps):
+        step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    timing = model.read_timing()
+    model.enable_timing(False)
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_step = dt * 1e3 / a.steps
+    rays_per_s = n * world * a.steps / dt
+
+    # fine-level PSNR of the last step's batch (MseToPsnr, MipHelpers.cs:672)
+    last = pool[(a.warmup + a.steps - 1) % len(pool)]
+    comp = model.level_numpy(len(samples) - 1)["comp_rgb"]
+    mse = float(np.mean((comp - last["pix"].cpu().numpy()) ** 2))
+    psnr = -10.0 * math.log10(max(mse, 1e-12))
+
+    result = None
+    if rank == 0:
+        M = [n * s for s in samples]
+        flop = {"mlp_fwd": 2 * MACS_FWD * sum(M), "mlp_bwd": 2 * MACS_DX * sum(M), "wgrad": 2 * MACS_DW * sum(M)}
+        kernels = {}
+        for name, (ms, cnt) in timing.items():
+            if cnt:
+                kernels[name] = {"ms_per_step": round(ms / a.steps, 4), "launches_per_step": cnt // a.steps,
+                                 "avg_launch_ms": round(ms / cnt, 4)}
+        dom = max((k for k in flop if k in kernels), key=lambda k: kernels[k]["ms_per_step"])
+        fl_launch = flop[dom] / kernels[dom]["launches_per_step"]
+        achieved = fl_launch / (kernels[dom]["avg_launch_ms"] * 1e-3) / 1e12
+        mlp_ms = sum(kernels[k]["ms_per_step"] for k in flop if k in kernels)
+        mlp_tf = sum(flop.values()) / (mlp_ms * 1e-3) / 1e12
+        traffic = None
+        tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(tfile):
+            try:
+                traffic = json.load(open(tfile)).get(dom)
+            except (OSError, ValueError):
+                traffic = None
+        result = {
+            "metric": METRIC, "value": round(rays_per_s, 1), "unit": "rays/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic (Lego-shaped 800x800, 100 poses)",
+            "config": {"workload": "BASELINE configs[1]: 1024-ray batches x 128+128 samples, 8x256 MLP fwd/bwd + Adam",
+                       "rays_per_gpu": n, "global_batch": n * world, "samples": samples,
+                       "parallelism": f"dp{world}"},
+            "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_F32_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_TFLOPS, 4), "traffic": traffic,
+                         "flop_per_launch": fl_launch},
+            "mlp_all_kernels": {"achieved": round(mlp_tf, 2), "unit": "TFLOP/s",
+                                "frac": round(mlp_tf / PEAK_F32_TFLOPS, 4)},
+            "kernels": kernels,
+            "psnr_fine": round(psnr, 3),
+        }
+        if not a.no_integrator and world == 1:
+            result["roofline_integrator"] = integrator_roofline(torch, nof, dev)
+        if not a.no_cpu_baseline and world == 1:
+            result["cpu_baseline"] = cpu_baseline(samples, a.cpu_seconds)
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

@@ -30,88 +30,135 @@ __device__ __forceinline__ void blk_dma(const float* __restrict__ src, float* ds
   }
 }
 
+// One work item (problem P, k-blocks [kb0, kb1)) for a wave grid of 2 (rows) x 4 (cols): wave
+// (wr, wc) owns row tiles [wr*RB, wr*RB+RB) x col tiles [wc*CB, wc*CB+CB) of the problem's tile
+// grid, so a k-step costs RB + CB conflict-free ds_read_b32 for RB*CB MFMAs.  Operand reads are
+// unconditional (rows/cols clamped into range) and issued one k-step ahead; the MFMAs carry no
+// branches.  Tiles outside the problem are computed on clamped duplicates and never stored.
+template <int RB, int CB>
+__device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, float* lds, int tid, int lane,
+                                        int wave, float* slabs, float* bias_slabs, const int64_t* slab_off) {
+  const int h = lane >> 5, x = lane & 31;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int r0 = wr * RB, c0 = wc * CB;
+  const bool active = r0 < P.ntr && c0 < P.ntc;  // wave-uniform
+  int rowt[RB], colt[CB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) rowt[r] = min(r0 + r, P.ntr - 1);
+#pragma unroll
+  for (int c = 0; c < CB; ++c) colt[c] = min(c0 + c, P.ntc - 1);
+  const int nA4 = P.ntr * 32 * kBlk / 4, nB4 = P.ntc * 32 * kBlk / 4;
+  const float* Ab = P.A + (size_t)P.a_row0 * kBlk;
+  const float* Bb = P.B + (size_t)P.b_col0 * kBlk;
+  const size_t strideA = (size_t)P.FA * kBlk, strideB = (size_t)P.FB * kBlk;
+
+  f32x16 acc[RB][CB];
+  float bs[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    bs[r] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < CB; ++c)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[r][c][e] = 0.0f;
+  }
+  // per-lane LDS row offsets: element (32*t + x, s) of a block image sits at (32*t + x)*32 + (s ^ x)
+  int aoff[RB], boff[CB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) aoff[r] = (rowt[r] * 32 + x) * kBlk;
+#pragma unroll
+  for (int c = 0; c < CB; ++c) boff[c] = (colt[c] * 32 + x) * kBlk;
+
+  blk_dma(Ab + item.kb0 * strideA, lds, nA4, tid);
+  blk_dma(Bb + item.kb0 * strideB, lds + kWgHalf, nB4, tid);
+  __syncthreads();
+  int cur = 0;
+  for (int kb = item.kb0; kb < item.kb1; ++kb) {
+    float* nxt = lds + (cur ^ 1) * 2 * kWgHalf;
+    if (kb + 1 < item.kb1) {
+      blk_dma(Ab + (kb + 1) * strideA, nxt, nA4, tid);
+      blk_dma(Bb + (kb + 1) * strideB, nxt + kWgHalf, nB4, tid);
+    }
+    if (active) {
+      const float* LA = lds + cur * 2 * kWgHalf;
+      const float* LB = LA + kWgHalf;
+      float a[RB], b[CB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) a[r] = LA[aoff[r] + (h ^ x)];
+#pragma unroll
+      for (int c = 0; c < CB; ++c) b[c] = LB[boff[c] + (h ^ x)];
+#pragma unroll
+      for (int c16 = 0; c16 < 16; ++c16) {
+        float an[RB], bn[CB];
+        if (c16 < 15) {
+          const int col = (2 * (c16 + 1) + h) ^ x;  // sample 2k + h of the next k-step
+#pragma unroll
+          for (int r = 0; r < RB; ++r) an[r] = LA[aoff[r] + col];
+#pragma unroll
+          for (int c = 0; c < CB; ++c) bn[c] = LB[boff[c] + col];
+        }
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+#pragma unroll
+          for (int c = 0; c < CB; ++c) acc[r][c] = mfma32(a[r], b[c], acc[r][c]);
+          bs[r] += a[r];
+        }
+        if (c16 < 15) {
+#pragma unroll
+          for (int r = 0; r < RB; ++r) a[r] = an[r];
+#pragma unroll
+          for (int c = 0; c < CB; ++c) b[c] = bn[c];
+        }
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  if (active) {
+    float* slab = slabs + slab_off[item.slab];
+    const int ld = P.ntc * 32;
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int c = 0; c < CB; ++c) {
+        if (r0 + r < P.ntr && c0 + c < P.ntc) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int row = rowt[r] * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            slab[(size_t)row * ld + colt[c] * 32 + x] = acc[r][c][e];
+          }
+        }
+      }
+    if (wc == 0) {  // column tile 0 owner: bias partial = row sums of delta over the item's samples
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        const float v = bs[r] + __shfl_xor(bs[r], 32, 64);
+        if (r0 + r < P.ntr && h == 0) bias_slabs[(size_t)item.slab * 256 + rowt[r] * 32 + x] = v;
+      }
+    }
+  }
+  __syncthreads();  // LDS ring reused by the next item
+}
+
 __global__ __launch_bounds__(kWgThreads, 1) void k_wgrad(const WgProblem* __restrict__ probs,
                                                          const WgItem* __restrict__ items,
                                                          const int* __restrict__ item_ptr,
                                                          const int64_t* __restrict__ slab_off, float* slabs,
                                                          float* bias_slabs) {
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [2 buffers][A | B] x kWgHalf
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, x = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int it0 = item_ptr[blockIdx.x], it1 = item_ptr[blockIdx.x + 1];
   for (int it = it0; it < it1; ++it) {
     const WgItem item = items[it];
     const WgProblem P = probs[item.prob];
-    const int ntiles = P.ntr * P.ntc;
-    const int nA4 = P.ntr * 32 * kBlk / 4, nB4 = P.ntc * 32 * kBlk / 4;
-    const float* Ab = P.A + (size_t)P.a_row0 * kBlk;
-    const float* Bb = P.B + (size_t)P.b_col0 * kBlk;
-    const size_t strideA = (size_t)P.FA * kBlk, strideB = (size_t)P.FB * kBlk;
-
-    int tr[8], tc[8];
-    bool tv[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int id = wave + 8 * i;
-      tv[i] = id < ntiles;
-      tr[i] = tv[i] ? id / P.ntc : 0;
-      tc[i] = tv[i] ? id - tr[i] * P.ntc : 0;
+    const int RB = (P.ntr + 1) >> 1, CB = (P.ntc + 3) >> 2;  // block per wave of the 2 x 4 wave grid
+    switch (RB * 10 + CB) {
+      case 11: wg_item<1, 1>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
+      case 21: wg_item<2, 1>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
+      case 32: wg_item<3, 2>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
+      case 41: wg_item<4, 1>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
+      default: wg_item<4, 2>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
     }
-    f32x16 acc[8];
-    float bs[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][r] = 0.0f;
-      bs[i] = 0.0f;
-    }
-
-    blk_dma(Ab + item.kb0 * strideA, lds, nA4, tid);
-    blk_dma(Bb + item.kb0 * strideB, lds + kWgHalf, nB4, tid);
-    __syncthreads();
-    int cur = 0;
-    for (int kb = item.kb0; kb < item.kb1; ++kb) {
-      float* nxt = lds + (cur ^ 1) * 2 * kWgHalf;
-      if (kb + 1 < item.kb1) {
-        blk_dma(Ab + (kb + 1) * strideA, nxt, nA4, tid);
-        blk_dma(Bb + (kb + 1) * strideB, nxt + kWgHalf, nB4, tid);
-      }
-      const float* LA = lds + cur * 2 * kWgHalf;
-      const float* LB = LA + kWgHalf;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const int s = 2 * c + h;           // sample of this k-step for lane half h
-        const int col = s ^ x;             // swizzled position: blk_off(32*t + x, s)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          if (tv[i]) {
-            const float av = LA[(tr[i] * 32 + x) * kBlk + col];
-            const float bv = LB[(tc[i] * 32 + x) * kBlk + col];
-            acc[i] = mfma32(av, bv, acc[i]);
-            if (tc[i] == 0) bs[i] += av;
-          }
-        }
-      }
-      __syncthreads();
-      cur ^= 1;
-    }
-    // partial slab [ntr*32][ntc*32], row-major; bias partial [ntr*32]
-    float* slab = slabs + slab_off[item.slab];
-    const int ld = P.ntc * 32;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      if (tv[i]) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = tr[i] * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          slab[(size_t)row * ld + tc[i] * 32 + x] = acc[i][r];
-        }
-        if (tc[i] == 0) {
-          const float v = bs[i] + __shfl_xor(bs[i], 32, 64);
-          if (h == 0) bias_slabs[(size_t)item.slab * 256 + tr[i] * 32 + x] = v;
-        }
-      }
-    }
-    __syncthreads();  // LDS ring reused by the next item
   }
 }
 

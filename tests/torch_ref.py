@@ -211,3 +211,22 @@ def step(P_np, rays, samples=(128, 128), seed=0, step_idx=0, ray_base=0, padding
     res["w"] = [w.detach().numpy() for w in res["w"]]
     res["C"] = [C.detach().numpy() for C in res["C"]]
     return res
+
+
+def glorot(net: Net, seed: int) -> np.ndarray:
+    """C#-semantics Glorot init (MLPcs:78-85): W = sqrt(6/(in+out)) (2u - 1), b = 0; u from Philox
+    (seed, step 0, level = layer, stream 3, ray = e >> 32, k = e)."""
+    P = []
+    for l in range(net.L):
+        cnt = net.outs[l] * net.ins[l]
+        e = np.arange(cnt, dtype=np.uint64)
+        k = (e & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+        c2 = np.uint32((l & 0xFFFF) | (3 << 16))
+        outs = philox(k >> np.uint32(2), (e >> np.uint64(32)).astype(np.uint32), np.full(cnt, c2, np.uint32),
+                      np.zeros(cnt, np.uint32), seed & 0xFFFFFFFF, seed >> 32)
+        sel = np.stack(outs, 0)[(k & np.uint32(3)).astype(np.int64), np.arange(cnt)]
+        u = (sel >> np.uint32(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+        g = np.sqrt(np.float32(6.0) / np.float32(net.ins[l] + net.outs[l])).astype(np.float32)
+        P.append((g * (u * np.float32(2) - np.float32(1))).astype(np.float32))
+    P += [np.zeros(o, np.float32) for o in net.outs]
+    return np.concatenate(P)

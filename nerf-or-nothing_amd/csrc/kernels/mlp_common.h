@@ -59,10 +59,12 @@ __device__ __forceinline__ void mlp_layer(const float (&bin)[8][16], const float
   for (int t = 0; t < NT_B + NT_I; ++t) {
     const bool has_next = !(last_in_schedule && t == NT_B + NT_I - 1);
     if (has_next) slice_dma(wsrc + kSliceFloats, lds + (cur ^ 1) * kSliceFloats, tid);
-    const float* W = lds + cur * kSliceFloats;
+    const float* W = lds + cur * kSliceFloats + row * 32;
+    // A operands of (q, ot) are read one group ahead so the ds_read latency hides under the
+    // previous group's 4 MFMAs (left alone, hipcc serialises read -> lgkmcnt(0) -> MFMA).
+    f32x4 a_cur = *reinterpret_cast<const f32x4*>(W + ((h ^ swz) << 2));
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int chunk = ((2 * q + h) ^ swz) << 2;
       f32x4 b4;
       if (t < NT_B) {
         const int tb = (t < NT_B) ? t : 0;
@@ -73,9 +75,22 @@ __device__ __forceinline__ void mlp_layer(const float (&bin)[8][16], const float
       }
 #pragma unroll
       for (int ot = 0; ot < OT; ++ot) {
-        const f32x4 a4 = *reinterpret_cast<const f32x4*>(W + (ot * 32 + row) * 32 + chunk);
+        // Touch a_cur first: the waitcnt for its read (issued one group earlier) lands here, before
+        // the next read is issued. hipcc models LDS-DMA as an lgkm event too, so it only ever emits
+        // lgkmcnt(0); waiting after issuing the next read would expose that read's full latency.
+        asm volatile("" ::"v"(a_cur));
+        f32x4 a_nxt = a_cur;
+        const bool more = !(q == 3 && ot == OT - 1);
+        if (more) {
+          const int q2 = ot == OT - 1 ? q + 1 : q;
+          const int ot2 = ot == OT - 1 ? 0 : ot + 1;
+          a_nxt = *reinterpret_cast<const f32x4*>(W + ot2 * 32 * 32 + (((2 * q2 + h) ^ swz) << 2));
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the next group's read above this group's MFMAs
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) acc[ot] = mfma32(a4[jj], b4[jj], acc[ot]);
+        for (int jj = 0; jj < 4; ++jj) acc[ot] = mfma32(a_cur[jj], b4[jj], acc[ot]);
+        __builtin_amdgcn_sched_barrier(0);
+        a_cur = a_nxt;
       }
     }
     __syncthreads();

@@ -27,11 +27,11 @@ constexpr int kSliceFloats = 8192;  // one packed weight slice: 256 rows x 32 co
 constexpr int kFwdSlices = 3 + 8 * 3 + 11 + 8 * 3 + 8;   // 70: L0 | L1-3 | L4 | L5-7 | L9
 constexpr int kBwdSlices = 4 + 8 * 7;                      // 60: L9 | L7..L1
 
-// Element (f, s) of a [F][32] activation block: sample index XOR-swizzled by the
-// feature row so that 32 lanes reading one sample of 32 consecutive features hit
-// 32 distinct LDS banks (ds_read_b32 bank = dword % 32), while 32 lanes writing one
-// feature for 32 consecutive samples still fill one whole 128-B line.
-__host__ __device__ inline int blk_off(int f, int s) { return f * kBlk + (s ^ (f & 31)); }
+// Element (f, s) of a [F][32] activation block: the 16-B chunk s >> 2 of row f is stored at
+// chunk (s >> 2) ^ (f & 7).  32 lanes writing one feature for 32 consecutive samples still fill
+// one whole 128-B line, and the weight-gradient GEMMs read 4 consecutive samples of a row per
+// lane (ds_read_b128) with the 8 lanes of each LDS phase on 8 distinct 16-B bank groups.
+__host__ __device__ inline int blk_off(int f, int s) { return f * kBlk + ((((s >> 2) ^ (f & 7)) << 2) | (s & 3)); }
 
 // Packed weight slice [rows][32]: logical 16-B chunk c of row r stored at c ^ ((r >> 1) & 7),
 // making the ds_read_b128 operand fetches of the MFMA A operand bank-conflict-free.

@@ -43,7 +43,9 @@ __device__ __forceinline__ void fwd_epilogue(const f32x16 (&acc)[8], float (&bin
         bin[ot][r] = hv;
         // shift-accumulate: bit of (ot, r) ends at position 31 - ((ot & 1) * 16 + r) of word ot >> 1
         mw[ot >> 1] = (mw[ot >> 1] << 1) | (hv > 0.0f ? 1u : 0u);
+#ifndef NOF_DIAG_NO_ACT_STORE
         act_blk[blk_off(fb + jj, j)] = hv;
+#endif
       }
     }
   }
@@ -78,7 +80,12 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
 #pragma unroll
     for (int tp = 0; tp < 3; ++tp)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) ipe[tp][r] = ipe_feature(tile_feature(tp, r, h), mean, cov);
+      for (int r = 0; r < 16; ++r)
+#ifndef NOF_DIAG_NO_IPE
+        ipe[tp][r] = ipe_feature(tile_feature(tp, r, h), mean, cov);
+#else
+        ipe[tp][r] = mean[r % 3] * (float)tile_feature(tp, r, h) + cov[r % 3];
+#endif
   } else {
 #pragma unroll
     for (int tp = 0; tp < 3; ++tp)

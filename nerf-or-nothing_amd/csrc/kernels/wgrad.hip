@@ -32,7 +32,7 @@ __device__ __forceinline__ void blk_dma(const float* __restrict__ src, float* ds
 
 // One work item (problem P, k-blocks [kb0, kb1)) for a wave grid of 2 (rows) x 4 (cols): wave
 // (wr, wc) owns row tiles [wr*RB, wr*RB+RB) x col tiles [wc*CB, wc*CB+CB) of the problem's tile
-// grid, so a k-step costs RB + CB conflict-free ds_read_b32 for RB*CB MFMAs.  Operand reads are
+// grid, so 4 k-steps cost RB + CB conflict-free ds_read_b128 for 4*RB*CB MFMAs.  Operand reads are
 // unconditional (rows/cols clamped into range) and issued one k-step ahead; the MFMAs carry no
 // branches.  Tiles outside the problem are computed on clamped duplicates and never stored.
 template <int RB, int CB>
@@ -62,12 +62,13 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[r][c][e] = 0.0f;
   }
-  // per-lane LDS row offsets: element (32*t + x, s) of a block image sits at (32*t + x)*32 + (s ^ x)
+  // per-lane LDS row offsets (row 32*t + x of a block image; chunk c of that row at c ^ (x & 7))
   int aoff[RB], boff[CB];
 #pragma unroll
   for (int r = 0; r < RB; ++r) aoff[r] = (rowt[r] * 32 + x) * kBlk;
 #pragma unroll
   for (int c = 0; c < CB; ++c) boff[c] = (colt[c] * 32 + x) * kBlk;
+  const int xs = x & 7;
 
   blk_dma(Ab + item.kb0 * strideA, lds, nA4, tid);
   blk_dma(Bb + item.kb0 * strideB, lds + kWgHalf, nB4, tid);
@@ -82,28 +83,32 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
     if (active) {
       const float* LA = lds + cur * 2 * kWgHalf;
       const float* LB = LA + kWgHalf;
-      float a[RB], b[CB];
+      // lane half h reads chunk 2cc + h (samples 8cc + 4h .. +3); MFMA i of the group then sums
+      // k = {8cc + i, 8cc + 4 + i}, the same pairing for A and B
+      f32x4 a[RB], b[CB];
 #pragma unroll
-      for (int r = 0; r < RB; ++r) a[r] = LA[aoff[r] + (h ^ x)];
+      for (int r = 0; r < RB; ++r) a[r] = *reinterpret_cast<const f32x4*>(LA + aoff[r] + ((h ^ xs) << 2));
 #pragma unroll
-      for (int c = 0; c < CB; ++c) b[c] = LB[boff[c] + (h ^ x)];
+      for (int c = 0; c < CB; ++c) b[c] = *reinterpret_cast<const f32x4*>(LB + boff[c] + ((h ^ xs) << 2));
 #pragma unroll
-      for (int c16 = 0; c16 < 16; ++c16) {
-        float an[RB], bn[CB];
-        if (c16 < 15) {
-          const int col = (2 * (c16 + 1) + h) ^ x;  // sample 2k + h of the next k-step
+      for (int cc = 0; cc < 4; ++cc) {
+        f32x4 an[RB], bn[CB];
+        if (cc < 3) {
+          const int ch = ((2 * (cc + 1) + h) ^ xs) << 2;
 #pragma unroll
-          for (int r = 0; r < RB; ++r) an[r] = LA[aoff[r] + col];
+          for (int r = 0; r < RB; ++r) an[r] = *reinterpret_cast<const f32x4*>(LA + aoff[r] + ch);
 #pragma unroll
-          for (int c = 0; c < CB; ++c) bn[c] = LB[boff[c] + col];
+          for (int c = 0; c < CB; ++c) bn[c] = *reinterpret_cast<const f32x4*>(LB + boff[c] + ch);
         }
 #pragma unroll
-        for (int r = 0; r < RB; ++r) {
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int c = 0; c < CB; ++c) acc[r][c] = mfma32(a[r], b[c], acc[r][c]);
-          bs[r] += a[r];
-        }
-        if (c16 < 15) {
+          for (int r = 0; r < RB; ++r) {
+#pragma unroll
+            for (int c = 0; c < CB; ++c) acc[r][c] = mfma32(a[r][i], b[c][i], acc[r][c]);
+            bs[r] += a[r][i];
+          }
+        if (cc < 3) {
 #pragma unroll
           for (int r = 0; r < RB; ++r) a[r] = an[r];
 #pragma unroll

@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG, "lib", "libnof.so")
+LIB_PATH = os.environ.get("NOF_LIB") or os.path.join(_PKG, "lib", "libnof.so")  # NOF_LIB: diagnostic builds
 
 NOF_MAX_LEVELS = 4
 NOF_NUM_TIMERS = 8

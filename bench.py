@@ -33,6 +33,9 @@ MACS_FWD = 544768
 MACS_DX = 492160
 MACS_DW = 544768
 PEAK_F32_TFLOPS = 157.3   # MI355X fp32 MFMA dense (= packed-fp32 VALU), MI355X_MICROARCH.md
+PEAK_BF16_TFLOPS = 2516.6  # MI355X bf16 dense MFMA (no sparsity)
+# split mode issues 6 bf16 MFMAs per fp32 product (mlp_common.h), so its fp32-equivalent ceiling is 1/6
+PEAK_SPLIT_TFLOPS = round(PEAK_BF16_TFLOPS / 6, 1)
 PEAK_HBM_GBS = 8000.0
 INTEGRATOR_FWD_B = lambda S: S * (12 + 4 + 4) + (S + 1) * 4 + 12 + 12  # rgb, sigma, w | t | d | C  (3100 @128)
 INTEGRATOR_BWD_B = lambda S: 12 + S * (12 + 4) + (S + 1) * 4 + 12 + S * (12 + 4)  # 4636 @128
@@ -45,6 +48,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--rays", type=int, default=1024, help="rays per GPU per step")
     p.add_argument("--samples", type=int, nargs="+", default=[128, 128])
+    p.add_argument("--precision", choices=["f32", "split"], default="f32",
+                   help="MLP contraction arithmetic: fp32 MFMA, or fp32 operands as bf16x3 split MFMAs")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-integrator", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work")
@@ -149,8 +154,9 @@ def main():
     samples = a.samples
     stream = torch.cuda.current_stream(dev).cuda_stream
     seed = 0x5EED0002
+    split = a.precision == "split"
     model = nof.AcceleratedMipNeRF(device=local, max_rays=n, num_samples=samples, seed=seed,
-                                   stream=stream)
+                                   stream=stream, precision=1 if split else 0)
     model.set_rng(seed, 0, rank * n)  # global ray ids: sharding never changes a sample
     opt = nof.AcceleratedAdamOptimizer(model.GetLayerSizes(), model.config)
     params = model.mlp.allParams
@@ -217,25 +223,27 @@ def main():
         achieved = fl_launch / (kernels[dom]["avg_launch_ms"] * 1e-3) / 1e12
         mlp_ms = sum(kernels[k]["ms_per_step"] for k in flop if k in kernels)
         mlp_tf = sum(flop.values()) / (mlp_ms * 1e-3) / 1e12
+        peak = PEAK_SPLIT_TFLOPS if split else PEAK_F32_TFLOPS
         traffic = None
         tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tfile):
             try:
-                traffic = json.load(open(tfile)).get(dom)
+                traffic = json.load(open(tfile)).get(dom + ("_split" if split else ""))
             except (OSError, ValueError):
                 traffic = None
         result = {
             "metric": METRIC, "value": round(rays_per_s, 1), "unit": "rays/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32", "data": "synthetic (Lego-shaped 800x800, 100 poses)",
+            "vs_baseline": None, "dtype": "f32 (bf16x3 split MFMA)" if split else "f32",
+            "data": "synthetic (Lego-shaped 800x800, 100 poses)",
             "config": {"workload": "BASELINE configs[1]: 1024-ray batches x 128+128 samples, 8x256 MLP fwd/bwd + Adam",
                        "rays_per_gpu": n, "global_batch": n * world, "samples": samples,
-                       "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_F32_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_TFLOPS, 4), "traffic": traffic,
+                       "parallelism": f"dp{world}", "precision": a.precision},
+            "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak,
+                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
                          "flop_per_launch": fl_launch},
             "mlp_all_kernels": {"achieved": round(mlp_tf, 2), "unit": "TFLOP/s",
-                                "frac": round(mlp_tf / PEAK_F32_TFLOPS, 4)},
+                                "frac": round(mlp_tf / peak, 4)},
             "kernels": kernels,
             "psnr_fine": round(psnr, 3),
         }

@@ -55,7 +55,15 @@ typedef struct nof_config {
   float coarse_loss_mult;                 /* 0.1 (TrainState.cs:69, AF:345) */
   uint64_t seed;                          /* Philox key (reference: time(nullptr), MNcpp:44) */
   void* stream;                           /* hipStream_t, NULL = default stream */
+  int32_t precision;                      /* NOF_PRECISION_*: MLP contraction arithmetic (build extension) */
 } nof_config;
+
+/* MLP contraction arithmetic.  Both modes hold every operand and accumulator in fp32 and meet the
+ * same fp32 parity tolerance; they differ only in how the MFMAs form products.
+ *   F32       : v_mfma_f32_32x32x2_f32 (exact fp32 fmaf chains).
+ *   F32_SPLIT : each fp32 operand as three bf16 pieces (24 significand bits), six
+ *               v_mfma_f32_32x32x16_bf16 per product, fp32 accumulation (~2.5x the F32 MFMA rate). */
+enum { NOF_PRECISION_F32 = 0, NOF_PRECISION_F32_SPLIT = 1 };
 
 void nof_config_default(nof_config* cfg);
 const char* nof_last_error(void);

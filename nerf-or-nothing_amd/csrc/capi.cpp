@@ -58,6 +58,7 @@ void nof_config_default(nof_config* c) {
   c->resample_padding = 0.01f; c->coarse_loss_mult = 0.1f;
   c->seed = 0x5EED0000ull;
   c->stream = nullptr;
+  c->precision = NOF_PRECISION_F32;
 }
 
 const char* nof_last_error(void) { return g_err.c_str(); }

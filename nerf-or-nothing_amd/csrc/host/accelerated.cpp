@@ -82,6 +82,7 @@ static void check_cfg(const nof_config& c) {
   if (c.net_depth != 8 || c.net_width != 256 || c.net_depth_condition != 1 || c.net_width_condition != 128 ||
       c.skip_layer != 4 || c.min_deg_point != 0 || c.max_deg_point != 16 || c.deg_view != 4)
     throw Error(NOF_ERR_UNSUPPORTED, "GPU path implements the reference network (8x256, 1x128, skip 4, PE 16/4)");
+  NOF_REQUIRE(c.precision == NOF_PRECISION_F32 || c.precision == NOF_PRECISION_F32_SPLIT, "unknown precision mode");
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -117,8 +118,14 @@ AcceleratedMLP::AcceleratedMLP(int deg_point, int deg_view, const nof_config& cf
   for (int l = 0; l < kLayers; ++l) { param_views_.push_back(params_.p + woff_[l]); grad_views_.push_back(grads_.p + woff_[l]); }
   for (int l = 0; l < kLayers; ++l) { param_views_.push_back(params_.p + boff_[l]); grad_views_.push_back(grads_.p + boff_[l]); }
 
-  wimg_f_.alloc(nof::kFwdImageFloats);
-  wimg_b_.alloc(nof::kBwdImageFloats);
+  split_ = cfg.precision == NOF_PRECISION_F32_SPLIT;
+  if (split_) {  // bf16 (hi, mid, lo) slices + the fp32 tails (mlp_common.h)
+    wimg_f_.alloc(nof::kFwdImageX3Floats + nof::kFwdTail);
+    wimg_b_.alloc(nof::kBwdImageX3Floats + nof::kBwdTail);
+  } else {
+    wimg_f_.alloc(nof::kFwdImageFloats);
+    wimg_b_.alloc(nof::kBwdImageFloats);
+  }
 
   lv_.resize(cfg.num_levels);
   for (int l = 0; l < cfg.num_levels; ++l) {
@@ -153,13 +160,15 @@ void AcceleratedMLP::pack_weights() {
   nof::PackArgs pa;
   for (int l = 0; l < kLayers; ++l) { pa.woff[l] = woff_[l]; pa.boff[l] = boff_[l]; }
   tb(kTPack);
-  NOF_HIP(nof::launch_pack_weights(params_.p, pa, wimg_f_.p, wimg_b_.p, st_));
+  if (split_) NOF_HIP(nof::launch_pack_weights_x3(params_.p, pa, wimg_f_.p, wimg_b_.p, st_));
+  else NOF_HIP(nof::launch_pack_weights(params_.p, pa, wimg_f_.p, wimg_b_.p, st_));
   te(kTPack);
 }
 
 void AcceleratedMLP::run_forward(int level, const nof::FwdArgs& a0) {
   Level& L = lv_[level];
   nof::FwdArgs a = a0;
+  a.split = split_ ? 1 : 0;
   a.wimg = wimg_f_.p;
   a.act_in = L.act_in.p;
   a.act_h = L.act_h.p;
@@ -339,6 +348,7 @@ float* const* AcceleratedMLP::get_gradient(const float* color_grad, const float*
   Schedule& sc = schedule(level, L.M);
   nof::BwdArgs b{};
   b.M = L.M;
+  b.split = split_ ? 1 : 0;
   b.dsigma = density_grad; b.drgb = color_grad; b.zhead = L.zhead.p;
   b.masks = L.masks.p;
   b.wimg_b = wimg_b_.p;
@@ -347,8 +357,12 @@ float* const* AcceleratedMLP::get_gradient(const float* color_grad, const float*
   NOF_HIP(nof::launch_mlp_bwd(b, st_));
   te(kTMlpBwd);
   tb(kTWgrad);
-  NOF_HIP(nof::launch_wgrad(sc.probs.p, sc.items.p, sc.item_ptr.p, sc.num_wg, sc.slab_off.p, slabs_.p,
-                            bias_slabs_.p, st_));
+  if (split_)
+    NOF_HIP(nof::launch_wgrad_x3(sc.probs.p, sc.items.p, sc.item_ptr.p, sc.num_wg, sc.slab_off.p, slabs_.p,
+                                 bias_slabs_.p, st_));
+  else
+    NOF_HIP(nof::launch_wgrad(sc.probs.p, sc.items.p, sc.item_ptr.p, sc.num_wg, sc.slab_off.p, slabs_.p,
+                              bias_slabs_.p, st_));
   te(kTWgrad);
   tb(kTWgradReduce);
   NOF_HIP(nof::launch_wgrad_reduce(sc.outs.p, sc.nouts, sc.max_elems, sc.items.p, sc.probs.p, sc.slab_off.p,

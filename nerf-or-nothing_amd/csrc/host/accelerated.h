@@ -142,6 +142,7 @@ class AcceleratedMLP {
   nof_config cfg_;
   hipStream_t st_;
   int num_cu_ = 256;
+  bool split_ = false;  // NOF_PRECISION_F32_SPLIT
   size_t P_ = 0;
   std::array<int, kLayers> out_{}, in_{}, woff_{}, boff_{};
   DevBuf<float> params_, grads_, wimg_f_, wimg_b_;

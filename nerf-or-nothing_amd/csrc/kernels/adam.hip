@@ -108,6 +108,72 @@ __global__ void k_pack_weights(const float* __restrict__ P, PackArgs pa, float* 
   }
 }
 
+// Split-mode images (mlp_common.h): slices of bf16 (hi, mid, lo) fragments + the same fp32 tails.
+// One thread per 16-B fragment chunk (8 bf16) or per tail float.
+__device__ inline float fwd_tail_value(const float* __restrict__ P, const PackArgs& pa, int t) {
+  if (t < kFwdTailW8) {
+    const int l = t / 256, x = t % 256;
+    return x < layer_out(l) ? P[pa.boff[l] + x] : 0.0f;
+  }
+  if (t < kFwdTailW10) return P[pa.woff[8] + (t - kFwdTailW8)];
+  if (t < kFwdTailW9d) return P[pa.woff[10] + (t - kFwdTailW10)];
+  const int o = (t - kFwdTailW9d) / 32, k = (t - kFwdTailW9d) % 32;
+  return k < kDirIn ? P[pa.woff[9] + (int64_t)o * 283 + 256 + k] : 0.0f;
+}
+__device__ inline float bwd_tail_value(const float* __restrict__ P, const PackArgs& pa, int t) {
+  return t < kBwdTailW10 ? P[pa.woff[8] + t] : P[pa.woff[10] + (t - kBwdTailW10)];
+}
+__device__ inline __bf16 split_piece(float w, int piece) {
+  const float hi = (float)(__bf16)w;
+  if (piece == 0) return (__bf16)w;
+  const float r1 = w - hi;
+  const float mid = (float)(__bf16)r1;
+  if (piece == 1) return (__bf16)r1;
+  return (__bf16)(r1 - mid);
+}
+
+constexpr int kX3SliceChunks = kX3SliceFloats / 4;  // 3072 fragments of 16 B
+
+__global__ void k_pack_weights_x3(const float* __restrict__ P, PackArgs pa, float* __restrict__ wf,
+                                  float* __restrict__ wb) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nfc = (int64_t)kFwdSlices * kX3SliceChunks, nbc = (int64_t)kBwdSlices * kX3SliceChunks;
+  if (gid < nfc + nbc) {
+    const bool fwd = gid < nfc;
+    const int64_t c = fwd ? gid : gid - nfc;
+    const int slice = (int)(c / kX3SliceChunks), q = (int)(c % kX3SliceChunks);
+    const int lane = q & 63, rest = q >> 6, piece = rest % 3, so = rest / 3, ot = so & 7, s = so >> 3;
+    const int h = lane >> 5, row = ot * 32 + (lane & 31);
+    int l, base;
+    if (fwd) fwd_slice(slice, l, base);
+    else bwd_slice(slice, l, base);
+    const int in = layer_in(l);
+    bf16x8 out;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kf = 16 * s + 8 * (j >> 2) + 4 * h + (j & 3);
+      float w;
+      if (fwd) w = (row < layer_out(l) && base + kf < in) ? P[pa.woff[l] + (int64_t)row * in + base + kf] : 0.0f;
+      else w = P[pa.woff[l] + (int64_t)(base + kf) * in + row];
+      out[j] = split_piece(w, piece);
+    }
+    float* dst = (fwd ? wf : wb) + (size_t)slice * kX3SliceFloats + (size_t)q * 4;
+    *reinterpret_cast<bf16x8*>(dst) = out;
+  } else {
+    const int t = (int)(gid - nfc - nbc);
+    if (t < kFwdTail) wf[kFwdImageX3Floats + t] = fwd_tail_value(P, pa, t);
+    else if (t < kFwdTail + kBwdTail) wb[kBwdImageX3Floats + (t - kFwdTail)] = bwd_tail_value(P, pa, t - kFwdTail);
+  }
+}
+
+hipError_t launch_pack_weights_x3(const float* params, const PackArgs& pa, float* wimg_f, float* wimg_b,
+                                  hipStream_t st) {
+  const int64_t total = (int64_t)(kFwdSlices + kBwdSlices) * kX3SliceChunks + kFwdTail + kBwdTail;
+  hipLaunchKernelGGL(k_pack_weights_x3, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, params, pa, wimg_f,
+                     wimg_b);
+  return hipGetLastError();
+}
+
 hipError_t launch_pack_weights(const float* params, const PackArgs& pa, float* wimg_f, float* wimg_b, hipStream_t st) {
   const int64_t total = (int64_t)kFwdImageFloats + (int64_t)kBwdImageFloats;
   hipLaunchKernelGGL(k_pack_weights, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, params, pa, wimg_f,

@@ -34,6 +34,7 @@ hipError_t launch_output_gradient(int n, const float* C, const float* pix, const
 // ---- mlp_fwd.hip / mlp_bwd.hip -----------------------------------------------------------------
 struct FwdArgs {
   int M, S, encoded;
+  int split;                               // 1: split-bf16 image and MFMAs (mlp_common.h)
   const float *t, *origins, *dirs, *radii;  // fused-encoding inputs
   const float *enc_pos, *enc_dir;          // encoded inputs (API path): [M][96], [n][27]
   const float* wimg;                       // packed forward image (slices + tail)
@@ -49,6 +50,7 @@ hipError_t launch_mlp_fwd(const FwdArgs& a, hipStream_t st);
 
 struct BwdArgs {
   int M;
+  int split;
   const float *dsigma, *drgb, *zhead;
   const uint32_t* masks;
   const float* wimg_b;                     // packed backward image (slices + tail)
@@ -73,6 +75,8 @@ struct WgOut {
 };
 hipError_t launch_wgrad(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,
                         const int64_t* slab_off, float* slabs, float* bias_slabs, hipStream_t st);
+hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,
+                        const int64_t* slab_off, float* slabs, float* bias_slabs, hipStream_t st);
 hipError_t launch_wgrad_reduce(const WgOut* outs, int nouts, int max_elems, const WgItem* items,
                                const WgProblem* probs, const int64_t* slab_off, const float* slabs,
                                const float* bias_slabs, int accumulate, hipStream_t st);
@@ -82,5 +86,7 @@ hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v, 
                        hipStream_t st);
 struct PackArgs { int woff[11]; int boff[11]; };
 hipError_t launch_pack_weights(const float* params, const PackArgs& pa, float* wimg_f, float* wimg_b, hipStream_t st);
+hipError_t launch_pack_weights_x3(const float* params, const PackArgs& pa, float* wimg_f, float* wimg_b,
+                                  hipStream_t st);
 
 }  // namespace nof

@@ -41,17 +41,18 @@ __device__ __forceinline__ void bwd_epilogue(const f32x16 (&acc)[8], float (&bin
   }
 }
 
+template <bool X3>
 __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
-  __shared__ __attribute__((aligned(16))) float lds[2 * kSliceFloats];
+  __shared__ __attribute__((aligned(16))) float lds[ring_floats<X3>()];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
   const int nblk = a.M / kBlk;
   const int blk_raw = blockIdx.x * 4 + wave;
   const int blk = blk_raw < nblk ? blk_raw : nblk - 1;  // tail waves duplicate the last block
   const int m = blk * kBlk + j;
-  const float* tail = a.wimg_b + (size_t)kBwdSlices * kSliceFloats;
+  const float* tail = a.wimg_b + (size_t)kBwdSlices * slice_floats<X3>();
   const size_t layer_stride = (size_t)nblk * kWidth * kBlk;
 
-  slice_dma(a.wimg_b, lds, tid);
+  first_slice_dma<X3>(a.wimg_b, lds, tid);
 
   // ---- heads (MNcs:410-415) ------------------------------------------------------------
   const f32x4 zh = reinterpret_cast<const f32x4*>(a.zhead)[m];
@@ -98,7 +99,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
   const float* wsrc = a.wimg_b;
   f32x16 acc[8];
   // ---- dh7 = W9[:, :256]^T delta9 + w8 dz_s ; delta7 ---------------------------------------
-  mlp_layer<4, 0, 8>(bin, nullptr, acc, lds, cur, wsrc, false, tid, lane);
+  dense_layer<X3, 4, 0, 8>(bin, nullptr, acc, lds, cur, wsrc, false, tid, lane);
   {
     const uint4 mk = reinterpret_cast<const uint4*>(mask_ptr(const_cast<uint32_t*>(a.masks), blk, 7))[lane];
     bwd_epilogue<true>(acc, bin, tail + kBwdTailW8, dzs, mk, a.delta + 7 * layer_stride + (size_t)blk * kWidth * kBlk,
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
   }
   // ---- dh_{l-1} = W_l[:, :256]^T delta_l ; delta_{l-1}, l = 7..1 --------------------------
   for (int l = kDepth - 1; l >= 1; --l) {
-    mlp_layer<8, 0, 8>(bin, nullptr, acc, lds, cur, wsrc, l == 1, tid, lane);
+    dense_layer<X3, 8, 0, 8>(bin, nullptr, acc, lds, cur, wsrc, l == 1, tid, lane);
     const uint4 mk = reinterpret_cast<const uint4*>(mask_ptr(const_cast<uint32_t*>(a.masks), blk, l - 1))[lane];
     bwd_epilogue<false>(acc, bin, nullptr, 0.0f, mk, a.delta + (l - 1) * layer_stride + (size_t)blk * kWidth * kBlk,
                         lane);
@@ -117,7 +118,8 @@ hipError_t launch_mlp_bwd(const BwdArgs& a, hipStream_t st) {
   if (a.M <= 0) return hipSuccess;
   if (a.M % kBlk != 0) return hipErrorInvalidValue;
   const int nblk = a.M / kBlk;
-  hipLaunchKernelGGL(k_mlp_bwd, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
+  if (a.split) hipLaunchKernelGGL(k_mlp_bwd<true>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
+  else hipLaunchKernelGGL(k_mlp_bwd<false>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
   return hipGetLastError();
 }
 

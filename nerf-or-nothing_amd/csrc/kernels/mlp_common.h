@@ -99,6 +99,186 @@ __device__ __forceinline__ void mlp_layer(const float (&bin)[8][16], const float
   }
 }
 
+// ============================================================================================
+// Split mode (nof_config.precision = NOF_PRECISION_F32_SPLIT): every fp32 operand x is carried as
+// three bf16 pieces hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid) (24 significand
+// bits, fp32's exponent range, no scaling), and a product a.b as the six bf16 MFMAs whose terms
+// are >= 2^-16 of it (lo.hi, hi.lo, mid.mid, mid.hi, hi.mid, hi.hi) accumulated in fp32.  One
+// v_mfma_f32_32x32x16_bf16 does 8x the k of v_mfma_f32_32x32x2_f32 in half the cycles, so six of
+// them cost 3/8 of the fp32 MFMA time; measured error vs fp64 equals the fp32 MFMA's
+// (tools/probe/x3_probe.hip: rel L2 8.4e-7 vs 9.7e-7 at K = 4096).
+//
+// Fragment maps (32x32x16 bf16, verified by the probe): lane l = (h = l >> 5, x = l & 31) holds
+// A[row x][k = 8h + j] and B[k = 8h + j][col x], j = 0..7.  K-step s of an activation tile
+// (registers 8s..8s+7 of its accumulator) therefore carries feature 16s + 8(j >> 2) + 4h + (j & 3)
+// in element j, and the packed weight pieces follow that order.
+// ============================================================================================
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+struct Frag3 {
+  bf16x8 p[3];  // hi, mid, lo
+};
+
+// split elements (i, i + 1) of a fragment: exact fp32 residuals, RNE conversions (v_cvt_pk_bf16_f32)
+__device__ __forceinline__ void split2(float x0, float x1, bf16x2& a, bf16x2& b, bf16x2& c) {
+  const f32x2 v = {x0, x1};
+  a = __builtin_convertvector(v, bf16x2);
+  const f32x2 r1 = v - __builtin_convertvector(a, f32x2);
+  b = __builtin_convertvector(r1, bf16x2);
+  const f32x2 r2 = r1 - __builtin_convertvector(b, f32x2);
+  c = __builtin_convertvector(r2, bf16x2);
+}
+__device__ __forceinline__ bf16x8 cat4(bf16x2 a, bf16x2 b, bf16x2 c, bf16x2 d) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  const bf16x4 lo = __builtin_shufflevector(a, b, 0, 1, 2, 3);
+  const bf16x4 hi = __builtin_shufflevector(c, d, 0, 1, 2, 3);
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ void split_pair(float x0, float x1, Frag3& f, int i) {
+  bf16x2 a, b, c;
+  split2(x0, x1, a, b, c);
+  f.p[0][i] = a[0]; f.p[0][i + 1] = a[1];
+  f.p[1][i] = b[0]; f.p[1][i + 1] = b[1];
+  f.p[2][i] = c[0]; f.p[2][i + 1] = c[1];
+}
+__device__ __forceinline__ void split8(const float (&v)[8], Frag3& f) {
+  bf16x2 a[4], b[4], c[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) split2(v[2 * i], v[2 * i + 1], a[i], b[i], c[i]);
+  f.p[0] = cat4(a[0], a[1], a[2], a[3]);
+  f.p[1] = cat4(b[0], b[1], b[2], b[3]);
+  f.p[2] = cat4(c[0], c[1], c[2], c[3]);
+}
+__device__ __forceinline__ void split44(const f32x4& u, const f32x4& v, Frag3& f) {
+  const float e[8] = {u[0], u[1], u[2], u[3], v[0], v[1], v[2], v[3]};
+  split8(e, f);
+}
+
+__device__ __forceinline__ f32x16 mfma_x3(const Frag3& a, const Frag3& b, f32x16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[2], b.p[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[0], c, 0, 0, 0);
+  return c;
+}
+
+// Split-mode weight slice: 32 input features (2 k-steps) x 256 rows (8 row tiles) x 3 pieces;
+// 16-B chunk ((s * 8 + ot) * 3 + piece) * 64 + lane holds lane's 8 bf16 of that fragment, so each
+// fragment is one conflict-free ds_read_b128 (1 KB contiguous per wave).  48 KB.
+constexpr int kX3SliceFloats = 2 * 8 * 3 * 64 * 4;
+constexpr size_t kFwdImageX3Floats = (size_t)kFwdSlices * kX3SliceFloats;  // + fwd tail (fp32)
+constexpr size_t kBwdImageX3Floats = (size_t)kBwdSlices * kX3SliceFloats;  // + bwd tail (fp32)
+
+__device__ __forceinline__ void slice_dma_x3(const float* __restrict__ src, float* dst, int tid) {
+  const int wave = tid >> 6;
+#pragma unroll
+  for (int i = 0; i < kX3SliceFloats / 4 / kMlpThreads; ++i) {
+    const int chunk = kMlpThreads * i + tid;
+    __builtin_amdgcn_global_load_lds((gptr_t)(src + chunk * 4), (lptr_t)(dst + (kMlpThreads * i + 64 * wave) * 4),
+                                     16, 0, 0);
+  }
+}
+
+// raw fp32 B values of k-step kk of a split-mode layer: tiles t < NT_B from the register-resident
+// activations, the rest from the wave's IPE copy in LDS ([tp][q][lane][4] floats)
+template <int NT_B>
+__device__ __forceinline__ void x3_b_values(const float (&bin)[8][16], const float* ipe_lds, int kk, int lane,
+                                            float (&v)[8]) {
+  const int t = kk >> 1, s = kk & 1;
+  if (t < NT_B) {
+    const int tb = t < NT_B ? t : 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = bin[tb][8 * s + j];
+  } else {
+    const int ti = t - NT_B;
+    const f32x4 u0 = *reinterpret_cast<const f32x4*>(ipe_lds + ((ti * 4 + 2 * s) * 64 + lane) * 4);
+    const f32x4 u1 = *reinterpret_cast<const f32x4*>(ipe_lds + ((ti * 4 + 2 * s + 1) * 64 + lane) * 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = u0[j]; v[4 + j] = u1[j]; }
+  }
+}
+
+// Split-mode dense layer: same contract as mlp_layer (slices of the split image, one barrier per
+// slice).  Per (k-step, row tile): three ds_read_b128 (issued one group ahead) and six MFMAs; the
+// next k-step's B fragment is split pair by pair in the shadow of the current k-step's MFMAs.
+template <int NT_B, int NT_I, int OT>
+__device__ __forceinline__ void mlp_layer_x3(const float (&bin)[8][16], const float* ipe_lds, f32x16 (&acc)[8],
+                                             float* lds, int& cur, const float*& wsrc, bool last_in_schedule,
+                                             int tid, int lane) {
+  constexpr int NK = 2 * (NT_B + NT_I);
+  constexpr int PER = OT / 4;  // row-tile groups per split pair
+#pragma unroll
+  for (int ot = 0; ot < OT; ++ot) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[ot][r] = 0.0f;
+  }
+  Frag3 b_cur, b_nxt;
+  {
+    float v[8];
+    x3_b_values<NT_B>(bin, ipe_lds, 0, lane, v);
+    split8(v, b_cur);
+  }
+#pragma unroll
+  for (int t = 0; t < NT_B + NT_I; ++t) {
+    const bool has_next = !(last_in_schedule && t == NT_B + NT_I - 1);
+    if (has_next) slice_dma_x3(wsrc + kX3SliceFloats, lds + (cur ^ 1) * kX3SliceFloats, tid);
+    const bf16x8* W = reinterpret_cast<const bf16x8*>(lds + cur * kX3SliceFloats) + lane;
+    Frag3 a_cur;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) a_cur.p[p] = W[p * 64];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int kk = 2 * t + s;
+      float vn[8];
+      if (kk + 1 < NK) x3_b_values<NT_B>(bin, ipe_lds, kk + 1, lane, vn);
+#pragma unroll
+      for (int ot = 0; ot < OT; ++ot) {
+        asm volatile("" ::"v"(a_cur.p[0]), "v"(a_cur.p[1]), "v"(a_cur.p[2]));  // wait here, before the next reads
+        Frag3 a_nxt = a_cur;
+        const bool more = !(s == 1 && ot == OT - 1);
+        if (more) {
+          const int s2 = ot == OT - 1 ? s + 1 : s;
+          const int ot2 = ot == OT - 1 ? 0 : ot + 1;
+#pragma unroll
+          for (int p = 0; p < 3; ++p) a_nxt.p[p] = W[((s2 * 8 + ot2) * 3 + p) * 64];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        acc[ot] = mfma_x3(a_cur, b_cur, acc[ot]);
+        if (kk + 1 < NK && ot % PER == 0) {
+          const int i = 2 * (ot / PER);
+          split_pair(vn[i], vn[i + 1], b_nxt, i);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        a_cur = a_nxt;
+      }
+      b_cur = b_nxt;
+    }
+    __syncthreads();
+    cur ^= 1;
+    wsrc += kX3SliceFloats;
+  }
+}
+
+// mode dispatch for the fused kernels
+template <bool X3, int NT_B, int NT_I, int OT>
+__device__ __forceinline__ void dense_layer(const float (&bin)[8][16], const float* ipe_lds, f32x16 (&acc)[8],
+                                            float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
+                                            int lane) {
+  if constexpr (X3) mlp_layer_x3<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane);
+  else mlp_layer<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane);
+}
+template <bool X3>
+__device__ __forceinline__ void first_slice_dma(const float* src, float* dst, int tid) {
+  if constexpr (X3) slice_dma_x3(src, dst, tid);
+  else slice_dma(src, dst, tid);
+}
+template <bool X3> constexpr int ring_floats() { return 2 * (X3 ? kX3SliceFloats : kSliceFloats); }
+template <bool X3> constexpr int slice_floats() { return X3 ? kX3SliceFloats : kSliceFloats; }
+
 // feature index held by register r of accumulator tile ot in lane half h
 __device__ __forceinline__ int tile_feature(int ot, int r, int h) { return ot * 32 + 8 * (r >> 2) + 4 * h + (r & 3); }
 

@@ -54,8 +54,10 @@ __device__ __forceinline__ void fwd_epilogue(const f32x16 (&acc)[8], float (&bin
   reinterpret_cast<uint4*>(mask_dst)[lv] = mv;
 }
 
+template <bool X3>
 __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
-  __shared__ __attribute__((aligned(16))) float lds[2 * kSliceFloats + 4 * kIpeLdsFloats + 4 * 128];
+  constexpr int kRing = ring_floats<X3>();
+  __shared__ __attribute__((aligned(16))) float lds[kRing + 4 * kIpeLdsFloats + 4 * 128];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
   const int nblk = a.M / kBlk;
   const int blk_raw = blockIdx.x * 4 + wave;
@@ -64,9 +66,9 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
   const int ray = m0 / a.S;
   const int s0 = m0 - ray * a.S;
   const int m = m0 + j;
-  const float* tail = a.wimg + (size_t)kFwdSlices * kSliceFloats;
+  const float* tail = a.wimg + (size_t)kFwdSlices * slice_floats<X3>();
 
-  slice_dma(a.wimg, lds, tid);  // first slice in flight while the encodings are computed
+  first_slice_dma<X3>(a.wimg, lds, tid);  // first slice in flight while the encodings are computed
 
   // ---- encodings: 48 IPE features per lane in B-operand order ----------------------------
   float ipe[3][16];
@@ -112,7 +114,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
     }
   }
   // view-direction part of layer 9 folded into a per-ray bias: b9 + W9[:, 256:283] . PE(d)
-  float* ipe_lds = lds + 2 * kSliceFloats + wave * kIpeLdsFloats;
+  float* ipe_lds = lds + kRing + wave * kIpeLdsFloats;
 #pragma unroll
   for (int tp = 0; tp < 3; ++tp)
 #pragma unroll
@@ -121,7 +123,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
       v[0] = ipe[tp][4 * q]; v[1] = ipe[tp][4 * q + 1]; v[2] = ipe[tp][4 * q + 2]; v[3] = ipe[tp][4 * q + 3];
       *reinterpret_cast<f32x4*>(ipe_lds + ((tp * 4 + q) * 64 + lane) * 4) = v;
     }
-  float* dirb = lds + 2 * kSliceFloats + 4 * kIpeLdsFloats + wave * 128;
+  float* dirb = lds + kRing + 4 * kIpeLdsFloats + wave * 128;
 #pragma unroll
   for (int rep = 0; rep < 2; ++rep) {
     const int o = lane + 64 * rep;
@@ -140,12 +142,12 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
   const size_t layer_stride = (size_t)nblk * kWidth * kBlk;
 
   // ---- trunk ----------------------------------------------------------------------------
-  mlp_layer<0, 3, 8>(bin, ipe_lds, acc, lds, cur, wsrc, false, tid, lane);
+  dense_layer<X3, 0, 3, 8>(bin, ipe_lds, acc, lds, cur, wsrc, false, tid, lane);
   fwd_epilogue<8>(acc, bin, tail + kFwdTailBias, a.act_h + (size_t)blk * kWidth * kBlk, mask_ptr(a.masks, blk, 0),
                   lane);
   for (int l = 1; l < kDepth; ++l) {
-    if (l == kSkip) mlp_layer<8, 3, 8>(bin, ipe_lds, acc, lds, cur, wsrc, false, tid, lane);
-    else mlp_layer<8, 0, 8>(bin, ipe_lds, acc, lds, cur, wsrc, false, tid, lane);
+    if (l == kSkip) dense_layer<X3, 8, 3, 8>(bin, ipe_lds, acc, lds, cur, wsrc, false, tid, lane);
+    else dense_layer<X3, 8, 0, 8>(bin, ipe_lds, acc, lds, cur, wsrc, false, tid, lane);
     fwd_epilogue<8>(acc, bin, tail + kFwdTailBias + l * 256,
                     a.act_h + l * layer_stride + (size_t)blk * kWidth * kBlk, mask_ptr(a.masks, blk, l), lane);
   }
@@ -164,7 +166,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
   zs += tail[kFwdTailBias + 8 * 256];
 
   // ---- view layer 9: relu(W9[:, :256] h7 + dirbias) --------------------------------------
-  mlp_layer<8, 0, 4>(bin, ipe_lds, acc, lds, cur, wsrc, true, tid, lane);
+  dense_layer<X3, 8, 0, 4>(bin, ipe_lds, acc, lds, cur, wsrc, true, tid, lane);
   fwd_epilogue<4>(acc, bin, dirb, a.act_h9 + (size_t)blk * kWidthCond * kBlk, mask_ptr(a.masks, blk, 8), lane);
 
   // ---- RGB head (layer 10) ------------------------------------------------------------
@@ -197,7 +199,8 @@ hipError_t launch_mlp_fwd(const FwdArgs& a, hipStream_t st) {
   if (a.M <= 0) return hipSuccess;
   if (a.M % kBlk != 0 || a.S % kBlk != 0) return hipErrorInvalidValue;
   const int nblk = a.M / kBlk;
-  hipLaunchKernelGGL(k_mlp_fwd, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
+  if (a.split) hipLaunchKernelGGL(k_mlp_fwd<true>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
+  else hipLaunchKernelGGL(k_mlp_fwd<false>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
   return hipGetLastError();
 }
 

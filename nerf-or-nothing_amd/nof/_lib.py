@@ -24,6 +24,9 @@ class NofError(RuntimeError):
         self.status = status
 
 
+NOF_PRECISION_F32, NOF_PRECISION_F32_SPLIT = 0, 1
+
+
 class nof_config(C.Structure):
     _fields_ = [
         ("device", C.c_int32), ("max_rays", C.c_int32), ("num_levels", C.c_int32),
@@ -33,7 +36,7 @@ class nof_config(C.Structure):
         ("skip_layer", C.c_int32), ("min_deg_point", C.c_int32), ("max_deg_point", C.c_int32),
         ("deg_view", C.c_int32), ("randomized", C.c_int32), ("white_bkgd", C.c_int32),
         ("resample_padding", C.c_float), ("coarse_loss_mult", C.c_float),
-        ("seed", C.c_uint64), ("stream", C.c_void_p),
+        ("seed", C.c_uint64), ("stream", C.c_void_p), ("precision", C.c_int32),
     ]
 
 

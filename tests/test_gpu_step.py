@@ -26,14 +26,18 @@ def _run_gpu(model, r, dev, msum=None):
     return model.get_gradient_device(n, d["o"], d["d"], d["radius"], d["near"], d["far"], d["lossmult"], d["pix"], msum)
 
 
+PRECISIONS = [0, 1]  # NOF_PRECISION_F32, NOF_PRECISION_F32_SPLIT: same fp32 tolerance for both
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("n,samples", [(16, (64, 64)), (8, (128, 128)), (6, (64, 128))])
-def test_step_parity(gpu, oracle, n, samples):
+def test_step_parity(gpu, oracle, n, samples, precision):
     import torch
     import nof
     from nof import synth
 
     seed, step, ray_base = 0x1234, 3, 500
-    model = nof.AcceleratedMipNeRF(seed=seed, max_rays=n, num_samples=samples)
+    model = nof.AcceleratedMipNeRF(seed=seed, max_rays=n, num_samples=samples, precision=precision)
     model.set_rng(seed, step, ray_base)
     r = synth.blender_rays(n, seed=11)
     grads = _run_gpu(model, r, gpu)
@@ -133,7 +137,8 @@ def test_encoded_get_output_equals_fused(gpu):
     assert np.array_equal(nof.to_numpy(rptr, (n, S, 3)), v0["rgb"])
 
 
-def test_gradients_deterministic(gpu):
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_gradients_deterministic(gpu, precision):
     import torch
     import nof
     from nof import synth
@@ -142,7 +147,7 @@ def test_gradients_deterministic(gpu):
     r = synth.blender_rays(n, seed=2)
     outs = []
     for _ in range(2):
-        m = nof.AcceleratedMipNeRF(seed=5, max_rays=n)
+        m = nof.AcceleratedMipNeRF(seed=5, max_rays=n, precision=precision)
         _run_gpu(m, r, gpu)
         torch.cuda.synchronize()
         outs.append(nof.to_numpy(m.mlp.flat_grads()[0], (546948,)))

@@ -169,101 +169,108 @@ __global__ __launch_bounds__(kWgThreads, 1) void k_wgrad(const WgProblem* __rest
   }
 }
 
-// ---- split mode (mlp_common.h): bf16x3 operands, six bf16 MFMAs per 32x32x16 product ---------
-// Same 2 x 4 wave grid and schedule as the fp32 kernel (8 waves, two per SIMD, up to 4 x 2 output
-// tiles each).  Per 16-sample k-step a lane reads its rows' 8 consecutive samples as two
-// ds_read_b128 (chunk-swizzled blocks, common.h), splits them into (hi, mid, lo) and issues
-// 6 * RB * CB MFMAs; B fragments are split one column tile ahead in the MFMAs' shadow.
-constexpr int kWgX3Threads = kWgThreads;
+// ---- split mode (mlp_common.h): bf16x3 operands, six bf16 MFMAs per 32x32x16 product -----------
+// Per 16-sample k-step:
+//   * wave w loads row tile w of A and column tile w of B straight into registers (two 16-B loads
+//     per lane per tile: samples 8h .. 8h + 7 of feature 32w + x), two k-steps ahead;
+//   * it splits them ONCE into (hi, mid, lo) fragment images in LDS (double-buffered, 2 x 48 KB),
+//     so no split is repeated by the waves that share a tile;
+//   * the MFMA waves (same 2 x 4 grid as fp32) read each fragment piece as one conflict-free
+//     ds_read_b128 and issue 6 * RB * CB MFMAs.
+// One barrier per k-step; the split of k-step k + 1 and the MFMAs of k-step k are independent and
+// interleave.
+constexpr int kX3Frag = 3 * 8 * 64 * 4;  // floats per operand fragment image: [piece][tile][lane][16 B]
+constexpr int kX3Lds = 2 * 2 * kX3Frag;   // 96 KB
+
+struct X3Raw {
+  f32x4 a0, a1, b0, b1;
+};
 
 template <int RB, int CB>
 __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& P, float* lds, int tid, int lane,
                                            int wave, float* slabs, float* bias_slabs, const int64_t* slab_off) {
-  // opaque lane copy: keeps the lane-derived offsets of the six instantiations from being hoisted
-  // out of the item loop all at once (they would spill)
-  int lv = lane;
-  asm volatile("" : "+v"(lv));
-  const int h = lv >> 5, x = lv & 31;
+  const int h = lane >> 5, x = lane & 31;
   const int wr = wave >> 2, wc = wave & 3;
   const int r0 = wr * RB, c0 = wc * CB;
   const bool active = r0 < P.ntr && c0 < P.ntc;  // wave-uniform
+  const bool ldA = wave < P.ntr, ldB = wave < P.ntc;
   int rowt[RB], colt[CB];
 #pragma unroll
   for (int r = 0; r < RB; ++r) rowt[r] = min(r0 + r, P.ntr - 1);
 #pragma unroll
   for (int c = 0; c < CB; ++c) colt[c] = min(c0 + c, P.ntc - 1);
-  const int nA4 = P.ntr * 32 * kBlk / 4, nB4 = P.ntc * 32 * kBlk / 4;
-  const float* Ab = P.A + (size_t)P.a_row0 * kBlk;
-  const float* Bb = P.B + (size_t)P.b_col0 * kBlk;
   const size_t strideA = (size_t)P.FA * kBlk, strideB = (size_t)P.FB * kBlk;
+  // this lane's feature rows (row & 7 == x & 7 since tiles are 32-aligned) in k-block 0
+  const float* rowA = P.A + (size_t)item.kb0 * strideA + (size_t)(P.a_row0 + min(wave, P.ntr - 1) * 32 + x) * kBlk;
+  const float* rowB = P.B + (size_t)item.kb0 * strideB + (size_t)(P.b_col0 + min(wave, P.ntc - 1) * 32 + x) * kBlk;
+  const int K = 2 * (item.kb1 - item.kb0);
+
+  auto load = [&](int k, X3Raw& q) {  // logical chunks 4(k&1) + 2h, + 1 of the row, chunk-swizzled
+    const int c = 4 * (k & 1) + 2 * h, sw = x & 7;
+    const size_t kb = (size_t)(k >> 1);
+    if (ldA) {
+      q.a0 = *reinterpret_cast<const f32x4*>(rowA + kb * strideA + ((c ^ sw) << 2));
+      q.a1 = *reinterpret_cast<const f32x4*>(rowA + kb * strideA + (((c + 1) ^ sw) << 2));
+    }
+    if (ldB) {
+      q.b0 = *reinterpret_cast<const f32x4*>(rowB + kb * strideB + ((c ^ sw) << 2));
+      q.b1 = *reinterpret_cast<const f32x4*>(rowB + kb * strideB + (((c + 1) ^ sw) << 2));
+    }
+  };
+  float bsum = 0.0f;  // row sum of delta for (row tile = wave, lane)
+  auto split = [&](const X3Raw& q, int buf) {
+    float* img = lds + buf * 2 * kX3Frag;
+    if (ldA) {
+      Frag3 f;
+      split44(q.a0, q.a1, f);
+      bsum += ((q.a0[0] + q.a0[1]) + (q.a0[2] + q.a0[3])) + ((q.a1[0] + q.a1[1]) + (q.a1[2] + q.a1[3]));
+#pragma unroll
+      for (int p = 0; p < 3; ++p) reinterpret_cast<bf16x8*>(img)[(p * 8 + wave) * 64 + lane] = f.p[p];
+    }
+    if (ldB) {
+      Frag3 f;
+      split44(q.b0, q.b1, f);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) reinterpret_cast<bf16x8*>(img + kX3Frag)[(p * 8 + wave) * 64 + lane] = f.p[p];
+    }
+  };
 
   f32x16 acc[RB][CB];
-  float bs[RB];
 #pragma unroll
-  for (int r = 0; r < RB; ++r) {
-    bs[r] = 0.0f;
+  for (int r = 0; r < RB; ++r)
 #pragma unroll
     for (int c = 0; c < CB; ++c)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[r][c][e] = 0.0f;
-  }
-  blk_dma<kWgX3Threads>(Ab + item.kb0 * strideA, lds, nA4, tid);
-  blk_dma<kWgX3Threads>(Bb + item.kb0 * strideB, lds + kWgHalf, nB4, tid);
+
+  X3Raw q0, q1;
+  load(0, q0);
+  if (K > 1) load(1, q1);
+  split(q0, 0);
   __syncthreads();
-  int cur = 0;
-  for (int kb = item.kb0; kb < item.kb1; ++kb) {
-    float* nxt = lds + (cur ^ 1) * 2 * kWgHalf;
-    int tk = tid;
-    asm volatile("" : "+v"(tk));  // DMA lane addresses recomputed per k-block (see lk below)
-    if (kb + 1 < item.kb1) {
-      blk_dma<kWgX3Threads>(Ab + (kb + 1) * strideA, nxt, nA4, tk);
-      blk_dma<kWgX3Threads>(Bb + (kb + 1) * strideB, nxt + kWgHalf, nB4, tk);
-    }
+  for (int k = 0; k < K; ++k) {
+    X3Raw q2;
+    if (k + 2 < K) load(k + 2, q2);
+    if (k + 1 < K) split(q1, (k + 1) & 1);
     if (active) {
-      const float* LA = lds + cur * 2 * kWgHalf;
-      const float* LB = LA + kWgHalf;
-      // lane-derived offsets recomputed per k-block from an opaque lane copy (not hoisted: they
-      // would pin ~40 VGPRs beside the 256 accumulators and spill)
-      const int lk = tk & 63;
-      const int hk = lk >> 5, xk = lk & 31, xsk = xk & 7;
-      int aoff[RB], boff[CB];
+      const bf16x8* FA = reinterpret_cast<const bf16x8*>(lds + (k & 1) * 2 * kX3Frag) + lane;
+      const bf16x8* FB = FA + kX3Frag / 4;
 #pragma unroll
-      for (int r = 0; r < RB; ++r) aoff[r] = (rowt[r] * 32 + xk) * kBlk;
+      for (int c = 0; c < CB; ++c) {
+        Frag3 fb;
 #pragma unroll
-      for (int c = 0; c < CB; ++c) boff[c] = (colt[c] * 32 + xk) * kBlk;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {  // samples 16s + 8h + j in fragment element j
-        const int o0 = ((4 * s + 2 * hk) ^ xsk) << 2, o1 = ((4 * s + 2 * hk + 1) ^ xsk) << 2;
-        Frag3 fa[RB];
+        for (int p = 0; p < 3; ++p) fb.p[p] = FB[(p * 8 + colt[c]) * 64];
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
-          const f32x4 u = *reinterpret_cast<const f32x4*>(LA + aoff[r] + o0);
-          const f32x4 v = *reinterpret_cast<const f32x4*>(LA + aoff[r] + o1);
-          split44(u, v, fa[r]);
-          bs[r] += ((u[0] + u[1]) + (u[2] + u[3])) + ((v[0] + v[1]) + (v[2] + v[3]));
-        }
-        // B fragments one column tile at a time, double-buffered by column parity: column c + 1 is
-        // read before and split during the MFMAs of column c
-        Frag3 fb[2];
-        f32x4 bu = *reinterpret_cast<const f32x4*>(LB + boff[0] + o0);
-        f32x4 bv = *reinterpret_cast<const f32x4*>(LB + boff[0] + o1);
-        split44(bu, bv, fb[0]);
+          Frag3 fa;
 #pragma unroll
-        for (int c = 0; c < CB; ++c) {
-          if (c + 1 < CB) {
-            bu = *reinterpret_cast<const f32x4*>(LB + boff[c + 1] + o0);
-            bv = *reinterpret_cast<const f32x4*>(LB + boff[c + 1] + o1);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int r = 0; r < RB; ++r) acc[r][c] = mfma_x3(fa[r], fb[c & 1], acc[r][c]);
-          if (c + 1 < CB) split44(bu, bv, fb[(c + 1) & 1]);
-          __builtin_amdgcn_sched_barrier(0);
+          for (int p = 0; p < 3; ++p) fa.p[p] = FA[(p * 8 + rowt[r]) * 64];
+          acc[r][c] = mfma_x3(fa, fb, acc[r][c]);
         }
       }
     }
     __syncthreads();
-    cur ^= 1;
+    q1 = q2;
   }
   if (active) {
     float* slab = slabs + slab_off[item.slab];
@@ -280,22 +287,18 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
           }
         }
       }
-    if (wc == 0) {
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        const float v = bs[r] + __shfl_xor(bs[r], 32, 64);
-        if (r0 + r < P.ntr && h == 0) bias_slabs[(size_t)item.slab * 256 + rowt[r] * 32 + x] = v;
-      }
-    }
   }
-  __syncthreads();
+  if (ldA) {
+    const float v = bsum + __shfl_xor(bsum, 32, 64);
+    if (h == 0) bias_slabs[(size_t)item.slab * 256 + wave * 32 + x] = v;
+  }
 }
 
-__global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_x3(const WgProblem* __restrict__ probs,
-                                                              const WgItem* __restrict__ items,
-                                                              const int* __restrict__ item_ptr,
-                                                              const int64_t* __restrict__ slab_off, float* slabs,
-                                                              float* bias_slabs) {
+__global__ __launch_bounds__(kWgThreads, 1) void k_wgrad_x3(const WgProblem* __restrict__ probs,
+                                                            const WgItem* __restrict__ items,
+                                                            const int* __restrict__ item_ptr,
+                                                            const int64_t* __restrict__ slab_off, float* slabs,
+                                                            float* bias_slabs) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int it0 = item_ptr[blockIdx.x], it1 = item_ptr[blockIdx.x + 1];
@@ -316,7 +319,7 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_x3(const WgProblem* _
 hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,
                            const int64_t* slab_off, float* slabs, float* bias_slabs, hipStream_t st) {
   if (num_wg <= 0) return hipSuccess;
-  const size_t shm = sizeof(float) * 4 * kWgHalf;
+  const size_t shm = sizeof(float) * kX3Lds;  // 96 KB
   static bool attr = false;
   if (!attr) {
     const hipError_t e =
@@ -324,7 +327,7 @@ hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const in
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL(k_wgrad_x3, dim3(num_wg), dim3(kWgX3Threads), shm, st, probs, items, item_ptr, slab_off, slabs,
+  hipLaunchKernelGGL(k_wgrad_x3, dim3(num_wg), dim3(kWgThreads), shm, st, probs, items, item_ptr, slab_off, slabs,
                      bias_slabs);
   return hipGetLastError();
 }

@@ -170,20 +170,20 @@ __global__ __launch_bounds__(kWgThreads, 1) void k_wgrad(const WgProblem* __rest
 }
 
 // ---- split mode (mlp_common.h): bf16x3 operands, six bf16 MFMAs per 32x32x16 product -----------
-// Per 16-sample k-step:
-//   * wave w loads row tile w of A and column tile w of B straight into registers (two 16-B loads
-//     per lane per tile: samples 8h .. 8h + 7 of feature 32w + x), two k-steps ahead;
-//   * it splits them ONCE into (hi, mid, lo) fragment images in LDS (double-buffered, 2 x 48 KB),
-//     so no split is repeated by the waves that share a tile;
+// Per 16-sample k-step (the 64-B half of every feature row of a chunk-swizzled block, common.h):
+//   * every thread loads 16-B chunks straight into registers, three k-steps ahead, with each
+//     wave-instruction covering 16 feature rows x 64 contiguous bytes;
+//   * it splits each chunk ONCE into (hi, mid, lo) and writes the three 8-B pieces to the k-step's
+//     fragment images in LDS (double-buffered, 2 x 48 KB), so no split is repeated by the waves
+//     that share a tile;
 //   * the MFMA waves (same 2 x 4 grid as fp32) read each fragment piece as one conflict-free
 //     ds_read_b128 and issue 6 * RB * CB MFMAs.
-// One barrier per k-step; the split of k-step k + 1 and the MFMAs of k-step k are independent and
-// interleave.
+// One barrier per k-step; the split of k-step k + 1 and the MFMAs of k-step k interleave.
 constexpr int kX3Frag = 3 * 8 * 64 * 4;  // floats per operand fragment image: [piece][tile][lane][16 B]
 constexpr int kX3Lds = 2 * 2 * kX3Frag;   // 96 KB
 
 struct X3Raw {
-  f32x4 a0, a1, b0, b1;
+  f32x4 a[2], b[2];  // chunk i of this thread: row (tid >> 2) + 128 i, logical chunk tid & 3 of the k-step
 };
 
 template <int RB, int CB>
@@ -193,45 +193,53 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
   const int wr = wave >> 2, wc = wave & 3;
   const int r0 = wr * RB, c0 = wc * CB;
   const bool active = r0 < P.ntr && c0 < P.ntc;  // wave-uniform
-  const bool ldA = wave < P.ntr, ldB = wave < P.ntc;
   int rowt[RB], colt[CB];
 #pragma unroll
   for (int r = 0; r < RB; ++r) rowt[r] = min(r0 + r, P.ntr - 1);
 #pragma unroll
   for (int c = 0; c < CB; ++c) colt[c] = min(c0 + c, P.ntc - 1);
   const size_t strideA = (size_t)P.FA * kBlk, strideB = (size_t)P.FB * kBlk;
-  // this lane's feature rows (row & 7 == x & 7 since tiles are 32-aligned) in k-block 0
-  const float* rowA = P.A + (size_t)item.kb0 * strideA + (size_t)(P.a_row0 + min(wave, P.ntr - 1) * 32 + x) * kBlk;
-  const float* rowB = P.B + (size_t)item.kb0 * strideB + (size_t)(P.b_col0 + min(wave, P.ntc - 1) * 32 + x) * kBlk;
+  const int nrA = P.ntr * 32, nrB = P.ntc * 32;
+  // loader role: chunk lc = tid & 3 (samples 4 lc .. 4 lc + 3 of the k-step) of rows (tid >> 2) + 128 i
+  const int lc = tid & 3, lrow = tid >> 2;
+  const float* baseA = P.A + (size_t)item.kb0 * strideA + (size_t)P.a_row0 * kBlk;
+  const float* baseB = P.B + (size_t)item.kb0 * strideB + (size_t)P.b_col0 * kBlk;
   const int K = 2 * (item.kb1 - item.kb0);
 
-  auto load = [&](int k, X3Raw& q) {  // logical chunks 4(k&1) + 2h, + 1 of the row, chunk-swizzled
-    const int c = 4 * (k & 1) + 2 * h, sw = x & 7;
+  auto load = [&](int k, X3Raw& q) {
     const size_t kb = (size_t)(k >> 1);
-    if (ldA) {
-      q.a0 = *reinterpret_cast<const f32x4*>(rowA + kb * strideA + ((c ^ sw) << 2));
-      q.a1 = *reinterpret_cast<const f32x4*>(rowA + kb * strideA + (((c + 1) ^ sw) << 2));
-    }
-    if (ldB) {
-      q.b0 = *reinterpret_cast<const f32x4*>(rowB + kb * strideB + ((c ^ sw) << 2));
-      q.b1 = *reinterpret_cast<const f32x4*>(rowB + kb * strideB + (((c + 1) ^ sw) << 2));
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = lrow + 128 * i;
+      const int phys = (4 * (k & 1) + lc) ^ (row & 7);
+      if (row < nrA) q.a[i] = *reinterpret_cast<const f32x4*>(baseA + kb * strideA + (size_t)row * kBlk + phys * 4);
+      if (row < nrB) q.b[i] = *reinterpret_cast<const f32x4*>(baseB + kb * strideB + (size_t)row * kBlk + phys * 4);
     }
   };
-  float bsum = 0.0f;  // row sum of delta for (row tile = wave, lane)
+  float bsum[2] = {0.0f, 0.0f};  // partial row sums of delta (rows lrow, lrow + 128; this chunk's samples)
+  // chunk lc of row (t, xr) = samples 4 lc .. 4 lc + 3 = elements 4 (lc & 1) .. +3 of fragment lane
+  // (h = lc >> 1, xr): one 8-B piece per (piece, row)
+  auto put = [&](float* img, int row, const f32x4& v) {
+    bf16x2 a0, b0, c0_, a1, b1, c1;
+    split2(v[0], v[1], a0, b0, c0_);
+    split2(v[2], v[3], a1, b1, c1);
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    const int t = row >> 5, xr = row & 31;
+    bf16x4* dst = reinterpret_cast<bf16x4*>(img) + (((t * 64 + (lc >> 1) * 32 + xr) * 2) + (lc & 1));
+    dst[0] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3);
+    dst[8 * 64 * 2] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3);
+    dst[2 * 8 * 64 * 2] = __builtin_shufflevector(c0_, c1, 0, 1, 2, 3);
+  };
   auto split = [&](const X3Raw& q, int buf) {
     float* img = lds + buf * 2 * kX3Frag;
-    if (ldA) {
-      Frag3 f;
-      split44(q.a0, q.a1, f);
-      bsum += ((q.a0[0] + q.a0[1]) + (q.a0[2] + q.a0[3])) + ((q.a1[0] + q.a1[1]) + (q.a1[2] + q.a1[3]));
 #pragma unroll
-      for (int p = 0; p < 3; ++p) reinterpret_cast<bf16x8*>(img)[(p * 8 + wave) * 64 + lane] = f.p[p];
-    }
-    if (ldB) {
-      Frag3 f;
-      split44(q.b0, q.b1, f);
-#pragma unroll
-      for (int p = 0; p < 3; ++p) reinterpret_cast<bf16x8*>(img + kX3Frag)[(p * 8 + wave) * 64 + lane] = f.p[p];
+    for (int i = 0; i < 2; ++i) {
+      const int row = lrow + 128 * i;
+      if (row < nrA) {
+        put(img, row, q.a[i]);
+        bsum[i] += (q.a[i][0] + q.a[i][1]) + (q.a[i][2] + q.a[i][3]);
+      }
+      if (row < nrB) put(img + kX3Frag, row, q.b[i]);
     }
   };
 
@@ -243,16 +251,25 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[r][c][e] = 0.0f;
 
-  X3Raw q0, q1;
+  X3Raw q0, q1, q2;
   load(0, q0);
   if (K > 1) load(1, q1);
+  if (K > 2) load(2, q2);
   split(q0, 0);
   __syncthreads();
   for (int k = 0; k < K; ++k) {
-    X3Raw q2;
-    if (k + 2 < K) load(k + 2, q2);
+    X3Raw q3;
+    if (k + 3 < K) load(k + 3, q3);  // rows stay in flight for two k-steps
+#ifndef NOF_DIAG_X3_NOSPLIT
     if (k + 1 < K) split(q1, (k + 1) & 1);
+#else
+    if (k + 1 < K && q1.a[0][0] == 12345.0f) split(q1, (k + 1) & 1);
+#endif
+#ifndef NOF_DIAG_X3_NOMFMA
     if (active) {
+#else
+    if (active && K < 0) {
+#endif
       const bf16x8* FA = reinterpret_cast<const bf16x8*>(lds + (k & 1) * 2 * kX3Frag) + lane;
       const bf16x8* FB = FA + kX3Frag / 4;
 #pragma unroll
@@ -271,6 +288,7 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
     }
     __syncthreads();
     q1 = q2;
+    q2 = q3;
   }
   if (active) {
     float* slab = slabs + slab_off[item.slab];
@@ -288,9 +306,13 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
         }
       }
   }
-  if (ldA) {
-    const float v = bsum + __shfl_xor(bsum, 32, 64);
-    if (h == 0) bias_slabs[(size_t)item.slab * 256 + wave * 32 + x] = v;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // the 4 chunk-lanes of a row are lanes 4 lrow .. 4 lrow + 3
+    float v = bsum[i];
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    const int row = lrow + 128 * i;
+    if (row < nrA && lc == 0) bias_slabs[(size_t)item.slab * 256 + row] = v;
   }
 }
 

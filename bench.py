@@ -50,6 +50,7 @@ def parse():
     p.add_argument("--samples", type=int, nargs="+", default=[128, 128])
     p.add_argument("--precision", choices=["f32", "split"], default="f32",
                    help="MLP contraction arithmetic: fp32 MFMA, or fp32 operands as bf16x3 split MFMAs")
+    p.add_argument("--no-alt", action="store_true", help="skip the other precision mode's secondary measurement")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-integrator", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work")
@@ -154,15 +155,6 @@ def main():
     samples = a.samples
     stream = torch.cuda.current_stream(dev).cuda_stream
     seed = 0x5EED0002
-    split = a.precision == "split"
-    model = nof.AcceleratedMipNeRF(device=local, max_rays=n, num_samples=samples, seed=seed,
-                                   stream=stream, precision=1 if split else 0)
-    model.set_rng(seed, 0, rank * n)  # global ray ids: sharding never changes a sample
-    opt = nof.AcceleratedAdamOptimizer(model.GetLayerSizes(), model.config)
-    params = model.mlp.allParams
-    gptr, P = model.mlp.flat_grads()
-    grad_view = nof.device_tensor(gptr, (P,), device=dev)
-
     # pre-staged synthetic batches (views of a 100-pose Lego-shaped scene; shard = disjoint views)
     pool = []
     for i in range(4):
@@ -170,47 +162,57 @@ def main():
         pool.append({k: torch.from_numpy(v).to(dev) for k, v in r.items()})
     msum_global = float(n * world)  # lossmult = 1 everywhere: sum over all shards (D14, DP-global)
 
-    def step(k):
-        b = pool[k % len(pool)]
-        grads = model.get_gradient_device(n, b["o"], b["d"], b["radius"], b["near"], b["far"], b["lossmult"],
-                                          b["pix"], msum_global)
+    def measure(split):
+        """W untimed + K timed training steps of one precision mode; returns (s, timing, psnr)."""
+        model = nof.AcceleratedMipNeRF(device=local, max_rays=n, num_samples=samples, seed=seed,
+                                       stream=stream, precision=1 if split else 0)
+        model.set_rng(seed, 0, rank * n)  # global ray ids: sharding never changes a sample
+        opt = nof.AcceleratedAdamOptimizer(model.GetLayerSizes(), model.config)
+        params = model.mlp.allParams
+        gptr, P = model.mlp.flat_grads()
+        grad_view = nof.device_tensor(gptr, (P,), device=dev)
+
+        def step(k):
+            b = pool[k % len(pool)]
+            grads = model.get_gradient_device(n, b["o"], b["d"], b["radius"], b["near"], b["far"],
+                                              b["lossmult"], b["pix"], msum_global)
+            if world > 1:
+                dist.all_reduce(grad_view)  # sum of per-shard gradient sums (no averaging: L is a sum)
+            opt.step(params, grads, nof.learning_rate_decay(k + 1))
+
+        for k in range(a.warmup):
+            step(k)
+        torch.cuda.synchronize()
         if world > 1:
-            dist.all_reduce(grad_view)  # sum of per-shard gradient sums (no averaging: L is a sum)
-        opt.step(params, grads, nof.learning_rate_decay(k + 1))
+            dist.barrier()
+        model.enable_timing(True)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for k in range(a.warmup, a.warmup + a.steps):
+            step(k)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        timing = model.read_timing()
+        model.enable_timing(False)
+        if world > 1:
+            t = torch.tensor([dt], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        # fine-level PSNR of the last step's batch (MseToPsnr, MipHelpers.cs:672)
+        last = pool[(a.warmup + a.steps - 1) % len(pool)]
+        comp = model.level_numpy(len(samples) - 1)["comp_rgb"]
+        mse = float(np.mean((comp - last["pix"].cpu().numpy()) ** 2))
+        psnr = -10.0 * math.log10(max(mse, 1e-12))
+        opt.close()
+        model.close()
+        return dt, timing, psnr
 
-    for k in range(a.warmup):
-        step(k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    model.enable_timing(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for k in range(a.warmup, a.warmup + a.steps):
-        step(k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    timing = model.read_timing()
-    model.enable_timing(False)
-    if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    ms_step = dt * 1e3 / a.steps
-    rays_per_s = n * world * a.steps / dt
-
-    # fine-level PSNR of the last step's batch (MseToPsnr, MipHelpers.cs:672)
-    last = pool[(a.warmup + a.steps - 1) % len(pool)]
-    comp = model.level_numpy(len(samples) - 1)["comp_rgb"]
-    mse = float(np.mean((comp - last["pix"].cpu().numpy()) ** 2))
-    psnr = -10.0 * math.log10(max(mse, 1e-12))
-
-    result = None
-    if rank == 0:
+    def summarize(split, dt, timing):
+        ms_step = dt * 1e3 / a.steps
         M = [n * s for s in samples]
         flop = {"mlp_fwd": 2 * MACS_FWD * sum(M), "mlp_bwd": 2 * MACS_DX * sum(M), "wgrad": 2 * MACS_DW * sum(M)}
         kernels = {}
@@ -231,6 +233,23 @@ def main():
                 traffic = json.load(open(tfile)).get(dom + ("_split" if split else ""))
             except (OSError, ValueError):
                 traffic = None
+        return ms_step, kernels, {
+            "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak,
+                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                         "flop_per_launch": fl_launch},
+            "mlp_all_kernels": {"achieved": round(mlp_tf, 2), "unit": "TFLOP/s", "frac": round(mlp_tf / peak, 4)},
+        }
+
+    split = a.precision == "split"
+    dt, timing, psnr = measure(split)
+    rays_per_s = n * world * a.steps / dt
+    alt = None
+    if world == 1 and not a.no_alt:
+        alt = (not split,) + measure(not split)
+
+    result = None
+    if rank == 0:
+        ms_step, kernels, roof = summarize(split, dt, timing)
         result = {
             "metric": METRIC, "value": round(rays_per_s, 1), "unit": "rays/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
@@ -239,14 +258,17 @@ def main():
             "config": {"workload": "BASELINE configs[1]: 1024-ray batches x 128+128 samples, 8x256 MLP fwd/bwd + Adam",
                        "rays_per_gpu": n, "global_batch": n * world, "samples": samples,
                        "parallelism": f"dp{world}", "precision": a.precision},
-            "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak,
-                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
-                         "flop_per_launch": fl_launch},
-            "mlp_all_kernels": {"achieved": round(mlp_tf, 2), "unit": "TFLOP/s",
-                                "frac": round(mlp_tf / peak, 4)},
+            **roof,
             "kernels": kernels,
             "psnr_fine": round(psnr, 3),
         }
+        if alt is not None:  # the other precision mode, same workload (parity-tested at the same tolerance)
+            asplit, adt, atiming, apsnr = alt
+            ams, akernels, aroof = summarize(asplit, adt, atiming)
+            result["alt_precision"] = {
+                "precision": "split" if asplit else "f32", "value": round(n * a.steps / adt, 1), "unit": "rays/s",
+                "ms_per_step": round(ams, 4), **aroof,
+                "kernels": {k: v["avg_launch_ms"] for k, v in akernels.items()}, "psnr_fine": round(apsnr, 3)}
         if not a.no_integrator and world == 1:
             result["roofline_integrator"] = integrator_roofline(torch, nof, dev)
         if not a.no_cpu_baseline and world == 1:

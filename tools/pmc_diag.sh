@@ -4,7 +4,7 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=$1; shift
-ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-integrator $*"
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-integrator --no-alt $*"
 mkdir -p $OUT
 i=0
 for pass in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" \

@@ -7,6 +7,7 @@ coalesced streaming read on gfx950 (MI355X_MICROARCH.md, HBM section), WRITE_SIZ
 import csv, collections, json, os, shutil, sys
 
 src, tag = sys.argv[1], sys.argv[2]
+suffix = sys.argv[3] if len(sys.argv) > 3 else ""  # "_split" for the split-precision kernels
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 dst = os.path.join(root, "profiles")
 os.makedirs(dst, exist_ok=True)
@@ -35,10 +36,13 @@ for k, s in stats.items():
         e["eff_clock_GHz"] = grbm / 8 / (avg_ns * 1e-9) / 1e9
     out[k] = e
 json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
-# traffic lookup used by bench.py (bench kernel-timer names)
-names = {"k_mlp_fwd": "mlp_fwd", "k_mlp_bwd": "mlp_bwd", "k_wgrad": "wgrad", "k_render_fwd<2>": "render_fwd",
-         "k_render_bwd<2>": "render_bwd"}
-json.dump({names[k]: v.get("hbm_bytes_per_launch") for k, v in out.items() if k in names},
-          open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
+# traffic lookup used by bench.py (bench kernel-timer names; split-mode kernels keyed with "_split")
+names = {"k_mlp_fwd<false>": "mlp_fwd", "k_mlp_bwd<false>": "mlp_bwd", "k_wgrad": "wgrad",
+         "k_mlp_fwd<true>": "mlp_fwd_split", "k_mlp_bwd<true>": "mlp_bwd_split", "k_wgrad_x3": "wgrad_split",
+         "k_render_fwd<2>": "render_fwd" + suffix, "k_render_bwd<2>": "render_bwd" + suffix}
+tfile = os.path.join(dst, "pmc_traffic.json")
+traffic = json.load(open(tfile)) if os.path.exists(tfile) else {}
+traffic.update({names[k]: v.get("hbm_bytes_per_launch") for k, v in out.items() if k in names})
+json.dump(traffic, open(tfile, "w"), indent=1, sort_keys=True)
 for k, v in out.items():
     print(k, json.dumps(v))

@@ -124,6 +124,30 @@ nof_status nof_mipnerf_level_view(nof_mipnerf* h, int32_t level, nof_level_view*
 /* sum over rays and levels of lambda_l * m_r |C - p|^2 / sum m (fused path only; synchronises) */
 nof_status nof_mipnerf_loss(nof_mipnerf* h, float* out);
 
+/* ---- evaluation ------------------------------------------------------------
+ * Forward-only two-level render: replaces MipNerfModel.Call(rays, randomized, whiteBackground)
+ * (MipNerfModel.cs:36-97, whose level-1 resampling reads an empty array: D22).  Per level the
+ * composite rgb, the clamped weighted-midpoint distance and the accumulated opacity
+ * (VolumetricRendering, MipHelpers.cs:472-492).  Inputs device-resident; outputs device, borrowed
+ * until the next call on h.  randomized != 0 draws jitter from the model's Philox state (set_rng)
+ * without advancing it. */
+typedef struct nof_render_out {
+  int32_t num_levels;
+  const float* comp_rgb[NOF_MAX_LEVELS];  /* [n][3] */
+  const float* distance[NOF_MAX_LEVELS];  /* [n] */
+  const float* acc[NOF_MAX_LEVELS];       /* [n] */
+} nof_render_out;
+nof_status nof_mipnerf_render_device(nof_mipnerf* h, int32_t n, const float* dev_origins, const float* dev_dirs,
+                                     const float* dev_radii, const float* dev_nears, const float* dev_fars,
+                                     int32_t randomized, int32_t white_bkgd, nof_render_out* out);
+
+/* Image metrics on device images [H][W][3] (float, any range; max_val as MathHelpers' maxVal):
+ * psnr = MseToPsnr(mean squared error) (MipHelpers.cs:672); ssim = ComputeSsimAverage with the
+ * reference defaults (11x11 Gaussian, sigma 1.5, k1 0.01, k2 0.03, zero-padded 'same' convolution,
+ * variances and covariance clipped at 0; MipHelpers.cs:685-736,903-927).  Synchronises the stream. */
+nof_status nof_image_metrics(const float* dev_img0, const float* dev_img1, int32_t width, int32_t height,
+                             float max_val, float* psnr, float* ssim, void* stream);
+
 /* ---- AcceleratedMLP (AcceleratedMLP.h:7-45) -------------------------------------------------- */
 /* get_output MLPcpp:214-255: encoded inputs in device memory (enc_pos [n*S][96] in the reference's
  * feature order, enc_dir [n][27] per ray, D5) -> (density [n*S], rgb [n*S][3]) borrowed.  The

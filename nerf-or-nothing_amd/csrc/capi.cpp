@@ -128,6 +128,22 @@ nof_status nof_mipnerf_level_view(nof_mipnerf* h, int32_t level, nof_level_view*
 nof_status nof_mipnerf_loss(nof_mipnerf* h, float* out) {
   return guard([&] { ARG(h && out); *out = h->impl->loss(); });
 }
+nof_status nof_mipnerf_render_device(nof_mipnerf* h, int32_t n, const float* o, const float* d, const float* radii,
+                                     const float* nears, const float* fars, int32_t randomized, int32_t white_bkgd,
+                                     nof_render_out* out) {
+  return guard([&] {
+    ARG(h && out);
+    *out = nof_render_out{};
+    h->impl->Render(n, o, d, radii, nears, fars, randomized, white_bkgd, out);
+  });
+}
+nof_status nof_image_metrics(const float* img0, const float* img1, int32_t width, int32_t height, float max_val,
+                             float* psnr, float* ssim, void* stream) {
+  return guard([&] {
+    ARG(img0 && img1 && psnr && ssim && width > 0 && height > 0 && max_val > 0.0f);
+    NOF_HIP(nof::image_metrics(img0, img1, width, height, max_val, psnr, ssim, (hipStream_t)stream));
+  });
+}
 nof_status nof_mipnerf_enable_timing(nof_mipnerf* h, int32_t enable) {
   return guard([&] { ARG(h); h->impl->timer.enable(enable != 0, h->impl->mlp->stream()); });
 }

@@ -183,13 +183,14 @@ void AcceleratedMLP::run_forward(int level, const nof::FwdArgs& a0) {
 }
 
 void AcceleratedMLP::forward_fused(int level, int n, int samples, const float* t, const float* origins,
-                                   const float* dirs, const float* radii) {
+                                   const float* dirs, const float* radii, bool inference) {
   NOF_REQUIRE(level >= 0 && level < (int)lv_.size(), "level out of range");
   const int M = n * samples;
   NOF_REQUIRE(n > 0 && samples % kBlk == 0 && M <= lv_[level].cap, "batch exceeds the level's capacity");
   lv_[level].M = M; lv_[level].n = n; lv_[level].S = samples;
   nof::FwdArgs a{};
   a.M = M; a.S = samples; a.encoded = 0;
+  a.no_store = inference ? 1 : 0;
   a.t = t; a.origins = origins; a.dirs = dirs; a.radii = radii;
   run_forward(level, a);
 }
@@ -385,9 +386,10 @@ AcceleratedMipNeRF::AcceleratedMipNeRF(const nof_config& cfg) : mlp(nullptr), cf
   o_.alloc(3 * N); d_.alloc(3 * N); radii_.alloc(N); nears_.alloc(N); fars_.alloc(N); lm_.alloc(N); pix_.alloc(3 * N);
   const int L = cfg.num_levels;
   t_.resize(L); w_.resize(L); C_.resize(L); dsig_.resize(L); drgb_.resize(L); loss_rays_.resize(L);
+  acc_.resize(L); dist_.resize(L);
   for (int l = 0; l < L; ++l) {
     const size_t S = cfg.num_samples[l];
-    t_[l].alloc(N * (S + 1)); w_[l].alloc(N * S); C_[l].alloc(3 * N);
+    t_[l].alloc(N * (S + 1)); w_[l].alloc(N * S); C_[l].alloc(3 * N); acc_[l].alloc(N); dist_[l].alloc(N);
     dsig_[l].alloc(N * S); drgb_[l].alloc(3 * N * S); loss_rays_[l].alloc(N);
   }
 }
@@ -463,6 +465,33 @@ float* const* AcceleratedMipNeRF::run(int n, const float* o, const float* d, con
   last_fused_ = cb == nullptr;
   ++step_;
   return grads;
+}
+
+void AcceleratedMipNeRF::Render(int n, const float* o, const float* d, const float* radii, const float* nears,
+                                const float* fars, int randomized, int white_bkgd, nof_render_out* out) {
+  NOF_REQUIRE(n > 0 && n <= cfg_.max_rays, "ray count out of range");
+  NOF_REQUIRE(o && d && radii && nears && fars && out, "null argument");
+  const int L = cfg_.num_levels;
+  mlp->pack_weights();
+  for (int lv = 0; lv < L; ++lv) {  // MNcs:40-95
+    const int S = cfg_.num_samples[lv];
+    if (lv == 0) {
+      NOF_HIP(nof::launch_sample_stratified(n, S, nears, fars, randomized, seed_, step_, 0, ray_base_, t_[0].p, st_));
+    } else {
+      NOF_HIP(nof::launch_sample_pdf(n, cfg_.num_samples[lv - 1], t_[lv - 1].p, w_[lv - 1].p, S,
+                                     cfg_.resample_padding, randomized, seed_, step_, (uint32_t)lv, ray_base_,
+                                     t_[lv].p, nullptr, st_));
+    }
+    mlp->forward_fused(lv, n, S, t_[lv].p, o, d, radii, /*inference=*/true);
+    NOF_HIP(nof::launch_render_fwd(n, S, mlp->density(lv), mlp->rgb(lv), t_[lv].p, d, white_bkgd, C_[lv].p,
+                                   w_[lv].p, st_, acc_[lv].p, dist_[lv].p));
+    out->comp_rgb[lv] = C_[lv].p;
+    out->distance[lv] = dist_[lv].p;
+    out->acc[lv] = acc_[lv].p;
+  }
+  out->num_levels = L;
+  last_n_ = n;
+  last_fused_ = false;  // no loss for a render
 }
 
 nof_level_view AcceleratedMipNeRF::level_view(int level) const {

@@ -111,7 +111,7 @@ class AcceleratedMLP {
 
   // fused path (AcceleratedMipNeRF): frustum + IPE computed inside the forward kernel
   void forward_fused(int level, int n, int samples, const float* t, const float* origins, const float* dirs,
-                     const float* radii);
+                     const float* radii, bool inference = false);
   void pack_weights();  // rebuild the packed weight images from the canonical arena
   const float* density(int level) const { return lv_[level].sigma.p; }
   const float* rgb(int level) const { return lv_[level].rgb.p; }
@@ -173,6 +173,11 @@ class AcceleratedMipNeRF {
   void get_rng(uint64_t* seed, uint32_t* step, uint32_t* ray_base) const { *seed = seed_; *step = step_; *ray_base = ray_base_; }
   nof_level_view level_view(int level) const;
   float loss();
+  // Forward-only two-level render (MipNerfModel.Call, MNcs:36-97, with its D22 defects fixed):
+  // per level comp_rgb [n][3], distance [n], acc [n] (device, borrowed until the next call).
+  // Uses the model's RNG (seed, step, ray_base) when randomized, never advances the step.
+  void Render(int n, const float* o, const float* d, const float* radii, const float* nears, const float* fars,
+              int randomized, int white_bkgd, nof_render_out* out);
   KernelTimer timer;
 
  private:
@@ -186,7 +191,7 @@ class AcceleratedMipNeRF {
   int last_n_ = 0;
   bool last_fused_ = false;
   DevBuf<float> o_, d_, radii_, nears_, fars_, lm_, pix_;
-  std::vector<DevBuf<float>> t_, w_, C_, dsig_, drgb_, loss_rays_;
+  std::vector<DevBuf<float>> t_, w_, C_, dsig_, drgb_, loss_rays_, acc_, dist_;
 };
 
 // ---------------------------------------------------------------------------------------------

@@ -21,8 +21,10 @@ hipError_t launch_encode(int n, int S, const float* mean, const float* cov, cons
 
 // ---- render.hip (volumetric_rendering AF:318-344, get_output_gradient AF:347-361,
 //      volumetric_rendering_gradient AF:362-402) -------------------------------------------------
+// acc / dist (optional): accumulated opacity and the clamped weighted-midpoint distance (MH:472-492)
 hipError_t launch_render_fwd(int n, int S, const float* sigma, const float* rgb, const float* t, const float* d,
-                             int white, float* C, float* w, hipStream_t st);
+                             int white, float* C, float* w, hipStream_t st, float* acc = nullptr,
+                             float* dist = nullptr);
 // g_ext != null: dL/dC supplied by the caller (callback path); else fused loss gradient from pix.
 hipError_t launch_render_bwd(int n, int S, const float* sigma, const float* rgb, const float* t, const float* d,
                              int white, const float* C, const float* g_ext, const float* pix,
@@ -34,6 +36,7 @@ hipError_t launch_output_gradient(int n, const float* C, const float* pix, const
 // ---- mlp_fwd.hip / mlp_bwd.hip -----------------------------------------------------------------
 struct FwdArgs {
   int M, S, encoded;
+  int no_store;                            // 1: inference only, skip the backward's side outputs
   int split;                               // 1: split-bf16 image and MFMAs (mlp_common.h)
   const float *t, *origins, *dirs, *radii;  // fused-encoding inputs
   const float *enc_pos, *enc_dir;          // encoded inputs (API path): [M][96], [n][27]
@@ -82,6 +85,10 @@ hipError_t launch_wgrad_reduce(const WgOut* outs, int nouts, int max_elems, cons
                                const float* bias_slabs, int accumulate, hipStream_t st);
 
 // ---- adam.hip ----------------------------------------------------------------------------------
+// ---- metrics.hip: PSNR / SSIM of device images [H][W][3] (synchronises st) ----
+hipError_t image_metrics(const float* a, const float* b, int W, int H, float max_val, float* psnr, float* ssim,
+                         hipStream_t st);
+
 hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v, float lr, float inv1, float inv2,
                        hipStream_t st);
 struct PackArgs { int woff[11]; int boff[11]; };

@@ -20,7 +20,7 @@ namespace nof {
 // bias + ReLU epilogue on OT accumulator tiles -> next layer's B operand, act block, mask.
 // No per-lane guards: a tail wave past the last block is clamped onto that block and
 // recomputes bit-identical values, so its duplicate stores are benign.
-template <int OT>
+template <int OT, bool store>
 __device__ __forceinline__ void fwd_epilogue(const f32x16 (&acc)[8], float (&bin)[8][16], const float* bias,
                                              float* __restrict__ act_blk, uint32_t* __restrict__ mask_dst, int lane) {
   // opaque copy of the lane index: keeps the 128 per-store offsets from being hoisted out of the
@@ -44,17 +44,17 @@ __device__ __forceinline__ void fwd_epilogue(const f32x16 (&acc)[8], float (&bin
         // shift-accumulate: bit of (ot, r) ends at position 31 - ((ot & 1) * 16 + r) of word ot >> 1
         mw[ot >> 1] = (mw[ot >> 1] << 1) | (hv > 0.0f ? 1u : 0u);
 #ifndef NOF_DIAG_NO_ACT_STORE
-        act_blk[blk_off(fb + jj, j)] = hv;
+        if constexpr (store) act_blk[blk_off(fb + jj, j)] = hv;
 #endif
       }
     }
   }
   uint4 mv;
   mv.x = mw[0]; mv.y = mw[1]; mv.z = mw[2]; mv.w = mw[3];
-  reinterpret_cast<uint4*>(mask_dst)[lv] = mv;
+  if constexpr (store) reinterpret_cast<uint4*>(mask_dst)[lv] = mv;
 }
 
-template <bool X3>
+template <bool X3, bool store>  // store: side outputs for the backward pass (off for inference)
 __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
   constexpr int kRing = ring_floats<X3>();
   __shared__ __attribute__((aligned(16))) float lds[kRing + 4 * kIpeLdsFloats + 4 * 128];
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
   for (int k = 0; k < kDirIn; ++k) pe[k] = a.encoded ? a.enc_dir[(size_t)ray * kDirIn + k] : dir_feature(k, d3);
 
   float* act_in_blk = a.act_in + (size_t)blk * kInF * kBlk;
-  {
+  if constexpr (store) {
 #pragma unroll
     for (int tp = 0; tp < 3; ++tp)
 #pragma unroll
@@ -143,12 +143,12 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
 
   // ---- trunk ----------------------------------------------------------------------------
   dense_layer<X3, 0, 3, 8>(bin, ipe_lds, acc, lds, cur, wsrc, false, tid, lane);
-  fwd_epilogue<8>(acc, bin, tail + kFwdTailBias, a.act_h + (size_t)blk * kWidth * kBlk, mask_ptr(a.masks, blk, 0),
+  fwd_epilogue<8, store>(acc, bin, tail + kFwdTailBias, a.act_h + (size_t)blk * kWidth * kBlk, mask_ptr(a.masks, blk, 0),
                   lane);
   for (int l = 1; l < kDepth; ++l) {
     if (l == kSkip) dense_layer<X3, 8, 3, 8>(bin, ipe_lds, acc, lds, cur, wsrc, false, tid, lane);
     else dense_layer<X3, 8, 0, 8>(bin, ipe_lds, acc, lds, cur, wsrc, false, tid, lane);
-    fwd_epilogue<8>(acc, bin, tail + kFwdTailBias + l * 256,
+    fwd_epilogue<8, store>(acc, bin, tail + kFwdTailBias + l * 256,
                     a.act_h + l * layer_stride + (size_t)blk * kWidth * kBlk, mask_ptr(a.masks, blk, l), lane);
   }
 
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
 
   // ---- view layer 9: relu(W9[:, :256] h7 + dirbias) --------------------------------------
   dense_layer<X3, 8, 0, 4>(bin, ipe_lds, acc, lds, cur, wsrc, true, tid, lane);
-  fwd_epilogue<4>(acc, bin, dirb, a.act_h9 + (size_t)blk * kWidthCond * kBlk, mask_ptr(a.masks, blk, 8), lane);
+  fwd_epilogue<4, store>(acc, bin, dirb, a.act_h9 + (size_t)blk * kWidthCond * kBlk, mask_ptr(a.masks, blk, 8), lane);
 
   // ---- RGB head (layer 10) ------------------------------------------------------------
   float zc[3] = {0.0f, 0.0f, 0.0f};
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
     for (int c = 0; c < 3; ++c) a.rgb[(size_t)m * 3 + c] = sigmoid_f(zc[c]) * kRgbScale - kRgbPadding;
     f32x4 zh;
     zh[0] = zs; zh[1] = zc[0]; zh[2] = zc[1]; zh[3] = zc[2];
-    reinterpret_cast<f32x4*>(a.zhead)[m] = zh;
+    if constexpr (store) reinterpret_cast<f32x4*>(a.zhead)[m] = zh;
   }
 }
 
@@ -199,8 +199,14 @@ hipError_t launch_mlp_fwd(const FwdArgs& a, hipStream_t st) {
   if (a.M <= 0) return hipSuccess;
   if (a.M % kBlk != 0 || a.S % kBlk != 0) return hipErrorInvalidValue;
   const int nblk = a.M / kBlk;
-  if (a.split) hipLaunchKernelGGL(k_mlp_fwd<true>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
-  else hipLaunchKernelGGL(k_mlp_fwd<false>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
+  const dim3 grid((nblk + 3) / 4), block(kMlpThreads);
+  if (a.split) {
+    if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd<true, false>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((k_mlp_fwd<true, true>), grid, block, 0, st, a);
+  } else {
+    if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd<false, false>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((k_mlp_fwd<false, true>), grid, block, 0, st, a);
+  }
   return hipGetLastError();
 }
 

@@ -54,7 +54,8 @@ template <int PER>
 __global__ __launch_bounds__(256) void k_render_fwd(int n, int S, const float* __restrict__ sigma,
                                                     const float* __restrict__ rgb, const float* __restrict__ t,
                                                     const float* __restrict__ d, int white, float* __restrict__ C,
-                                                    float* __restrict__ w) {
+                                                    float* __restrict__ w, float* __restrict__ acc_out,
+                                                    float* __restrict__ dist_out) {
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= n) return;  // wave-uniform; no block barriers below
@@ -62,7 +63,8 @@ __global__ __launch_bounds__(256) void k_render_fwd(int n, int S, const float* _
   ray_alpha_T<PER>(S, r, lane, sigma, t, d, rs);
   const int k0 = lane * PER;
   const float* cr = rgb + ((size_t)r * S + k0) * 3;
-  float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, acc = 0.0f;
+  const float* tr = t + (size_t)r * (S + 1) + k0;
+  float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, acc = 0.0f, wd = 0.0f;
 #pragma unroll
   for (int p = 0; p < PER; ++p) {
     const float wk = rs.a[p] * rs.T[p];
@@ -71,11 +73,19 @@ __global__ __launch_bounds__(256) void k_render_fwd(int n, int S, const float* _
     c1 += wk * cr[3 * p + 1];
     c2 += wk * cr[3 * p + 2];
     acc += wk;
+    if (dist_out) wd += wk * (tr[p] + tr[p + 1]) / 2.0f;  // weighted midpoint (MH:488)
   }
   c0 = wave_sum(c0); c1 = wave_sum(c1); c2 = wave_sum(c2); acc = wave_sum(acc);
+  if (dist_out) wd = wave_sum(wd);
   if (lane == 0) {
     const float bg = white ? (1.0f - acc) : 0.0f;
     C[3 * r] = c0 + bg; C[3 * r + 1] = c1 + bg; C[3 * r + 2] = c2 + bg;
+    if (acc_out) acc_out[r] = acc;
+    if (dist_out) {  // clamp(acc > 0 ? sum / acc : +inf, t_0, t_S)  (MH:490)
+      const float t0 = t[(size_t)r * (S + 1)], tS = t[(size_t)r * (S + 1) + S];
+      const float dv = acc > 0.0f ? wd / acc : __builtin_inff();
+      dist_out[r] = fminf(fmaxf(dv, t0), tS);
+    }
   }
 }
 
@@ -153,10 +163,11 @@ __global__ void k_output_gradient(int n, const float* __restrict__ C, const floa
   }
 
 hipError_t launch_render_fwd(int n, int S, const float* sigma, const float* rgb, const float* t, const float* d,
-                             int white, float* C, float* w, hipStream_t st) {
+                             int white, float* C, float* w, hipStream_t st, float* acc, float* dist) {
   if (n <= 0) return hipSuccess;
   const dim3 grid((n + 3) / 4), block(256);
-  NOF_RENDER_DISPATCH(S, hipLaunchKernelGGL(k_render_fwd<PER>, grid, block, 0, st, n, S, sigma, rgb, t, d, white, C, w));
+  NOF_RENDER_DISPATCH(S, hipLaunchKernelGGL(k_render_fwd<PER>, grid, block, 0, st, n, S, sigma, rgb, t, d, white, C, w,
+                                            acc, dist));
   return hipGetLastError();
 }
 

@@ -13,6 +13,7 @@ from .api import (  # noqa: F401
     OutputRetriever,
     device_count,
     device_tensor,
+    image_metrics,
     learning_rate_decay,
     to_numpy,
 )

@@ -50,6 +50,11 @@ class nof_mlp_debug(C.Structure):
                                      ("act_in", "act_h", "act_h9", "masks", "zhead", "delta", "delta9x")]
 
 
+class nof_render_out(C.Structure):
+    _fields_ = [("num_levels", C.c_int32), ("comp_rgb", C.c_void_p * NOF_MAX_LEVELS),
+                ("distance", C.c_void_p * NOF_MAX_LEVELS), ("acc", C.c_void_p * NOF_MAX_LEVELS)]
+
+
 OUTPUT_GRAD_FN = C.CFUNCTYPE(C.c_uint64, C.c_void_p, C.c_uint64, C.c_int32, C.c_float, C.c_uint64)
 
 P = C.c_void_p
@@ -74,6 +79,8 @@ SIGNATURES = {
     "nof_mipnerf_get_rng": [P, C.POINTER(U64), C.POINTER(U32), C.POINTER(U32)],
     "nof_mipnerf_level_view": [P, I32, C.POINTER(nof_level_view)],
     "nof_mipnerf_loss": [P, C.POINTER(F)],
+    "nof_mipnerf_render_device": [P, I32, P, P, P, P, P, I32, I32, C.POINTER(nof_render_out)],
+    "nof_image_metrics": [P, P, I32, I32, F, C.POINTER(F), C.POINTER(F), P],
     "nof_mipnerf_enable_timing": [P, I32],
     "nof_mipnerf_read_timing": [P, C.POINTER(F), C.POINTER(I32), I32],
     "nof_mlp_get_output": [P, P, P, I32, I32, I32, C.POINTER(U64), C.POINTER(U64)],

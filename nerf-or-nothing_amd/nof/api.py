@@ -211,6 +211,39 @@ class AcceleratedMipNeRF:
         call("nof_mipnerf_loss", self._h, C.byref(out))
         return out.value
 
+    def render_device(self, n, origins, directions, radii, nears, fars, randomized=False, white_bkgd=None):
+        """MipNerfModel.Call (MNcs:36-97): forward-only two-level render of device-resident rays.
+        Returns [{"comp_rgb": (ptr, (n, 3)), "distance": (ptr, (n,)), "acc": (ptr, (n,))}] per level."""
+        out = L.nof_render_out()
+        white = self.config.white_bkgd if white_bkgd is None else int(white_bkgd)
+        call("nof_mipnerf_render_device", self._h, n, _ptr(origins), _ptr(directions), _ptr(radii), _ptr(nears),
+             _ptr(fars), int(randomized), white, C.byref(out))
+        return [{"comp_rgb": (out.comp_rgb[l], (n, 3)), "distance": (out.distance[l], (n,)),
+                 "acc": (out.acc[l], (n,))} for l in range(out.num_levels)]
+
+    def render_rays(self, rays: dict, randomized=False, chunk=None, device=None) -> list[dict]:
+        """Render host rays (synth/record dict of numpy arrays) in chunks of max_rays; numpy results
+        per level: comp_rgb [N, 3], distance [N], acc [N]."""
+        import torch
+
+        dev = device or torch.device("cuda", self.config.device)
+        N = rays["o"].shape[0]
+        chunk = min(chunk or self.config.max_rays, self.config.max_rays)
+        keys = ("o", "d", "radius", "near", "far")
+        outs = None
+        for b in range(0, N, chunk):
+            e = min(N, b + chunk)
+            t = {k: torch.from_numpy(np.ascontiguousarray(rays[k][b:e], dtype=np.float32)).to(dev) for k in keys}
+            lv = self.render_device(e - b, t["o"], t["d"], t["radius"], t["near"], t["far"], randomized)
+            torch.cuda.synchronize(dev)
+            res = [{k: to_numpy(p, shp) for k, (p, shp) in L_.items()} for L_ in lv]
+            if outs is None:
+                outs = [{k: [] for k in r} for r in res]
+            for o, r in zip(outs, res):
+                for k, v in r.items():
+                    o[k].append(v)
+        return [{k: np.concatenate(v) for k, v in o.items()} for o in outs]
+
     def enable_timing(self, on: bool = True):
         call("nof_mipnerf_enable_timing", self._h, int(on))
 
@@ -290,6 +323,25 @@ class OutputRetriever:
         out = np.empty((size, 3), np.float32)
         call("nof_retrieve_output", C.c_uint64(dev_output), size, out.ctypes.data)
         return out
+
+
+def image_metrics(img0, img1, max_val=1.0, stream=None) -> tuple[float, float]:
+    """(PSNR, SSIM) of two [H, W, 3] images on the GPU (MipHelpers.cs:672, 685-736).  Accepts
+    device tensors, or numpy arrays (copied to the current device)."""
+    import torch
+
+    def dev(x):
+        if isinstance(x, np.ndarray):
+            return torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).cuda()
+        return x.contiguous()
+
+    a, b = dev(img0), dev(img1)
+    H, W = int(a.shape[0]), int(a.shape[1])
+    assert tuple(a.shape) == (H, W, 3) and tuple(b.shape) == (H, W, 3), "images must be [H, W, 3]"
+    psnr, ssim = C.c_float(), C.c_float()
+    call("nof_image_metrics", a.data_ptr(), b.data_ptr(), W, H, float(max_val), C.byref(psnr), C.byref(ssim),
+         stream)
+    return psnr.value, ssim.value
 
 
 def learning_rate_decay(step, lr_init=5e-4, lr_final=5e-6, max_steps=1000000, lr_delay_steps=2500,

@@ -141,6 +141,36 @@ nof_status nof_mipnerf_render_device(nof_mipnerf* h, int32_t n, const float* dev
                                      const float* dev_radii, const float* dev_nears, const float* dev_fars,
                                      int32_t randomized, int32_t white_bkgd, nof_render_out* out);
 
+/* ---- ray-batch ingestion ---------------------------------------------------
+ * Replaces BinDataset (BinDataset.cs:10-53): 64-byte little-endian records {origin[3], direction[3],
+ * viewdir[3], radius, near, far, lossmult, rgb[3]} (BinDataset.cs:40-49) held in HBM; a batch is a
+ * device gather of records drawn with replacement (BinDataset.cs:34: _rng.Next(numSamples)) by a
+ * Philox counter of (seed, step, global ray id), so shards of one batch draw what the whole batch
+ * would.  Batch buffers are device SoA owned by the dataset, valid until its next call. */
+typedef struct nof_dataset nof_dataset;
+typedef struct nof_batch {
+  int32_t n;
+  float *origins, *directions, *viewdirs; /* [n][3] */
+  float *radii, *nears, *fars, *loss_mults; /* [n] */
+  float* pixels;                          /* [n][3] */
+  int32_t* record_index;                  /* [n] record drawn for each ray */
+} nof_batch;
+nof_status nof_dataset_open(const char* path, int32_t device, nof_dataset** out);
+nof_status nof_dataset_from_host(const float* records /* count x 16 */, int64_t count, int32_t device,
+                                 nof_dataset** out);
+nof_status nof_dataset_count(nof_dataset* ds, int64_t* count);
+/* loss_mult_sum != NULL: also returns the batch's loss-multiplier sum (synchronises the stream) */
+nof_status nof_dataset_next(nof_dataset* ds, int32_t n, uint64_t seed, uint32_t step, uint32_t ray_base,
+                            void* stream, nof_batch* out, float* loss_mult_sum);
+nof_status nof_dataset_destroy(nof_dataset* ds);
+
+/* ---- training state ----------------------------------------------------------
+ * Config.SaveEvery (TrainState.cs:59) is declared but never implemented by the reference.  A
+ * checkpoint holds the parameters, Adam's moments and step, and the Philox state, so a resumed run
+ * continues bit-identically.  Files are checksummed and written atomically (tmp + rename). */
+nof_status nof_checkpoint_save(const char* path, nof_mipnerf* h, nof_adam* adam);
+nof_status nof_checkpoint_load(const char* path, nof_mipnerf* h, nof_adam* adam);
+
 /* Image metrics on device images [H][W][3] (float, any range; max_val as MathHelpers' maxVal):
  * psnr = MseToPsnr(mean squared error) (MipHelpers.cs:672); ssim = ComputeSsimAverage with the
  * reference defaults (11x11 Gaussian, sigma 1.5, k1 0.01, k2 0.03, zero-padded 'same' convolution,

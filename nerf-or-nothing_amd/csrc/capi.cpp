@@ -9,6 +9,7 @@
 
 #include "../../include/nof.h"
 #include "host/accelerated.h"
+#include "host/trainer.h"
 #include "kernels/launch.h"
 
 using namespace AcceleratedNeRFUtils;
@@ -16,6 +17,7 @@ using namespace AcceleratedNeRFUtils;
 struct nof_mipnerf { AcceleratedMipNeRF* impl; };
 struct nof_mlp { AcceleratedMLP* impl; };
 struct nof_adam { AcceleratedAdamOptimizer* impl; };
+struct nof_dataset { RayDataset* impl; };
 struct nof_gradcalc { AcceleratedGradientCalculator* impl; };
 
 static thread_local std::string g_err;
@@ -136,6 +138,45 @@ nof_status nof_mipnerf_render_device(nof_mipnerf* h, int32_t n, const float* o, 
     *out = nof_render_out{};
     h->impl->Render(n, o, d, radii, nears, fars, randomized, white_bkgd, out);
   });
+}
+nof_status nof_dataset_open(const char* path, int32_t device, nof_dataset** out) {
+  return guard([&] {
+    ARG(path && out);
+    auto* d = new nof_dataset{nullptr};
+    try { d->impl = new RayDataset(std::string(path), device); } catch (...) { delete d; throw; }
+    *out = d;
+  });
+}
+nof_status nof_dataset_from_host(const float* records, int64_t count, int32_t device, nof_dataset** out) {
+  return guard([&] {
+    ARG(records && out);
+    auto* d = new nof_dataset{nullptr};
+    try { d->impl = new RayDataset(records, count, device); } catch (...) { delete d; throw; }
+    *out = d;
+  });
+}
+nof_status nof_dataset_count(nof_dataset* ds, int64_t* count) {
+  return guard([&] { ARG(ds && count); *count = ds->impl->count(); });
+}
+nof_status nof_dataset_next(nof_dataset* ds, int32_t n, uint64_t seed, uint32_t step, uint32_t ray_base, void* stream,
+                            nof_batch* out, float* loss_mult_sum) {
+  return guard([&] {
+    ARG(ds && out);
+    ds->impl->next(n, seed, step, ray_base, (hipStream_t)stream, out, loss_mult_sum);
+  });
+}
+nof_status nof_dataset_destroy(nof_dataset* ds) {
+  return guard([&] {
+    if (!ds) return;
+    delete ds->impl;
+    delete ds;
+  });
+}
+nof_status nof_checkpoint_save(const char* path, nof_mipnerf* h, nof_adam* adam) {
+  return guard([&] { ARG(path && h && adam); save_checkpoint(path, *h->impl, *adam->impl); });
+}
+nof_status nof_checkpoint_load(const char* path, nof_mipnerf* h, nof_adam* adam) {
+  return guard([&] { ARG(path && h && adam); load_checkpoint(path, *h->impl, *adam->impl); });
 }
 nof_status nof_image_metrics(const float* img0, const float* img1, int32_t width, int32_t height, float max_val,
                              float* psnr, float* ssim, void* stream) {

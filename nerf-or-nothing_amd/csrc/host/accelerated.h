@@ -187,6 +187,11 @@ class AcceleratedMipNeRF {
   nof_config cfg_;
   hipStream_t st_;
   uint64_t seed_;
+
+ public:
+  const nof_config& config() const { return cfg_; }
+
+ private:
   uint32_t step_ = 0, ray_base_ = 0;
   int last_n_ = 0;
   bool last_fused_ = false;
@@ -202,6 +207,12 @@ class AcceleratedAdamOptimizer {
   AcceleratedAdamOptimizer(const std::vector<int>& layer_sizes, const nof_config& cfg);
   void step(float* const* params, float* const* grads, float learning_rate);
   int iteration() const { return iteration_; }
+  // checkpoint access (trainer.cpp): first moments, second moments, step counter
+  float* m() const { return m_.p; }
+  float* v() const { return v_.p; }
+  int64_t size() const { return total_; }
+  void set_iteration(int it) { iteration_ = it; }
+  hipStream_t stream() const { return st_; }
 
  private:
   std::vector<int> sizes_;

@@ -1,0 +1,154 @@
+#include "trainer.h"
+
+#include <cstdio>
+#include <cstring>
+#include <memory>
+
+namespace AcceleratedNeRFUtils {
+
+// ---- RayDataset -----------------------------------------------------------------------------------
+RayDataset::RayDataset(const float* host_records, int64_t count, int device) : device_(device), count_(count) {
+  NOF_REQUIRE(host_records && count > 0 && count <= 0xFFFFFFFFll, "record count out of range");
+  NOF_HIP(hipSetDevice(device));
+  rec_.alloc((size_t)count * 16);
+  NOF_HIP(hipMemcpy(rec_.p, host_records, (size_t)count * 64, hipMemcpyHostToDevice));
+}
+
+RayDataset::RayDataset(const std::string& path, int device) : device_(device) {
+  std::unique_ptr<FILE, int (*)(FILE*)> f(std::fopen(path.c_str(), "rb"), &std::fclose);
+  NOF_REQUIRE(f != nullptr, "cannot open record file " + path);
+  std::fseek(f.get(), 0, SEEK_END);
+  const long long bytes = std::ftell(f.get());
+  std::fseek(f.get(), 0, SEEK_SET);
+  NOF_REQUIRE(bytes > 0 && bytes % 64 == 0, "record file size must be a positive multiple of 64 bytes");
+  count_ = bytes / 64;  // BinDataset.cs:15
+  NOF_REQUIRE(count_ <= 0xFFFFFFFFll, "too many records");
+  NOF_HIP(hipSetDevice(device));
+  rec_.alloc((size_t)count_ * 16);
+  // stream through a pinned staging buffer (64 MB chunks): never the whole file in host memory
+  const size_t chunk = 64u << 20;
+  void* stage = nullptr;
+  NOF_HIP(hipHostMalloc(&stage, chunk, hipHostMallocDefault));
+  std::unique_ptr<void, hipError_t (*)(void*)> guard(stage, &hipHostFree);
+  size_t done = 0;
+  while (done < (size_t)bytes) {
+    const size_t want = std::min(chunk, (size_t)bytes - done);
+    const size_t got = std::fread(stage, 1, want, f.get());
+    NOF_REQUIRE(got == want, "short read from record file");
+    NOF_HIP(hipMemcpy(reinterpret_cast<char*>(rec_.p) + done, stage, want, hipMemcpyHostToDevice));
+    done += want;
+  }
+}
+
+void RayDataset::reserve(int n, hipStream_t st) {
+  if (n <= cap_) return;
+  NOF_HIP(hipStreamSynchronize(st));  // the previous batch may still be read
+  o_.alloc(3 * (size_t)n); d_.alloc(3 * (size_t)n); vd_.alloc(3 * (size_t)n); r_.alloc(n); nr_.alloc(n);
+  fr_.alloc(n); lm_.alloc(n); pix_.alloc(3 * (size_t)n); idx_.alloc(n); msum_.alloc(1);
+  cap_ = n;
+}
+
+void RayDataset::next(int n, uint64_t seed, uint32_t step, uint32_t ray_base, hipStream_t st, nof_batch* out,
+                      float* host_msum) {
+  NOF_REQUIRE(n > 0 && out, "bad batch request");
+  NOF_HIP(hipSetDevice(device_));
+  reserve(n, st);
+  NOF_HIP(nof::launch_gather_batch(rec_.p, count_, n, seed, step, ray_base, o_.p, d_.p, vd_.p, r_.p, nr_.p, fr_.p,
+                                   lm_.p, pix_.p, idx_.p, host_msum ? msum_.p : nullptr, st));
+  out->n = n;
+  out->origins = o_.p; out->directions = d_.p; out->viewdirs = vd_.p; out->radii = r_.p;
+  out->nears = nr_.p; out->fars = fr_.p; out->loss_mults = lm_.p; out->pixels = pix_.p; out->record_index = idx_.p;
+  if (host_msum) {
+    NOF_HIP(hipMemcpyAsync(host_msum, msum_.p, sizeof(float), hipMemcpyDeviceToHost, st));
+    NOF_HIP(hipStreamSynchronize(st));
+  }
+}
+
+// ---- checkpoints ----------------------------------------------------------------------------------
+// little-endian file: header, then params[P], adam m[P], adam v[P] (fp32), then a 64-bit checksum of
+// all preceding bytes (sum of 32-bit words), so a truncated or corrupted file is rejected.
+namespace {
+constexpr char kMagic[8] = {'N', 'O', 'F', 'C', 'K', 'P', 'T', '1'};
+struct CkptHeader {
+  char magic[8];
+  int32_t version, precision, num_levels, num_tensors;
+  int64_t num_params;
+  int32_t adam_iteration, pad0;
+  uint64_t rng_seed;
+  uint32_t rng_step, rng_ray_base;
+  int32_t num_samples[NOF_MAX_LEVELS];
+  int32_t layer_sizes[32];
+};
+
+uint64_t word_sum(const void* p, size_t bytes, uint64_t acc) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+  for (size_t i = 0; i < bytes / 4; ++i) acc += w[i];
+  return acc;
+}
+}  // namespace
+
+void save_checkpoint(const std::string& path, AcceleratedMipNeRF& model, AcceleratedAdamOptimizer& adam) {
+  AcceleratedMLP& mlp = *model.mlp;
+  const int64_t P = mlp.num_params();
+  NOF_REQUIRE(adam.size() == P, "optimizer does not match the model's parameter count");
+  CkptHeader h{};
+  std::memcpy(h.magic, kMagic, 8);
+  h.version = 1;
+  const nof_config& c = model.config();
+  h.precision = c.precision;
+  h.num_levels = c.num_levels;
+  for (int l = 0; l < NOF_MAX_LEVELS; ++l) h.num_samples[l] = c.num_samples[l];
+  const std::vector<int> sizes = model.GetLayerSizes();
+  NOF_REQUIRE(sizes.size() <= 32, "too many tensors");
+  h.num_tensors = (int32_t)sizes.size();
+  for (size_t i = 0; i < sizes.size(); ++i) h.layer_sizes[i] = sizes[i];
+  h.num_params = P;
+  h.adam_iteration = adam.iteration();
+  model.get_rng(&h.rng_seed, &h.rng_step, &h.rng_ray_base);
+  std::vector<float> buf(3 * (size_t)P);
+  NOF_HIP(hipStreamSynchronize(mlp.stream()));
+  NOF_HIP(hipStreamSynchronize(adam.stream()));
+  NOF_HIP(hipMemcpy(buf.data(), mlp.flat_params(), P * sizeof(float), hipMemcpyDeviceToHost));
+  NOF_HIP(hipMemcpy(buf.data() + P, adam.m(), P * sizeof(float), hipMemcpyDeviceToHost));
+  NOF_HIP(hipMemcpy(buf.data() + 2 * P, adam.v(), P * sizeof(float), hipMemcpyDeviceToHost));
+  const uint64_t sum = word_sum(buf.data(), buf.size() * 4, word_sum(&h, sizeof(h), 0));
+  const std::string tmp = path + ".tmp";  // write then rename: a crash never leaves a torn checkpoint
+  {
+    std::unique_ptr<FILE, int (*)(FILE*)> f(std::fopen(tmp.c_str(), "wb"), &std::fclose);
+    NOF_REQUIRE(f != nullptr, "cannot create " + tmp);
+    NOF_REQUIRE(std::fwrite(&h, sizeof(h), 1, f.get()) == 1 &&
+                    std::fwrite(buf.data(), 4, buf.size(), f.get()) == buf.size() &&
+                    std::fwrite(&sum, sizeof(sum), 1, f.get()) == 1,
+                "short write to " + tmp);
+  }
+  NOF_REQUIRE(std::rename(tmp.c_str(), path.c_str()) == 0, "cannot rename " + tmp);
+}
+
+void load_checkpoint(const std::string& path, AcceleratedMipNeRF& model, AcceleratedAdamOptimizer& adam) {
+  std::unique_ptr<FILE, int (*)(FILE*)> f(std::fopen(path.c_str(), "rb"), &std::fclose);
+  NOF_REQUIRE(f != nullptr, "cannot open " + path);
+  CkptHeader h;
+  NOF_REQUIRE(std::fread(&h, sizeof(h), 1, f.get()) == 1 && std::memcmp(h.magic, kMagic, 8) == 0 && h.version == 1,
+              "not a nerf-or-nothing_amd checkpoint: " + path);
+  AcceleratedMLP& mlp = *model.mlp;
+  const int64_t P = mlp.num_params();
+  const std::vector<int> sizes = model.GetLayerSizes();
+  bool same = h.num_params == P && adam.size() == P && h.num_tensors == (int)sizes.size();
+  for (size_t i = 0; same && i < sizes.size(); ++i) same = h.layer_sizes[i] == sizes[i];
+  NOF_REQUIRE(same, "checkpoint parameter layout does not match the model");
+  std::vector<float> buf(3 * (size_t)P);
+  uint64_t sum = 0;
+  NOF_REQUIRE(std::fread(buf.data(), 4, buf.size(), f.get()) == buf.size() &&
+                  std::fread(&sum, sizeof(sum), 1, f.get()) == 1,
+              "truncated checkpoint " + path);
+  NOF_REQUIRE(sum == word_sum(buf.data(), buf.size() * 4, word_sum(&h, sizeof(h), 0)),
+              "checkpoint checksum mismatch " + path);
+  NOF_HIP(hipStreamSynchronize(mlp.stream()));
+  NOF_HIP(hipMemcpy(mlp.flat_params(), buf.data(), P * sizeof(float), hipMemcpyHostToDevice));
+  NOF_HIP(hipMemcpy(adam.m(), buf.data() + P, P * sizeof(float), hipMemcpyHostToDevice));
+  NOF_HIP(hipMemcpy(adam.v(), buf.data() + 2 * P, P * sizeof(float), hipMemcpyHostToDevice));
+  adam.set_iteration(h.adam_iteration);
+  model.set_rng(h.rng_seed, h.rng_step, h.rng_ray_base);
+}
+
+}  // namespace AcceleratedNeRFUtils

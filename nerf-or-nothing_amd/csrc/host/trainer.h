@@ -1,0 +1,34 @@
+// Data path and training-state persistence around the hot path:
+//   * RayDataset — BinDataset (BinDataset.cs:10-53) made device-resident: the 64-byte records live
+//     in HBM and a batch is one gather launch (dataset.hip) instead of 1024 file seeks per step;
+//   * checkpoints — Config.SaveEvery (TrainState.cs:59) is declared but never implemented by the
+//     reference; here a step's full state (parameters, Adam moments and step, Philox state) is
+//     written and restored bit-exactly.
+#pragma once
+#include "accelerated.h"
+
+namespace AcceleratedNeRFUtils {
+
+class RayDataset {
+ public:
+  RayDataset(const float* host_records, int64_t count, int device);  // copy of count x 16 floats
+  explicit RayDataset(const std::string& path, int device);          // stream a record file into HBM
+  int64_t count() const { return count_; }
+  // Gather n records for (seed, step, first global ray id); device SoA views owned by the dataset
+  // (valid until the next call).  host_msum != null: also the loss-multiplier sum (synchronises st).
+  void next(int n, uint64_t seed, uint32_t step, uint32_t ray_base, hipStream_t st, nof_batch* out, float* host_msum);
+
+ private:
+  void reserve(int n, hipStream_t st);
+  int device_;
+  int64_t count_ = 0;
+  DevBuf<float> rec_;
+  int cap_ = 0;
+  DevBuf<float> o_, d_, vd_, r_, nr_, fr_, lm_, pix_, msum_;
+  DevBuf<int> idx_;
+};
+
+void save_checkpoint(const std::string& path, AcceleratedMipNeRF& model, AcceleratedAdamOptimizer& adam);
+void load_checkpoint(const std::string& path, AcceleratedMipNeRF& model, AcceleratedAdamOptimizer& adam);
+
+}  // namespace AcceleratedNeRFUtils

@@ -85,6 +85,11 @@ hipError_t launch_wgrad_reduce(const WgOut* outs, int nouts, int max_elems, cons
                                const float* bias_slabs, int accumulate, hipStream_t st);
 
 // ---- adam.hip ----------------------------------------------------------------------------------
+// ---- dataset.hip: device-resident record set -> SoA batch gather (+ optional loss-mult sum) ----
+hipError_t launch_gather_batch(const float* records, int64_t count, int n, uint64_t seed, uint32_t step,
+                               uint32_t ray_base, float* o, float* d, float* vd, float* radius, float* near,
+                               float* far, float* lm, float* pix, int* idx_out, float* lm_sum, hipStream_t st);
+
 // ---- metrics.hip: PSNR / SSIM of device images [H][W][3] (synchronises st) ----
 hipError_t image_metrics(const float* a, const float* b, int W, int H, float max_val, float* psnr, float* ssim,
                          hipStream_t st);

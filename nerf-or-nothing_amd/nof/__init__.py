@@ -11,6 +11,9 @@ from .api import (  # noqa: F401
     AcceleratedMipNeRF,
     AcceleratedMLP,
     OutputRetriever,
+    RayDataset,
+    load_checkpoint,
+    save_checkpoint,
     device_count,
     device_tensor,
     image_metrics,

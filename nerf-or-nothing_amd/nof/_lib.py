@@ -55,6 +55,11 @@ class nof_render_out(C.Structure):
                 ("distance", C.c_void_p * NOF_MAX_LEVELS), ("acc", C.c_void_p * NOF_MAX_LEVELS)]
 
 
+class nof_batch(C.Structure):
+    _fields_ = [("n", C.c_int32)] + [(k, C.c_void_p) for k in (
+        "origins", "directions", "viewdirs", "radii", "nears", "fars", "loss_mults", "pixels", "record_index")]
+
+
 OUTPUT_GRAD_FN = C.CFUNCTYPE(C.c_uint64, C.c_void_p, C.c_uint64, C.c_int32, C.c_float, C.c_uint64)
 
 P = C.c_void_p
@@ -81,6 +86,13 @@ SIGNATURES = {
     "nof_mipnerf_loss": [P, C.POINTER(F)],
     "nof_mipnerf_render_device": [P, I32, P, P, P, P, P, I32, I32, C.POINTER(nof_render_out)],
     "nof_image_metrics": [P, P, I32, I32, F, C.POINTER(F), C.POINTER(F), P],
+    "nof_dataset_open": [C.c_char_p, I32, C.POINTER(P)],
+    "nof_dataset_from_host": [P, C.c_int64, I32, C.POINTER(P)],
+    "nof_dataset_count": [P, C.POINTER(C.c_int64)],
+    "nof_dataset_next": [P, I32, U64, U32, U32, P, C.POINTER(nof_batch), C.POINTER(F)],
+    "nof_dataset_destroy": [P],
+    "nof_checkpoint_save": [C.c_char_p, P, P],
+    "nof_checkpoint_load": [C.c_char_p, P, P],
     "nof_mipnerf_enable_timing": [P, I32],
     "nof_mipnerf_read_timing": [P, C.POINTER(F), C.POINTER(I32), I32],
     "nof_mlp_get_output": [P, P, P, I32, I32, I32, C.POINTER(U64), C.POINTER(U64)],

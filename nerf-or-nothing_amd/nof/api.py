@@ -325,6 +325,58 @@ class OutputRetriever:
         return out
 
 
+class RayDataset:
+    """BinDataset (BinDataset.cs:10-53) resident in HBM: 64-byte records, batches gathered on the
+    device with Philox-drawn record indices (with replacement)."""
+
+    FIELDS = {"o": ("origins", 3), "d": ("directions", 3), "viewdir": ("viewdirs", 3), "radius": ("radii", 1),
+              "near": ("nears", 1), "far": ("fars", 1), "lossmult": ("loss_mults", 1), "pix": ("pixels", 3)}
+
+    def __init__(self, path=None, records=None, device: int = 0):
+        h = C.c_void_p()
+        if path is not None:
+            call("nof_dataset_open", str(path).encode(), device, C.byref(h))
+        else:
+            rec = np.ascontiguousarray(records, dtype=np.float32).reshape(-1, 16)
+            call("nof_dataset_from_host", rec.ctypes.data, rec.shape[0], device, C.byref(h))
+        self._h = h
+
+    def __len__(self):
+        n = C.c_int64()
+        call("nof_dataset_count", self._h, C.byref(n))
+        return n.value
+
+    def next(self, n: int, seed: int, step: int, ray_base: int = 0, stream=None, with_sum: bool = True):
+        """Device SoA batch {key: (ptr, shape)} (+ 'record_index') and the loss-mult sum (or None)."""
+        b = L.nof_batch()
+        msum = C.c_float()
+        call("nof_dataset_next", self._h, n, seed, step, ray_base, stream, C.byref(b),
+             C.byref(msum) if with_sum else None)
+        out = {k: (getattr(b, f), (n, w) if w > 1 else (n,)) for k, (f, w) in self.FIELDS.items()}
+        out["record_index"] = (b.record_index, (n,))
+        return out, (msum.value if with_sum else None)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().nof_dataset_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def save_checkpoint(path, model: "AcceleratedMipNeRF", adam: "AcceleratedAdamOptimizer"):
+    """Parameters, Adam moments/step and Philox state -> checksummed file (atomic rename)."""
+    call("nof_checkpoint_save", str(path).encode(), model._h, adam._h)
+
+
+def load_checkpoint(path, model: "AcceleratedMipNeRF", adam: "AcceleratedAdamOptimizer"):
+    call("nof_checkpoint_load", str(path).encode(), model._h, adam._h)
+
+
 def image_metrics(img0, img1, max_val=1.0, stream=None) -> tuple[float, float]:
     """(PSNR, SSIM) of two [H, W, 3] images on the GPU (MipHelpers.cs:672, 685-736).  Accepts
     device tensors, or numpy arrays (copied to the current device)."""

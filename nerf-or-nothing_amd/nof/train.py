@@ -1,0 +1,135 @@
+"""Training driver: Program.Train / TrainStep (Program.cs:21-62) on the device
+data path, with the checkpointing the reference declares (Config.SaveEvery, TrainState.cs:59) but
+never implements.
+
+    python -m nof.train --records train_data.bin --steps 1000 [--ckpt-dir ck --save-every 500 --resume]
+    python -m nof.train --synthetic 100000 --steps 200          (Lego-shaped synthetic records)
+
+One step = dataset batch (device gather) -> AcceleratedMipNeRF.get_gradient_device (fused loss
+gradient) -> [all-reduce of the gradient arena when torch.distributed is initialised] ->
+AcceleratedAdamOptimizer.step(lr = LearningRateDecay(step)).  Every `print_every` steps the fine
+level's loss is printed as Program.LossFn does (Program.cs:64).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import time
+
+import numpy as np
+
+from . import api
+from ._lib import default_config
+
+
+class Trainer:
+    def __init__(self, dataset: api.RayDataset, batch_size: int = 1024, seed: int = 0x5EED0000, device: int = 0,
+                 stream=None, print_every: int = 100, save_every: int = 0, ckpt_dir: str | None = None,
+                 lr_init=5e-4, lr_final=5e-6, max_steps=1000000, lr_delay_steps=2500, lr_delay_mult=0.01,
+                 **config):
+        import torch.distributed as dist
+
+        self.dist = dist if dist.is_available() and dist.is_initialized() else None
+        self.rank = self.dist.get_rank() if self.dist else 0
+        self.world = self.dist.get_world_size() if self.dist else 1
+        self.ds = dataset
+        self.n = batch_size
+        self.seed = seed
+        self.stream = stream
+        self.print_every, self.save_every, self.ckpt_dir = print_every, save_every, ckpt_dir
+        self.lr = dict(lr_init=lr_init, lr_final=lr_final, max_steps=max_steps, lr_delay_steps=lr_delay_steps,
+                       lr_delay_mult=lr_delay_mult)
+        self.cfg = default_config(device=device, max_rays=batch_size, seed=seed, stream=stream, **config)
+        self.model = api.AcceleratedMipNeRF(self.cfg)
+        self.adam = api.AcceleratedAdamOptimizer(self.model.GetLayerSizes(), self.cfg)
+        self.params = self.model.mlp.allParams
+        self.step_idx = 0  # completed steps (Program.cs counts from 1)
+        self.device = device
+        self._grad_view = None
+        self.last_loss = None
+
+    # --- checkpoints -----------------------------------------------------------------------------
+    def save(self, path):
+        api.save_checkpoint(path, self.model, self.adam)
+
+    def resume(self, path):
+        api.load_checkpoint(path, self.model, self.adam)
+        self.step_idx = self.adam.iteration
+
+    # --- one TrainStep (Program.cs:48-62) ---------------------------------------------------------
+    def step(self):
+        import torch
+
+        step = self.step_idx + 1
+        ray_base = self.rank * self.n  # global ray ids: shards draw what the whole batch would
+        b, msum = self.ds.next(self.n, self.seed, step, ray_base, self.stream)
+        if self.dist is not None:  # global loss-multiplier sum (D14 / SURVEY 8e)
+            t = torch.tensor([msum], dtype=torch.float64, device=f"cuda:{self.device}")
+            self.dist.all_reduce(t)
+            msum = float(t.item())
+        self.model.set_rng(self.seed, step, ray_base)
+        p = {k: v[0] for k, v in b.items()}
+        grads = self.model.get_gradient_device(self.n, p["o"], p["d"], p["radius"], p["near"], p["far"],
+                                               p["lossmult"], p["pix"], msum)
+        if self.dist is not None:
+            if self._grad_view is None:
+                gptr, P = self.model.mlp.flat_grads()
+                self._grad_view = api.device_tensor(gptr, (P,), device=torch.device("cuda", self.device))
+            self.dist.all_reduce(self._grad_view)
+        self.adam.step(self.params, grads, api.learning_rate_decay(step, **self.lr))
+        self.step_idx = step
+        if self.print_every and step % self.print_every == 0:
+            self.last_loss = self.fine_loss(b)
+            if self.rank == 0:
+                print(f"Step {step}/{self.lr['max_steps']}, Loss: {self.last_loss}", flush=True)
+        if self.save_every and self.ckpt_dir and step % self.save_every == 0 and self.rank == 0:
+            os.makedirs(self.ckpt_dir, exist_ok=True)
+            self.save(os.path.join(self.ckpt_dir, f"ckpt_{step:08d}.nof"))
+
+    def fine_loss(self, batch) -> float:
+        """Program.LossFn (Program.cs:64): sum m |C_fine - p|^2 / sum m over this rank's batch."""
+        L = self.cfg.num_levels
+        C = self.model.level_numpy(L - 1)["comp_rgb"]
+        pix = api.to_numpy(batch["pix"][0], (self.n, 3))
+        m = api.to_numpy(batch["lossmult"][0], (self.n,))
+        return float(np.sum(m * np.sum((C - pix) ** 2, axis=1)) / np.sum(m))
+
+    def train(self, steps: int):
+        for _ in range(steps):
+            self.step()
+        return self
+
+
+def main(argv=None):
+    from . import synth
+
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    src = ap.add_mutually_exclusive_group(required=True)
+    src.add_argument("--records", help="BinDataset file of 64-byte records")
+    src.add_argument("--synthetic", type=int, help="number of synthetic Lego-shaped records")
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--precision", choices=["f32", "split"], default="f32")
+    ap.add_argument("--print-every", type=int, default=100)
+    ap.add_argument("--save-every", type=int, default=0)
+    ap.add_argument("--ckpt-dir")
+    ap.add_argument("--resume", help="checkpoint to resume from")
+    a = ap.parse_args(argv)
+    ds = (api.RayDataset(a.records, device=a.device) if a.records else
+          api.RayDataset(records=synth.pack_records(synth.blender_rays(a.synthetic, seed=1)), device=a.device))
+    tr = Trainer(ds, batch_size=a.batch, device=a.device, print_every=a.print_every, save_every=a.save_every,
+                 ckpt_dir=a.ckpt_dir, precision=1 if a.precision == "split" else 0)
+    if a.resume:
+        tr.resume(a.resume)
+    t0 = time.perf_counter()
+    tr.train(a.steps)
+    import torch
+
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    print(f"{a.steps} steps in {dt:.3f} s: {a.steps * a.batch / dt:.1f} rays/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -164,6 +164,24 @@ nof_status nof_dataset_next(nof_dataset* ds, int32_t n, uint64_t seed, uint32_t 
                             void* stream, nof_batch* out, float* loss_mult_sum);
 nof_status nof_dataset_destroy(nof_dataset* ds);
 
+/* ---- device ray generation ---------------------------------------------------
+ * Dataset.GenerateRays (Dataset.cs:111-176): pinhole directions d = R ((x - w/2 + .5)/f,
+ * -(y - h/2 + .5)/f, -1) (unnormalised), origin = pose translation, viewdir = normalize(d),
+ * radius = |d(x,y) - d(x+1,y)| 2/sqrt(12) (0 in the last column, as the reference), lossmult 1;
+ * ndc != 0: the LLFF override (Dataset.cs:268-293): ConvertToNdc (near 1, :295-308) and the radius
+ * from the NDC origins of the x and y neighbours.  poses: host, V x 12 floats (rotation row-major,
+ * then translation).  images: device [V][H][W][3] or NULL (rgb = 0).  Output: BinDataset records
+ * (V*H*W x 16 floats, view-major then row-major pixels) on the device. */
+nof_status nof_generate_rays(const float* host_poses, int32_t num_views, int32_t width, int32_t height, float focal,
+                             float near_, float far_, int32_t ndc, const float* dev_images, float* dev_records,
+                             void* stream);
+/* The same, straight into a device-resident dataset (then nof_dataset_next). */
+nof_status nof_dataset_generate(const float* host_poses, int32_t num_views, int32_t width, int32_t height, float focal,
+                                float near_, float far_, int32_t ndc, const float* dev_images, int32_t device,
+                                nof_dataset** out);
+/* LLFFDataset.RecenterPoses (Dataset.cs:309-319) in place on host poses (V x 12). */
+nof_status nof_recenter_poses(float* host_poses, int32_t num_views);
+
 /* ---- training state ----------------------------------------------------------
  * Config.SaveEvery (TrainState.cs:59) is declared but never implemented by the reference.  A
  * checkpoint holds the parameters, Adam's moments and step, and the Philox state, so a resumed run

@@ -172,6 +172,22 @@ nof_status nof_dataset_destroy(nof_dataset* ds) {
     delete ds;
   });
 }
+nof_status nof_generate_rays(const float* poses, int32_t V, int32_t w, int32_t h, float focal, float near_, float far_,
+                             int32_t ndc, const float* dev_images, float* dev_records, void* stream) {
+  return guard([&] { generate_rays(poses, V, w, h, focal, near_, far_, ndc, dev_images, dev_records, (hipStream_t)stream); });
+}
+nof_status nof_dataset_generate(const float* poses, int32_t V, int32_t w, int32_t h, float focal, float near_,
+                                float far_, int32_t ndc, const float* dev_images, int32_t device, nof_dataset** out) {
+  return guard([&] {
+    ARG(poses && out);
+    auto* d = new nof_dataset{nullptr};
+    try { d->impl = new RayDataset(poses, V, w, h, focal, near_, far_, ndc, dev_images, device); } catch (...) { delete d; throw; }
+    *out = d;
+  });
+}
+nof_status nof_recenter_poses(float* poses, int32_t V) {
+  return guard([&] { recenter_poses(poses, V); });
+}
 nof_status nof_checkpoint_save(const char* path, nof_mipnerf* h, nof_adam* adam) {
   return guard([&] { ARG(path && h && adam); save_checkpoint(path, *h->impl, *adam->impl); });
 }

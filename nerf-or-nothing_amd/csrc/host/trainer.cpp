@@ -40,6 +40,59 @@ RayDataset::RayDataset(const std::string& path, int device) : device_(device) {
   }
 }
 
+RayDataset::RayDataset(const float* host_poses, int V, int w, int h, float focal, float near, float far, int ndc,
+                       const float* dev_images, int device)
+    : device_(device) {
+  NOF_REQUIRE(V > 0 && w > 1 && h > 1, "bad image set");
+  count_ = (int64_t)V * w * h;
+  NOF_REQUIRE(count_ <= 0xFFFFFFFFll, "too many rays");
+  NOF_HIP(hipSetDevice(device));
+  rec_.alloc((size_t)count_ * 16);
+  generate_rays(host_poses, V, w, h, focal, near, far, ndc, dev_images, rec_.p, nullptr);
+  NOF_HIP(hipStreamSynchronize(nullptr));
+}
+
+void generate_rays(const float* host_poses, int V, int w, int h, float focal, float near, float far, int ndc,
+                   const float* dev_images, float* dev_records, hipStream_t st) {
+  NOF_REQUIRE(host_poses && dev_records && V > 0 && w > 1 && h > 1 && focal > 0.0f, "bad ray-generation arguments");
+  DevBuf<float> poses;
+  poses.alloc((size_t)V * 12);
+  NOF_HIP(hipMemcpyAsync(poses.p, host_poses, (size_t)V * 12 * sizeof(float), hipMemcpyHostToDevice, st));
+  NOF_HIP(nof::launch_generate_rays(poses.p, V, w, h, focal, near, far, ndc, dev_images, dev_records, st));
+  NOF_HIP(hipStreamSynchronize(st));  // the pose buffer is released on return
+}
+
+void recenter_poses(float* P, int V) {
+  NOF_REQUIRE(P && V > 0, "bad poses");
+  // average = (sum R / V, sum t / V) with Aggregate's left fold (Dataset.cs:311-312)
+  float R[9], t[3];
+  for (int k = 0; k < 9; ++k) R[k] = P[k];
+  for (int k = 0; k < 3; ++k) t[k] = P[9 + k];
+  for (int i = 1; i < V; ++i) {
+    for (int k = 0; k < 9; ++k) R[k] = R[k] + P[12 * i + k];
+    for (int k = 0; k < 3; ++k) t[k] = t[k] + P[12 * i + 9 + k];
+  }
+  for (int k = 0; k < 9; ++k) R[k] = R[k] / (float)V;
+  for (int k = 0; k < 3; ++k) t[k] = t[k] / (float)V;
+  // averageInverse = (R^T, -R^T * t)  (Dataset.cs:313)
+  float Ri[9];
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) Ri[3 * r + c] = R[3 * c + r];
+  float ti[3];
+  for (int r = 0; r < 3; ++r) ti[r] = (-Ri[3 * r] * t[0] + -Ri[3 * r + 1] * t[1]) + -Ri[3 * r + 2] * t[2];
+  for (int i = 0; i < V; ++i) {  // Dataset.cs:314-318
+    float* Rp = P + 12 * i;
+    float* tp = Rp + 9;
+    float u[3];
+    for (int r = 0; r < 3; ++r) u[r] = (Rp[3 * r] * ti[0] + Rp[3 * r + 1] * ti[1]) + Rp[3 * r + 2] * ti[2];
+    for (int r = 0; r < 3; ++r) tp[r] = tp[r] - u[r];
+    float M[9];
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) M[3 * r + c] = (Rp[3 * r] * Ri[c] + Rp[3 * r + 1] * Ri[3 + c]) + Rp[3 * r + 2] * Ri[6 + c];
+    for (int k = 0; k < 9; ++k) Rp[k] = M[k];
+  }
+}
+
 void RayDataset::reserve(int n, hipStream_t st) {
   if (n <= cap_) return;
   NOF_HIP(hipStreamSynchronize(st));  // the previous batch may still be read

@@ -13,6 +13,9 @@ class RayDataset {
  public:
   RayDataset(const float* host_records, int64_t count, int device);  // copy of count x 16 floats
   explicit RayDataset(const std::string& path, int device);          // stream a record file into HBM
+  // generate the records on the device from poses (V x 12 floats, host) and optional device images
+  RayDataset(const float* host_poses, int V, int w, int h, float focal, float near, float far, int ndc,
+             const float* dev_images, int device);
   int64_t count() const { return count_; }
   // Gather n records for (seed, step, first global ray id); device SoA views owned by the dataset
   // (valid until the next call).  host_msum != null: also the loss-multiplier sum (synchronises st).
@@ -27,6 +30,13 @@ class RayDataset {
   DevBuf<float> o_, d_, vd_, r_, nr_, fr_, lm_, pix_, msum_;
   DevBuf<int> idx_;
 };
+
+// Dataset.GenerateRays (+ the LLFF NDC override) on the device: poses (host, V x [R row-major | t]),
+// optional device images [V][H][W][3] -> device records (V*H*W x 16 floats).
+void generate_rays(const float* host_poses, int V, int w, int h, float focal, float near, float far, int ndc,
+                   const float* dev_images, float* dev_records, hipStream_t st);
+// LLFFDataset.RecenterPoses (Dataset.cs:309-319), in place on host poses (fp32, C# evaluation order).
+void recenter_poses(float* poses, int V);
 
 void save_checkpoint(const std::string& path, AcceleratedMipNeRF& model, AcceleratedAdamOptimizer& adam);
 void load_checkpoint(const std::string& path, AcceleratedMipNeRF& model, AcceleratedAdamOptimizer& adam);

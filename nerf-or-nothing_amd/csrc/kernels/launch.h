@@ -90,6 +90,10 @@ hipError_t launch_gather_batch(const float* records, int64_t count, int n, uint6
                                uint32_t ray_base, float* o, float* d, float* vd, float* radius, float* near,
                                float* far, float* lm, float* pix, int* idx_out, float* lm_sum, hipStream_t st);
 
+// ---- raygen.hip: poses (V x [R row-major | t]) (+ images [V][H][W][3]) -> 64-byte records ----
+hipError_t launch_generate_rays(const float* poses, int V, int w, int h, float focal, float near, float far, int ndc,
+                                const float* images, float* records, hipStream_t st);
+
 // ---- metrics.hip: PSNR / SSIM of device images [H][W][3] (synchronises st) ----
 hipError_t image_metrics(const float* a, const float* b, int W, int H, float max_val, float* psnr, float* ssim,
                          hipStream_t st);

@@ -13,9 +13,11 @@ from .api import (  # noqa: F401
     OutputRetriever,
     RayDataset,
     load_checkpoint,
+    recenter_poses,
     save_checkpoint,
     device_count,
     device_tensor,
+    generate_rays,
     image_metrics,
     learning_rate_decay,
     to_numpy,

@@ -91,6 +91,9 @@ SIGNATURES = {
     "nof_dataset_count": [P, C.POINTER(C.c_int64)],
     "nof_dataset_next": [P, I32, U64, U32, U32, P, C.POINTER(nof_batch), C.POINTER(F)],
     "nof_dataset_destroy": [P],
+    "nof_generate_rays": [P, I32, I32, I32, F, F, F, I32, P, P, P],
+    "nof_dataset_generate": [P, I32, I32, I32, F, F, F, I32, P, I32, C.POINTER(P)],
+    "nof_recenter_poses": [P, I32],
     "nof_checkpoint_save": [C.c_char_p, P, P],
     "nof_checkpoint_load": [C.c_char_p, P, P],
     "nof_mipnerf_enable_timing": [P, I32],

@@ -332,9 +332,18 @@ class RayDataset:
     FIELDS = {"o": ("origins", 3), "d": ("directions", 3), "viewdir": ("viewdirs", 3), "radius": ("radii", 1),
               "near": ("nears", 1), "far": ("fars", 1), "lossmult": ("loss_mults", 1), "pix": ("pixels", 3)}
 
-    def __init__(self, path=None, records=None, device: int = 0):
+    def __init__(self, path=None, records=None, device: int = 0, generate: dict | None = None):
+        """path: record file; records: host [N, 16] array; generate: dict(poses [V, 12], width, height,
+        focal, near, far, ndc=False, images=device tensor [V, H, W, 3] or None) -> rays made on the GPU."""
         h = C.c_void_p()
-        if path is not None:
+        if generate is not None:
+            g = dict(generate)
+            poses = np.ascontiguousarray(g["poses"], dtype=np.float32).reshape(-1, 12)
+            img = g.get("images")
+            call("nof_dataset_generate", poses.ctypes.data, poses.shape[0], int(g["width"]), int(g["height"]),
+                 float(g["focal"]), float(g["near"]), float(g["far"]), int(bool(g.get("ndc", False))),
+                 _ptr(img) if img is not None else None, device, C.byref(h))
+        elif path is not None:
             call("nof_dataset_open", str(path).encode(), device, C.byref(h))
         else:
             rec = np.ascontiguousarray(records, dtype=np.float32).reshape(-1, 16)
@@ -366,6 +375,26 @@ class RayDataset:
             self.close()
         except Exception:
             pass
+
+
+def generate_rays(poses, width, height, focal, near, far, ndc=False, images=None, out=None, stream=None):
+    """Dataset.GenerateRays on the GPU -> device records tensor [V*H*W, 16] (torch)."""
+    import torch
+
+    poses = np.ascontiguousarray(poses, dtype=np.float32).reshape(-1, 12)
+    n = poses.shape[0] * int(width) * int(height)
+    if out is None:
+        out = torch.empty((n, 16), dtype=torch.float32, device="cuda")
+    call("nof_generate_rays", poses.ctypes.data, poses.shape[0], int(width), int(height), float(focal), float(near),
+         float(far), int(bool(ndc)), _ptr(images) if images is not None else None, out.data_ptr(), stream)
+    return out
+
+
+def recenter_poses(poses) -> np.ndarray:
+    """LLFFDataset.RecenterPoses (Dataset.cs:309-319) on host poses [V, 12] (returns a copy)."""
+    p = np.array(poses, dtype=np.float32).reshape(-1, 12).copy()
+    call("nof_recenter_poses", p.ctypes.data, p.shape[0])
+    return p
 
 
 def save_checkpoint(path, model: "AcceleratedMipNeRF", adam: "AcceleratedAdamOptimizer"):

@@ -170,25 +170,41 @@ __global__ __launch_bounds__(kWgThreads, 1) void k_wgrad(const WgProblem* __rest
 }
 
 // ---- split mode (mlp_common.h): bf16x3 operands, six bf16 MFMAs per 32x32x16 product -----------
-// Per 16-sample k-step (the 64-B half of every feature row of a chunk-swizzled block, common.h):
-//   * every thread loads 16-B chunks straight into registers, three k-steps ahead, with each
-//     wave-instruction covering 16 feature rows x 64 contiguous bytes;
-//   * it splits each chunk ONCE into (hi, mid, lo) and writes the three 8-B pieces to the k-step's
+// Same 2 x 4 wave grid as fp32 (8 waves, two per SIMD, up to 4 x 2 output tiles each).  Per
+// 16-sample k-step (the 64-B half of every feature row of a chunk-swizzled block, common.h):
+//   * every thread loads two 16-B chunks of A and two of B straight into registers, two k-steps
+//     ahead, each wave-instruction covering 16 feature rows x 64 contiguous bytes.  The loads are
+//     unconditional (rows past the problem re-read its last row), the k loop is unrolled by two
+//     so the two register sets are never copied, and the k-step barrier is a bare s_barrier after
+//     lgkmcnt(0) (__syncthreads' release fence would wait vmcnt(0)): the compiler then waits with
+//     counted vmcnt and two k-steps of loads stay in flight across barriers;
+//   * each chunk is split ONCE into (hi, mid, lo) and its three 8-B pieces written to the k-step's
 //     fragment images in LDS (double-buffered, 2 x 48 KB), so no split is repeated by the waves
-//     that share a tile;
-//   * the MFMA waves (same 2 x 4 grid as fp32) read each fragment piece as one conflict-free
-//     ds_read_b128 and issue 6 * RB * CB MFMAs.
-// One barrier per k-step; the split of k-step k + 1 and the MFMAs of k-step k interleave.
+//     sharing a tile;
+//   * the MFMA waves read each fragment piece as one conflict-free ds_read_b128 and issue
+//     6 * RB * CB MFMAs.
+// The split of k-step k + 1 and the MFMAs of k-step k interleave.
+constexpr int kWgX3Threads = kWgThreads;
 constexpr int kX3Frag = 3 * 8 * 64 * 4;  // floats per operand fragment image: [piece][tile][lane][16 B]
 constexpr int kX3Lds = 2 * 2 * kX3Frag;   // 96 KB
 
 struct X3Raw {
-  f32x4 a[2], b[2];  // chunk i of this thread: row (tid >> 2) + 128 i, logical chunk tid & 3 of the k-step
+  f32x4 a0, a1, b0, b1;  // chunk i: row (tid >> 2) + 128 i, logical chunk tid & 3 of the k-step
 };
+
+// LDS writes of this wave done, then a bare workgroup barrier; the "memory" clobber keeps the
+// compiler from moving LDS accesses across it.  Global loads in flight are NOT waited for.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 template <int RB, int CB>
 __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& P, float* lds, int tid, int lane,
                                            int wave, float* slabs, float* bias_slabs, const int64_t* slab_off) {
+  // opaque thread index: the lane-derived offsets of the five instantiations are recomputed per
+  // item instead of being hoisted to the kernel entry all at once (they would spill)
+  int tq = tid;
+  asm volatile("" : "+v"(tq));
+  tid = tq;
+  lane = tq & 63;
   const int h = lane >> 5, x = lane & 31;
   const int wr = wave >> 2, wc = wave & 3;
   const int r0 = wr * RB, c0 = wc * CB;
@@ -200,23 +216,28 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
   for (int c = 0; c < CB; ++c) colt[c] = min(c0 + c, P.ntc - 1);
   const size_t strideA = (size_t)P.FA * kBlk, strideB = (size_t)P.FB * kBlk;
   const int nrA = P.ntr * 32, nrB = P.ntc * 32;
-  // loader role: chunk lc = tid & 3 (samples 4 lc .. 4 lc + 3 of the k-step) of rows (tid >> 2) + 128 i
-  const int lc = tid & 3, lrow = tid >> 2;
+  const int lc = tid & 3, lrow = tid >> 2;  // loader role: rows lrow, lrow + 128; chunk lc
   const float* baseA = P.A + (size_t)item.kb0 * strideA + (size_t)P.a_row0 * kBlk;
   const float* baseB = P.B + (size_t)item.kb0 * strideB + (size_t)P.b_col0 * kBlk;
+  const int ra0 = min(lrow, nrA - 1), ra1 = min(lrow + 128, nrA - 1);
+  const int rb0 = min(lrow, nrB - 1), rb1 = min(lrow + 128, nrB - 1);
   const int K = 2 * (item.kb1 - item.kb0);
 
-  auto load = [&](int k, X3Raw& q) {
-    const size_t kb = (size_t)(k >> 1);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = lrow + 128 * i;
-      const int phys = (4 * (k & 1) + lc) ^ (row & 7);
-      if (row < nrA) q.a[i] = *reinterpret_cast<const f32x4*>(baseA + kb * strideA + (size_t)row * kBlk + phys * 4);
-      if (row < nrB) q.b[i] = *reinterpret_cast<const f32x4*>(baseB + kb * strideB + (size_t)row * kBlk + phys * 4);
-    }
+  // global (not flat) loads: the operand pointers come from the problem table, so without the
+  // address-space cast hipcc emits flat_load, which also counts in lgkmcnt and would be drained by
+  // every LDS wait
+  auto ld = [&](const float* base, size_t stride, int k, int row) {
+    const int c = 4 * (k & 1) + lc;
+    typedef const __attribute__((address_space(1))) f32x4* gf4;
+    return *(gf4)(base + (size_t)(k >> 1) * stride + (size_t)row * kBlk + ((c ^ (row & 7)) << 2));
   };
-  float bsum[2] = {0.0f, 0.0f};  // partial row sums of delta (rows lrow, lrow + 128; this chunk's samples)
+  auto load = [&](int k, X3Raw& q) {
+    q.a0 = ld(baseA, strideA, k, ra0);
+    q.a1 = ld(baseA, strideA, k, ra1);
+    q.b0 = ld(baseB, strideB, k, rb0);
+    q.b1 = ld(baseB, strideB, k, rb1);
+  };
+  float bs0 = 0.0f, bs1 = 0.0f;  // partial row sums of delta (rows lrow, lrow + 128)
   // chunk lc of row (t, xr) = samples 4 lc .. 4 lc + 3 = elements 4 (lc & 1) .. +3 of fragment lane
   // (h = lc >> 1, xr): one 8-B piece per (piece, row)
   auto put = [&](float* img, int row, const f32x4& v) {
@@ -232,15 +253,16 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
   };
   auto split = [&](const X3Raw& q, int buf) {
     float* img = lds + buf * 2 * kX3Frag;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = lrow + 128 * i;
-      if (row < nrA) {
-        put(img, row, q.a[i]);
-        bsum[i] += (q.a[i][0] + q.a[i][1]) + (q.a[i][2] + q.a[i][3]);
-      }
-      if (row < nrB) put(img + kX3Frag, row, q.b[i]);
+    if (lrow < nrA) {
+      put(img, lrow, q.a0);
+      bs0 += (q.a0[0] + q.a0[1]) + (q.a0[2] + q.a0[3]);
     }
+    if (lrow + 128 < nrA) {
+      put(img, lrow + 128, q.a1);
+      bs1 += (q.a1[0] + q.a1[1]) + (q.a1[2] + q.a1[3]);
+    }
+    if (lrow < nrB) put(img + kX3Frag, lrow, q.b0);
+    if (lrow + 128 < nrB) put(img + kX3Frag, lrow + 128, q.b1);
   };
 
   f32x16 acc[RB][CB];
@@ -251,20 +273,7 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[r][c][e] = 0.0f;
 
-  X3Raw q0, q1, q2;
-  load(0, q0);
-  if (K > 1) load(1, q1);
-  if (K > 2) load(2, q2);
-  split(q0, 0);
-  __syncthreads();
-  for (int k = 0; k < K; ++k) {
-    X3Raw q3;
-    if (k + 3 < K) load(k + 3, q3);  // rows stay in flight for two k-steps
-#ifndef NOF_DIAG_X3_NOSPLIT
-    if (k + 1 < K) split(q1, (k + 1) & 1);
-#else
-    if (k + 1 < K && q1.a[0][0] == 12345.0f) split(q1, (k + 1) & 1);
-#endif
+  auto mfma_step = [&](int k) {
 #ifndef NOF_DIAG_X3_NOMFMA
     if (active) {
 #else
@@ -286,13 +295,38 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
         }
       }
     }
-    __syncthreads();
-    q1 = q2;
-    q2 = q3;
+  };
+  // k-step k: k + 1's registers are split into image (k + 1) & 1 and refilled with k + 3's rows,
+  // image k & 1 feeds the MFMAs.  Two register sets rotate statically (loop unrolled by two).
+  X3Raw qa, qb;
+  {
+    X3Raw q0;
+    load(0, q0);
+    load(min(1, K - 1), qa);
+    load(min(2, K - 1), qb);
+    split(q0, 0);
   }
+  lds_barrier();
+  auto step = [&](int k, X3Raw& next) {
+#ifndef NOF_DIAG_X3_NOSPLIT
+    if (k + 1 < K) split(next, (k + 1) & 1);
+#else
+    if (k + 1 < K && next.a0[0] == 12345.0f) split(next, (k + 1) & 1);
+#endif
+    load(min(k + 3, K - 1), next);  // unconditional (clamped): every path issues the same loads
+    mfma_step(k);
+    lds_barrier();
+  };
+  int k = 0;
+  for (; k + 2 <= K; k += 2) {
+    step(k, qa);
+    step(k + 1, qb);
+  }
+  if (k < K) step(k, qa);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the clamped tail loads
   if (active) {
     float* slab = slabs + slab_off[item.slab];
-    const int ld = P.ntc * 32;
+    const int ld_ = P.ntc * 32;
 #pragma unroll
     for (int r = 0; r < RB; ++r)
 #pragma unroll
@@ -301,26 +335,28 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const int row = rowt[r] * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-            slab[(size_t)row * ld + colt[c] * 32 + x] = acc[r][c][e];
+            slab[(size_t)row * ld_ + colt[c] * 32 + x] = acc[r][c][e];
           }
         }
       }
   }
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {  // the 4 chunk-lanes of a row are lanes 4 lrow .. 4 lrow + 3
-    float v = bsum[i];
-    v += __shfl_xor(v, 1, 64);
-    v += __shfl_xor(v, 2, 64);
-    const int row = lrow + 128 * i;
-    if (row < nrA && lc == 0) bias_slabs[(size_t)item.slab * 256 + row] = v;
+  {  // the 4 chunk-lanes of a row are lanes 4 lrow .. 4 lrow + 3
+    float v0 = bs0, v1 = bs1;
+    v0 += __shfl_xor(v0, 1, 64);
+    v0 += __shfl_xor(v0, 2, 64);
+    v1 += __shfl_xor(v1, 1, 64);
+    v1 += __shfl_xor(v1, 2, 64);
+    if (lrow < nrA && lc == 0) bias_slabs[(size_t)item.slab * 256 + lrow] = v0;
+    if (lrow + 128 < nrA && lc == 0) bias_slabs[(size_t)item.slab * 256 + lrow + 128] = v1;
   }
+  __syncthreads();  // images are reused by the next item
 }
 
-__global__ __launch_bounds__(kWgThreads, 1) void k_wgrad_x3(const WgProblem* __restrict__ probs,
-                                                            const WgItem* __restrict__ items,
-                                                            const int* __restrict__ item_ptr,
-                                                            const int64_t* __restrict__ slab_off, float* slabs,
-                                                            float* bias_slabs) {
+__global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_x3(const WgProblem* __restrict__ probs,
+                                                              const WgItem* __restrict__ items,
+                                                              const int* __restrict__ item_ptr,
+                                                              const int64_t* __restrict__ slab_off, float* slabs,
+                                                              float* bias_slabs) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int it0 = item_ptr[blockIdx.x], it1 = item_ptr[blockIdx.x + 1];
@@ -349,7 +385,7 @@ hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const in
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL(k_wgrad_x3, dim3(num_wg), dim3(kWgThreads), shm, st, probs, items, item_ptr, slab_off, slabs,
+  hipLaunchKernelGGL(k_wgrad_x3, dim3(num_wg), dim3(kWgX3Threads), shm, st, probs, items, item_ptr, slab_off, slabs,
                      bias_slabs);
   return hipGetLastError();
 }

@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--precision", choices=["f32", "split"], default="f32",
                    help="MLP contraction arithmetic: fp32 MFMA, or fp32 operands as bf16x3 split MFMAs")
     p.add_argument("--no-alt", action="store_true", help="skip the other precision mode's secondary measurement")
+    p.add_argument("--dp", choices=["torch", "native"], default="torch",
+                   help="N>1 gradient all-reduce: torch.distributed (RCCL) or the C ABI's nof_dp_* (RCCL)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-integrator", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work")
@@ -162,6 +164,14 @@ def main():
         pool.append({k: torch.from_numpy(v).to(dev) for k, v in r.items()})
     msum_global = float(n * world)  # lossmult = 1 everywhere: sum over all shards (D14, DP-global)
 
+    native = None
+    if world > 1 and a.dp == "native":  # C-ABI RCCL communicator; the id travels over torch.distributed
+        from nof.dp import NativeDP
+
+        obj = [NativeDP.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        native = NativeDP.init_rank(obj[0], world, rank, local)
+
     def measure(split):
         """W untimed + K timed training steps of one precision mode; returns (s, timing, psnr)."""
         model = nof.AcceleratedMipNeRF(device=local, max_rays=n, num_samples=samples, seed=seed,
@@ -176,7 +186,9 @@ def main():
             b = pool[k % len(pool)]
             grads = model.get_gradient_device(n, b["o"], b["d"], b["radius"], b["near"], b["far"],
                                               b["lossmult"], b["pix"], msum_global)
-            if world > 1:
+            if native is not None:
+                native.allreduce_grads(model, stream)
+            elif world > 1:
                 dist.all_reduce(grad_view)  # sum of per-shard gradient sums (no averaging: L is a sum)
             opt.step(params, grads, nof.learning_rate_decay(k + 1))
 
@@ -257,7 +269,8 @@ def main():
             "data": "synthetic (Lego-shaped 800x800, 100 poses)",
             "config": {"workload": "BASELINE configs[1]: 1024-ray batches x 128+128 samples, 8x256 MLP fwd/bwd + Adam",
                        "rays_per_gpu": n, "global_batch": n * world, "samples": samples,
-                       "parallelism": f"dp{world}", "precision": a.precision},
+                       "parallelism": f"dp{world}", "precision": a.precision,
+                       "allreduce": a.dp if world > 1 else None},
             **roof,
             "kernels": kernels,
             "psnr_fine": round(psnr, 3),

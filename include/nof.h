@@ -189,6 +189,25 @@ nof_status nof_recenter_poses(float* host_poses, int32_t num_views);
 nof_status nof_checkpoint_save(const char* path, nof_mipnerf* h, nof_adam* adam);
 nof_status nof_checkpoint_load(const char* path, nof_mipnerf* h, nof_adam* adam);
 
+/* ---- data parallelism over RCCL (SURVEY.md 8b "(new) DP", 8e) --------------------------------------
+ * Rays shard across GPUs (global ray ids via nof_mipnerf_set_rng; the global loss-mult sum passed
+ * to get_gradient_device); the only exchange is an in-place all-reduce (sum) of the flat gradient
+ * arena, after which every rank runs the same Adam step on identical bits.  For hosts without
+ * torch.distributed (the reference's C# driver):
+ *   one process per GPU: rank 0 calls nof_dp_unique_id and shares the 128 bytes (any channel);
+ *                        every rank calls nof_dp_init_rank;
+ *   one process, n GPUs: nof_dp_init_all fills n handles; nof_dp_allreduce_grads_all groups the
+ *                        n all-reduces. */
+typedef struct nof_dp nof_dp;
+nof_status nof_dp_unique_id(uint8_t id[128]);
+nof_status nof_dp_init_rank(const uint8_t id[128], int32_t world, int32_t rank, int32_t device, nof_dp** out);
+nof_status nof_dp_init_all(int32_t ndev, const int32_t* devices, nof_dp** out /* ndev handles */);
+nof_status nof_dp_allreduce(nof_dp* dp, float* dev_buf, int64_t count, void* stream);
+/* all-reduce of the model's gradient arena on its stream (or streams[i]) */
+nof_status nof_dp_allreduce_grads(nof_dp* dp, nof_mipnerf* h, void* stream);
+nof_status nof_dp_allreduce_grads_all(int32_t n, nof_dp* const* dps, nof_mipnerf* const* hs, void* const* streams);
+nof_status nof_dp_destroy(nof_dp* dp);
+
 /* Image metrics on device images [H][W][3] (float, any range; max_val as MathHelpers' maxVal):
  * psnr = MseToPsnr(mean squared error) (MipHelpers.cs:672); ssim = ComputeSsimAverage with the
  * reference defaults (11x11 Gaussian, sigma 1.5, k1 0.01, k2 0.03, zero-padded 'same' convolution,

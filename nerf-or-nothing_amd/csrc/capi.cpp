@@ -6,10 +6,12 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/nof.h"
 #include "host/accelerated.h"
 #include "host/trainer.h"
+#include "host/dp.h"
 #include "kernels/launch.h"
 
 using namespace AcceleratedNeRFUtils;
@@ -193,6 +195,42 @@ nof_status nof_checkpoint_save(const char* path, nof_mipnerf* h, nof_adam* adam)
 }
 nof_status nof_checkpoint_load(const char* path, nof_mipnerf* h, nof_adam* adam) {
   return guard([&] { ARG(path && h && adam); load_checkpoint(path, *h->impl, *adam->impl); });
+}
+nof_status nof_dp_unique_id(uint8_t id[128]) {
+  return guard([&] { ARG(id); dp_unique_id(id); });
+}
+nof_status nof_dp_init_rank(const uint8_t id[128], int32_t world, int32_t rank, int32_t device, nof_dp** out) {
+  return guard([&] { ARG(id && out); *out = dp_init_rank(id, world, rank, device); });
+}
+nof_status nof_dp_init_all(int32_t ndev, const int32_t* devices, nof_dp** out) {
+  return guard([&] { dp_init_all(ndev, devices, out); });
+}
+nof_status nof_dp_allreduce(nof_dp* dp, float* buf, int64_t count, void* stream) {
+  return guard([&] { dp_allreduce(dp, buf, count, (hipStream_t)stream); });
+}
+nof_status nof_dp_allreduce_grads(nof_dp* dp, nof_mipnerf* h, void* stream) {
+  return guard([&] {
+    ARG(dp && h);
+    AcceleratedMipNeRF* m = h->impl;
+    hipStream_t st = stream ? (hipStream_t)stream : m->mlp->stream();
+    dp_allreduce_grads(1, &dp, &m, &st);
+  });
+}
+nof_status nof_dp_allreduce_grads_all(int32_t n, nof_dp* const* dps, nof_mipnerf* const* hs, void* const* streams) {
+  return guard([&] {
+    ARG(n >= 1 && dps && hs);
+    std::vector<AcceleratedMipNeRF*> ms(n);
+    std::vector<hipStream_t> st(n);
+    for (int i = 0; i < n; ++i) {
+      ARG(hs[i]);
+      ms[i] = hs[i]->impl;
+      st[i] = streams && streams[i] ? (hipStream_t)streams[i] : ms[i]->mlp->stream();
+    }
+    dp_allreduce_grads(n, dps, ms.data(), st.data());
+  });
+}
+nof_status nof_dp_destroy(nof_dp* dp) {
+  return guard([&] { dp_destroy(dp); });
 }
 nof_status nof_image_metrics(const float* img0, const float* img1, int32_t width, int32_t height, float max_val,
                              float* psnr, float* ssim, void* stream) {

@@ -1,0 +1,12 @@
+// RCCL data parallelism behind the nof_dp_* entry points (dp.cpp).
+#pragma once
+#include "accelerated.h"
+
+namespace AcceleratedNeRFUtils {
+void dp_unique_id(uint8_t out[128]);
+nof_dp* dp_init_rank(const uint8_t id[128], int world, int rank, int device);
+void dp_init_all(int ndev, const int* devices, nof_dp** out);
+void dp_allreduce(nof_dp* dp, float* buf, int64_t count, hipStream_t st);
+void dp_allreduce_grads(int n, nof_dp* const* dps, AcceleratedMipNeRF* const* models, hipStream_t const* streams);
+void dp_destroy(nof_dp* dp);
+}  // namespace AcceleratedNeRFUtils

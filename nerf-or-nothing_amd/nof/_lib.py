@@ -94,6 +94,13 @@ SIGNATURES = {
     "nof_generate_rays": [P, I32, I32, I32, F, F, F, I32, P, P, P],
     "nof_dataset_generate": [P, I32, I32, I32, F, F, F, I32, P, I32, C.POINTER(P)],
     "nof_recenter_poses": [P, I32],
+    "nof_dp_unique_id": [P],
+    "nof_dp_init_rank": [P, I32, I32, I32, C.POINTER(P)],
+    "nof_dp_init_all": [I32, C.POINTER(I32), C.POINTER(P)],
+    "nof_dp_allreduce": [P, P, C.c_int64, P],
+    "nof_dp_allreduce_grads": [P, P, P],
+    "nof_dp_allreduce_grads_all": [I32, C.POINTER(P), C.POINTER(P), C.POINTER(P)],
+    "nof_dp_destroy": [P],
     "nof_checkpoint_save": [C.c_char_p, P, P],
     "nof_checkpoint_load": [C.c_char_p, P, P],
     "nof_mipnerf_enable_timing": [P, I32],

@@ -33,3 +33,66 @@ def global_loss_mult_sum(rays: dict) -> float:
     """sum of loss multipliers over the WHOLE batch, accumulated in float as the reference
     intends (it truncates to int, MNcpp:61-65, D14)."""
     return float(np.sum(np.asarray(rays["lossmult"], np.float32), dtype=np.float32))
+
+
+class NativeDP:
+    """The C ABI's RCCL data parallelism (nof_dp_*, include/nof.h) for hosts without
+    torch.distributed: one in-place all-reduce (sum) of the gradient arena per step."""
+
+    def __init__(self, handle):
+        self._h = handle
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes as C
+        from ._lib import call
+
+        buf = (C.c_uint8 * 128)()
+        call("nof_dp_unique_id", buf)
+        return bytes(buf)
+
+    @classmethod
+    def init_rank(cls, uid: bytes, world: int, rank: int, device: int) -> "NativeDP":
+        import ctypes as C
+        from ._lib import call
+
+        h = C.c_void_p()
+        call("nof_dp_init_rank", (C.c_uint8 * 128).from_buffer_copy(uid), world, rank, device, C.byref(h))
+        return cls(h)
+
+    @classmethod
+    def init_all(cls, devices) -> list:
+        import ctypes as C
+        from ._lib import call
+
+        n = len(devices)
+        hs = (C.c_void_p * n)()
+        call("nof_dp_init_all", n, (C.c_int32 * n)(*devices), hs)
+        return [cls(C.c_void_p(h)) for h in hs]
+
+    def allreduce(self, ptr: int, count: int, stream=None):
+        from ._lib import call
+
+        call("nof_dp_allreduce", self._h, ptr, count, stream)
+
+    def allreduce_grads(self, model, stream=None):
+        from ._lib import call
+
+        call("nof_dp_allreduce_grads", self._h, model._h, stream)
+
+    @staticmethod
+    def allreduce_grads_all(dps, models, streams=None):
+        import ctypes as C
+        from ._lib import call
+
+        n = len(dps)
+        st = (C.c_void_p * n)(*(streams or [None] * n))
+        call("nof_dp_allreduce_grads_all", n, (C.c_void_p * n)(*[d._h.value for d in dps]),
+             (C.c_void_p * n)(*[m._h.value for m in models]), st)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            from ._lib import lib
+
+            lib().nof_dp_destroy(self._h)
+            self._h = None

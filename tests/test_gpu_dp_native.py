@@ -1,0 +1,45 @@
+"""The C ABI's native RCCL data parallelism (nof_dp_*) on the one GPU of the box: world size 1
+(a multi-rank communicator needs distinct GPUs).  All-reduce of one rank is the identity, so the
+gradient arena must come back bit-identical; the grouped single-process path likewise."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _step(gpu, seed):
+    import torch
+    import nof
+    from nof import synth
+
+    n = 64
+    r = synth.blender_rays(n, seed=seed)
+    d = {k: torch.from_numpy(v).to(gpu) for k, v in r.items()}
+    m = nof.AcceleratedMipNeRF(seed=3, max_rays=n, num_samples=(64, 64))
+    m.get_gradient_device(n, d["o"], d["d"], d["radius"], d["near"], d["far"], d["lossmult"], d["pix"], float(n))
+    torch.cuda.synchronize()
+    return m
+
+
+def test_native_dp_world1_identity(gpu):
+    import torch
+    import nof
+    from nof.dp import NativeDP
+
+    m = _step(gpu, 1)
+    g0 = nof.to_numpy(m.mlp.flat_grads()[0], (546948,)).copy()
+    dp = NativeDP.init_rank(NativeDP.unique_id(), 1, 0, 0)
+    dp.allreduce_grads(m)
+    torch.cuda.synchronize()
+    assert np.array_equal(nof.to_numpy(m.mlp.flat_grads()[0], (546948,)), g0)
+    t = torch.arange(1000, dtype=torch.float32, device=gpu)
+    dp.allreduce(t.data_ptr(), 1000)
+    torch.cuda.synchronize()
+    assert torch.equal(t, torch.arange(1000, dtype=torch.float32, device=gpu))
+    dp.close()
+    (d1,) = NativeDP.init_all([0])
+    NativeDP.allreduce_grads_all([d1], [m])
+    torch.cuda.synchronize()
+    assert np.array_equal(nof.to_numpy(m.mlp.flat_grads()[0], (546948,)), g0)
+    d1.close()
+    m.close()

@@ -17,10 +17,9 @@ namespace nof {
 // delta = mask ? acc (+ w8 * dzs) : 0 -> B operand + delta block.
 template <bool kDensity>
 __device__ __forceinline__ void bwd_epilogue(const f32x16 (&acc)[8], float (&bin)[8][16], const float* w8, float dzs,
-                                             const uint4 mk, float* __restrict__ dst_blk, int lane) {
-  int lv = lane;
-  asm volatile("" : "+v"(lv));  // keep per-store offsets out of the layer loop (see fwd_epilogue)
-  const int h = lv >> 5, j = lv & 31;
+                                             const uint4 mk, float* __restrict__ dst_blk, int lane,
+                                             const BlkStore& bst) {
+  const int h = lane >> 5;
 #pragma unroll
   for (int ot = 0; ot < 8; ++ot) {
 #pragma unroll
@@ -35,16 +34,26 @@ __device__ __forceinline__ void bwd_epilogue(const f32x16 (&acc)[8], float (&bin
         if (kDensity) v += w4[jj] * dzs;
         v = mask_bit(mk, ot, r) ? v : 0.0f;
         bin[ot][r] = v;
-        dst_blk[blk_off(fb + jj, j)] = v;
       }
     }
+    float* tile = dst_blk + ot * 32 * kBlk;  // uniform: one scalar add per tile
+    blk_store<0, 0>(tile, bst, bin[ot][0]);   blk_store<0, 1>(tile, bst, bin[ot][1]);
+    blk_store<0, 2>(tile, bst, bin[ot][2]);   blk_store<0, 3>(tile, bst, bin[ot][3]);
+    blk_store<0, 4>(tile, bst, bin[ot][4]);   blk_store<0, 5>(tile, bst, bin[ot][5]);
+    blk_store<0, 6>(tile, bst, bin[ot][6]);   blk_store<0, 7>(tile, bst, bin[ot][7]);
+    blk_store<0, 8>(tile, bst, bin[ot][8]);   blk_store<0, 9>(tile, bst, bin[ot][9]);
+    blk_store<0, 10>(tile, bst, bin[ot][10]); blk_store<0, 11>(tile, bst, bin[ot][11]);
+    blk_store<0, 12>(tile, bst, bin[ot][12]); blk_store<0, 13>(tile, bst, bin[ot][13]);
+    blk_store<0, 14>(tile, bst, bin[ot][14]); blk_store<0, 15>(tile, bst, bin[ot][15]);
   }
 }
 
 template <bool X3>
 __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
   __shared__ __attribute__((aligned(16))) float lds[ring_floats<X3>()];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, j = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: block pointers stay in SGPRs
+  const BlkStore bst(lane);
   const int nblk = a.M / kBlk;
   const int blk_raw = blockIdx.x * 4 + wave;
   const int blk = blk_raw < nblk ? blk_raw : nblk - 1;  // tail waves duplicate the last block
@@ -63,12 +72,12 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
     const float s = sigmoid_f(zh[1 + c]);
     dzc[c] = a.drgb[(size_t)m * 3 + c] * (s * (1.0f - s)) * kRgbScale;
   }
-  float* d9 = a.delta9x + (size_t)blk * kD9F * kBlk;
-  if (h == 0) {
-    d9[blk_off(128, j)] = dzs;
-    d9[blk_off(129, j)] = dzc[0];
-    d9[blk_off(130, j)] = dzc[1];
-    d9[blk_off(131, j)] = dzc[2];
+  float* d9 = a.delta9x + (size_t)blk * kD9F * kBlk;  // uniform block base
+  if (h == 0) {  // rows 128..131 = tile 4, registers 0..3 of lane half 0
+    blk_store<4, 0>(d9, bst, dzs);
+    blk_store<4, 1>(d9, bst, dzc[0]);
+    blk_store<4, 2>(d9, bst, dzc[1]);
+    blk_store<4, 3>(d9, bst, dzc[2]);
   }
   // ---- delta9 = (W10^T dz_rgb) * relu'(layer 9) ------------------------------------------
   float bin[8][16];
@@ -89,9 +98,20 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
           float v = (wa[jj] * dzc[0] + wb[jj] * dzc[1]) + wc[jj] * dzc[2];
           v = mask_bit(mk, ot, r) ? v : 0.0f;
           bin[ot][r] = v;
-          d9[blk_off(fb + jj, j)] = v;
         }
       }
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot) {
+      float* tile = d9 + ot * 32 * kBlk;
+      blk_store<0, 0>(tile, bst, bin[ot][0]);   blk_store<0, 1>(tile, bst, bin[ot][1]);
+      blk_store<0, 2>(tile, bst, bin[ot][2]);   blk_store<0, 3>(tile, bst, bin[ot][3]);
+      blk_store<0, 4>(tile, bst, bin[ot][4]);   blk_store<0, 5>(tile, bst, bin[ot][5]);
+      blk_store<0, 6>(tile, bst, bin[ot][6]);   blk_store<0, 7>(tile, bst, bin[ot][7]);
+      blk_store<0, 8>(tile, bst, bin[ot][8]);   blk_store<0, 9>(tile, bst, bin[ot][9]);
+      blk_store<0, 10>(tile, bst, bin[ot][10]); blk_store<0, 11>(tile, bst, bin[ot][11]);
+      blk_store<0, 12>(tile, bst, bin[ot][12]); blk_store<0, 13>(tile, bst, bin[ot][13]);
+      blk_store<0, 14>(tile, bst, bin[ot][14]); blk_store<0, 15>(tile, bst, bin[ot][15]);
+    }
   }
   __syncthreads();
 
@@ -103,14 +123,14 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
   {
     const uint4 mk = reinterpret_cast<const uint4*>(mask_ptr(const_cast<uint32_t*>(a.masks), blk, 7))[lane];
     bwd_epilogue<true>(acc, bin, tail + kBwdTailW8, dzs, mk, a.delta + 7 * layer_stride + (size_t)blk * kWidth * kBlk,
-                       lane);
+                       lane, bst);
   }
   // ---- dh_{l-1} = W_l[:, :256]^T delta_l ; delta_{l-1}, l = 7..1 --------------------------
   for (int l = kDepth - 1; l >= 1; --l) {
     dense_layer<X3, 8, 0, 8>(bin, nullptr, acc, lds, cur, wsrc, l == 1, tid, lane);
     const uint4 mk = reinterpret_cast<const uint4*>(mask_ptr(const_cast<uint32_t*>(a.masks), blk, l - 1))[lane];
     bwd_epilogue<false>(acc, bin, nullptr, 0.0f, mk, a.delta + (l - 1) * layer_stride + (size_t)blk * kWidth * kBlk,
-                        lane);
+                        lane, bst);
   }
 }
 

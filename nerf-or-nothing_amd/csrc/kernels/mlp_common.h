@@ -279,6 +279,28 @@ __device__ __forceinline__ void first_slice_dma(const float* src, float* dst, in
 template <bool X3> constexpr int ring_floats() { return 2 * (X3 ? kX3SliceFloats : kSliceFloats); }
 template <bool X3> constexpr int slice_floats() { return X3 ? kX3SliceFloats : kSliceFloats; }
 
+// Stores of accumulator tiles into a chunk-swizzled [F][32] block (common.h) with no per-store
+// VALU: the wave-uniform block base lives in SGPRs (+ 4 KB per 32-feature tile, a scalar add), the
+// lane part is one of four 32-bit offsets chosen by r & 3, and the rest is the instruction's
+// immediate, (8 (r >> 2) + (r & 3)) * 128 B <= 3456.  Element (f, s) of lane (h, j) register r of
+// tile ot: f = 32 ot + 8 (r >> 2) + 4h + (r & 3), so f & 7 = 4h + (r & 3) and
+//   byte(f, j) = 4096 ot + imm(r) + 512 h + ((((j >> 2) ^ (4h + (r & 3))) << 4) | ((j & 3) << 2)).
+struct BlkStore {
+  uint32_t voff[4];
+  __device__ __forceinline__ explicit BlkStore(int lane) {
+    const int h = lane >> 5, j = lane & 31;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) voff[c] = 512u * h + ((((j >> 2) ^ (4 * h + c)) << 4) | ((j & 3) << 2));
+  }
+};
+template <int OT_, int R>
+__device__ __forceinline__ void blk_store(float* sbase, const BlkStore& bs, float v) {
+  typedef __attribute__((address_space(1))) char gchar;
+  typedef __attribute__((address_space(1))) float gfloat;
+  gchar* p = (gchar*)sbase + OT_ * 4096 + (size_t)bs.voff[R & 3] + (8 * (R >> 2) + (R & 3)) * 128;
+  *(gfloat*)p = v;
+}
+
 // feature index held by register r of accumulator tile ot in lane half h
 __device__ __forceinline__ int tile_feature(int ot, int r, int h) { return ot * 32 + 8 * (r >> 2) + 4 * h + (r & 3); }
 

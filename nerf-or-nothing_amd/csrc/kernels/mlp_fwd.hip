@@ -22,12 +22,9 @@ namespace nof {
 // recomputes bit-identical values, so its duplicate stores are benign.
 template <int OT, bool store>
 __device__ __forceinline__ void fwd_epilogue(const f32x16 (&acc)[8], float (&bin)[8][16], const float* bias,
-                                             float* __restrict__ act_blk, uint32_t* __restrict__ mask_dst, int lane) {
-  // opaque copy of the lane index: keeps the 128 per-store offsets from being hoisted out of the
-  // layer loop (they would pin 256 VGPRs of addresses); recomputing them is a few VALU ops each
-  int lv = lane;
-  asm volatile("" : "+v"(lv));
-  const int h = lv >> 5, j = lv & 31;
+                                             float* __restrict__ act_blk, uint32_t* __restrict__ mask_dst, int lane,
+                                             const BlkStore& bst) {
+  const int h = lane >> 5;
   uint32_t mw[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int ot = 0; ot < OT; ++ot) {
@@ -43,22 +40,33 @@ __device__ __forceinline__ void fwd_epilogue(const f32x16 (&acc)[8], float (&bin
         bin[ot][r] = hv;
         // shift-accumulate: bit of (ot, r) ends at position 31 - ((ot & 1) * 16 + r) of word ot >> 1
         mw[ot >> 1] = (mw[ot >> 1] << 1) | (hv > 0.0f ? 1u : 0u);
-#ifndef NOF_DIAG_NO_ACT_STORE
-        if constexpr (store) act_blk[blk_off(fb + jj, j)] = hv;
-#endif
       }
     }
+#ifndef NOF_DIAG_NO_ACT_STORE
+    if constexpr (store) {
+      float* tile = act_blk + ot * 32 * kBlk;  // uniform: one scalar add per tile
+      blk_store<0, 0>(tile, bst, bin[ot][0]);   blk_store<0, 1>(tile, bst, bin[ot][1]);
+      blk_store<0, 2>(tile, bst, bin[ot][2]);   blk_store<0, 3>(tile, bst, bin[ot][3]);
+      blk_store<0, 4>(tile, bst, bin[ot][4]);   blk_store<0, 5>(tile, bst, bin[ot][5]);
+      blk_store<0, 6>(tile, bst, bin[ot][6]);   blk_store<0, 7>(tile, bst, bin[ot][7]);
+      blk_store<0, 8>(tile, bst, bin[ot][8]);   blk_store<0, 9>(tile, bst, bin[ot][9]);
+      blk_store<0, 10>(tile, bst, bin[ot][10]); blk_store<0, 11>(tile, bst, bin[ot][11]);
+      blk_store<0, 12>(tile, bst, bin[ot][12]); blk_store<0, 13>(tile, bst, bin[ot][13]);
+      blk_store<0, 14>(tile, bst, bin[ot][14]); blk_store<0, 15>(tile, bst, bin[ot][15]);
+    }
+#endif
   }
   uint4 mv;
   mv.x = mw[0]; mv.y = mw[1]; mv.z = mw[2]; mv.w = mw[3];
-  if constexpr (store) reinterpret_cast<uint4*>(mask_dst)[lv] = mv;
+  if constexpr (store) reinterpret_cast<uint4*>(mask_dst)[lane] = mv;
 }
 
 template <bool X3, bool store>  // store: side outputs for the backward pass (off for inference)
 __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
   constexpr int kRing = ring_floats<X3>();
   __shared__ __attribute__((aligned(16))) float lds[kRing + 4 * kIpeLdsFloats + 4 * 128];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, j = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, j = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: block pointers stay in SGPRs
   const int nblk = a.M / kBlk;
   const int blk_raw = blockIdx.x * 4 + wave;
   const int blk = blk_raw < nblk ? blk_raw : nblk - 1;  // tail waves duplicate the last block
@@ -135,6 +143,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
   }
   __syncthreads();
 
+  const BlkStore bst(lane);
   int cur = 0;
   const float* wsrc = a.wimg;
   f32x16 acc[8];
@@ -144,12 +153,12 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
   // ---- trunk ----------------------------------------------------------------------------
   dense_layer<X3, 0, 3, 8>(bin, ipe_lds, acc, lds, cur, wsrc, false, tid, lane);
   fwd_epilogue<8, store>(acc, bin, tail + kFwdTailBias, a.act_h + (size_t)blk * kWidth * kBlk, mask_ptr(a.masks, blk, 0),
-                  lane);
+                  lane, bst);
   for (int l = 1; l < kDepth; ++l) {
     if (l == kSkip) dense_layer<X3, 8, 3, 8>(bin, ipe_lds, acc, lds, cur, wsrc, false, tid, lane);
     else dense_layer<X3, 8, 0, 8>(bin, ipe_lds, acc, lds, cur, wsrc, false, tid, lane);
     fwd_epilogue<8, store>(acc, bin, tail + kFwdTailBias + l * 256,
-                    a.act_h + l * layer_stride + (size_t)blk * kWidth * kBlk, mask_ptr(a.masks, blk, l), lane);
+                    a.act_h + l * layer_stride + (size_t)blk * kWidth * kBlk, mask_ptr(a.masks, blk, l), lane, bst);
   }
 
   // ---- density head (layer 8): z_s = w8 . h7 + b8 ---------------------------------------
@@ -167,7 +176,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
 
   // ---- view layer 9: relu(W9[:, :256] h7 + dirbias) --------------------------------------
   dense_layer<X3, 8, 0, 4>(bin, ipe_lds, acc, lds, cur, wsrc, true, tid, lane);
-  fwd_epilogue<4, store>(acc, bin, dirb, a.act_h9 + (size_t)blk * kWidthCond * kBlk, mask_ptr(a.masks, blk, 8), lane);
+  fwd_epilogue<4, store>(acc, bin, dirb, a.act_h9 + (size_t)blk * kWidthCond * kBlk, mask_ptr(a.masks, blk, 8), lane, bst);
 
   // ---- RGB head (layer 10) ------------------------------------------------------------
   float zc[3] = {0.0f, 0.0f, 0.0f};

@@ -14,43 +14,70 @@
 
 namespace nof {
 
-// delta = mask ? acc (+ w8 * dzs) : 0 -> B operand + delta block.
+// delta = mask ? acc (+ w8 * dzs) : 0 -> B operand + delta block, run a quarter tile per call inside
+// the next layer's MFMA stream (see FwdEpi in mlp_fwd.hip): part (t, q) handles registers 4q..4q+3 of tile t; w8 values are loaded one part
+// ahead; the layer's ReLU mask word is loaded by begin(), a layer ahead of its first use.
 template <bool kDensity>
-__device__ __forceinline__ void bwd_epilogue(const f32x16 (&acc)[8], float (&bin)[8][16], const float* w8, float dzs,
-                                             const uint4 mk, float* __restrict__ dst_blk, int lane,
-                                             const BlkStore& bst) {
-  const int h = lane >> 5;
-#pragma unroll
-  for (int ot = 0; ot < 8; ++ot) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int fb = ot * 32 + 8 * q + 4 * h;
-      f32x4 w4 = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (kDensity) w4 = *reinterpret_cast<const f32x4*>(w8 + fb);
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const int r = 4 * q + jj;
-        float v = acc[ot][r];
-        if (kDensity) v += w4[jj] * dzs;
-        v = mask_bit(mk, ot, r) ? v : 0.0f;
-        bin[ot][r] = v;
-      }
+struct BwdEpi {
+#ifndef NOF_DIAG_NO_ACT_STORE
+  static constexpr int kVmPerPart = 4;
+#else
+  static constexpr int kVmPerPart = 0;
+#endif
+  const f32x16 (&acc)[8];
+  float (&bin)[8][16];
+  const BlkStore& bst;
+  const int h;
+  const float* w8;  // LDS, + 4h
+  float dzs;
+  float* dst_blk;
+  uint4 mk;
+  f32x4 wnext;
+
+  __device__ __forceinline__ BwdEpi(const f32x16 (&acc_)[8], float (&bin_)[8][16], const BlkStore& bst_, int lane)
+      : acc(acc_), bin(bin_), bst(bst_), h(lane >> 5) {}
+  __device__ __forceinline__ void begin(const uint32_t* mask, float* dst_blk_, int lane, const float* w8_ = nullptr,
+                                        float dzs_ = 0.0f) {
+    mk = reinterpret_cast<const uint4*>(mask)[lane];
+    dst_blk = dst_blk_;
+    if constexpr (kDensity) {
+      w8 = w8_ + 4 * h;
+      dzs = dzs_;
+      wnext = *reinterpret_cast<const f32x4*>(w8);
     }
-    float* tile = dst_blk + ot * 32 * kBlk;  // uniform: one scalar add per tile
-    blk_store<0, 0>(tile, bst, bin[ot][0]);   blk_store<0, 1>(tile, bst, bin[ot][1]);
-    blk_store<0, 2>(tile, bst, bin[ot][2]);   blk_store<0, 3>(tile, bst, bin[ot][3]);
-    blk_store<0, 4>(tile, bst, bin[ot][4]);   blk_store<0, 5>(tile, bst, bin[ot][5]);
-    blk_store<0, 6>(tile, bst, bin[ot][6]);   blk_store<0, 7>(tile, bst, bin[ot][7]);
-    blk_store<0, 8>(tile, bst, bin[ot][8]);   blk_store<0, 9>(tile, bst, bin[ot][9]);
-    blk_store<0, 10>(tile, bst, bin[ot][10]); blk_store<0, 11>(tile, bst, bin[ot][11]);
-    blk_store<0, 12>(tile, bst, bin[ot][12]); blk_store<0, 13>(tile, bst, bin[ot][13]);
-    blk_store<0, 14>(tile, bst, bin[ot][14]); blk_store<0, 15>(tile, bst, bin[ot][15]);
   }
-}
+  __device__ __forceinline__ void operator()(int t, int q) {
+#ifdef NOF_DIAG_NO_EPI
+    return;
+#endif
+    f32x4 w4;
+    if constexpr (kDensity) {
+      w4 = wnext;
+      if (!(t == 7 && q == 3)) wnext = *reinterpret_cast<const f32x4*>(w8 + 32 * t + 8 * q + 8);
+    }
+    float* tile = dst_blk + t * 32 * kBlk;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int r = 4 * q + jj;
+      float v = acc[t][r];
+      if constexpr (kDensity) v += w4[jj] * dzs;
+      v = mask_bit(mk, t, r) ? v : 0.0f;
+      bin[t][r] = v;
+#ifndef NOF_DIAG_NO_ACT_STORE
+      blk_store_at(tile, bst, 0, r, v);
+#endif
+    }
+  }
+  __device__ __forceinline__ void tile0() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) (*this)(0, q);
+  }
+};
 
 template <bool X3>
 __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
-  __shared__ __attribute__((aligned(16))) float lds[ring_floats<X3>()];
+  __shared__ __attribute__((aligned(16))) float lds[ring_floats<X3>() + 256];
+  float* w8_lds = lds + ring_floats<X3>();
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, j = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: block pointers stay in SGPRs
   const BlkStore bst(lane);
@@ -113,25 +140,38 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
       blk_store<0, 14>(tile, bst, bin[ot][14]); blk_store<0, 15>(tile, bst, bin[ot][15]);
     }
   }
+  if (tid < 64) reinterpret_cast<f32x4*>(w8_lds)[tid] = reinterpret_cast<const f32x4*>(tail + kBwdTailW8)[tid];
   __syncthreads();
 
   int cur = 0;
   const float* wsrc = a.wimg_b;
-  f32x16 acc[8];
+  f32x16 accA[8], accB[8];  // ping-pong, as in the forward
+  const uint32_t* masks = a.masks;
+  float* delta_blk = a.delta + (size_t)blk * kWidth * kBlk;
   // ---- dh7 = W9[:, :256]^T delta9 + w8 dz_s ; delta7 ---------------------------------------
-  dense_layer<X3, 4, 0, 8>(bin, nullptr, acc, lds, cur, wsrc, false, tid, lane);
-  {
-    const uint4 mk = reinterpret_cast<const uint4*>(mask_ptr(const_cast<uint32_t*>(a.masks), blk, 7))[lane];
-    bwd_epilogue<true>(acc, bin, tail + kBwdTailW8, dzs, mk, a.delta + 7 * layer_stride + (size_t)blk * kWidth * kBlk,
-                       lane, bst);
+  BwdEpi<true> e7(accA, bin, bst, lane);
+  e7.begin(masks + ((size_t)blk * kMaskSlots + 7) * 256, delta_blk + 7 * layer_stride, lane, w8_lds, dzs);
+  dense_layer<X3, 4, 0, 8>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane);
+  e7.tile0();
+  // ---- dh_{l-1} = W_l[:, :256]^T delta_l ; delta_{l-1}, l = 7..1 (l odd: A -> B) ------------
+  BwdEpi<false> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
+  eb.begin(masks + ((size_t)blk * kMaskSlots + 6) * 256, delta_blk + 6 * layer_stride, lane);
+  dense_layer<X3, 8, 0, 8>(bin, nullptr, accB, lds, cur, wsrc, false, tid, lane, e7);
+  eb.tile0();
+  static_assert(kDepth == 8, "bwd pairing assumes 8 trunk layers");
+  for (int l = kDepth - 2; l >= 2; l -= 2) {
+    ea.begin(masks + ((size_t)blk * kMaskSlots + l - 1) * 256, delta_blk + (l - 1) * layer_stride, lane);
+    dense_layer<X3, 8, 0, 8>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane, eb);
+    ea.tile0();
+    eb.begin(masks + ((size_t)blk * kMaskSlots + l - 2) * 256, delta_blk + (l - 2) * layer_stride, lane);
+    dense_layer<X3, 8, 0, 8>(bin, nullptr, accB, lds, cur, wsrc, l == 2, tid, lane, ea);
+    eb.tile0();
   }
-  // ---- dh_{l-1} = W_l[:, :256]^T delta_l ; delta_{l-1}, l = 7..1 --------------------------
-  for (int l = kDepth - 1; l >= 1; --l) {
-    dense_layer<X3, 8, 0, 8>(bin, nullptr, acc, lds, cur, wsrc, l == 1, tid, lane);
-    const uint4 mk = reinterpret_cast<const uint4*>(mask_ptr(const_cast<uint32_t*>(a.masks), blk, l - 1))[lane];
-    bwd_epilogue<false>(acc, bin, nullptr, 0.0f, mk, a.delta + (l - 1) * layer_stride + (size_t)blk * kWidth * kBlk,
-                        lane, bst);
-  }
+  // delta0: nothing left to hide it under
+#pragma unroll
+  for (int t = 1; t < 8; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) eb(t, q);
 }
 
 hipError_t launch_mlp_bwd(const BwdArgs& a, hipStream_t st) {

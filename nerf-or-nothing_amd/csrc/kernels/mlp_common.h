@@ -37,28 +37,72 @@ __device__ __forceinline__ void slice_dma(const float* __restrict__ src, float* 
   }
 }
 
+// Step i of a slice DMA (either precision: thread tid moves 16-B chunk 256 i + tid).  The fused
+// layers spread a slice's steps over the first MFMA groups of the previous slice instead of
+// issuing them as one burst, which would queue 4 waves x 8-12 requests on the CU's texture unit
+// and stall every wave's MFMA issue behind it.
+__device__ __forceinline__ void slice_dma_step(const float* __restrict__ src, float* dst, int tid, int i) {
+  const int wave = tid >> 6;
+  const int chunk = kMlpThreads * i + tid;
+  __builtin_amdgcn_global_load_lds((gptr_t)(src + chunk * 4), (lptr_t)(dst + (kMlpThreads * i + 64 * wave) * 4), 16,
+                                   0, 0);
+}
+
 // Per-wave LDS copy of the 48 IPE B-operands: [tp][q][lane][4] floats (12 KB / wave).
 constexpr int kIpeLdsFloats = 3 * 4 * 64 * 4;
+
+// Epilogue hook of a dense layer: the previous layer's epilogue runs a quarter tile at a time,
+// epi(t + 1, q) during slice t (t + 1 < NT_B), in the shadow of this layer's MFMAs, so that tile
+// t + 1 of `bin` is complete before slice t + 1 reads it.  Tile 0 is the caller's (exposed).
+// Epi::kVmPerPart = global stores one part issues (all after the slice's DMA: see slice_barrier).
+struct NoEpi {
+  static constexpr int kVmPerPart = 0;
+  __device__ __forceinline__ void operator()(int, int) {}
+};
+
+// End-of-slice barrier.  This wave's DMA of the next slice must have landed before any wave reads
+// it, but the epilogue stores issued after its last step (n_after of them, counted low: vmcnt
+// retires in issue order, so waiting down to <= n_after outstanding retires the DMA) may stay in
+// flight — __syncthreads() would wait for them too (or, with no wait of its own, leave the DMA
+// unretired).  lgkmcnt(0): this slice's ds_reads are done before the next DMA overwrites the slot.
+__device__ __forceinline__ void slice_barrier(int n_after) {
+#ifndef NOF_DIAG_NO_BARRIER
+  if (n_after >= 16) asm volatile("s_waitcnt vmcnt(16)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if (n_after >= 12) asm volatile("s_waitcnt vmcnt(12)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if (n_after >= 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if (n_after >= 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
+}
+
+static_assert(kSliceFloats / 4 / kMlpThreads == 8, "fp32 slice = 8 DMA steps");
+// fp32 layer: slice DMA steps in MFMA groups 0..7; epilogue part q in group q OT + 1
+template <int OT> constexpr int f32_parts_after_dma() {
+  int n = 0;
+  for (int q = 0; q < 4; ++q) n += (q * OT + 1 > 7) ? 1 : 0;
+  return n;
+}
+// split layer (the 48-KB slice is 12 steps, checked below): two DMA steps in each of groups 0..5; parts in groups s OT + 1 and s OT + OT/2 + 1
+template <int OT> constexpr int x3_parts_after_dma() {
+  int n = 0;
+  for (int s = 0; s < 2; ++s) n += ((s * OT + 1 > 5) ? 1 : 0) + ((s * OT + OT / 2 + 1 > 5) ? 1 : 0);
+  return n;
+}
 
 // One dense layer: acc[ot] (ot < OT) = sum over NT_B slices with B from `bin` (registers) and
 // NT_I slices with B from the wave's IPE copy in LDS.  Consumes NT_B + NT_I slices of the
 // ring with one workgroup barrier each; the next slice's DMA is in flight during the MFMAs.
-template <int NT_B, int NT_I, int OT>
+// The first MFMA of each accumulator takes C = 0 (inline constant) instead of a zeroing pass.
+template <int NT_B, int NT_I, int OT, class Epi>
 __device__ __forceinline__ void mlp_layer(const float (&bin)[8][16], const float* ipe_lds, f32x16 (&acc)[8],
                                           float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
-                                          int lane) {
+                                          int lane, Epi& epi) {
   const int h = lane >> 5;
   const int row = lane & 31;
   const int swz = (row >> 1) & 7;
 #pragma unroll
-  for (int ot = 0; ot < OT; ++ot) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[ot][r] = 0.0f;
-  }
-#pragma unroll
   for (int t = 0; t < NT_B + NT_I; ++t) {
     const bool has_next = !(last_in_schedule && t == NT_B + NT_I - 1);
-    if (has_next) slice_dma(wsrc + kSliceFloats, lds + (cur ^ 1) * kSliceFloats, tid);
     const float* W = lds + cur * kSliceFloats + row * 32;
     // A operands of (q, ot) are read one group ahead so the ds_read latency hides under the
     // previous group's 4 MFMAs (left alone, hipcc serialises read -> lgkmcnt(0) -> MFMA).
@@ -86,14 +130,21 @@ __device__ __forceinline__ void mlp_layer(const float (&bin)[8][16], const float
           const int ot2 = ot == OT - 1 ? 0 : ot + 1;
           a_nxt = *reinterpret_cast<const f32x4*>(W + ot2 * 32 * 32 + (((2 * q2 + h) ^ swz) << 2));
         }
+#ifndef NOF_DIAG_NO_DMA
+        if (has_next && q * OT + ot < 8)
+          slice_dma_step(wsrc + kSliceFloats, lds + (cur ^ 1) * kSliceFloats, tid, q * OT + ot);
+#endif
         __builtin_amdgcn_sched_barrier(0);  // keep the next group's read above this group's MFMAs
+        if (t == 0 && q == 0) acc[ot] = mfma32(a_cur[0], b4[0], f32x16{});
+        else acc[ot] = mfma32(a_cur[0], b4[0], acc[ot]);
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) acc[ot] = mfma32(a_cur[jj], b4[jj], acc[ot]);
+        for (int jj = 1; jj < 4; ++jj) acc[ot] = mfma32(a_cur[jj], b4[jj], acc[ot]);
+        if (t + 1 < NT_B && ot == 1) epi(t + 1, q);
         __builtin_amdgcn_sched_barrier(0);
         a_cur = a_nxt;
       }
     }
-    __syncthreads();
+    slice_barrier(t + 1 < NT_B ? f32_parts_after_dma<OT>() * Epi::kVmPerPart : 0);
     cur ^= 1;
     wsrc += kSliceFloats;
   }
@@ -173,6 +224,7 @@ constexpr int kX3SliceFloats = 2 * 8 * 3 * 64 * 4;
 constexpr size_t kFwdImageX3Floats = (size_t)kFwdSlices * kX3SliceFloats;  // + fwd tail (fp32)
 constexpr size_t kBwdImageX3Floats = (size_t)kBwdSlices * kX3SliceFloats;  // + bwd tail (fp32)
 
+static_assert(kX3SliceFloats / 4 / kMlpThreads == 12, "split slice = 12 DMA steps");
 __device__ __forceinline__ void slice_dma_x3(const float* __restrict__ src, float* dst, int tid) {
   const int wave = tid >> 6;
 #pragma unroll
@@ -205,17 +257,14 @@ __device__ __forceinline__ void x3_b_values(const float (&bin)[8][16], const flo
 // Split-mode dense layer: same contract as mlp_layer (slices of the split image, one barrier per
 // slice).  Per (k-step, row tile): three ds_read_b128 (issued one group ahead) and six MFMAs; the
 // next k-step's B fragment is split pair by pair in the shadow of the current k-step's MFMAs.
-template <int NT_B, int NT_I, int OT>
+// Epilogue parts: k-step s of slice t runs epi(t + 1, 2s) and epi(t + 1, 2s + 1), so the first half
+// of tile t + 1 is in `bin` before k-step 1 of slice t splits it as the next B fragment.
+template <int NT_B, int NT_I, int OT, class Epi>
 __device__ __forceinline__ void mlp_layer_x3(const float (&bin)[8][16], const float* ipe_lds, f32x16 (&acc)[8],
                                              float* lds, int& cur, const float*& wsrc, bool last_in_schedule,
-                                             int tid, int lane) {
+                                             int tid, int lane, Epi& epi) {
   constexpr int NK = 2 * (NT_B + NT_I);
   constexpr int PER = OT / 4;  // row-tile groups per split pair
-#pragma unroll
-  for (int ot = 0; ot < OT; ++ot) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[ot][r] = 0.0f;
-  }
   Frag3 b_cur, b_nxt;
   {
     float v[8];
@@ -225,7 +274,6 @@ __device__ __forceinline__ void mlp_layer_x3(const float (&bin)[8][16], const fl
 #pragma unroll
   for (int t = 0; t < NT_B + NT_I; ++t) {
     const bool has_next = !(last_in_schedule && t == NT_B + NT_I - 1);
-    if (has_next) slice_dma_x3(wsrc + kX3SliceFloats, lds + (cur ^ 1) * kX3SliceFloats, tid);
     const bf16x8* W = reinterpret_cast<const bf16x8*>(lds + cur * kX3SliceFloats) + lane;
     Frag3 a_cur;
 #pragma unroll
@@ -246,30 +294,44 @@ __device__ __forceinline__ void mlp_layer_x3(const float (&bin)[8][16], const fl
 #pragma unroll
           for (int p = 0; p < 3; ++p) a_nxt.p[p] = W[((s2 * 8 + ot2) * 3 + p) * 64];
         }
+#ifndef NOF_DIAG_NO_DMA
+        if (has_next && s * OT + ot < 6) {
+          slice_dma_step(wsrc + kX3SliceFloats, lds + (cur ^ 1) * kX3SliceFloats, tid, 2 * (s * OT + ot));
+          slice_dma_step(wsrc + kX3SliceFloats, lds + (cur ^ 1) * kX3SliceFloats, tid, 2 * (s * OT + ot) + 1);
+        }
+#endif
         __builtin_amdgcn_sched_barrier(0);
-        acc[ot] = mfma_x3(a_cur, b_cur, acc[ot]);
+        acc[ot] = mfma_x3(a_cur, b_cur, kk == 0 ? f32x16{} : acc[ot]);
         if (kk + 1 < NK && ot % PER == 0) {
           const int i = 2 * (ot / PER);
           split_pair(vn[i], vn[i + 1], b_nxt, i);
         }
+        if (t + 1 < NT_B && (ot == 1 || ot == OT / 2 + 1)) epi(t + 1, 2 * s + (ot == 1 ? 0 : 1));
         __builtin_amdgcn_sched_barrier(0);
         a_cur = a_nxt;
       }
       b_cur = b_nxt;
     }
-    __syncthreads();
+    slice_barrier(t + 1 < NT_B ? x3_parts_after_dma<OT>() * Epi::kVmPerPart : 0);
     cur ^= 1;
     wsrc += kX3SliceFloats;
   }
 }
 
 // mode dispatch for the fused kernels
+template <bool X3, int NT_B, int NT_I, int OT, class Epi>
+__device__ __forceinline__ void dense_layer(const float (&bin)[8][16], const float* ipe_lds, f32x16 (&acc)[8],
+                                            float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
+                                            int lane, Epi& epi) {
+  if constexpr (X3) mlp_layer_x3<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi);
+  else mlp_layer<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi);
+}
 template <bool X3, int NT_B, int NT_I, int OT>
 __device__ __forceinline__ void dense_layer(const float (&bin)[8][16], const float* ipe_lds, f32x16 (&acc)[8],
                                             float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
                                             int lane) {
-  if constexpr (X3) mlp_layer_x3<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane);
-  else mlp_layer<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane);
+  NoEpi none;
+  dense_layer<X3, NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, none);
 }
 template <bool X3>
 __device__ __forceinline__ void first_slice_dma(const float* src, float* dst, int tid) {
@@ -298,6 +360,14 @@ __device__ __forceinline__ void blk_store(float* sbase, const BlkStore& bs, floa
   typedef __attribute__((address_space(1))) char gchar;
   typedef __attribute__((address_space(1))) float gfloat;
   gchar* p = (gchar*)sbase + OT_ * 4096 + (size_t)bs.voff[R & 3] + (8 * (R >> 2) + (R & 3)) * 128;
+  *(gfloat*)p = v;
+}
+
+// same, for a tile/register known only after unrolling (folds to the same immediate offsets)
+__device__ __forceinline__ void blk_store_at(float* sbase, const BlkStore& bs, int ot, int r, float v) {
+  typedef __attribute__((address_space(1))) char gchar;
+  typedef __attribute__((address_space(1))) float gfloat;
+  gchar* p = (gchar*)sbase + ot * 4096 + (size_t)bs.voff[r & 3] + (8 * (r >> 2) + (r & 3)) * 128;
   *(gfloat*)p = v;
 }
 

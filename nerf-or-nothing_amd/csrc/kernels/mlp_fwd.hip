@@ -61,10 +61,92 @@ __device__ __forceinline__ void fwd_epilogue(const f32x16 (&acc)[8], float (&bin
   if constexpr (store) reinterpret_cast<uint4*>(mask_dst)[lane] = mv;
 }
 
+// The same epilogue for the trunk layers, run a quarter tile per call (part (t, q): registers
+// 4q..4q+3 of accumulator tile t) so that tiles 1..7 execute inside the next layer's MFMA stream
+// (mlp_layer's epilogue hook) while that layer accumulates into the other accumulator set.  Bias
+// values are loaded one part ahead (part (t, q) uses features 32t + 8q + 4h.., the next part
+// always sits 8 further); biases and w8 come from the workgroup's LDS copy, so the only vector-memory
+// ops of a part are its stores.  kDensity folds the density head (w8 . h7) into layer 7's epilogue.
+template <bool store, bool kDensity>
+struct FwdEpi {
+#ifndef NOF_DIAG_NO_ACT_STORE
+  static constexpr int kVmPerPart = store ? 4 : 0;
+#else
+  static constexpr int kVmPerPart = 0;
+#endif
+  const f32x16 (&acc)[8];
+  float (&bin)[8][16];
+  const BlkStore& bst;
+  const int h;
+  const float* bias;  // LDS, + 4h
+  const float* w8;    // LDS, + 4h
+  float* act_blk;
+  uint4* mask_dst;    // + lane
+  uint32_t mw[4];
+  f32x4 bnext, wnext;
+  float zs;
+
+  __device__ __forceinline__ FwdEpi(const f32x16 (&acc_)[8], float (&bin_)[8][16], const BlkStore& bst_, int lane)
+      : acc(acc_), bin(bin_), bst(bst_), h(lane >> 5) {}
+  __device__ __forceinline__ void begin(const float* bias_, float* act_blk_, uint32_t* mask_, int lane,
+                                        const float* w8_ = nullptr) {
+    bias = bias_ + 4 * h;
+    act_blk = act_blk_;
+    mask_dst = reinterpret_cast<uint4*>(mask_) + lane;
+    mw[0] = mw[1] = mw[2] = mw[3] = 0u;
+    bnext = *reinterpret_cast<const f32x4*>(bias);
+    if constexpr (kDensity) {
+      w8 = w8_ + 4 * h;
+      wnext = *reinterpret_cast<const f32x4*>(w8);
+      zs = 0.0f;
+    }
+  }
+  __device__ __forceinline__ void operator()(int t, int q) {
+#ifdef NOF_DIAG_NO_EPI
+    return;
+#endif
+    const int fo = 32 * t + 8 * q;
+    const f32x4 b4 = bnext;
+    const bool more = !(t == 7 && q == 3);
+    if (more) bnext = *reinterpret_cast<const f32x4*>(bias + fo + 8);
+    f32x4 w4;
+    if constexpr (kDensity) {
+      w4 = wnext;
+      if (more) wnext = *reinterpret_cast<const f32x4*>(w8 + fo + 8);
+    }
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int r = 4 * q + jj;
+      const float z = acc[t][r] + b4[jj];
+      const float hv = z > 0.0f ? z : 0.0f;
+      bin[t][r] = hv;
+      mw[t >> 1] = (mw[t >> 1] << 1) | (hv > 0.0f ? 1u : 0u);
+      if constexpr (kDensity) zs += w4[jj] * hv;
+    }
+#ifndef NOF_DIAG_NO_ACT_STORE
+    if constexpr (store) {
+      float* tile = act_blk + t * 32 * kBlk;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) blk_store_at(tile, bst, 0, 4 * q + jj, bin[t][4 * q + jj]);
+    }
+#endif
+    if (!more) {
+      uint4 mv;
+      mv.x = mw[0]; mv.y = mw[1]; mv.z = mw[2]; mv.w = mw[3];
+      if constexpr (store) *mask_dst = mv;
+    }
+  }
+  __device__ __forceinline__ void tile0() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) (*this)(0, q);
+  }
+};
+
 template <bool X3, bool store>  // store: side outputs for the backward pass (off for inference)
 __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
   constexpr int kRing = ring_floats<X3>();
-  __shared__ __attribute__((aligned(16))) float lds[kRing + 4 * kIpeLdsFloats + 4 * 128];
+  constexpr int kBiasLds = 8 * 256 + 256;
+  __shared__ __attribute__((aligned(16))) float lds[kRing + 4 * kIpeLdsFloats + 4 * 128 + kBiasLds];
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, j = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: block pointers stay in SGPRs
   const int nblk = a.M / kBlk;
@@ -132,6 +214,12 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
       *reinterpret_cast<f32x4*>(ipe_lds + ((tp * 4 + q) * 64 + lane) * 4) = v;
     }
   float* dirb = lds + kRing + 4 * kIpeLdsFloats + wave * 128;
+  // trunk biases (layers 0..7) and w8 -> LDS for the epilogues
+  float* bias_lds = lds + kRing + 4 * kIpeLdsFloats + 4 * 128;
+  for (int i = tid; i < kBiasLds / 4; i += kMlpThreads) {
+    const float* src = i < 512 ? tail + kFwdTailBias + 4 * i : tail + kFwdTailW8 + 4 * (i - 512);
+    *reinterpret_cast<f32x4*>(bias_lds + 4 * i) = *reinterpret_cast<const f32x4*>(src);
+  }
 #pragma unroll
   for (int rep = 0; rep < 2; ++rep) {
     const int o = lane + 64 * rep;
@@ -146,37 +234,39 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
   const BlkStore bst(lane);
   int cur = 0;
   const float* wsrc = a.wimg;
-  f32x16 acc[8];
+  f32x16 accA[8], accB[8];  // ping-pong: layer l accumulates into one set while l - 1's epilogue drains the other
   float bin[8][16];
   const size_t layer_stride = (size_t)nblk * kWidth * kBlk;
+  const float* biases = bias_lds;
+  float* act_h_blk = a.act_h + (size_t)blk * kWidth * kBlk;
 
-  // ---- trunk ----------------------------------------------------------------------------
-  dense_layer<X3, 0, 3, 8>(bin, ipe_lds, acc, lds, cur, wsrc, false, tid, lane);
-  fwd_epilogue<8, store>(acc, bin, tail + kFwdTailBias, a.act_h + (size_t)blk * kWidth * kBlk, mask_ptr(a.masks, blk, 0),
-                  lane, bst);
-  for (int l = 1; l < kDepth; ++l) {
-    if (l == kSkip) dense_layer<X3, 8, 3, 8>(bin, ipe_lds, acc, lds, cur, wsrc, false, tid, lane);
-    else dense_layer<X3, 8, 0, 8>(bin, ipe_lds, acc, lds, cur, wsrc, false, tid, lane);
-    fwd_epilogue<8, store>(acc, bin, tail + kFwdTailBias + l * 256,
-                    a.act_h + l * layer_stride + (size_t)blk * kWidth * kBlk, mask_ptr(a.masks, blk, l), lane, bst);
+  // ---- trunk: layer l writes acc(l odd ? B : A) ------------------------------------------
+  FwdEpi<store, false> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
+  ea.begin(biases, act_h_blk, mask_ptr(a.masks, blk, 0), lane);
+  dense_layer<X3, 0, 3, 8>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane);
+  ea.tile0();
+  for (int l = 1; l < kDepth - 1; l += 2) {
+    eb.begin(biases + l * 256, act_h_blk + l * layer_stride, mask_ptr(a.masks, blk, l), lane);
+    dense_layer<X3, 8, 0, 8>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea);
+    eb.tile0();
+    ea.begin(biases + (l + 1) * 256, act_h_blk + (l + 1) * layer_stride, mask_ptr(a.masks, blk, l + 1), lane);
+    if (l + 1 == kSkip) dense_layer<X3, 8, 3, 8>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, eb);
+    else dense_layer<X3, 8, 0, 8>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, eb);
+    ea.tile0();
   }
+  static_assert(kDepth == 8 && kSkip % 2 == 0, "trunk pairing assumes 8 layers and an even skip layer");
+  FwdEpi<store, true> e7(accB, bin, bst, lane);  // + density head (layer 8): z_s = w8 . h7 + b8
+  e7.begin(biases + 7 * 256, act_h_blk + 7 * layer_stride, mask_ptr(a.masks, blk, 7), lane, bias_lds + 8 * 256);
+  dense_layer<X3, 8, 0, 8>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea);
+  e7.tile0();
 
-  // ---- density head (layer 8): z_s = w8 . h7 + b8 ---------------------------------------
-  float zs = 0.0f;
-#pragma unroll
-  for (int ot = 0; ot < 8; ++ot)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 w4 = *reinterpret_cast<const f32x4*>(tail + kFwdTailW8 + ot * 32 + 8 * q + 4 * h);
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) zs += w4[jj] * bin[ot][4 * q + jj];
-    }
+  // ---- view layer 9: relu(W9[:, :256] h7 + dirbias); h7 tiles 1..7 finish in its shadow -------
+  dense_layer<X3, 8, 0, 4>(bin, ipe_lds, accA, lds, cur, wsrc, true, tid, lane, e7);
+  float zs = e7.zs;
   zs += __shfl_xor(zs, 32, 64);
   zs += tail[kFwdTailBias + 8 * 256];
-
-  // ---- view layer 9: relu(W9[:, :256] h7 + dirbias) --------------------------------------
-  dense_layer<X3, 8, 0, 4>(bin, ipe_lds, acc, lds, cur, wsrc, true, tid, lane);
-  fwd_epilogue<4, store>(acc, bin, dirb, a.act_h9 + (size_t)blk * kWidthCond * kBlk, mask_ptr(a.masks, blk, 8), lane, bst);
+  fwd_epilogue<4, store>(accA, bin, dirb, a.act_h9 + (size_t)blk * kWidthCond * kBlk, mask_ptr(a.masks, blk, 8), lane,
+                         bst);
 
   // ---- RGB head (layer 10) ------------------------------------------------------------
   float zc[3] = {0.0f, 0.0f, 0.0f};

@@ -258,13 +258,20 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M) {
   p = prob(delta9x_.p, nof::kD9F, 128, 1, L.act_h9.p, 128, 0, 4);
   os.push_back({p, 1, 3, 0, 128, Wg(10), in_[10], 0, Bg(10)});
 
-  // cost per k-block: MFMAs per wave of the 2x4 wave grid (RB x CB tiles, wgrad.hip) vs staging bytes
-  // (4 KB per 32-row operand block; ~16 KB per MFMA round keeps a CU under its HBM share)
+  // cost per k-block (wgrad.hip): MFMA time of the busiest SIMD vs staging bytes (4 KB per 32-row
+  // operand block).  fp32: 2 x 4 waves of RB x CB tiles, ~16 KB per MFMA round keeps a CU under its
+  // HBM share.  split: 2 x 2 waves (one per SIMD) of RB x CB tiles, six bf16 MFMAs per product —
+  // a 32-row block of loads costs about one tile's MFMAs at the CU's HBM share.
   std::vector<int64_t> cost(P.size());
   int64_t total = 0;
   for (size_t i = 0; i < P.size(); ++i) {
-    const int RB = (P[i].ntr + 1) / 2, CB = (P[i].ntc + 3) / 4;
-    cost[i] = std::max(RB * CB, (P[i].ntr + P[i].ntc + 3) / 4);
+    if (split_) {
+      const int RB = (P[i].ntr + 1) / 2, CB = (P[i].ntc + 1) / 2;
+      cost[i] = std::max(RB * CB, P[i].ntr + P[i].ntc);
+    } else {
+      const int RB = (P[i].ntr + 1) / 2, CB = (P[i].ntc + 3) / 4;
+      cost[i] = std::max(RB * CB, (P[i].ntr + P[i].ntc + 3) / 4);
+    }
     total += cost[i] * nblk;
   }
   const int G_wg = num_cu_;

@@ -66,7 +66,9 @@ struct NoEpi {
 // flight — __syncthreads() would wait for them too (or, with no wait of its own, leave the DMA
 // unretired).  lgkmcnt(0): this slice's ds_reads are done before the next DMA overwrites the slot.
 __device__ __forceinline__ void slice_barrier(int n_after) {
-#ifndef NOF_DIAG_NO_BARRIER
+#if defined(NOF_DIAG_DMA_NOWAIT)
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#elif !defined(NOF_DIAG_NO_BARRIER)
   if (n_after >= 16) asm volatile("s_waitcnt vmcnt(16)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   else if (n_after >= 12) asm volatile("s_waitcnt vmcnt(12)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   else if (n_after >= 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -125,7 +127,11 @@ __device__ __forceinline__ void mlp_layer(const float (&bin)[8][16], const float
         asm volatile("" ::"v"(a_cur));
         f32x4 a_nxt = a_cur;
         const bool more = !(q == 3 && ot == OT - 1);
+#ifdef NOF_DIAG_NO_AREAD
+        if (more && t == 0) {
+#else
         if (more) {
+#endif
           const int q2 = ot == OT - 1 ? q + 1 : q;
           const int ot2 = ot == OT - 1 ? 0 : ot + 1;
           a_nxt = *reinterpret_cast<const f32x4*>(W + ot2 * 32 * 32 + (((2 * q2 + h) ^ swz) << 2));
@@ -146,7 +152,9 @@ __device__ __forceinline__ void mlp_layer(const float (&bin)[8][16], const float
     }
     slice_barrier(t + 1 < NT_B ? f32_parts_after_dma<OT>() * Epi::kVmPerPart : 0);
     cur ^= 1;
+#ifndef NOF_DIAG_DMA_SAME
     wsrc += kSliceFloats;
+#endif
   }
 }
 
@@ -288,7 +296,11 @@ __device__ __forceinline__ void mlp_layer_x3(const float (&bin)[8][16], const fl
         asm volatile("" ::"v"(a_cur.p[0]), "v"(a_cur.p[1]), "v"(a_cur.p[2]));  // wait here, before the next reads
         Frag3 a_nxt = a_cur;
         const bool more = !(s == 1 && ot == OT - 1);
+#ifdef NOF_DIAG_NO_AREAD
+        if (more && t == 0) {
+#else
         if (more) {
+#endif
           const int s2 = ot == OT - 1 ? s + 1 : s;
           const int ot2 = ot == OT - 1 ? 0 : ot + 1;
 #pragma unroll
@@ -314,7 +326,9 @@ __device__ __forceinline__ void mlp_layer_x3(const float (&bin)[8][16], const fl
     }
     slice_barrier(t + 1 < NT_B ? x3_parts_after_dma<OT>() * Epi::kVmPerPart : 0);
     cur ^= 1;
+#ifndef NOF_DIAG_DMA_SAME
     wsrc += kX3SliceFloats;
+#endif
   }
 }
 

@@ -78,15 +78,38 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
   int cur = 0;
   for (int kb = item.kb0; kb < item.kb1; ++kb) {
     float* nxt = lds + (cur ^ 1) * 2 * kWgHalf;
-    if (kb + 1 < item.kb1) {
-      blk_dma(Ab + (kb + 1) * strideA, nxt, nA4, tid);
-      blk_dma(Bb + (kb + 1) * strideB, nxt + kWgHalf, nB4, tid);
-    }
+    const bool more = kb + 1 < item.kb1;
+    const float* srcA = Ab + (kb + 1) * strideA;
+    const float* srcB = Bb + (kb + 1) * strideB;
+    // next block's DMA, two of its (up to) 4 + 4 wave-instructions per chunk pair, so the
+    // texture unit sees a steady trickle instead of one burst that stalls every wave's issue
+    auto dma_steps = [&](int cc) {
+#ifdef NOF_DIAG_WG_NODMA
+      if (more && kb < 0) {
+#else
+      if (more) {
+#endif
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int st = 2 * cc + u;
+          const int f4 = (st & 3) * kWgThreads + tid;
+          if (st < 4) {
+            if (f4 < nA4) __builtin_amdgcn_global_load_lds((wg_gptr_t)(srcA + f4 * 4),
+                                                           (wg_lptr_t)(nxt + (f4 - lane) * 4), 16, 0, 0);
+          } else {
+            if (f4 < nB4) __builtin_amdgcn_global_load_lds((wg_gptr_t)(srcB + f4 * 4),
+                                                           (wg_lptr_t)(nxt + kWgHalf + (f4 - lane) * 4), 16, 0, 0);
+          }
+        }
+      }
+    };
     if (active) {
       const float* LA = lds + cur * 2 * kWgHalf;
       const float* LB = LA + kWgHalf;
       // lane half h reads chunk 2cc + h (samples 8cc + 4h .. +3); MFMA i of the group then sums
-      // k = {8cc + i, 8cc + 4 + i}, the same pairing for A and B
+      // k = {8cc + i, 8cc + 4 + i}, the same pairing for A and B.  Chunk pair cc + 1 is read
+      // while cc's MFMAs run (the fences keep hipcc from hoisting all reads to the top, which
+      // would stall both waves of a SIMD on LDS at the same time after every barrier).
       f32x4 a[RB], b[CB];
 #pragma unroll
       for (int r = 0; r < RB; ++r) a[r] = *reinterpret_cast<const f32x4*>(LA + aoff[r] + ((h ^ xs) << 2));
@@ -95,13 +118,23 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
 #pragma unroll
       for (int cc = 0; cc < 4; ++cc) {
         f32x4 an[RB], bn[CB];
+#pragma unroll
+        for (int r = 0; r < RB; ++r) asm volatile("" ::"v"(a[r]));
+#pragma unroll
+        for (int c = 0; c < CB; ++c) asm volatile("" ::"v"(b[c]));
+        dma_steps(cc);
+#ifdef NOF_DIAG_WG_NOREAD
+        if (cc < 3 && kb < 0) {
+#else
         if (cc < 3) {
+#endif
           const int ch = ((2 * (cc + 1) + h) ^ xs) << 2;
 #pragma unroll
           for (int r = 0; r < RB; ++r) an[r] = *reinterpret_cast<const f32x4*>(LA + aoff[r] + ch);
 #pragma unroll
           for (int c = 0; c < CB; ++c) bn[c] = *reinterpret_cast<const f32x4*>(LB + boff[c] + ch);
         }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -110,6 +143,7 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
             for (int c = 0; c < CB; ++c) acc[r][c] = mfma32(a[r][i], b[c][i], acc[r][c]);
             bs[r] += a[r][i];
           }
+        __builtin_amdgcn_sched_barrier(0);
         if (cc < 3) {
 #pragma unroll
           for (int r = 0; r < RB; ++r) a[r] = an[r];
@@ -117,8 +151,14 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
           for (int c = 0; c < CB; ++c) b[c] = bn[c];
         }
       }
+    } else {
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) dma_steps(cc);
     }
-    __syncthreads();
+    // the DMA above must have landed (vmcnt) and this block's LDS reads retired before the swap
+#ifndef NOF_DIAG_WG_NOBAR
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
     cur ^= 1;
   }
   if (active) {
@@ -170,43 +210,47 @@ __global__ __launch_bounds__(kWgThreads, 1) void k_wgrad(const WgProblem* __rest
 }
 
 // ---- split mode (mlp_common.h): bf16x3 operands, six bf16 MFMAs per 32x32x16 product -----------
-// Same 2 x 4 wave grid as fp32 (8 waves, two per SIMD, up to 4 x 2 output tiles each).  Per
-// 16-sample k-step (the 64-B half of every feature row of a chunk-swizzled block, common.h):
-//   * every thread loads two 16-B chunks of A and two of B straight into registers, two k-steps
-//     ahead, each wave-instruction covering 16 feature rows x 64 contiguous bytes.  The loads are
-//     unconditional (rows past the problem re-read its last row), the k loop is unrolled by two
-//     so the two register sets are never copied, and the k-step barrier is a bare s_barrier after
-//     lgkmcnt(0) (__syncthreads' release fence would wait vmcnt(0)): the compiler then waits with
-//     counted vmcnt and two k-steps of loads stay in flight across barriers;
+// 4 waves, one per SIMD, on a 2 x 2 grid: wave (wr, wc) owns row tiles [wr RB, wr RB + RB) x col
+// tiles [wc CB, wc CB + CB) (up to 4 x 4 tiles = 256 accumulator registers), so the whole MFMA
+// stream of a CU runs from one wave per SIMD and each fragment read feeds RB or CB products.
+// Per 16-sample k-step (the 64-B half of every feature row of a chunk-swizzled block, common.h):
+//   * every thread loads 8 16-B chunks (4 rows of A, 4 of B; 16 rows x 64 contiguous bytes per
+//     wave-instruction) straight into registers, two k-steps ahead: two register sets rotate
+//     statically (k loop unrolled by two), so up to 64 KB per CU are in flight.  Loads are
+//     unconditional (rows past the problem re-read its last row; steps past the end re-read the
+//     last step) so vmcnt counts are static;
 //   * each chunk is split ONCE into (hi, mid, lo) and its three 8-B pieces written to the k-step's
-//     fragment images in LDS (double-buffered, 2 x 48 KB), so no split is repeated by the waves
-//     sharing a tile;
-//   * the MFMA waves read each fragment piece as one conflict-free ds_read_b128 and issue
-//     6 * RB * CB MFMAs.
-// The split of k-step k + 1 and the MFMAs of k-step k interleave.
-constexpr int kWgX3Threads = kWgThreads;
+//     fragment images in LDS (double-buffered, 2 x 48 KB), in the shadow of the MFMAs of the
+//     previous k-step, whose fragments are one conflict-free ds_read_b128 each;
+//   * one bare barrier per k-step (lgkmcnt(0) + s_barrier: __syncthreads' release fence would
+//     wait for the loads in flight).
+constexpr int kWgX3Threads = 256;
 constexpr int kX3Frag = 3 * 8 * 64 * 4;  // floats per operand fragment image: [piece][tile][lane][16 B]
 constexpr int kX3Lds = 2 * 2 * kX3Frag;   // 96 KB
 
 struct X3Raw {
-  f32x4 a0, a1, b0, b1;  // chunk i: row (tid >> 2) + 128 i, logical chunk tid & 3 of the k-step
+  f32x4 a[4], b[4];  // chunk lc of rows lrow + 64 i
 };
 
 // LDS writes of this wave done, then a bare workgroup barrier; the "memory" clobber keeps the
 // compiler from moving LDS accesses across it.  Global loads in flight are NOT waited for.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// product order of mfma_x3 (smallest terms first): pieces of A and B for product pp
+__device__ __forceinline__ constexpr int x3_pa(int pp) { return pp == 0 ? 2 : (pp == 2 || pp == 3) ? 1 : 0; }
+__device__ __forceinline__ constexpr int x3_pb(int pp) { return pp == 1 ? 2 : (pp == 2 || pp == 4) ? 1 : 0; }
+
 template <int RB, int CB>
-__device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& P, float* lds, int tid, int lane,
-                                           int wave, float* slabs, float* bias_slabs, const int64_t* slab_off) {
+__device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& P, float* lds, int tid, int wave,
+                                           float* slabs, float* bias_slabs, const int64_t* slab_off) {
   // opaque thread index: the lane-derived offsets of the five instantiations are recomputed per
   // item instead of being hoisted to the kernel entry all at once (they would spill)
   int tq = tid;
   asm volatile("" : "+v"(tq));
   tid = tq;
-  lane = tq & 63;
+  const int lane = tq & 63;
   const int h = lane >> 5, x = lane & 31;
-  const int wr = wave >> 2, wc = wave & 3;
+  const int wr = wave >> 1, wc = wave & 1;
   const int r0 = wr * RB, c0 = wc * CB;
   const bool active = r0 < P.ntr && c0 < P.ntc;  // wave-uniform
   int rowt[RB], colt[CB];
@@ -216,28 +260,29 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
   for (int c = 0; c < CB; ++c) colt[c] = min(c0 + c, P.ntc - 1);
   const size_t strideA = (size_t)P.FA * kBlk, strideB = (size_t)P.FB * kBlk;
   const int nrA = P.ntr * 32, nrB = P.ntc * 32;
-  const int lc = tid & 3, lrow = tid >> 2;  // loader role: rows lrow, lrow + 128; chunk lc
+  const int lc = tid & 3, lrow = tid >> 2;  // loader role: rows lrow + 64 i, chunk lc
   const float* baseA = P.A + (size_t)item.kb0 * strideA + (size_t)P.a_row0 * kBlk;
   const float* baseB = P.B + (size_t)item.kb0 * strideB + (size_t)P.b_col0 * kBlk;
-  const int ra0 = min(lrow, nrA - 1), ra1 = min(lrow + 128, nrA - 1);
-  const int rb0 = min(lrow, nrB - 1), rb1 = min(lrow + 128, nrB - 1);
   const int K = 2 * (item.kb1 - item.kb0);
-
-  // global (not flat) loads: the operand pointers come from the problem table, so without the
-  // address-space cast hipcc emits flat_load, which also counts in lgkmcnt and would be drained by
-  // every LDS wait
-  auto ld = [&](const float* base, size_t stride, int k, int row) {
-    const int c = 4 * (k & 1) + lc;
-    typedef const __attribute__((address_space(1))) f32x4* gf4;
-    return *(gf4)(base + (size_t)(k >> 1) * stride + (size_t)row * kBlk + ((c ^ (row & 7)) << 2));
+  // byte offset of chunk lc of row `row` in an even k-step (odd: ^ 64, chunk 4 + lc)
+  uint32_t offA[4], offB[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ra = min(lrow + 64 * i, nrA - 1), rb = min(lrow + 64 * i, nrB - 1);
+    offA[i] = (uint32_t)(ra * kBlk * 4 + ((lc ^ (ra & 7)) << 4));
+    offB[i] = (uint32_t)(rb * kBlk * 4 + ((lc ^ (rb & 7)) << 4));
+  }
+  typedef const __attribute__((address_space(1))) f32x4 gf4;
+  auto load = [&](int k, X3Raw& q) {  // global (not flat) loads: flat_load would count in lgkmcnt
+    const char* A = reinterpret_cast<const char*>(baseA + (size_t)(k >> 1) * strideA);
+    const char* B = reinterpret_cast<const char*>(baseB + (size_t)(k >> 1) * strideB);
+    const uint32_t par = (uint32_t)(k & 1) << 6;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q.a[i] = *(gf4*)(A + (offA[i] ^ par));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q.b[i] = *(gf4*)(B + (offB[i] ^ par));
   };
-  auto load = [&](int k, X3Raw& q) {
-    q.a0 = ld(baseA, strideA, k, ra0);
-    q.a1 = ld(baseA, strideA, k, ra1);
-    q.b0 = ld(baseB, strideB, k, rb0);
-    q.b1 = ld(baseB, strideB, k, rb1);
-  };
-  float bs0 = 0.0f, bs1 = 0.0f;  // partial row sums of delta (rows lrow, lrow + 128)
+  float bs[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // partial row sums of delta (rows lrow + 64 i)
   // chunk lc of row (t, xr) = samples 4 lc .. 4 lc + 3 = elements 4 (lc & 1) .. +3 of fragment lane
   // (h = lc >> 1, xr): one 8-B piece per (piece, row)
   auto put = [&](float* img, int row, const f32x4& v) {
@@ -251,78 +296,78 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
     dst[8 * 64 * 2] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3);
     dst[2 * 8 * 64 * 2] = __builtin_shufflevector(c0_, c1, 0, 1, 2, 3);
   };
-  auto split = [&](const X3Raw& q, int buf) {
+  // chunk i of the loader role (0..3: A rows, 4..7: B rows) -> image `buf`
+  auto split_chunk = [&](const X3Raw& q, int buf, int i) {
     float* img = lds + buf * 2 * kX3Frag;
-    if (lrow < nrA) {
-      put(img, lrow, q.a0);
-      bs0 += (q.a0[0] + q.a0[1]) + (q.a0[2] + q.a0[3]);
+    const int row = lrow + 64 * (i & 3);
+    if (i < 4) {
+      if (row < nrA) {
+        put(img, row, q.a[i]);
+        bs[i] += (q.a[i][0] + q.a[i][1]) + (q.a[i][2] + q.a[i][3]);
+      }
+    } else {
+      if (row < nrB) put(img + kX3Frag, row, q.b[i - 4]);
     }
-    if (lrow + 128 < nrA) {
-      put(img, lrow + 128, q.a1);
-      bs1 += (q.a1[0] + q.a1[1]) + (q.a1[2] + q.a1[3]);
-    }
-    if (lrow < nrB) put(img + kX3Frag, lrow, q.b0);
-    if (lrow + 128 < nrB) put(img + kX3Frag, lrow + 128, q.b1);
   };
 
   f32x16 acc[RB][CB];
 #pragma unroll
   for (int r = 0; r < RB; ++r)
 #pragma unroll
-    for (int c = 0; c < CB; ++c)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[r][c][e] = 0.0f;
-
-  auto mfma_step = [&](int k) {
-#ifndef NOF_DIAG_X3_NOMFMA
+    for (int c = 0; c < CB; ++c) acc[r][c] = f32x16{};
+  // k-step k: MFMAs on image k & 1, with the split of set `nx` (k-step k + 1) into image (k + 1) & 1
+  // spread over the row groups (two chunks each for RB = 4)
+  auto step = [&](int k, const X3Raw& nx) {
+    const bool do_split = k + 1 < K;
+    const bf16x8* FA = reinterpret_cast<const bf16x8*>(lds + (k & 1) * 2 * kX3Frag) + (lane & 63);
+    const bf16x8* FB = FA + kX3Frag / 4;
+    Frag3 fb[CB];
     if (active) {
-#else
-    if (active && K < 0) {
-#endif
-      const bf16x8* FA = reinterpret_cast<const bf16x8*>(lds + (k & 1) * 2 * kX3Frag) + lane;
-      const bf16x8* FB = FA + kX3Frag / 4;
 #pragma unroll
-      for (int c = 0; c < CB; ++c) {
-        Frag3 fb;
+      for (int c = 0; c < CB; ++c)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) fb.p[p] = FB[(p * 8 + colt[c]) * 64];
+        for (int p = 0; p < 3; ++p) fb[c].p[p] = FB[(p * 8 + colt[c]) * 64];
+    }
 #pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          Frag3 fa;
+    for (int r = 0; r < RB; ++r) {
+      if (active) {
+        Frag3 fa;
 #pragma unroll
-          for (int p = 0; p < 3; ++p) fa.p[p] = FA[(p * 8 + rowt[r]) * 64];
-          acc[r][c] = mfma_x3(fa, fb, acc[r][c]);
-        }
+        for (int p = 0; p < 3; ++p) fa.p[p] = FA[(p * 8 + rowt[r]) * 64];
+#pragma unroll
+        for (int pp = 0; pp < 6; ++pp)
+#pragma unroll
+          for (int c = 0; c < CB; ++c)
+            acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.p[x3_pa(pp)], fb[c].p[x3_pb(pp)], acc[r][c], 0, 0,
+                                                                 0);
+      }
+      if (do_split) {
+#pragma unroll
+        for (int i = (8 * r) / RB; i < (8 * (r + 1)) / RB; ++i) split_chunk(nx, (k + 1) & 1, i);
       }
     }
   };
-  // k-step k: k + 1's registers are split into image (k + 1) & 1 and refilled with k + 3's rows,
-  // image k & 1 feeds the MFMAs.  Two register sets rotate statically (loop unrolled by two).
-  X3Raw qa, qb;
-  {
-    X3Raw q0;
-    load(0, q0);
-    load(min(1, K - 1), qa);
-    load(min(2, K - 1), qb);
-    split(q0, 0);
-  }
+  X3Raw s0, s1;
+  load(0, s0);
+  load(min(1, K - 1), s1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) split_chunk(s0, 0, i);
+  load(min(2, K - 1), s0);
   lds_barrier();
-  auto step = [&](int k, X3Raw& next) {
-#ifndef NOF_DIAG_X3_NOSPLIT
-    if (k + 1 < K) split(next, (k + 1) & 1);
-#else
-    if (k + 1 < K && next.a0[0] == 12345.0f) split(next, (k + 1) & 1);
-#endif
-    load(min(k + 3, K - 1), next);  // unconditional (clamped): every path issues the same loads
-    mfma_step(k);
-    lds_barrier();
-  };
+  // at step k the sets hold k + 1 (split now, then refilled with k + 3) and k + 2
   int k = 0;
   for (; k + 2 <= K; k += 2) {
-    step(k, qa);
-    step(k + 1, qb);
+    step(k, s1);
+    load(min(k + 3, K - 1), s1);
+    lds_barrier();
+    step(k + 1, s0);
+    load(min(k + 4, K - 1), s0);
+    lds_barrier();
   }
-  if (k < K) step(k, qa);
+  if (k < K) {
+    step(k, s1);
+    lds_barrier();
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the clamped tail loads
   if (active) {
     float* slab = slabs + slab_off[item.slab];
@@ -340,14 +385,12 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
         }
       }
   }
-  {  // the 4 chunk-lanes of a row are lanes 4 lrow .. 4 lrow + 3
-    float v0 = bs0, v1 = bs1;
-    v0 += __shfl_xor(v0, 1, 64);
-    v0 += __shfl_xor(v0, 2, 64);
-    v1 += __shfl_xor(v1, 1, 64);
-    v1 += __shfl_xor(v1, 2, 64);
-    if (lrow < nrA && lc == 0) bias_slabs[(size_t)item.slab * 256 + lrow] = v0;
-    if (lrow + 128 < nrA && lc == 0) bias_slabs[(size_t)item.slab * 256 + lrow + 128] = v1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // the 4 chunk-lanes of a row are lanes 4 lrow' .. 4 lrow' + 3
+    float v = bs[i];
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    if (lrow + 64 * i < nrA && lc == 0) bias_slabs[(size_t)item.slab * 256 + lrow + 64 * i] = v;
   }
   __syncthreads();  // images are reused by the next item
 }
@@ -358,18 +401,20 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_x3(const WgProblem* _
                                                               const int64_t* __restrict__ slab_off, float* slabs,
                                                               float* bias_slabs) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int it0 = item_ptr[blockIdx.x], it1 = item_ptr[blockIdx.x + 1];
   for (int it = it0; it < it1; ++it) {
     const WgItem item = items[it];
     const WgProblem P = probs[item.prob];
-    const int RB = (P.ntr + 1) >> 1, CB = (P.ntc + 3) >> 2;  // same wave grid as k_wgrad
+    const int RB = (P.ntr + 1) >> 1, CB = (P.ntc + 1) >> 1;  // 2 x 2 wave grid
     switch (RB * 10 + CB) {
-      case 11: wg_item_x3<1, 1>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
-      case 21: wg_item_x3<2, 1>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
-      case 32: wg_item_x3<3, 2>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
-      case 41: wg_item_x3<4, 1>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
-      default: wg_item_x3<4, 2>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
+      case 11: wg_item_x3<1, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+      case 12: wg_item_x3<1, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+      case 21: wg_item_x3<2, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+      case 34: wg_item_x3<3, 4>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+      case 42: wg_item_x3<4, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+      default: wg_item_x3<4, 4>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
     }
   }
 }

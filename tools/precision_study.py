@@ -4,7 +4,7 @@ Runs the full two-level step in fp64 autograd with every dense-layer contraction
 simulated MFMA: operands rounded to `mode`'s input type, products accumulated exactly (fp64 here,
 fp32 on the device).  Reports per-tensor relative L2 error of the 22 gradients and the outputs vs
 the exact fp64 step.  Modes: f32, bf16, f16 (per-sample power-of-2 scaling of the backward
-deltas), f16x2 (hi + lo split, 3 products), bf16x3 (3-way split, 6 products)."""
+deltas), f16x2 (hi + lo split, 3 products), bf16x2 (hi + mid, 3 products), bf16x3 (3-way split, 6 products)."""
 import sys, os
 import numpy as np
 import torch
@@ -27,6 +27,9 @@ def split(x, mode):
     if mode == "f16": return [rnd(x, torch.float16)]
     if mode == "f16x2":
         x = rnd(x, torch.float32); hi = rnd(x, torch.float16); lo = rnd(x - hi, torch.float16); return [hi, lo]
+    if mode == "bf16x2":
+        x = rnd(x, torch.float32); a = rnd(x, torch.bfloat16); b = rnd(x - a, torch.bfloat16)
+        return [a, b]
     if mode == "bf16x3":
         x = rnd(x, torch.float32); a = rnd(x, torch.bfloat16); b = rnd(x - a, torch.bfloat16); c = rnd(x - a - b, torch.bfloat16)
         return [a, b, c]
@@ -36,7 +39,7 @@ def mm(a, b, mode, scale_a=False):
     """a @ b with simulated split products; a's rows optionally power-of-2 scaled first."""
     s = col_scale(a) if scale_a else torch.ones_like(a[..., :1])
     A, B = split(a * s, mode), split(b, mode)
-    if mode == "f16x2":
+    if mode in ("f16x2", "bf16x2"):
         out = A[0] @ B[0] + A[0] @ B[1] + A[1] @ B[0]
     elif mode == "bf16x3":
         out = A[0] @ B[0] + A[0] @ B[1] + A[1] @ B[0] + A[1] @ B[1] + A[0] @ B[2] + A[2] @ B[0]
@@ -85,7 +88,7 @@ def main(n=48, samples=(64, 64)):
     TR.Net.forward = patched_forward
     sizes = [o * i for o, i in zip(net.outs, net.ins)] + list(net.outs)
     cuts = np.cumsum(sizes)[:-1]
-    for mode in ["f32", "bf16", "f16", "f16x2", "bf16x3"]:
+    for mode in ["f32", "bf16", "f16", "f16x2", "bf16x2", "bf16x3"]:
         QLinear.mode = mode
         r = TR.step(P, rays, samples=samples, seed=3, net=net, t_override={1: exact["t"][1]})
         errs = [np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)

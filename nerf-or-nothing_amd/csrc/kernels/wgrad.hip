@@ -214,8 +214,8 @@ __global__ __launch_bounds__(kWgThreads, 1) void k_wgrad(const WgProblem* __rest
 // tiles [wc CB, wc CB + CB) (up to 4 x 4 tiles = 256 accumulator registers), so the whole MFMA
 // stream of a CU runs from one wave per SIMD and each fragment read feeds RB or CB products.
 // Per 16-sample k-step (the 64-B half of every feature row of a chunk-swizzled block, common.h):
-//   * every thread loads 8 16-B chunks (4 rows of A, 4 of B; 16 rows x 64 contiguous bytes per
-//     wave-instruction) straight into registers, two k-steps ahead: two register sets rotate
+//   * every thread loads up to 8 16-B chunks (16 rows x 64 contiguous bytes per wave-instruction)
+//     straight into registers, two k-steps ahead: two register sets rotate
 //     statically (k loop unrolled by two), so up to 64 KB per CU are in flight.  Loads are
 //     unconditional (rows past the problem re-read its last row; steps past the end re-read the
 //     last step) so vmcnt counts are static;
@@ -228,8 +228,9 @@ constexpr int kWgX3Threads = 256;
 constexpr int kX3Frag = 3 * 8 * 64 * 4;  // floats per operand fragment image: [piece][tile][lane][16 B]
 constexpr int kX3Lds = 2 * 2 * kX3Frag;   // 96 KB
 
+template <int N>
 struct X3Raw {
-  f32x4 a[4], b[4];  // chunk lc of rows lrow + 64 i
+  f32x4 v[N];  // chunk c: concatenated row 64 c + lrow, chunk lc of the k-step
 };
 
 // LDS writes of this wave done, then a bare workgroup barrier; the "memory" clobber keeps the
@@ -240,11 +241,17 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 __device__ __forceinline__ constexpr int x3_pa(int pp) { return pp == 0 ? 2 : (pp == 2 || pp == 3) ? 1 : 0; }
 __device__ __forceinline__ constexpr int x3_pb(int pp) { return pp == 1 ? 2 : (pp == 2 || pp == 4) ? 1 : 0; }
 
+// Loader roles: the k-step's rows are the concatenation [A rows 0..nrA) ++ [B rows 0..nrB); thread
+// tid moves chunk lc = tid & 3 of concatenated rows R = 64 c + (tid >> 2), c < NCH = RB + CB (the
+// grid's problem has at most 64 (RB + CB) rows).  A 16-row group of one wave never straddles the
+// A/B boundary (both are multiples of 32 rows), so operand choice is wave-uniform and no chunk is
+// wasted on rows outside the problem (only the last chunk can fall past the end: skipped).
 template <int RB, int CB>
 __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& P, float* lds, int tid, int wave,
                                            float* slabs, float* bias_slabs, const int64_t* slab_off) {
-  // opaque thread index: the lane-derived offsets of the five instantiations are recomputed per
-  // item instead of being hoisted to the kernel entry all at once (they would spill)
+  constexpr int NCH = RB + CB;
+  // opaque thread index: the lane-derived offsets of the instantiations are recomputed per item
+  // instead of being hoisted to the kernel entry all at once (they would spill)
   int tq = tid;
   asm volatile("" : "+v"(tq));
   tid = tq;
@@ -259,30 +266,40 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
 #pragma unroll
   for (int c = 0; c < CB; ++c) colt[c] = min(c0 + c, P.ntc - 1);
   const size_t strideA = (size_t)P.FA * kBlk, strideB = (size_t)P.FB * kBlk;
-  const int nrA = P.ntr * 32, nrB = P.ntc * 32;
-  const int lc = tid & 3, lrow = tid >> 2;  // loader role: rows lrow + 64 i, chunk lc
+  const int nrA = P.ntr * 32, nrB = P.ntc * 32, nrT = nrA + nrB;
+  const int lc = tid & 3, lrow = tid >> 2;
+  const int wrow = __builtin_amdgcn_readfirstlane(lrow & ~15);  // the wave's first row (uniform)
   const float* baseA = P.A + (size_t)item.kb0 * strideA + (size_t)P.a_row0 * kBlk;
   const float* baseB = P.B + (size_t)item.kb0 * strideB + (size_t)P.b_col0 * kBlk;
   const int K = 2 * (item.kb1 - item.kb0);
-  // byte offset of chunk lc of row `row` in an even k-step (odd: ^ 64, chunk 4 + lc)
-  uint32_t offA[4], offB[4];
+  // per chunk: operand (uniform), operand row, and byte offset in an even k-step (odd: ^ 64)
+  uint32_t off[NCH];
+  int orow[NCH];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int ra = min(lrow + 64 * i, nrA - 1), rb = min(lrow + 64 * i, nrB - 1);
-    offA[i] = (uint32_t)(ra * kBlk * 4 + ((lc ^ (ra & 7)) << 4));
-    offB[i] = (uint32_t)(rb * kBlk * 4 + ((lc ^ (rb & 7)) << 4));
+  for (int c = 0; c < NCH; ++c) {
+    const int R = 64 * c + lrow;
+    const bool isA = 64 * c + wrow < nrA;
+    const int rr = isA ? R : min(R - nrA, nrB - 1);
+    orow[c] = isA ? R : R - nrA;
+    off[c] = (uint32_t)(rr * kBlk * 4 + ((lc ^ (rr & 7)) << 4));
   }
   typedef const __attribute__((address_space(1))) f32x4 gf4;
-  auto load = [&](int k, X3Raw& q) {  // global (not flat) loads: flat_load would count in lgkmcnt
+  auto load = [&](int k, X3Raw<NCH>& q) {  // global (not flat) loads: flat_load would count in lgkmcnt
+#ifdef NOF_DIAG_X3_SAMEK
+    k &= 1;
+#endif
     const char* A = reinterpret_cast<const char*>(baseA + (size_t)(k >> 1) * strideA);
     const char* B = reinterpret_cast<const char*>(baseB + (size_t)(k >> 1) * strideB);
     const uint32_t par = (uint32_t)(k & 1) << 6;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) q.a[i] = *(gf4*)(A + (offA[i] ^ par));
-#pragma unroll
-    for (int i = 0; i < 4; ++i) q.b[i] = *(gf4*)(B + (offB[i] ^ par));
+    for (int c = 0; c < NCH; ++c) {
+      const bool isA = 64 * c + wrow < nrA;  // uniform: scalar select of the base
+      q.v[c] = *(gf4*)((isA ? A : B) + (off[c] ^ par));
+    }
   };
-  float bs[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // partial row sums of delta (rows lrow + 64 i)
+  float bs[NCH];  // partial row sums of delta (A chunks only)
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) bs[c] = 0.0f;
   // chunk lc of row (t, xr) = samples 4 lc .. 4 lc + 3 = elements 4 (lc & 1) .. +3 of fragment lane
   // (h = lc >> 1, xr): one 8-B piece per (piece, row)
   auto put = [&](float* img, int row, const f32x4& v) {
@@ -296,18 +313,15 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
     dst[8 * 64 * 2] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3);
     dst[2 * 8 * 64 * 2] = __builtin_shufflevector(c0_, c1, 0, 1, 2, 3);
   };
-  // chunk i of the loader role (0..3: A rows, 4..7: B rows) -> image `buf`
-  auto split_chunk = [&](const X3Raw& q, int buf, int i) {
-    float* img = lds + buf * 2 * kX3Frag;
-    const int row = lrow + 64 * (i & 3);
-    if (i < 4) {
-      if (row < nrA) {
-        put(img, row, q.a[i]);
-        bs[i] += (q.a[i][0] + q.a[i][1]) + (q.a[i][2] + q.a[i][3]);
-      }
-    } else {
-      if (row < nrB) put(img + kX3Frag, row, q.b[i - 4]);
-    }
+  // chunk c -> image `buf` (A or B half); live = false (the last step's clamped duplicate) keeps it
+  // out of the bias sums
+  auto split_chunk = [&](const X3Raw<NCH>& q, int buf, int c, bool live) {
+    const bool isA = 64 * c + wrow < nrA;
+    if (c == NCH - 1 && 64 * c + wrow >= nrT) return;  // past the problem (uniform)
+    float* img = lds + buf * 2 * kX3Frag + (isA ? 0 : kX3Frag);
+    put(img, orow[c], q.v[c]);
+    const float sum = (q.v[c][0] + q.v[c][1]) + (q.v[c][2] + q.v[c][3]);
+    bs[c] += (live && isA) ? sum : 0.0f;
   };
 
   f32x16 acc[RB][CB];
@@ -315,43 +329,58 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
   for (int r = 0; r < RB; ++r)
 #pragma unroll
     for (int c = 0; c < CB; ++c) acc[r][c] = f32x16{};
-  // k-step k: MFMAs on image k & 1, with the split of set `nx` (k-step k + 1) into image (k + 1) & 1
-  // spread over the row groups (two chunks each for RB = 4)
-  auto step = [&](int k, const X3Raw& nx) {
-    const bool do_split = k + 1 < K;
+  // k-step k: MFMAs on image k & 1 (every wave, on clamped tiles if inactive: no branches), with
+  // the split of set `nx` (k-step k + 1) into image (k + 1) & 1 spread over the MFMA groups and the
+  // next row group's A fragment read one group ahead.  The last step splits a clamped duplicate
+  // nobody reads rather than branching.
+  auto step = [&](int k, const X3Raw<NCH>& nx) {
+    const bool live = k + 1 < K;
     const bf16x8* FA = reinterpret_cast<const bf16x8*>(lds + (k & 1) * 2 * kX3Frag) + (lane & 63);
     const bf16x8* FB = FA + kX3Frag / 4;
-    Frag3 fb[CB];
-    if (active) {
+    Frag3 fb[CB], fa;
+#ifdef NOF_WG_SPLIT_FRONT
 #pragma unroll
-      for (int c = 0; c < CB; ++c)
+    for (int c = 0; c < NCH; ++c) split_chunk(nx, (k + 1) & 1, c, live);
+#endif
 #pragma unroll
-        for (int p = 0; p < 3; ++p) fb[c].p[p] = FB[(p * 8 + colt[c]) * 64];
-    }
+    for (int c = 0; c < CB; ++c)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fb[c].p[p] = FB[(p * 8 + colt[c]) * 64];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) fa.p[p] = FA[(p * 8 + rowt[0]) * 64];
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
-      if (active) {
-        Frag3 fa;
+      Frag3 fn = fa;
+      if (r + 1 < RB) {
 #pragma unroll
-        for (int p = 0; p < 3; ++p) fa.p[p] = FA[(p * 8 + rowt[r]) * 64];
-#pragma unroll
-        for (int pp = 0; pp < 6; ++pp)
-#pragma unroll
-          for (int c = 0; c < CB; ++c)
-            acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.p[x3_pa(pp)], fb[c].p[x3_pb(pp)], acc[r][c], 0, 0,
-                                                                 0);
+        for (int p = 0; p < 3; ++p) fn.p[p] = FA[(p * 8 + rowt[r + 1]) * 64];
       }
-      if (do_split) {
 #pragma unroll
-        for (int i = (8 * r) / RB; i < (8 * (r + 1)) / RB; ++i) split_chunk(nx, (k + 1) & 1, i);
+      for (int pp = 0; pp < 6; ++pp) {
+#ifndef NOF_DIAG_X3_NOMFMA
+#pragma unroll
+        for (int c = 0; c < CB; ++c)
+          acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.p[x3_pa(pp)], fb[c].p[x3_pb(pp)], acc[r][c], 0, 0, 0);
+#endif
+#ifndef NOF_WG_SPLIT_FRONT
+        // chunks [NCH r / RB, NCH (r + 1) / RB): one after each MFMA group, the rest after the last
+        const int i0 = (NCH * r) / RB, i1 = (NCH * (r + 1)) / RB;
+#pragma unroll
+        for (int i = i0 + pp; i < (pp == 5 ? i1 : min(i0 + pp + 1, i1)); ++i)
+#ifdef NOF_DIAG_X3_NOSPLIT
+          if (nx.v[0][0] == 12345.0f)
+#endif
+            split_chunk(nx, (k + 1) & 1, i, live);
+#endif
       }
+      fa = fn;
     }
   };
-  X3Raw s0, s1;
+  X3Raw<NCH> s0, s1;
   load(0, s0);
   load(min(1, K - 1), s1);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) split_chunk(s0, 0, i);
+  for (int c = 0; c < NCH; ++c) split_chunk(s0, 0, c, true);
   load(min(2, K - 1), s0);
   lds_barrier();
   // at step k the sets hold k + 1 (split now, then refilled with k + 3) and k + 2
@@ -386,11 +415,12 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
       }
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {  // the 4 chunk-lanes of a row are lanes 4 lrow' .. 4 lrow' + 3
-    float v = bs[i];
+  for (int c = 0; c < NCH; ++c) {  // the 4 chunk-lanes of a row are lanes 4 lrow' .. 4 lrow' + 3
+    float v = bs[c];
     v += __shfl_xor(v, 1, 64);
     v += __shfl_xor(v, 2, 64);
-    if (lrow + 64 * i < nrA && lc == 0) bias_slabs[(size_t)item.slab * 256 + lrow + 64 * i] = v;
+    const int R = 64 * c + lrow;
+    if (R < nrA && lc == 0) bias_slabs[(size_t)item.slab * 256 + R] = v;
   }
   __syncthreads();  // images are reused by the next item
 }

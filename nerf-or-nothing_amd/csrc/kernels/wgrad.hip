@@ -342,12 +342,23 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
 #pragma unroll
     for (int c = 0; c < NCH; ++c) split_chunk(nx, (k + 1) & 1, c, live);
 #endif
+    // first row group's fragments in the order its MFMAs consume them (lo.hi, hi.lo, mid.mid, ...):
+    // the first MFMAs start after two reads instead of after all of them
 #pragma unroll
-    for (int c = 0; c < CB; ++c)
+    for (int pp = 0; pp < 6; ++pp) {
+      const int pa = x3_pa(pp), pb = x3_pb(pp);
+      bool a_new = true, b_new = true;
 #pragma unroll
-      for (int p = 0; p < 3; ++p) fb[c].p[p] = FB[(p * 8 + colt[c]) * 64];
+      for (int q = 0; q < pp; ++q) {
+        a_new = a_new && x3_pa(q) != pa;
+        b_new = b_new && x3_pb(q) != pb;
+      }
+      if (a_new) fa.p[pa] = FA[(pa * 8 + rowt[0]) * 64];
+      if (b_new) {
 #pragma unroll
-    for (int p = 0; p < 3; ++p) fa.p[p] = FA[(p * 8 + rowt[0]) * 64];
+        for (int c = 0; c < CB; ++c) fb[c].p[pb] = FB[(pb * 8 + colt[c]) * 64];
+      }
+    }
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
       Frag3 fn = fa;

@@ -41,12 +41,24 @@ __device__ __forceinline__ void slice_dma(const float* __restrict__ src, float* 
 // layers spread a slice's steps over the first MFMA groups of the previous slice instead of
 // issuing them as one burst, which would queue 4 waves x 8-12 requests on the CU's texture unit
 // and stall every wave's MFMA issue behind it.
+#ifndef NOF_DMA_GLOBAL
+// buffer_load_dwordx4 ... lds: the slice base lives in the (scalar) buffer descriptor, the step in
+// soffset and the lane's 16 B in a constant voffset, so a step costs no per-lane address math.
+__device__ __forceinline__ void slice_dma_step(const float* __restrict__ src, float* dst, int tid, int i) {
+  const int wave = tid >> 6;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0,
+                                                                        0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lptr_t)(dst + (kMlpThreads * i + 64 * wave) * 4), 16, tid * 16,
+                                           i * kMlpThreads * 16, 0, 0);
+}
+#else
 __device__ __forceinline__ void slice_dma_step(const float* __restrict__ src, float* dst, int tid, int i) {
   const int wave = tid >> 6;
   const int chunk = kMlpThreads * i + tid;
   __builtin_amdgcn_global_load_lds((gptr_t)(src + chunk * 4), (lptr_t)(dst + (kMlpThreads * i + 64 * wave) * 4), 16,
                                    0, 0);
 }
+#endif
 
 // Per-wave LDS copy of the 48 IPE B-operands: [tp][q][lane][4] floats (12 KB / wave).
 constexpr int kIpeLdsFloats = 3 * 4 * 64 * 4;
@@ -84,10 +96,18 @@ template <int OT> constexpr int f32_parts_after_dma() {
   for (int q = 0; q < 4; ++q) n += (q * OT + 1 > 7) ? 1 : 0;
   return n;
 }
-// split layer (the 48-KB slice is 12 steps, checked below): two DMA steps in each of groups 0..5; parts in groups s OT + 1 and s OT + OT/2 + 1
+// split layer (the 48-KB slice is 12 steps, checked below): kX3DmaPer DMA steps in each of the first
+// groups; parts in groups s OT + 1 and s OT + OT/2 + 1
+#ifndef NOF_X3_DMA_PER_GROUP
+#define NOF_X3_DMA_PER_GROUP 2
+#endif
+constexpr int kX3DmaPer = NOF_X3_DMA_PER_GROUP;                       // DMA steps per MFMA group
+constexpr int kX3DmaGroups = (12 + kX3DmaPer - 1) / kX3DmaPer;       // groups carrying DMA steps
+static_assert(kX3DmaGroups <= 8, "the OT = 4 layer has 8 MFMA groups per slice");
 template <int OT> constexpr int x3_parts_after_dma() {
   int n = 0;
-  for (int s = 0; s < 2; ++s) n += ((s * OT + 1 > 5) ? 1 : 0) + ((s * OT + OT / 2 + 1 > 5) ? 1 : 0);
+  for (int s = 0; s < 2; ++s)
+    n += ((s * OT + 1 > kX3DmaGroups - 1) ? 1 : 0) + ((s * OT + OT / 2 + 1 > kX3DmaGroups - 1) ? 1 : 0);
   return n;
 }
 
@@ -307,9 +327,12 @@ __device__ __forceinline__ void mlp_layer_x3(const float (&bin)[8][16], const fl
           for (int p = 0; p < 3; ++p) a_nxt.p[p] = W[((s2 * 8 + ot2) * 3 + p) * 64];
         }
 #ifndef NOF_DIAG_NO_DMA
-        if (has_next && s * OT + ot < 6) {
-          slice_dma_step(wsrc + kX3SliceFloats, lds + (cur ^ 1) * kX3SliceFloats, tid, 2 * (s * OT + ot));
-          slice_dma_step(wsrc + kX3SliceFloats, lds + (cur ^ 1) * kX3SliceFloats, tid, 2 * (s * OT + ot) + 1);
+        if (has_next && s * OT + ot < kX3DmaGroups) {
+#pragma unroll
+          for (int u = 0; u < kX3DmaPer; ++u) {
+            const int st = kX3DmaPer * (s * OT + ot) + u;
+            if (st < 12) slice_dma_step(wsrc + kX3SliceFloats, lds + (cur ^ 1) * kX3SliceFloats, tid, st);
+          }
         }
 #endif
         __builtin_amdgcn_sched_barrier(0);

@@ -78,38 +78,15 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
   int cur = 0;
   for (int kb = item.kb0; kb < item.kb1; ++kb) {
     float* nxt = lds + (cur ^ 1) * 2 * kWgHalf;
-    const bool more = kb + 1 < item.kb1;
-    const float* srcA = Ab + (kb + 1) * strideA;
-    const float* srcB = Bb + (kb + 1) * strideB;
-    // next block's DMA, two of its (up to) 4 + 4 wave-instructions per chunk pair, so the
-    // texture unit sees a steady trickle instead of one burst that stalls every wave's issue
-    auto dma_steps = [&](int cc) {
-#ifdef NOF_DIAG_WG_NODMA
-      if (more && kb < 0) {
-#else
-      if (more) {
-#endif
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int st = 2 * cc + u;
-          const int f4 = (st & 3) * kWgThreads + tid;
-          if (st < 4) {
-            if (f4 < nA4) __builtin_amdgcn_global_load_lds((wg_gptr_t)(srcA + f4 * 4),
-                                                           (wg_lptr_t)(nxt + (f4 - lane) * 4), 16, 0, 0);
-          } else {
-            if (f4 < nB4) __builtin_amdgcn_global_load_lds((wg_gptr_t)(srcB + f4 * 4),
-                                                           (wg_lptr_t)(nxt + kWgHalf + (f4 - lane) * 4), 16, 0, 0);
-          }
-        }
-      }
-    };
+    if (kb + 1 < item.kb1) {
+      blk_dma(Ab + (kb + 1) * strideA, nxt, nA4, tid);
+      blk_dma(Bb + (kb + 1) * strideB, nxt + kWgHalf, nB4, tid);
+    }
     if (active) {
       const float* LA = lds + cur * 2 * kWgHalf;
       const float* LB = LA + kWgHalf;
       // lane half h reads chunk 2cc + h (samples 8cc + 4h .. +3); MFMA i of the group then sums
-      // k = {8cc + i, 8cc + 4 + i}, the same pairing for A and B.  Chunk pair cc + 1 is read
-      // while cc's MFMAs run (the fences keep hipcc from hoisting all reads to the top, which
-      // would stall both waves of a SIMD on LDS at the same time after every barrier).
+      // k = {8cc + i, 8cc + 4 + i}, the same pairing for A and B
       f32x4 a[RB], b[CB];
 #pragma unroll
       for (int r = 0; r < RB; ++r) a[r] = *reinterpret_cast<const f32x4*>(LA + aoff[r] + ((h ^ xs) << 2));
@@ -118,23 +95,13 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
 #pragma unroll
       for (int cc = 0; cc < 4; ++cc) {
         f32x4 an[RB], bn[CB];
-#pragma unroll
-        for (int r = 0; r < RB; ++r) asm volatile("" ::"v"(a[r]));
-#pragma unroll
-        for (int c = 0; c < CB; ++c) asm volatile("" ::"v"(b[c]));
-        dma_steps(cc);
-#ifdef NOF_DIAG_WG_NOREAD
-        if (cc < 3 && kb < 0) {
-#else
         if (cc < 3) {
-#endif
           const int ch = ((2 * (cc + 1) + h) ^ xs) << 2;
 #pragma unroll
           for (int r = 0; r < RB; ++r) an[r] = *reinterpret_cast<const f32x4*>(LA + aoff[r] + ch);
 #pragma unroll
           for (int c = 0; c < CB; ++c) bn[c] = *reinterpret_cast<const f32x4*>(LB + boff[c] + ch);
         }
-        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -143,7 +110,6 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
             for (int c = 0; c < CB; ++c) acc[r][c] = mfma32(a[r][i], b[c][i], acc[r][c]);
             bs[r] += a[r][i];
           }
-        __builtin_amdgcn_sched_barrier(0);
         if (cc < 3) {
 #pragma unroll
           for (int r = 0; r < RB; ++r) a[r] = an[r];
@@ -151,14 +117,8 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
           for (int c = 0; c < CB; ++c) b[c] = bn[c];
         }
       }
-    } else {
-#pragma unroll
-      for (int cc = 0; cc < 4; ++cc) dma_steps(cc);
     }
-    // the DMA above must have landed (vmcnt) and this block's LDS reads retired before the swap
-#ifndef NOF_DIAG_WG_NOBAR
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
+    __syncthreads();
     cur ^= 1;
   }
   if (active) {

@@ -260,14 +260,15 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M) {
 
   // cost per k-block (wgrad.hip): MFMA time of the busiest SIMD vs staging bytes (4 KB per 32-row
   // operand block).  fp32: 2 x 4 waves of RB x CB tiles, ~16 KB per MFMA round keeps a CU under its
-  // HBM share.  split: 2 x 2 waves (one per SIMD) of RB x CB tiles, six bf16 MFMAs per product —
-  // a 32-row block of loads costs about one tile's MFMAs at the CU's HBM share.
+  // HBM share.  split: 2 x C waves (C/2 per SIMD) of RB x CB tiles, six bf16 MFMAs per product — a
+  // 32-row block of loads costs about one tile's MFMAs at the CU's HBM share.
   std::vector<int64_t> cost(P.size());
   int64_t total = 0;
   for (size_t i = 0; i < P.size(); ++i) {
     if (split_) {
-      const int RB = (P[i].ntr + 1) / 2, CB = (P[i].ntc + 1) / 2;
-      cost[i] = std::max(RB * CB, P[i].ntr + P[i].ntc);
+      const int WC = nof::wgrad_x3_grid_cols();  // C/2 waves per SIMD
+      const int RB = (P[i].ntr + 1) / 2, CB = (P[i].ntc + WC - 1) / WC;
+      cost[i] = std::max(RB * CB * WC / 2, P[i].ntr + P[i].ntc);
     } else {
       const int RB = (P[i].ntr + 1) / 2, CB = (P[i].ntc + 3) / 4;
       cost[i] = std::max(RB * CB, (P[i].ntr + P[i].ntc + 3) / 4);

@@ -78,6 +78,7 @@ struct WgOut {
 };
 hipError_t launch_wgrad(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,
                         const int64_t* slab_off, float* slabs, float* bias_slabs, hipStream_t st);
+int wgrad_x3_grid_cols();  // columns of k_wgrad_x3's 2 x C wave grid (schedule cost model)
 hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,
                         const int64_t* slab_off, float* slabs, float* bias_slabs, hipStream_t st);
 hipError_t launch_wgrad_reduce(const WgOut* outs, int nouts, int max_elems, const WgItem* items,

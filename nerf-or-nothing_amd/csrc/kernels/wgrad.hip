@@ -184,13 +184,18 @@ __global__ __launch_bounds__(kWgThreads, 1) void k_wgrad(const WgProblem* __rest
 //     previous k-step, whose fragments are one conflict-free ds_read_b128 each;
 //   * one bare barrier per k-step (lgkmcnt(0) + s_barrier: __syncthreads' release fence would
 //     wait for the loads in flight).
-constexpr int kWgX3Threads = 256;
+#ifndef NOF_X3_WC
+#define NOF_X3_WC 4
+#endif
+constexpr int kX3WC = NOF_X3_WC;                  // wave-grid columns (2 rows): 4 -> 8 waves, 2 per SIMD
+constexpr int kWgX3Threads = 64 * 2 * kX3WC;
+constexpr int kX3RowsPerC = kWgX3Threads / 4;      // concatenated rows one loader chunk index covers
 constexpr int kX3Frag = 3 * 8 * 64 * 4;  // floats per operand fragment image: [piece][tile][lane][16 B]
 constexpr int kX3Lds = 2 * 2 * kX3Frag;   // 96 KB
 
 template <int N>
 struct X3Raw {
-  f32x4 v[N];  // chunk c: concatenated row 64 c + lrow, chunk lc of the k-step
+  f32x4 v[N];  // chunk c: concatenated row kX3RowsPerC c + lrow, chunk lc of the k-step
 };
 
 // LDS writes of this wave done, then a bare workgroup barrier; the "memory" clobber keeps the
@@ -209,7 +214,8 @@ __device__ __forceinline__ constexpr int x3_pb(int pp) { return pp == 1 ? 2 : (p
 template <int RB, int CB>
 __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& P, float* lds, int tid, int wave,
                                            float* slabs, float* bias_slabs, const int64_t* slab_off) {
-  constexpr int NCH = RB + CB;
+  // chunks per thread: the grid's largest problem has 2 RB + kX3WC CB row tiles of 128 chunks
+  constexpr int NCH = ((2 * RB + kX3WC * CB) * 128 + kWgX3Threads - 1) / kWgX3Threads;
   // opaque thread index: the lane-derived offsets of the instantiations are recomputed per item
   // instead of being hoisted to the kernel entry all at once (they would spill)
   int tq = tid;
@@ -217,7 +223,7 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
   tid = tq;
   const int lane = tq & 63;
   const int h = lane >> 5, x = lane & 31;
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = wave / kX3WC, wc = wave % kX3WC;
   const int r0 = wr * RB, c0 = wc * CB;
   const bool active = r0 < P.ntr && c0 < P.ntc;  // wave-uniform
   int rowt[RB], colt[CB];
@@ -237,8 +243,8 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
   int orow[NCH];
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    const int R = 64 * c + lrow;
-    const bool isA = 64 * c + wrow < nrA;
+    const int R = kX3RowsPerC * c + lrow;
+    const bool isA = kX3RowsPerC * c + wrow < nrA;
     const int rr = isA ? R : min(R - nrA, nrB - 1);
     orow[c] = isA ? R : R - nrA;
     off[c] = (uint32_t)(rr * kBlk * 4 + ((lc ^ (rr & 7)) << 4));
@@ -253,7 +259,7 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
     const uint32_t par = (uint32_t)(k & 1) << 6;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      const bool isA = 64 * c + wrow < nrA;  // uniform: scalar select of the base
+      const bool isA = kX3RowsPerC * c + wrow < nrA;  // uniform: scalar select of the base
       q.v[c] = *(gf4*)((isA ? A : B) + (off[c] ^ par));
     }
   };
@@ -276,8 +282,8 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
   // chunk c -> image `buf` (A or B half); live = false (the last step's clamped duplicate) keeps it
   // out of the bias sums
   auto split_chunk = [&](const X3Raw<NCH>& q, int buf, int c, bool live) {
-    const bool isA = 64 * c + wrow < nrA;
-    if (c == NCH - 1 && 64 * c + wrow >= nrT) return;  // past the problem (uniform)
+    const bool isA = kX3RowsPerC * c + wrow < nrA;
+    if (c == NCH - 1 && kX3RowsPerC * c + wrow >= nrT) return;  // past the problem (uniform)
     float* img = lds + buf * 2 * kX3Frag + (isA ? 0 : kX3Frag);
     put(img, orow[c], q.v[c]);
     const float sum = (q.v[c][0] + q.v[c][1]) + (q.v[c][2] + q.v[c][3]);
@@ -390,7 +396,7 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
     float v = bs[c];
     v += __shfl_xor(v, 1, 64);
     v += __shfl_xor(v, 2, 64);
-    const int R = 64 * c + lrow;
+    const int R = kX3RowsPerC * c + lrow;
     if (R < nrA && lc == 0) bias_slabs[(size_t)item.slab * 256 + R] = v;
   }
   __syncthreads();  // images are reused by the next item
@@ -408,17 +414,29 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_x3(const WgProblem* _
   for (int it = it0; it < it1; ++it) {
     const WgItem item = items[it];
     const WgProblem P = probs[item.prob];
-    const int RB = (P.ntr + 1) >> 1, CB = (P.ntc + 1) >> 1;  // 2 x 2 wave grid
-    switch (RB * 10 + CB) {
-      case 11: wg_item_x3<1, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-      case 12: wg_item_x3<1, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-      case 21: wg_item_x3<2, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-      case 34: wg_item_x3<3, 4>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-      case 42: wg_item_x3<4, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-      default: wg_item_x3<4, 4>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+    const int RB = (P.ntr + 1) >> 1, CB = (P.ntc + kX3WC - 1) / kX3WC;  // 2 x kX3WC wave grid
+    if constexpr (kX3WC == 2) {
+      switch (RB * 10 + CB) {
+        case 11: wg_item_x3<1, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        case 12: wg_item_x3<1, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        case 21: wg_item_x3<2, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        case 34: wg_item_x3<3, 4>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        case 42: wg_item_x3<4, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        default: wg_item_x3<4, 4>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+      }
+    } else {
+      switch (RB * 10 + CB) {
+        case 11: wg_item_x3<1, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        case 21: wg_item_x3<2, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        case 32: wg_item_x3<3, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        case 41: wg_item_x3<4, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        default: wg_item_x3<4, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+      }
     }
   }
 }
+
+int wgrad_x3_grid_cols() { return kX3WC; }
 
 hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,
                            const int64_t* slab_off, float* slabs, float* bias_slabs, hipStream_t st) {

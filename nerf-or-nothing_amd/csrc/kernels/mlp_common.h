@@ -235,6 +235,10 @@ __device__ __forceinline__ void split44(const f32x4& u, const f32x4& v, Frag3& f
   split8(e, f);
 }
 
+// product order of mfma_x3 (smallest terms first): pieces of A and B for product pp
+__device__ __forceinline__ constexpr int x3_pa(int pp) { return pp == 0 ? 2 : (pp == 2 || pp == 3) ? 1 : 0; }
+__device__ __forceinline__ constexpr int x3_pb(int pp) { return pp == 1 ? 2 : (pp == 2 || pp == 4) ? 1 : 0; }
+
 __device__ __forceinline__ f32x16 mfma_x3(const Frag3& a, const Frag3& b, f32x16 c) {
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[2], b.p[0], c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[2], c, 0, 0, 0);

@@ -202,9 +202,6 @@ struct X3Raw {
 // compiler from moving LDS accesses across it.  Global loads in flight are NOT waited for.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// product order of mfma_x3 (smallest terms first): pieces of A and B for product pp
-__device__ __forceinline__ constexpr int x3_pa(int pp) { return pp == 0 ? 2 : (pp == 2 || pp == 3) ? 1 : 0; }
-__device__ __forceinline__ constexpr int x3_pb(int pp) { return pp == 1 ? 2 : (pp == 2 || pp == 4) ? 1 : 0; }
 
 // Loader roles: the k-step's rows are the concatenation [A rows 0..nrA) ++ [B rows 0..nrB); thread
 // tid moves chunk lc = tid & 3 of concatenated rows R = 64 c + (tid >> 2), c < NCH = RB + CB (the

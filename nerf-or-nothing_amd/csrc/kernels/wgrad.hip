@@ -18,17 +18,26 @@
 namespace nof {
 
 constexpr int kWgThreads = 512;       // 8 waves
-constexpr int kWgHalf = 256 * kBlk;   // floats per staged operand (max 256 rows x 32 samples)
+// LDS image of a staged operand: 8-row (1-KB) DMA pieces placed so that piece G starts 128 B past a
+// 256-B boundary when G & 2 (+ 256 B of padding per 4 pieces to make room).  A ds_read_b128 lane group
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31} and the same +32) reads rows from all four 8-row pieces of a
+// 32-row tile; with the chunk XOR alone rows r and r + 8 share banks (2-way on every operand read),
+// with the 128-B shift of pieces 2 and 3 every group covers the 16 bank slots once.
+__host__ __device__ constexpr int wg_piece_off(int g) { return g * 8 * kBlk + 64 * (g >> 2) + 32 * ((g >> 1) & 1); }
+constexpr int kWgHalf = wg_piece_off(32);  // floats per staged operand image (max 256 rows): 34 KB
+__device__ __forceinline__ int wg_row_off(int row) { return wg_piece_off(row >> 3) + (row & 7) * kBlk; }
 
 typedef const __attribute__((address_space(1))) void* wg_gptr_t;
 typedef __attribute__((address_space(3))) void* wg_lptr_t;
 
-// DMA `nf4` float4s (multiple of 64) from src to dst, 1 KB per wave-instruction.
+// DMA `nf4` float4s (multiple of 64) from src to the image dst, 1 KB (one 8-row piece) per
+// wave-instruction.
 template <int NT = kWgThreads>
 __device__ __forceinline__ void blk_dma(const float* __restrict__ src, float* dst, int nf4, int tid) {
   const int wave = tid >> 6, lane = tid & 63;
   for (int base = wave * 64; base < nf4; base += NT) {
-    __builtin_amdgcn_global_load_lds((wg_gptr_t)(src + (base + lane) * 4), (wg_lptr_t)(dst + base * 4), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((wg_gptr_t)(src + (base + lane) * 4), (wg_lptr_t)(dst + wg_piece_off(base >> 6)),
+                                     16, 0, 0);
   }
 }
 
@@ -67,9 +76,9 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
   // per-lane LDS row offsets (row 32*t + x of a block image; chunk c of that row at c ^ (x & 7))
   int aoff[RB], boff[CB];
 #pragma unroll
-  for (int r = 0; r < RB; ++r) aoff[r] = (rowt[r] * 32 + x) * kBlk;
+  for (int r = 0; r < RB; ++r) aoff[r] = wg_row_off(rowt[r] * 32 + x);
 #pragma unroll
-  for (int c = 0; c < CB; ++c) boff[c] = (colt[c] * 32 + x) * kBlk;
+  for (int c = 0; c < CB; ++c) boff[c] = wg_row_off(colt[c] * 32 + x);
   const int xs = x & 7;
 
   blk_dma(Ab + item.kb0 * strideA, lds, nA4, tid);
@@ -78,7 +87,11 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
   int cur = 0;
   for (int kb = item.kb0; kb < item.kb1; ++kb) {
     float* nxt = lds + (cur ^ 1) * 2 * kWgHalf;
+#ifdef NOF_DIAG_WG_NODMA
+    if (kb + 1 < item.kb1 && kb < 0) {
+#else
     if (kb + 1 < item.kb1) {
+#endif
       blk_dma(Ab + (kb + 1) * strideA, nxt, nA4, tid);
       blk_dma(Bb + (kb + 1) * strideB, nxt + kWgHalf, nB4, tid);
     }
@@ -95,7 +108,11 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
 #pragma unroll
       for (int cc = 0; cc < 4; ++cc) {
         f32x4 an[RB], bn[CB];
+#ifdef NOF_DIAG_WG_NOREAD
+        if (cc < 3 && kb < 0) {
+#else
         if (cc < 3) {
+#endif
           const int ch = ((2 * (cc + 1) + h) ^ xs) << 2;
 #pragma unroll
           for (int r = 0; r < RB; ++r) an[r] = *reinterpret_cast<const f32x4*>(LA + aoff[r] + ch);
@@ -475,7 +492,7 @@ __global__ void k_wgrad_reduce(const WgOut* __restrict__ outs, const WgItem* __r
 hipError_t launch_wgrad(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,
                         const int64_t* slab_off, float* slabs, float* bias_slabs, hipStream_t st) {
   if (num_wg <= 0) return hipSuccess;
-  const size_t shm = sizeof(float) * 4 * kWgHalf;  // 128 KB of the CU's 160 KB
+  const size_t shm = sizeof(float) * 4 * kWgHalf;  // 136 KB of the CU's 160 KB
   static bool attr = false;
   if (!attr) {
     const hipError_t e = hipFuncSetAttribute((const void*)k_wgrad, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);

@@ -27,26 +27,18 @@ __host__ __device__ constexpr int wg_piece_off(int g) { return g * 8 * kBlk + 64
 constexpr int kWgHalf = wg_piece_off(32);  // floats per staged operand image (max 256 rows): 34 KB
 __device__ __forceinline__ int wg_row_off(int row) { return wg_piece_off(row >> 3) + (row & 7) * kBlk; }
 
-typedef const __attribute__((address_space(1))) void* wg_gptr_t;
 typedef __attribute__((address_space(3))) void* wg_lptr_t;
-
-// DMA `nf4` float4s (multiple of 64) from src to the image dst, 1 KB (one 8-row piece) per
-// wave-instruction.
-template <int NT = kWgThreads>
-__device__ __forceinline__ void blk_dma(const float* __restrict__ src, float* dst, int nf4, int tid) {
-  const int wave = tid >> 6, lane = tid & 63;
-  for (int base = wave * 64; base < nf4; base += NT) {
-    __builtin_amdgcn_global_load_lds((wg_gptr_t)(src + (base + lane) * 4), (wg_lptr_t)(dst + wg_piece_off(base >> 6)),
-                                     16, 0, 0);
-  }
-}
 
 // One work item (problem P, k-blocks [kb0, kb1)) for a wave grid of 2 (rows) x 4 (cols): wave
 // (wr, wc) owns row tiles [wr*RB, wr*RB+RB) x col tiles [wc*CB, wc*CB+CB) of the problem's tile
 // grid, so 4 k-steps cost RB + CB conflict-free ds_read_b128 for 4*RB*CB MFMAs.  Operand reads are
 // unconditional (rows/cols clamped into range) and issued one k-step ahead; the MFMAs carry no
 // branches.  Tiles outside the problem are computed on clamped duplicates and never stored.
-template <int RB, int CB>
+// The four waves of a grid row read the same A (delta) rows, so each keeps its row tiles rotated
+// by wc and sums only its first one (row tile r0 + wc % RB) for the bias partial: one packed add
+// per 4 samples instead of RB, and every row tile summed by exactly one wave (wc < RB).  ROT needs
+// at least RB active column waves; narrower problems (ntc < 4 CB) keep wave column 0 summing all RB.
+template <int RB, int CB, bool ROT>
 __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, float* lds, int tid, int lane,
                                         int wave, float* slabs, float* bias_slabs, const int64_t* slab_off) {
   const int h = lane >> 5, x = lane & 31;
@@ -55,19 +47,20 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
   const bool active = r0 < P.ntr && c0 < P.ntc;  // wave-uniform
   int rowt[RB], colt[CB];
 #pragma unroll
-  for (int r = 0; r < RB; ++r) rowt[r] = min(r0 + r, P.ntr - 1);
+  for (int r = 0; r < RB; ++r) rowt[r] = min(r0 + (ROT ? (r + wc) % RB : r), P.ntr - 1);
 #pragma unroll
   for (int c = 0; c < CB; ++c) colt[c] = min(c0 + c, P.ntc - 1);
-  const int nA4 = P.ntr * 32 * kBlk / 4, nB4 = P.ntc * 32 * kBlk / 4;
   const float* Ab = P.A + (size_t)P.a_row0 * kBlk;
   const float* Bb = P.B + (size_t)P.b_col0 * kBlk;
   const size_t strideA = (size_t)P.FA * kBlk, strideB = (size_t)P.FB * kBlk;
 
   f32x16 acc[RB][CB];
-  float bs[RB];
+  // bias partials, two sample phases: row tile rowt[0] (ROT) or all RB row tiles
+  f32x2 bs[ROT ? 1 : RB];
+#pragma unroll
+  for (int r = 0; r < (ROT ? 1 : RB); ++r) bs[r] = f32x2{0.0f, 0.0f};
 #pragma unroll
   for (int r = 0; r < RB; ++r) {
-    bs[r] = 0.0f;
 #pragma unroll
     for (int c = 0; c < CB; ++c)
 #pragma unroll
@@ -81,20 +74,32 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
   for (int c = 0; c < CB; ++c) boff[c] = wg_row_off(colt[c] * 32 + x);
   const int xs = x & 7;
 
-  blk_dma(Ab + item.kb0 * strideA, lds, nA4, tid);
-  blk_dma(Bb + item.kb0 * strideB, lds + kWgHalf, nB4, tid);
+  // Staging in DMA steps: step j moves 1-KB piece wave + 8 j of the block's [A pieces ++ B pieces]
+  // (clamped: the surplus steps of narrower problems repeat the last piece).  Inside the k loop the
+  // NJ steps of the next block ride one per MFMA group of the first two k-step groups, so no wave
+  // stalls at a burst of VMEM issues while its SIMD's MFMA pipe waits.
+  constexpr int NJ = RB + 2 * CB;  // >= (pieces of the template's largest problem) / 8
+  const int npA = P.ntr * 4, npT = npA + P.ntc * 4;
+  // buffer_load...lds: block base in the scalar descriptor, piece in soffset, the lane's 16 B in a
+  // loop-invariant voffset (no per-lane 64-bit addresses to keep live across the MFMA stream)
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  auto dma_step = [&](int kbn, float* buf, int j) {
+    const int p = min(wv + 8 * j, npT - 1);
+    const bool isA = p < npA;  // wave-uniform
+    const int q = isA ? p : p - npA;
+    const float* base = isA ? Ab + (size_t)kbn * strideA : Bb + (size_t)kbn * strideB;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (wg_lptr_t)(buf + (isA ? 0 : kWgHalf) + wg_piece_off(q)), 16,
+                                             lane * 16, q * 1024, 0, 0);
+  };
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) dma_step(item.kb0, lds, j);
   __syncthreads();
   int cur = 0;
   for (int kb = item.kb0; kb < item.kb1; ++kb) {
     float* nxt = lds + (cur ^ 1) * 2 * kWgHalf;
-#ifdef NOF_DIAG_WG_NODMA
-    if (kb + 1 < item.kb1 && kb < 0) {
-#else
-    if (kb + 1 < item.kb1) {
-#endif
-      blk_dma(Ab + (kb + 1) * strideA, nxt, nA4, tid);
-      blk_dma(Bb + (kb + 1) * strideB, nxt + kWgHalf, nB4, tid);
-    }
+    const int kbn = min(kb + 1, item.kb1 - 1);  // the last block re-stages itself into the idle buffer
     if (active) {
       const float* LA = lds + cur * 2 * kWgHalf;
       const float* LB = LA + kWgHalf;
@@ -120,13 +125,17 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
           for (int c = 0; c < CB; ++c) bn[c] = *reinterpret_cast<const f32x4*>(LB + boff[c] + ch);
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int r = 0; r < (ROT ? 1 : RB); ++r) bs[r] += f32x2{a[r][0], a[r][1]} + f32x2{a[r][2], a[r][3]};
 #pragma unroll
-          for (int r = 0; r < RB; ++r) {
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int r = 0; r < RB; ++r)
 #pragma unroll
             for (int c = 0; c < CB; ++c) acc[r][c] = mfma32(a[r][i], b[c][i], acc[r][c]);
-            bs[r] += a[r][i];
-          }
+#ifndef NOF_DIAG_WG_NODMA
+          if (cc * 4 + i < NJ) dma_step(kbn, nxt, cc * 4 + i);
+#endif
+        }
         if (cc < 3) {
 #pragma unroll
           for (int r = 0; r < RB; ++r) a[r] = an[r];
@@ -134,6 +143,9 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
           for (int c = 0; c < CB; ++c) b[c] = bn[c];
         }
       }
+    } else {  // idle waves still move their pieces
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) dma_step(kbn, nxt, j);
     }
     __syncthreads();
     cur ^= 1;
@@ -145,7 +157,7 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
     for (int r = 0; r < RB; ++r)
 #pragma unroll
       for (int c = 0; c < CB; ++c) {
-        if (r0 + r < P.ntr && c0 + c < P.ntc) {
+        if (r0 + (ROT ? (r + wc) % RB : r) < P.ntr && c0 + c < P.ntc) {  // unclamped row tile in range
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const int row = rowt[r] * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
@@ -153,12 +165,13 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
           }
         }
       }
-    if (wc == 0) {  // column tile 0 owner: bias partial = row sums of delta over the item's samples
+    // bias partial = row sums of delta over the item's samples
 #pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        const float v = bs[r] + __shfl_xor(bs[r], 32, 64);
-        if (r0 + r < P.ntr && h == 0) bias_slabs[(size_t)item.slab * 256 + rowt[r] * 32 + x] = v;
-      }
+    for (int r = 0; r < (ROT ? 1 : RB); ++r) {
+      const bool owner = ROT ? (wc < RB && r0 + wc < P.ntr) : (wc == 0 && r0 + r < P.ntr);
+      const float s = bs[r][0] + bs[r][1];
+      const float v = s + __shfl_xor(s, 32, 64);
+      if (owner && h == 0) bias_slabs[(size_t)item.slab * 256 + rowt[r] * 32 + x] = v;
     }
   }
   __syncthreads();  // LDS ring reused by the next item
@@ -176,12 +189,14 @@ __global__ __launch_bounds__(kWgThreads, 1) void k_wgrad(const WgProblem* __rest
     const WgItem item = items[it];
     const WgProblem P = probs[item.prob];
     const int RB = (P.ntr + 1) >> 1, CB = (P.ntc + 3) >> 2;  // block per wave of the 2 x 4 wave grid
-    switch (RB * 10 + CB) {
-      case 11: wg_item<1, 1>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
-      case 21: wg_item<2, 1>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
-      case 32: wg_item<3, 2>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
-      case 41: wg_item<4, 1>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
-      default: wg_item<4, 2>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
+    const bool rot = min(4, (P.ntc + CB - 1) / CB) >= RB;     // enough active column waves
+    switch (RB * 100 + CB * 10 + rot) {
+      case 111: wg_item<1, 1, true>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
+      case 210: wg_item<2, 1, false>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
+      case 321: wg_item<3, 2, true>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
+      case 410: wg_item<4, 1, false>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
+      case 421: wg_item<4, 2, true>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
+      default: wg_item<4, 2, false>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
     }
   }
 }

@@ -230,7 +230,7 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M) {
   std::vector<nof::WgProblem> P;
   auto prob = [&](const float* A, int FA, int a0, int ntr, const float* B, int FB, int b0, int ntc) {
     nof::WgProblem p;
-    p.A = A; p.FA = FA; p.a_row0 = a0; p.ntr = ntr; p.B = B; p.FB = FB; p.b_col0 = b0; p.ntc = ntc;
+    p.A = A; p.FA = FA; p.a_row0 = a0; p.ntr = ntr; p.B = B; p.FB = FB; p.b_col0 = b0; p.ntc = ntc; p.shape = 0;
     P.push_back(p);
     return (int)P.size() - 1;
   };
@@ -270,8 +270,9 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M) {
       const int RB = (P[i].ntr + 1) / 2, CB = (P[i].ntc + WC - 1) / WC;
       cost[i] = std::max(RB * CB * WC / 2, P[i].ntr + P[i].ntc);
     } else {
-      const int RB = (P[i].ntr + 1) / 2, CB = (P[i].ntc + 3) / 4;
-      cost[i] = std::max(RB * CB, (P[i].ntr + P[i].ntc + 3) / 4);
+      int c2 = 0;
+      P[i].shape = nof::wgrad_shape(P[i].ntr, P[i].ntc, &c2);
+      cost[i] = std::max(c2, (P[i].ntr + P[i].ntc + 1) / 2);
     }
     total += cost[i] * nblk;
   }

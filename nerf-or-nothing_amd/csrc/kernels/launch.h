@@ -67,6 +67,7 @@ struct WgProblem {
   const float* A; const float* B;
   int FA, a_row0, ntr;   // A rows [a_row0, a_row0 + 32*ntr) of an [FA][32]-block buffer
   int FB, b_col0, ntc;   // B rows (= output columns) [b_col0, b_col0 + 32*ntc)
+  int shape;             // fp32 k_wgrad wave-grid shape (wgrad_shape); unused by k_wgrad_x3
 };
 struct WgItem { int prob, kb0, kb1; int slab; };  // slab = index into slab_off[]
 struct WgOut {
@@ -78,6 +79,9 @@ struct WgOut {
 };
 hipError_t launch_wgrad(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,
                         const int64_t* slab_off, float* slabs, float* bias_slabs, hipStream_t st);
+// fp32 k_wgrad: the cheapest wave-grid shape for an ntr x ntc tile problem; *cost2 = MFMA tiles of
+// its busiest SIMD per 16 k-steps (2 per 32x32 tile-k-block at two waves per SIMD)
+int wgrad_shape(int ntr, int ntc, int* cost2);
 int wgrad_x3_grid_cols();  // columns of k_wgrad_x3's 2 x C wave grid (schedule cost model)
 hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,
                         const int64_t* slab_off, float* slabs, float* bias_slabs, hipStream_t st);

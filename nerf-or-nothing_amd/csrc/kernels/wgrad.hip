@@ -29,20 +29,28 @@ __device__ __forceinline__ int wg_row_off(int row) { return wg_piece_off(row >> 
 
 typedef __attribute__((address_space(3))) void* wg_lptr_t;
 
-// One work item (problem P, k-blocks [kb0, kb1)) for a wave grid of 2 (rows) x 4 (cols): wave
+// fp32 wave-grid shapes (8 waves as (8 / GC) rows x GC columns, RB x CB 32x32 tiles per wave).
+// Wave w runs on SIMD w % 4, so a shape's cost is the MFMA time of its busiest SIMD (waves s and
+// s + 4); the host picks the cheapest shape per problem (wgrad_shape), so narrow problems (96- or
+// 32-column inputs, the 1-row density head, the 160-row view layer) keep all four SIMDs busy.
+struct WgShape { int gc, rb, cb, rot; };
+constexpr WgShape kWgShapes[] = {{4, 4, 2, 1}, {1, 1, 3, 1}, {1, 1, 1, 1}, {8, 5, 1, 1}, {8, 1, 1, 1}, {4, 4, 2, 0}};
+constexpr int kWgNumShapes = sizeof(kWgShapes) / sizeof(kWgShapes[0]);
+
+// One work item (problem P, k-blocks [kb0, kb1)) for a wave grid of GR = 8 / GC rows x GC cols: wave
 // (wr, wc) owns row tiles [wr*RB, wr*RB+RB) x col tiles [wc*CB, wc*CB+CB) of the problem's tile
 // grid, so 4 k-steps cost RB + CB conflict-free ds_read_b128 for 4*RB*CB MFMAs.  Operand reads are
 // unconditional (rows/cols clamped into range) and issued one k-step ahead; the MFMAs carry no
 // branches.  Tiles outside the problem are computed on clamped duplicates and never stored.
-// The four waves of a grid row read the same A (delta) rows, so each keeps its row tiles rotated
-// by wc and sums only its first one (row tile r0 + wc % RB) for the bias partial: one packed add
-// per 4 samples instead of RB, and every row tile summed by exactly one wave (wc < RB).  ROT needs
-// at least RB active column waves; narrower problems (ntc < 4 CB) keep wave column 0 summing all RB.
-template <int RB, int CB, bool ROT>
+// The waves of a grid row read the same A (delta) rows, so each keeps its row tiles rotated by wc
+// and sums only its first one (row tile r0 + wc % RB) for the bias partial: one packed add per 4
+// samples instead of RB, and every row tile summed by exactly one wave (wc < RB).  ROT needs at
+// least RB active column waves; otherwise wave column 0 sums all RB.
+template <int GC, int RB, int CB, bool ROT>
 __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, float* lds, int tid, int lane,
                                         int wave, float* slabs, float* bias_slabs, const int64_t* slab_off) {
   const int h = lane >> 5, x = lane & 31;
-  const int wr = wave >> 2, wc = wave & 3;
+  const int wr = wave / GC, wc = wave % GC;
   const int r0 = wr * RB, c0 = wc * CB;
   const bool active = r0 < P.ntr && c0 < P.ntc;  // wave-uniform
   int rowt[RB], colt[CB];
@@ -78,7 +86,7 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
   // (clamped: the surplus steps of narrower problems repeat the last piece).  Inside the k loop the
   // NJ steps of the next block ride one per MFMA group of the first two k-step groups, so no wave
   // stalls at a burst of VMEM issues while its SIMD's MFMA pipe waits.
-  constexpr int NJ = RB + 2 * CB;  // >= (pieces of the template's largest problem) / 8
+  constexpr int NJ = ((8 / GC) * RB + GC * CB + 1) / 2;  // >= (pieces of the largest problem) / 8
   const int npA = P.ntr * 4, npT = npA + P.ntc * 4;
   // buffer_load...lds: block base in the scalar descriptor, piece in soffset, the lane's 16 B in a
   // loop-invariant voffset (no per-lane 64-bit addresses to keep live across the MFMA stream)
@@ -147,7 +155,9 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
 #pragma unroll
       for (int j = 0; j < NJ; ++j) dma_step(kbn, nxt, j);
     }
+#ifndef NOF_DIAG_WG_NOBAR
     __syncthreads();
+#endif
     cur ^= 1;
   }
   if (active) {
@@ -188,15 +198,15 @@ __global__ __launch_bounds__(kWgThreads, 1) void k_wgrad(const WgProblem* __rest
   for (int it = it0; it < it1; ++it) {
     const WgItem item = items[it];
     const WgProblem P = probs[item.prob];
-    const int RB = (P.ntr + 1) >> 1, CB = (P.ntc + 3) >> 2;  // block per wave of the 2 x 4 wave grid
-    const bool rot = min(4, (P.ntc + CB - 1) / CB) >= RB;     // enough active column waves
-    switch (RB * 100 + CB * 10 + rot) {
-      case 111: wg_item<1, 1, true>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
-      case 210: wg_item<2, 1, false>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
-      case 321: wg_item<3, 2, true>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
-      case 410: wg_item<4, 1, false>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
-      case 421: wg_item<4, 2, true>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
-      default: wg_item<4, 2, false>(item, P, lds, tid, lane, wave, slabs, bias_slabs, slab_off); break;
+    switch (P.shape) {  // kWgShapes
+#define NOF_WG_CASE(i)                                                                                     \
+  case i:                                                                                                  \
+    wg_item<kWgShapes[i].gc, kWgShapes[i].rb, kWgShapes[i].cb, (bool)kWgShapes[i].rot>(item, P, lds, tid, lane, wave, \
+                                                                                      slabs, bias_slabs, slab_off); \
+    break;
+      NOF_WG_CASE(0) NOF_WG_CASE(1) NOF_WG_CASE(2) NOF_WG_CASE(3) NOF_WG_CASE(4)
+      default: NOF_WG_CASE(5)
+#undef NOF_WG_CASE
     }
   }
 }
@@ -466,6 +476,26 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_x3(const WgProblem* _
 }
 
 int wgrad_x3_grid_cols() { return kX3WC; }
+
+int wgrad_shape(int ntr, int ntc, int* cost2) {
+  int best = kWgNumShapes - 1, best_cost = 1 << 30;
+  for (int i = 0; i < kWgNumShapes; ++i) {
+    const WgShape& g = kWgShapes[i];
+    const int gr = 8 / g.gc;
+    if (gr * g.rb < ntr || g.gc * g.cb < ntc) continue;               // does not cover the problem
+    if (g.rot && std::min(g.gc, (ntc + g.cb - 1) / g.cb) < g.rb) continue;  // too few column waves
+    int c = 0;
+    for (int s = 0; s < 4; ++s) {                                     // busiest SIMD: waves s, s + 4
+      int t = 0;
+      for (int w = s; w < 8; w += 4)
+        if ((w / g.gc) * g.rb < ntr && (w % g.gc) * g.cb < ntc) t += g.rb * g.cb;
+      c = std::max(c, t);
+    }
+    if (c < best_cost) { best = i; best_cost = c; }
+  }
+  if (cost2) *cost2 = best_cost;
+  return best;
+}
 
 hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,
                            const int64_t* slab_off, float* slabs, float* bias_slabs, hipStream_t st) {

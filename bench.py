@@ -147,11 +147,29 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 via torch.distributed.run")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # NOF_BENCH_DIST_BACKEND=gloo rehearses the N > 1 launch path (sharding, global sum of loss
+    # multipliers, barriers, max-over-ranks timing) with several ranks on one GPU: the all-reduces go
+    # through host memory, so its timings are not a scaling measurement.  Default: nccl (= RCCL).
+    backend = os.environ.get("NOF_BENCH_DIST_BACKEND", "nccl")
+    if backend not in ("nccl", "gloo"):
+        raise SystemExit(f"NOF_BENCH_DIST_BACKEND={backend}: nccl or gloo")
+    dev_idx = local if backend == "nccl" else local % torch.cuda.device_count()
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+
+    def allreduce(t, op=dist.ReduceOp.SUM):
+        if backend == "nccl":
+            dist.all_reduce(t, op=op)
+        else:  # rehearsal: through host memory
+            h = t.cpu()
+            dist.all_reduce(h, op=op)
+            t.copy_(h)
 
     n = a.rays
     samples = a.samples
@@ -170,11 +188,11 @@ def main():
 
         obj = [NativeDP.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        native = NativeDP.init_rank(obj[0], world, rank, local)
+        native = NativeDP.init_rank(obj[0], world, rank, dev_idx)
 
     def measure(split):
         """W untimed + K timed training steps of one precision mode; returns (s, timing, psnr)."""
-        model = nof.AcceleratedMipNeRF(device=local, max_rays=n, num_samples=samples, seed=seed,
+        model = nof.AcceleratedMipNeRF(device=dev_idx, max_rays=n, num_samples=samples, seed=seed,
                                        stream=stream, precision=1 if split else 0)
         model.set_rng(seed, 0, rank * n)  # global ray ids: sharding never changes a sample
         opt = nof.AcceleratedAdamOptimizer(model.GetLayerSizes(), model.config)
@@ -189,7 +207,7 @@ def main():
             if native is not None:
                 native.allreduce_grads(model, stream)
             elif world > 1:
-                dist.all_reduce(grad_view)  # sum of per-shard gradient sums (no averaging: L is a sum)
+                allreduce(grad_view)  # sum of per-shard gradient sums (no averaging: L is a sum)
             opt.step(params, grads, nof.learning_rate_decay(k + 1))
 
         for k in range(a.warmup):
@@ -210,10 +228,20 @@ def main():
         dt = time.perf_counter() - t0
         timing = model.read_timing()
         model.enable_timing(False)
+        in_sync = None
         if world > 1:
             t = torch.tensor([dt], device=dev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            allreduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
+            # DP invariant: identical all-reduced gradients + identical Adam -> every
+            # rank holds bitwise-identical parameters; compare a checksum's max and min over ranks
+            pptr, P = model.mlp.flat_params()
+            pv = nof.device_tensor(pptr, (P,), device=dev).view(torch.int32).to(torch.int64)
+            cs = (pv * torch.arange(1, P + 1, device=dev, dtype=torch.int64)).sum().reshape(1)
+            hi, lo = cs.clone(), -cs
+            allreduce(hi, op=dist.ReduceOp.MAX)
+            allreduce(lo, op=dist.ReduceOp.MAX)
+            in_sync = bool(hi.item() == -lo.item())
         # fine-level PSNR of the last step's batch (MseToPsnr, MipHelpers.cs:672)
         last = pool[(a.warmup + a.steps - 1) % len(pool)]
         comp = model.level_numpy(len(samples) - 1)["comp_rgb"]
@@ -221,7 +249,7 @@ def main():
         psnr = -10.0 * math.log10(max(mse, 1e-12))
         opt.close()
         model.close()
-        return dt, timing, psnr
+        return dt, timing, psnr, in_sync
 
     def summarize(split, dt, timing):
         ms_step = dt * 1e3 / a.steps
@@ -253,7 +281,7 @@ def main():
         }
 
     split = a.precision == "split"
-    dt, timing, psnr = measure(split)
+    dt, timing, psnr, in_sync = measure(split)
     rays_per_s = n * world * a.steps / dt
     alt = None
     if world == 1 and not a.no_alt:
@@ -275,8 +303,12 @@ def main():
             "kernels": kernels,
             "psnr_fine": round(psnr, 3),
         }
+        if world > 1:
+            result["params_in_sync"] = in_sync
+            if backend != "nccl":
+                result["rehearsal"] = f"{backend}: {world} ranks on {torch.cuda.device_count()} GPU(s), not a scaling run"
         if alt is not None:  # the other precision mode, same workload (parity-tested at the same tolerance)
-            asplit, adt, atiming, apsnr = alt
+            asplit, adt, atiming, apsnr, _ = alt
             ams, akernels, aroof = summarize(asplit, adt, atiming)
             result["alt_precision"] = {
                 "precision": "split" if asplit else "f32", "value": round(n * a.steps / adt, 1), "unit": "rays/s",

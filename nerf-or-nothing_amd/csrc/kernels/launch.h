@@ -61,6 +61,9 @@ struct BwdArgs {
   float* delta9x;  // [M/32][160][32]
 };
 hipError_t launch_mlp_bwd(const BwdArgs& a, hipStream_t st);
+// fp32-precision kernels (v_mfma_f32_16x16x4_f32, two waves per SIMD): mlp_fwd16.hip / mlp_bwd16.hip
+hipError_t launch_mlp_fwd16(const FwdArgs& a, hipStream_t st);
+hipError_t launch_mlp_bwd16(const BwdArgs& a, hipStream_t st);
 
 // ---- wgrad.hip: weight/bias gradients as one scheduled split-K launch + ordered reduce ------
 struct WgProblem {

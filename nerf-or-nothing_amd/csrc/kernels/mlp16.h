@@ -1,0 +1,187 @@
+// fp32 MLP kernels on v_mfma_f32_16x16x4_f32 at TWO waves per SIMD — shared machinery of
+// k_mlp_fwd16 / k_mlp_bwd16 (the fp32-precision path; split mode keeps mlp_common.h's kernels).
+//
+// One wave64 owns 16 consecutive samples (half of a 32-sample activation block): a 256-feature
+// activation is 16 accumulator tiles of 16x16 (f32x4) = 64 registers, so two ping-pong accumulator
+// sets + the B-operand copy fit in 256 registers and a workgroup of 8 waves runs two waves per
+// SIMD.  While one wave waits (slice barrier, LDS-DMA issue, IPE transcendentals, epilogue stores)
+// its partner keeps the SIMD's MFMA pipe busy — the 32x32x2 kernels at one wave per SIMD expose
+// every such stall.
+//
+// Register layout.  16x16x4: lane l = (g = l >> 4, j = l & 15) supplies A[row j][k = g] and
+// B[k = g][col j]; D register r of lane l is D[row 4g + r][col j].  Output tile t of a layer
+// therefore holds feature 16t + 4g + r of sample j in register r — and that is directly the B
+// operand of the next layer's k-step (t, r) if that k-step's four k values are the features
+// {16t + 4g + r : g = 0..3}.  The matching A operand is W[row][16t + 4g + r]: for r = 0..3 the four
+// CONTIGUOUS floats 16t + 4g .. +3 of the weight row, i.e. one ds_read_b128 of 16-B chunk 4t + g.
+// The packed slices (256 rows x 32 columns, chunk c of row r at c ^ ((r >> 1) & 7), common.h
+// slice_off) are therefore the same images the 32x32 kernels stream, and the 8 lanes of each
+// ds_read_b128 phase (rows j..j+7, one chunk) hit 8 distinct 16-B bank groups.
+//
+// Summation order: the MFMA is a k-ordered fmaf chain, so results differ from the 32x32 kernels
+// in the last bits only (both are fp32-accurate; parity vs the fp64 oracle is unchanged).
+#pragma once
+#include "mlp_common.h"
+
+namespace nof {
+
+constexpr int kMlp16Threads = 512;  // 8 waves = 4 blocks of 32 samples x 2 halves
+constexpr int kIpe16Floats = 6 * 64 * 4;  // per-wave LDS copy of the 24 IPE B values per lane (6 KB)
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// Step i (0..3) of a 32-KB slice DMA by 512 threads: thread tid moves 16-B chunk 512 i + tid
+// (buffer_load_dwordx4 ... lds: slice base in the scalar descriptor, step in soffset).
+__device__ __forceinline__ void slice16_dma_step(const float* __restrict__ src, float* dst, int tid, int i) {
+  const int wave = tid >> 6;
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lptr_t)(dst + (kMlp16Threads * i + 64 * wave) * 4), 16, tid * 16,
+                                           i * kMlp16Threads * 16, 0, 0);
+}
+__device__ __forceinline__ void slice16_dma(const float* __restrict__ src, float* dst, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) slice16_dma_step(src, dst, tid, i);
+}
+
+// Weight ring: 3 slots, the DMA of slice t + 2 issued during slice t (a full slice of L2 latency
+// to land), so the end-of-slice barrier only waits for slice t + 1, issued a slice earlier; the
+// DMA and epilogue stores issued during slice t itself stay in flight (counted vmcnt).
+constexpr int kRing16Slots = 3;
+constexpr int kRing16Floats = kRing16Slots * kSliceFloats;
+// prologue: slices 0 and 1 into slots 0 and 1 (retired by the prologue's __syncthreads)
+__device__ __forceinline__ void ring16_prologue(const float* __restrict__ img, float* lds, int tid) {
+  slice16_dma(img, lds, tid);
+  slice16_dma(img + kSliceFloats, lds + kSliceFloats, tid);
+}
+
+// Feature held by register r of tile t in lane group g.
+__device__ __forceinline__ constexpr int feat16(int t, int g, int r) { return 16 * t + 4 * g + r; }
+
+// Stores of one accumulator tile's 4 registers into a chunk-swizzled [F][32] block (common.h
+// blk_off) for sample 16 half + j: byte(f, s) = 128 f + ((((s >> 2) ^ (f & 7)) << 4) | ((s & 3) << 2))
+// with f = 16t + 4g + r, so f & 7 = 4 (g & 1) + r and the lane part is one of four offsets (by r);
+// the tile (t) part 2048 t + 128 r is the instruction's immediate.
+struct BlkStore16 {
+  uint32_t voff[4];
+  __device__ __forceinline__ BlkStore16(int lane, int half) {
+    const int g = lane >> 4, s = 16 * half + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      voff[r] = 512u * g + ((((s >> 2) ^ (4 * (g & 1) + r)) << 4) | ((s & 3) << 2));
+  }
+  __device__ __forceinline__ void store(float* blk, int t, int r, float v) const {
+    typedef __attribute__((address_space(1))) char gchar;
+    typedef __attribute__((address_space(1))) float gfloat;
+    *(gfloat*)((gchar*)blk + (size_t)voff[r] + 2048 * t + 128 * r) = v;
+  }
+};
+
+// ReLU masks of the 16-sample kernels: per 32-sample block and slot (trunk layers 0..7, view layer
+// 9) 1 KB = [half][64 lanes][uint2]; bit of (tile t, register r) at position 31 - ((t & 7) 4 + r) of
+// word t >> 3 (shift-accumulated in tile order).
+__device__ __forceinline__ uint2* mask16_ptr(uint32_t* masks, int blk, int slot, int half, int lane) {
+  return reinterpret_cast<uint2*>(mask_ptr(masks, blk, slot) + half * 128) + lane;
+}
+__device__ __forceinline__ bool mask16_bit(const uint2& m, int t, int r) {
+  return ((t >> 3 ? m.y : m.x) >> (31 - ((t & 7) * 4 + r))) & 1u;
+}
+
+// Epilogue hook of mlp_layer16: epi(tile) finishes one accumulator tile of the PREVIOUS layer
+// (4 registers) into `bin`; tiles 2t + 2 and 2t + 3 run during slice t (in MFMA groups 1 and
+// kEpiGroup2), so both are complete before slice t + 1 reads them.  Tiles 0 and 1 are the caller's.
+// kVmPerPart = vector-memory ops one tile issues (at least; stores), for the counted slice barrier.
+struct NoEpi16 {
+  static constexpr int kVmPerPart = 0;
+  __device__ __forceinline__ void operator()(int) {}
+};
+
+// One dense layer: acc[ot] (ot < OT) = sum over NT_B slices with B from `bin` (registers, tiles
+// 2t, 2t + 1 of slice t) and NT_I slices with B from the wave's IPE copy in LDS.  Per slice: 2
+// input tiles x OT/2 row-tile pairs = OT MFMA groups of 8 (two accumulators interleaved: the
+// 16x16x4 dependent latency is 40 cycles against a 32-cycle issue), each group's two A operands
+// read one group ahead; the 4 DMA steps of slice t + 2 ride groups 0..3; one barrier per slice.
+template <int NT_B, int NT_I, int OT, class Epi>
+__device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16],
+                                            float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
+                                            int lane, Epi& epi) {
+  static_assert(OT % 2 == 0 && OT <= 16, "row tiles come in pairs");
+  constexpr int NG = OT;  // groups per slice: 2 input tiles x OT / 2 pairs
+#ifndef NOF_EPI16_G1
+#define NOF_EPI16_G1 4
+#endif
+  constexpr int kEpiGroup1 = NOF_EPI16_G1;
+  constexpr int kEpiGroup2 = (NG / 2 + NOF_EPI16_G1 < NG) ? NG / 2 + NOF_EPI16_G1 : NG - 1;
+  const int g = lane >> 4;
+  const int row = lane & 15;
+  const int swz = (row >> 1) & 7;
+#pragma unroll
+  for (int t = 0; t < NT_B + NT_I; ++t) {
+    const bool dma = !(last_in_schedule && t + 2 >= NT_B + NT_I);  // slice t + 2 exists
+    const int nxt2 = cur == 0 ? 2 : cur - 1;                         // (cur + 2) % 3
+    const float* W = lds + cur * kSliceFloats + row * 32;
+    // group q = tt * (OT / 2) + p: input tile tt of the slice, row tiles 2p, 2p + 1
+    auto aread = [&](int q, int which) {
+      const int tt = q / (OT / 2), p = q % (OT / 2);
+      return *reinterpret_cast<const f32x4*>(W + (2 * p + which) * 16 * 32 + (((4 * tt + g) ^ swz) << 2));
+    };
+    f32x4 a0 = aread(0, 0), a1 = aread(0, 1);
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      const int tt = q / (OT / 2), p = q % (OT / 2);
+      f32x4 b4;
+      if (t < NT_B) {
+        const int tb = (t < NT_B) ? 2 * t + tt : 0;
+        b4[0] = bin[tb][0]; b4[1] = bin[tb][1]; b4[2] = bin[tb][2]; b4[3] = bin[tb][3];
+      } else {
+        const int ti = (t >= NT_B) ? 2 * (t - NT_B) + tt : 0;
+        b4 = *reinterpret_cast<const f32x4*>(ipe_lds + (ti * 64 + lane) * 4);
+      }
+      asm volatile("" ::"v"(a0), "v"(a1));  // this group's reads land here, before the next ones issue
+      f32x4 n0 = a0, n1 = a1;
+#ifdef NOF_DIAG_NO_AREAD
+      if (q + 1 < NG && t == 0) {
+#else
+      if (q + 1 < NG) {
+#endif
+        n0 = aread(q + 1, 0);
+        n1 = aread(q + 1, 1);
+      }
+#ifndef NOF_DIAG_NO_DMA
+      if (dma && q < 4) slice16_dma_step(wsrc + 2 * kSliceFloats, lds + nxt2 * kSliceFloats, tid, q);
+#endif
+#ifndef NOF_NO_SCHED_BARRIER
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+      const bool first = t == 0 && tt == 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        acc[2 * p] = mfma16(a0[r], b4[r], (first && r == 0) ? f32x4{} : acc[2 * p]);
+        acc[2 * p + 1] = mfma16(a1[r], b4[r], (first && r == 0) ? f32x4{} : acc[2 * p + 1]);
+      }
+      if (t + 1 < NT_B && q == kEpiGroup1) epi(2 * t + 2);
+      if (t + 1 < NT_B && q == kEpiGroup2) epi(2 * t + 3);
+#ifndef NOF_NO_SCHED_BARRIER
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+      a0 = n0;
+      a1 = n1;
+    }
+    // slice t + 1 (issued during slice t - 1) must have landed; everything issued during this
+    // slice (the DMA of t + 2, both epilogue parts' stores) may stay in flight
+    slice_barrier((dma ? 4 : 0) + (t + 1 < NT_B ? 2 * Epi::kVmPerPart : 0));
+    cur = cur == 2 ? 0 : cur + 1;
+    wsrc += kSliceFloats;
+  }
+}
+template <int NT_B, int NT_I, int OT>
+__device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16],
+                                            float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
+                                            int lane) {
+  NoEpi16 none;
+  mlp_layer16<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, none);
+}
+
+}  // namespace nof

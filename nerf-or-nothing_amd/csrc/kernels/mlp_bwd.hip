@@ -179,7 +179,11 @@ hipError_t launch_mlp_bwd(const BwdArgs& a, hipStream_t st) {
   if (a.M % kBlk != 0) return hipErrorInvalidValue;
   const int nblk = a.M / kBlk;
   if (a.split) hipLaunchKernelGGL(k_mlp_bwd<true>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
+#ifdef NOF_F32_MFMA32
   else hipLaunchKernelGGL(k_mlp_bwd<false>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
+#else
+  else return launch_mlp_bwd16(a, st);
+#endif
   return hipGetLastError();
 }
 

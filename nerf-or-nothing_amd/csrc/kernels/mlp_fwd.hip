@@ -303,8 +303,12 @@ hipError_t launch_mlp_fwd(const FwdArgs& a, hipStream_t st) {
     if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd<true, false>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((k_mlp_fwd<true, true>), grid, block, 0, st, a);
   } else {
+#ifdef NOF_F32_MFMA32  // the 32x32x2, one-wave-per-SIMD fp32 kernels (diagnostic builds only)
     if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd<false, false>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((k_mlp_fwd<false, true>), grid, block, 0, st, a);
+#else
+    return launch_mlp_fwd16(a, st);
+#endif
   }
   return hipGetLastError();
 }

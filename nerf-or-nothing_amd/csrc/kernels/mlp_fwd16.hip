@@ -1,0 +1,251 @@
+// Fused conical-frustum + IPE + 8x256 MLP + density/RGB heads forward, fp32 precision, on
+// v_mfma_f32_16x16x4_f32 at two waves per SIMD (mlp16.h).
+//
+// Replaces cast_rays (AF:292-317), encode_input_data (AF:187-221) and the 11 per-layer
+// launches of AcceleratedMLP::get_output (MLPcpp:214-255: get_neuron_output*, AF:36-90) with
+// one launch per level.  Semantics per MLP.CallCached (MLPcs:112-136) and the C# heads
+// (MNcs:307-309, D23): sigma = softplus(z_s - 1), rgb = sigmoid(z_c) * 1.002 - 0.001.
+//
+// Per wave (16 samples of one ray): the 24 IPE features of its lanes computed in registers and
+// parked in LDS (B operand of layer 0 and of the skip layer), then 11 layers with activations
+// resident in registers.  Side outputs for the backward pass: every layer's activations in the
+// block-swizzled [F][32] layout (weight-gradient GEMMs), packed ReLU masks (dX chain), raw heads.
+#include "common.h"
+#include "geometry.h"
+#include "launch.h"
+#include "mlp16.h"
+
+namespace nof {
+
+// bias + ReLU epilogue of one accumulator tile -> next layer's B operand, act block, mask bits;
+// NT tiles per layer, run in tile order (the mask words are shift-accumulated).  Biases (and w8)
+// come from the workgroup's LDS copy, loaded one tile ahead.  kDensity folds the density head
+// (z_s = w8 . h7) into layer 7's epilogue.  A tail wave clamped onto the last block recomputes
+// bit-identical values, so its duplicate stores are benign.
+template <bool store, bool kDensity, int NT>
+struct FwdEpi16 {
+#ifndef NOF_DIAG_NO_ACT_STORE
+  static constexpr int kVmPerPart = store ? 4 : 0;
+#else
+  static constexpr int kVmPerPart = 0;
+#endif
+  const f32x4 (&acc)[16];
+  float (&bin)[16][4];
+  const BlkStore16& bst;
+  const int g;
+  const float* bias;  // LDS, + 4g
+  const float* w8;    // LDS, + 4g
+  float* act_blk;
+  uint2* mask_dst;
+  uint32_t mw[2];
+  f32x4 bnext, wnext;
+  float zs;
+
+  __device__ __forceinline__ FwdEpi16(const f32x4 (&acc_)[16], float (&bin_)[16][4], const BlkStore16& bst_, int lane)
+      : acc(acc_), bin(bin_), bst(bst_), g(lane >> 4) {}
+  __device__ __forceinline__ void begin(const float* bias_, float* act_blk_, uint2* mask_dst_,
+                                        const float* w8_ = nullptr) {
+    bias = bias_ + 4 * g;
+    act_blk = act_blk_;
+    mask_dst = mask_dst_;
+    mw[0] = mw[1] = 0u;
+    bnext = *reinterpret_cast<const f32x4*>(bias);
+    if constexpr (kDensity) {
+      w8 = w8_ + 4 * g;
+      wnext = *reinterpret_cast<const f32x4*>(w8);
+      zs = 0.0f;
+    }
+  }
+  __device__ __forceinline__ void operator()(int t) {
+    const f32x4 b4 = bnext;
+    const bool more = t + 1 < NT;
+    if (more) bnext = *reinterpret_cast<const f32x4*>(bias + 16 * (t + 1));
+    f32x4 w4;
+    if constexpr (kDensity) {
+      w4 = wnext;
+      if (more) wnext = *reinterpret_cast<const f32x4*>(w8 + 16 * (t + 1));
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float z = acc[t][r] + b4[r];
+      const float hv = z > 0.0f ? z : 0.0f;
+      bin[t][r] = hv;
+      mw[t >> 3] = (mw[t >> 3] << 1) | (hv > 0.0f ? 1u : 0u);
+      if constexpr (kDensity) zs += w4[r] * hv;
+    }
+    if constexpr (store && kVmPerPart > 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bst.store(act_blk, t, r, bin[t][r]);
+      if (!more) *mask_dst = make_uint2(mw[0], mw[1]);
+    }
+  }
+  __device__ __forceinline__ void tile01() {
+    (*this)(0);
+    (*this)(1);
+  }
+};
+
+template <bool store>  // store: side outputs for the backward pass (off for inference)
+__global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
+  constexpr int kRing = kRing16Floats;
+  constexpr int kBiasLds = 8 * 256 + 256;
+  __shared__ __attribute__((aligned(16))) float lds[kRing + 8 * kIpe16Floats + 8 * 128 + kBiasLds];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: block pointers stay in SGPRs
+  const int half = wave & 1;
+  const int nblk = a.M / kBlk;
+  const int blk_raw = blockIdx.x * 4 + (wave >> 1);
+  const int blk = blk_raw < nblk ? blk_raw : nblk - 1;  // tail waves duplicate the last block
+  const int m0 = blk * kBlk;
+  const int ray = m0 / a.S;
+  const int s0 = m0 - ray * a.S + 16 * half;
+  const int m = m0 + 16 * half + j;
+  const float* tail = a.wimg + (size_t)kFwdSlices * kSliceFloats;
+
+  ring16_prologue(a.wimg, lds, tid);  // first two slices in flight while the encodings are computed
+
+  // ---- encodings: IPE feature 16t + 4g + r in ipe[t][r] (the B-operand order) ---------------
+  float ipe[6][4];
+  float d3[3];
+  if (!a.encoded) {
+    d3[0] = a.dirs[3 * ray]; d3[1] = a.dirs[3 * ray + 1]; d3[2] = a.dirs[3 * ray + 2];
+    const float o3[3] = {a.origins[3 * ray], a.origins[3 * ray + 1], a.origins[3 * ray + 2]};
+    const float* tr = a.t + (size_t)ray * (a.S + 1) + s0 + j;
+    float mean[3], cov[3];
+    frustum_gaussian(tr[0], tr[1], o3, d3, a.radii[ray], mean, cov);
+#pragma unroll
+    for (int t = 0; t < 6; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#ifndef NOF_DIAG_NO_IPE
+        ipe[t][r] = ipe_feature(feat16(t, g, r), mean, cov);
+#else
+        ipe[t][r] = mean[r % 3] * (float)feat16(t, g, r) + cov[r % 3];
+#endif
+  } else {
+#pragma unroll
+    for (int t = 0; t < 6; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ipe[t][r] = a.enc_pos[(size_t)m * kPosIn + feat16(t, g, r)];
+  }
+  float pe[kDirIn];
+#pragma unroll
+  for (int k = 0; k < kDirIn; ++k) pe[k] = a.encoded ? a.enc_dir[(size_t)ray * kDirIn + k] : dir_feature(k, d3);
+
+  const BlkStore16 bst(lane, half);
+  if constexpr (store) {
+    float* act_in_blk = a.act_in + (size_t)blk * kInF * kBlk;
+#pragma unroll
+    for (int t = 0; t < 6; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bst.store(act_in_blk, t, r, ipe[t][r]);
+#pragma unroll
+    for (int t = 6; t < 8; ++t)  // view PE rows 96..122, zero rows 123..127
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = feat16(t, g, r) - kPosIn;
+        float v = 0.0f;
+#pragma unroll
+        for (int kk = 0; kk < kDirIn; ++kk) v = (kk == k) ? pe[kk] : v;
+        bst.store(act_in_blk, t, r, v);
+      }
+  }
+  float* ipe_lds = lds + kRing + wave * kIpe16Floats;
+#pragma unroll
+  for (int t = 0; t < 6; ++t) {
+    f32x4 v;
+    v[0] = ipe[t][0]; v[1] = ipe[t][1]; v[2] = ipe[t][2]; v[3] = ipe[t][3];
+    *reinterpret_cast<f32x4*>(ipe_lds + (t * 64 + lane) * 4) = v;
+  }
+  // view-direction part of layer 9 folded into a per-ray bias: b9 + W9[:, 256:283] . PE(d)
+  float* dirb = lds + kRing + 8 * kIpe16Floats + wave * 128;
+  float* bias_lds = lds + kRing + 8 * kIpe16Floats + 8 * 128;  // trunk biases (layers 0..7) and w8
+  for (int i = tid; i < kBiasLds / 4; i += kMlp16Threads) {
+    const float* src = i < 512 ? tail + kFwdTailBias + 4 * i : tail + kFwdTailW8 + 4 * (i - 512);
+    *reinterpret_cast<f32x4*>(bias_lds + 4 * i) = *reinterpret_cast<const f32x4*>(src);
+  }
+#pragma unroll
+  for (int rep = 0; rep < 2; ++rep) {
+    const int o = lane + 64 * rep;
+    float s = tail[kFwdTailBias + 9 * 256 + o];
+    const float* w9 = tail + kFwdTailW9d + o * 32;
+#pragma unroll
+    for (int k = 0; k < kDirIn; ++k) s += w9[k] * pe[k];
+    dirb[o] = s;
+  }
+  __syncthreads();
+
+  int cur = 0;
+  const float* wsrc = a.wimg;
+  f32x4 accA[16], accB[16];  // ping-pong: layer l accumulates into one set while l - 1's epilogue drains the other
+  float bin[16][4];
+  const size_t layer_stride = (size_t)nblk * kWidth * kBlk;
+  const float* biases = bias_lds;
+  float* act_h_blk = a.act_h + (size_t)blk * kWidth * kBlk;
+
+  // ---- trunk: layer l writes acc(l odd ? B : A) ------------------------------------------
+  FwdEpi16<store, false, 16> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
+  ea.begin(biases, act_h_blk, mask16_ptr(a.masks, blk, 0, half, lane));
+  mlp_layer16<0, 3, 16>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane);
+  ea.tile01();
+  for (int l = 1; l < kDepth - 1; l += 2) {
+    eb.begin(biases + l * 256, act_h_blk + l * layer_stride, mask16_ptr(a.masks, blk, l, half, lane));
+    mlp_layer16<8, 0, 16>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea);
+    eb.tile01();
+    ea.begin(biases + (l + 1) * 256, act_h_blk + (l + 1) * layer_stride, mask16_ptr(a.masks, blk, l + 1, half, lane));
+    if (l + 1 == kSkip) mlp_layer16<8, 3, 16>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, eb);
+    else mlp_layer16<8, 0, 16>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, eb);
+    ea.tile01();
+  }
+  static_assert(kDepth == 8 && kSkip % 2 == 0, "trunk pairing assumes 8 layers and an even skip layer");
+  FwdEpi16<store, true, 16> e7(accB, bin, bst, lane);  // + density head (layer 8): z_s = w8 . h7 + b8
+  e7.begin(biases + 7 * 256, act_h_blk + 7 * layer_stride, mask16_ptr(a.masks, blk, 7, half, lane),
+           bias_lds + 8 * 256);
+  mlp_layer16<8, 0, 16>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea);
+  e7.tile01();
+
+  // ---- view layer 9: relu(W9[:, :256] h7 + dirbias); h7 tiles 2..15 finish in its shadow -------
+  mlp_layer16<8, 0, 8>(bin, ipe_lds, accA, lds, cur, wsrc, true, tid, lane, e7);
+  float zs = e7.zs;
+  zs += __shfl_xor(zs, 16, 64);
+  zs += __shfl_xor(zs, 32, 64);
+  zs += tail[kFwdTailBias + 8 * 256];
+  FwdEpi16<store, false, 8> e9(accA, bin, bst, lane);
+  e9.begin(dirb, a.act_h9 + (size_t)blk * kWidthCond * kBlk, mask16_ptr(a.masks, blk, 8, half, lane));
+#pragma unroll
+  for (int t = 0; t < 8; ++t) e9(t);
+
+  // ---- RGB head (layer 10) ------------------------------------------------------------
+  float zc[3] = {0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const f32x4 w4 = *reinterpret_cast<const f32x4*>(tail + kFwdTailW10 + c * 128 + 16 * t + 4 * g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) zc[c] += w4[r] * bin[t][r];
+    }
+    zc[c] += __shfl_xor(zc[c], 16, 64);
+    zc[c] += __shfl_xor(zc[c], 32, 64);
+    zc[c] += tail[kFwdTailBias + 10 * 256 + c];
+  }
+
+  if (g == 0) {
+    a.sigma[m] = softplus_f(zs + kDensityBias);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) a.rgb[(size_t)m * 3 + c] = sigmoid_f(zc[c]) * kRgbScale - kRgbPadding;
+    f32x4 zh;
+    zh[0] = zs; zh[1] = zc[0]; zh[2] = zc[1]; zh[3] = zc[2];
+    if constexpr (store) reinterpret_cast<f32x4*>(a.zhead)[m] = zh;
+  }
+}
+
+hipError_t launch_mlp_fwd16(const FwdArgs& a, hipStream_t st) {
+  const int nblk = a.M / kBlk;
+  const dim3 grid((nblk + 3) / 4), block(kMlp16Threads);
+  if (a.no_store) hipLaunchKernelGGL(k_mlp_fwd16<false>, grid, block, 0, st, a);
+  else hipLaunchKernelGGL(k_mlp_fwd16<true>, grid, block, 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace nof

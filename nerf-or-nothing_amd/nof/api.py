@@ -104,10 +104,23 @@ class AcceleratedMLP:
         dv = self.debug_view(level)
         M = dv["M"]
         nb = M // 32
+        out = np.zeros((M, 8 * 256 + 128), np.uint8)
+        if self._owner.config.precision == 0:  # fp32 16x16x4 kernels (mlp16.h): [half][lane][uint2]
+            raw = to_numpy(dv["masks"], (nb, 9, 2, 64, 2), np.uint32)
+            lane = np.arange(64)
+            j, g = lane & 15, lane >> 4
+            for slot in range(9):
+                base = slot * 256
+                for t in range(16 if slot < 8 else 8):
+                    for r in range(4):
+                        f = 16 * t + 4 * g + r  # [64]
+                        bit = (raw[:, slot, :, :, t >> 3] >> np.uint32(31 - ((t & 7) * 4 + r))) & np.uint32(1)
+                        rows = np.arange(nb)[:, None, None] * 32 + 16 * np.arange(2)[None, :, None] + j[None, None, :]
+                        out[rows, base + f[None, None, :]] = bit.astype(np.uint8)
+            return out
         raw = to_numpy(dv["masks"], (nb, 9, 64, 4), np.uint32)
         lane = np.arange(64)
         j, h = lane & 31, lane >> 5
-        out = np.zeros((M, 8 * 256 + 128), np.uint8)
         for slot in range(9):
             ntile = 8 if slot < 8 else 4
             base = slot * 256

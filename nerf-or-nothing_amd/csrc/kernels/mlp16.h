@@ -72,12 +72,16 @@ struct BlkStore16 {
     for (int r = 0; r < 4; ++r)
       voff[r] = 512u * g + ((((s >> 2) ^ (4 * (g & 1) + r)) << 4) | ((s & 3) << 2));
   }
-  __device__ __forceinline__ void store(float* blk, int t, int r, float v) const {
-    typedef __attribute__((address_space(1))) char gchar;
-    typedef __attribute__((address_space(1))) float gfloat;
-    *(gfloat*)((gchar*)blk + (size_t)voff[r] + 2048 * t + 128 * r) = v;
+  // buffer_store_dword: block base in the scalar descriptor, tile/register part in soffset, the
+  // lane part a 32-bit voffset (a flat 64-bit address per lane would cost a VALU add per store and
+  // 8 VGPRs of hoisted offsets)
+  __device__ __forceinline__ void store(__amdgpu_buffer_rsrc_t blk, int t, int r, float v) const {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), blk, (int)voff[r], 2048 * t + 128 * r, 0);
   }
 };
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t blk_rsrc(float* blk) {
+  return __builtin_amdgcn_make_buffer_rsrc(blk, (short)0, 0x7fffffff, 0x00020000);
+}
 
 // ReLU masks of the 16-sample kernels: per 32-sample block and slot (trunk layers 0..7, view layer
 // 9) 1 KB = [half][64 lanes][uint2]; bit of (tile t, register r) at position 31 - ((t & 7) 4 + r) of

@@ -26,7 +26,7 @@ struct BwdEpi16 {
   const int g;
   const float* w8;  // LDS, + 4g
   float dzs;
-  float* dst_blk;
+  __amdgpu_buffer_rsrc_t dst_blk;
   uint2 mk;
   f32x4 wnext;
 
@@ -35,7 +35,7 @@ struct BwdEpi16 {
   __device__ __forceinline__ void begin(const uint2* mask, float* dst_blk_, const float* w8_ = nullptr,
                                         float dzs_ = 0.0f) {
     mk = *mask;
-    dst_blk = dst_blk_;
+    dst_blk = blk_rsrc(dst_blk_);
     if constexpr (kDensity) {
       w8 = w8_ + 4 * g;
       dzs = dzs_;
@@ -89,7 +89,7 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
     const float s = sigmoid_f(zh[1 + c]);
     dzc[c] = a.drgb[(size_t)m * 3 + c] * (s * (1.0f - s)) * kRgbScale;
   }
-  float* d9 = a.delta9x + (size_t)blk * kD9F * kBlk;  // uniform block base
+  const __amdgpu_buffer_rsrc_t d9 = blk_rsrc(a.delta9x + (size_t)blk * kD9F * kBlk);  // uniform block base
   // rows 128..143 = tile 8: dz_sigma, dz_rgb in lane group 0, zeros above
 #pragma unroll
   for (int r = 0; r < 4; ++r) bst.store(d9, 8, r, g == 0 ? (r == 0 ? dzs : dzc[r - 1]) : 0.0f);

@@ -35,7 +35,7 @@ struct FwdEpi16 {
   const int g;
   const float* bias;  // LDS, + 4g
   const float* w8;    // LDS, + 4g
-  float* act_blk;
+  __amdgpu_buffer_rsrc_t act_blk;
   uint2* mask_dst;
   uint32_t mw[2];
   f32x4 bnext, wnext;
@@ -46,7 +46,7 @@ struct FwdEpi16 {
   __device__ __forceinline__ void begin(const float* bias_, float* act_blk_, uint2* mask_dst_,
                                         const float* w8_ = nullptr) {
     bias = bias_ + 4 * g;
-    act_blk = act_blk_;
+    act_blk = blk_rsrc(act_blk_);
     mask_dst = mask_dst_;
     mw[0] = mw[1] = 0u;
     bnext = *reinterpret_cast<const f32x4*>(bias);
@@ -134,11 +134,11 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
 
   const BlkStore16 bst(lane, half);
   if constexpr (store) {
-    float* act_in_blk = a.act_in + (size_t)blk * kInF * kBlk;
+    const __amdgpu_buffer_rsrc_t act_in_rs = blk_rsrc(a.act_in + (size_t)blk * kInF * kBlk);
 #pragma unroll
     for (int t = 0; t < 6; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) bst.store(act_in_blk, t, r, ipe[t][r]);
+      for (int r = 0; r < 4; ++r) bst.store(act_in_rs, t, r, ipe[t][r]);
 #pragma unroll
     for (int t = 6; t < 8; ++t)  // view PE rows 96..122, zero rows 123..127
 #pragma unroll
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
         float v = 0.0f;
 #pragma unroll
         for (int kk = 0; kk < kDirIn; ++kk) v = (kk == k) ? pe[kk] : v;
-        bst.store(act_in_blk, t, r, v);
+        bst.store(act_in_rs, t, r, v);
       }
   }
   float* ipe_lds = lds + kRing + wave * kIpe16Floats;

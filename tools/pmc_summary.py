@@ -37,7 +37,8 @@ for k, s in stats.items():
     out[k] = e
 json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
 # traffic lookup used by bench.py (bench kernel-timer names; split-mode kernels keyed with "_split")
-names = {"k_mlp_fwd<false, true>": "mlp_fwd", "k_mlp_bwd<false>": "mlp_bwd", "k_wgrad": "wgrad",
+names = {"k_mlp_fwd16<true>": "mlp_fwd", "k_mlp_bwd16": "mlp_bwd", "k_wgrad": "wgrad",
+         "k_mlp_fwd<false, true>": "mlp_fwd", "k_mlp_bwd<false>": "mlp_bwd",  # NOF_F32_MFMA32 builds
          "k_mlp_fwd<true, true>": "mlp_fwd_split", "k_mlp_bwd<true>": "mlp_bwd_split", "k_wgrad_x3": "wgrad_split",
          "k_render_fwd<2>": "render_fwd" + suffix, "k_render_bwd<2>": "render_bwd" + suffix}
 tfile = os.path.join(dst, "pmc_traffic.json")

@@ -11,11 +11,48 @@
 
 namespace nof {
 
+// Per-lane contiguous runs as the widest aligned vector accesses: N floats at p (p aligned to A
+// floats, A in {1, 2, 4}).  sigma / w / dsigma runs of PER floats are PER-aligned; rgb / drgb runs
+// of 3 PER floats are 8-B aligned at PER = 2 and 16-B aligned at PER >= 4 (kRgbAlign).
+template <int N, int A>
+__device__ __forceinline__ void vload(const float* __restrict__ p, float (&v)[N]) {
+  if constexpr (A >= 4 && N % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < N / 4; ++i) {
+      const f32x4 x = reinterpret_cast<const f32x4*>(p)[i];
+      v[4 * i] = x[0]; v[4 * i + 1] = x[1]; v[4 * i + 2] = x[2]; v[4 * i + 3] = x[3];
+    }
+  } else if constexpr (A >= 2 && N % 2 == 0) {
+#pragma unroll
+    for (int i = 0; i < N / 2; ++i) {
+      const float2 x = reinterpret_cast<const float2*>(p)[i];
+      v[2 * i] = x.x; v[2 * i + 1] = x.y;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = p[i];
+  }
+}
+template <int N, int A>
+__device__ __forceinline__ void vstore(float* __restrict__ p, const float (&v)[N]) {
+  if constexpr (A >= 4 && N % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < N / 4; ++i) reinterpret_cast<f32x4*>(p)[i] = f32x4{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
+  } else if constexpr (A >= 2 && N % 2 == 0) {
+#pragma unroll
+    for (int i = 0; i < N / 2; ++i) reinterpret_cast<float2*>(p)[i] = make_float2(v[2 * i], v[2 * i + 1]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) p[i] = v[i];
+  }
+}
+template <int PER> constexpr int kRgbAlign = PER >= 4 ? 4 : PER;  // floats: 3 PER lane * 4 B
+
 template <int PER>
 struct RayState {
   float a[PER];      // alpha_k
   float T[PER];      // T_k (exclusive transmittance)
-  float delta[PER];  // t_{k+1} - t_k
+  float tv[PER + 1]; // t_k .. t_{k+PER}
   float dl;          // |d|
 };
 
@@ -26,13 +63,24 @@ __device__ inline void ray_alpha_T(int S, int r, int lane, const float* __restri
   const float dx = d[3 * r], dy = d[3 * r + 1], dz = d[3 * r + 2];
   rs.dl = sqrtf((dx * dx + dy * dy) + dz * dz);
   const int k0 = lane * PER;
-  const float* tr = t + (size_t)r * (S + 1) + k0;
-  const float* sr = sigma + (size_t)r * S + k0;
+  const float* tr = t + (size_t)r * (S + 1);
+  float tl[PER], sg[PER];
+  if constexpr (PER > 1) {
+    // the ray's t row starts at r (S + 1) floats: even S + 1 rows are only 4-B aligned
+#pragma unroll
+    for (int p = 0; p < PER; ++p) tl[p] = tr[k0 + p];
+  } else {
+    tl[0] = tr[k0];
+  }
+  vload<PER, PER>(sigma + (size_t)r * S + k0, sg);
+  const float tnext = __shfl_down(tl[0], 1, 64);  // t_{k0 + PER} = next lane's first
+#pragma unroll
+  for (int p = 0; p < PER; ++p) rs.tv[p] = tl[p];
+  rs.tv[PER] = lane == 63 ? tr[S] : tnext;
   float lp = 1.0f;
 #pragma unroll
   for (int p = 0; p < PER; ++p) {
-    rs.delta[p] = tr[p + 1] - tr[p];
-    rs.a[p] = 1.0f - expf(-sr[p] * rs.delta[p] * rs.dl);
+    rs.a[p] = 1.0f - expf(-sg[p] * (rs.tv[p + 1] - rs.tv[p]) * rs.dl);
     lp *= (1.0f - rs.a[p]);
   }
   float inc = lp;  // inclusive product scan over lanes
@@ -62,19 +110,19 @@ __global__ __launch_bounds__(256) void k_render_fwd(int n, int S, const float* _
   RayState<PER> rs;
   ray_alpha_T<PER>(S, r, lane, sigma, t, d, rs);
   const int k0 = lane * PER;
-  const float* cr = rgb + ((size_t)r * S + k0) * 3;
-  const float* tr = t + (size_t)r * (S + 1) + k0;
+  float cr[3 * PER], wk[PER];
+  vload<3 * PER, kRgbAlign<PER>>(rgb + ((size_t)r * S + k0) * 3, cr);
   float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f, acc = 0.0f, wd = 0.0f;
 #pragma unroll
   for (int p = 0; p < PER; ++p) {
-    const float wk = rs.a[p] * rs.T[p];
-    w[(size_t)r * S + k0 + p] = wk;
-    c0 += wk * cr[3 * p];
-    c1 += wk * cr[3 * p + 1];
-    c2 += wk * cr[3 * p + 2];
-    acc += wk;
-    if (dist_out) wd += wk * (tr[p] + tr[p + 1]) / 2.0f;  // weighted midpoint (MH:488)
+    wk[p] = rs.a[p] * rs.T[p];
+    c0 += wk[p] * cr[3 * p];
+    c1 += wk[p] * cr[3 * p + 1];
+    c2 += wk[p] * cr[3 * p + 2];
+    acc += wk[p];
+    if (dist_out) wd += wk[p] * (rs.tv[p] + rs.tv[p + 1]) / 2.0f;  // weighted midpoint (MH:488)
   }
+  vstore<PER, PER>(w + (size_t)r * S + k0, wk);
   c0 = wave_sum(c0); c1 = wave_sum(c1); c2 = wave_sum(c2); acc = wave_sum(acc);
   if (dist_out) wd = wave_sum(wd);
   if (lane == 0) {
@@ -116,17 +164,18 @@ __global__ __launch_bounds__(256) void k_render_bwd(int n, int S, const float* _
   }
   const float G = white ? (g0 + g1 + g2) : 0.0f;
   const int k0 = lane * PER;
-  const float* cr = rgb + ((size_t)r * S + k0) * 3;
-  float* dcr = drgb + ((size_t)r * S + k0) * 3;
+  float cr[3 * PER], dc[3 * PER], ds[PER];
+  vload<3 * PER, kRgbAlign<PER>>(rgb + ((size_t)r * S + k0) * 3, cr);
   float wk[PER], ek[PER];
   float ls = 0.0f;
 #pragma unroll
   for (int p = 0; p < PER; ++p) {
     wk[p] = rs.a[p] * rs.T[p];
     ek[p] = (g0 * cr[3 * p] + g1 * cr[3 * p + 1]) + g2 * cr[3 * p + 2] - G;
-    dcr[3 * p] = g0 * wk[p]; dcr[3 * p + 1] = g1 * wk[p]; dcr[3 * p + 2] = g2 * wk[p];
+    dc[3 * p] = g0 * wk[p]; dc[3 * p + 1] = g1 * wk[p]; dc[3 * p + 2] = g2 * wk[p];
     ls += wk[p] * ek[p];
   }
+  vstore<3 * PER, kRgbAlign<PER>>(drgb + ((size_t)r * S + k0) * 3, dc);
   float inc = ls;  // inclusive suffix sum over lanes
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -135,13 +184,13 @@ __global__ __launch_bounds__(256) void k_render_bwd(int n, int S, const float* _
   }
   float after = __shfl_down(inc, 1, 64);  // sum over lanes > lane
   if (lane == 63) after = 0.0f;
-  float* dsr = dsigma + (size_t)r * S + k0;
 #pragma unroll
   for (int p = PER - 1; p >= 0; --p) {
     const float Tn = rs.T[p] * (1.0f - rs.a[p]);
-    dsr[p] = (Tn * ek[p] - after) * rs.delta[p] * rs.dl;
+    ds[p] = (Tn * ek[p] - after) * (rs.tv[p + 1] - rs.tv[p]) * rs.dl;
     after += wk[p] * ek[p];
   }
+  vstore<PER, PER>(dsigma + (size_t)r * S + k0, ds);
 }
 
 __global__ void k_output_gradient(int n, const float* __restrict__ C, const float* __restrict__ pix,

@@ -4,7 +4,8 @@ Runs the full two-level step in fp64 autograd with every dense-layer contraction
 simulated MFMA: operands rounded to `mode`'s input type, products accumulated exactly (fp64 here,
 fp32 on the device).  Reports per-tensor relative L2 error of the 22 gradients and the outputs vs
 the exact fp64 step.  Modes: f32, bf16, f16 (per-sample power-of-2 scaling of the backward
-deltas), f16x2 (hi + lo split, 3 products), bf16x2 (hi + mid, 3 products), bf16x3 (3-way split, 6 products)."""
+deltas), f16x2 (hi + lo split, 3 products), f16x2t / f16x2t4 (both operands per-tensor power-of-2 scaled to max
+2^12, then hi + lo fp16: 3 / 4 products), bf16x2 (hi + mid, 3 products), bf16x3 (3-way split, 6 products)."""
 import sys, os
 import numpy as np
 import torch
@@ -35,8 +36,19 @@ def split(x, mode):
         return [a, b, c]
     raise ValueError(mode)
 
+def tensor_scale(x, top=12):  # one power of 2 for the whole operand: max |x| -> [2^top, 2^(top+1))
+    m = x.abs().max().clamp_min(1e-30)
+    return torch.exp2(top - torch.floor(torch.log2(m)))
+
 def mm(a, b, mode, scale_a=False):
     """a @ b with simulated split products; a's rows optionally power-of-2 scaled first."""
+    if mode in ("f16x2t", "f16x2t4"):  # per-tensor power-of-2 scaling of BOTH operands, hi + lo fp16
+        sa, sb = tensor_scale(a), tensor_scale(b)
+        A, B = split(a * sa, "f16x2"), split(b * sb, "f16x2")
+        out = A[0] @ B[0] + A[0] @ B[1] + A[1] @ B[0]
+        if mode == "f16x2t4":
+            out = out + A[1] @ B[1]
+        return out / (sa * sb)
     s = col_scale(a) if scale_a else torch.ones_like(a[..., :1])
     A, B = split(a * s, mode), split(b, mode)
     if mode in ("f16x2", "bf16x2"):
@@ -62,7 +74,11 @@ class QLinear(torch.autograd.Function):
         dx = mm(g2, W, QLinear.mode, scale_a=scale).reshape(sh)
         # dW = g^T x: scale g per output feature (row of g^T) — per-tensor-row scaling in wgrad
         gs = col_scale(g2.T) if scale else torch.ones_like(g2.T[..., :1])
-        dW = mm(g2.T * gs, x2, QLinear.mode) / gs if QLinear.mode != "f32" else g2.T @ x2
+        if QLinear.mode in ("f16x2t", "f16x2t4"):
+            dx = mm(g2, W, QLinear.mode).reshape(sh)
+            dW = mm(g2.T, x2, QLinear.mode)
+        else:
+            dW = mm(g2.T * gs, x2, QLinear.mode) / gs if QLinear.mode != "f32" else g2.T @ x2
         return dx, dW
 
 def patched_forward(self, P, enc, dirv):
@@ -88,7 +104,7 @@ def main(n=48, samples=(64, 64)):
     TR.Net.forward = patched_forward
     sizes = [o * i for o, i in zip(net.outs, net.ins)] + list(net.outs)
     cuts = np.cumsum(sizes)[:-1]
-    for mode in ["f32", "bf16", "f16", "f16x2", "bf16x2", "bf16x3"]:
+    for mode in (sys.argv[1:] or ["f32", "bf16", "f16", "f16x2", "f16x2t", "f16x2t4", "bf16x2", "bf16x3"]):
         QLinear.mode = mode
         r = TR.step(P, rays, samples=samples, seed=3, net=net, t_override={1: exact["t"][1]})
         errs = [np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)

@@ -34,8 +34,13 @@ MACS_DX = 492160
 MACS_DW = 544768
 PEAK_F32_TFLOPS = 157.3   # MI355X fp32 MFMA dense (= packed-fp32 VALU), MI355X_MICROARCH.md
 PEAK_BF16_TFLOPS = 2516.6  # MI355X bf16 dense MFMA (no sparsity)
-# split mode issues 6 bf16 MFMAs per fp32 product (mlp_common.h), so its fp32-equivalent ceiling is 1/6
+# split mode issues 6 bf16 MFMAs per fp32 product (mlp_common.h), so its fp32-equivalent ceiling is 1/6;
+# the f16x2 perf mode issues 3 fp16 MFMAs (same dense rate as bf16) per product
 PEAK_SPLIT_TFLOPS = round(PEAK_BF16_TFLOPS / 6, 1)
+PEAK_F16X2_TFLOPS = round(PEAK_BF16_TFLOPS / 3, 1)
+PRECISIONS = {"f32": 0, "split": 1, "f16x2": 2}  # NOF_PRECISION_*
+PEAKS = {"f32": PEAK_F32_TFLOPS, "split": PEAK_SPLIT_TFLOPS, "f16x2": PEAK_F16X2_TFLOPS}
+DTYPES = {"f32": "f32", "split": "f32 (bf16x3 split MFMA)", "f16x2": "f16x2 (fp16 hi+lo, 3 MFMAs; perf mode, 2e-3)"}
 PEAK_HBM_GBS = 8000.0
 INTEGRATOR_FWD_B = lambda S: S * (12 + 4 + 4) + (S + 1) * 4 + 12 + 12  # rgb, sigma, w | t | d | C  (3100 @128)
 INTEGRATOR_BWD_B = lambda S: 12 + S * (12 + 4) + (S + 1) * 4 + 12 + S * (12 + 4)  # 4636 @128
@@ -48,9 +53,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--rays", type=int, default=1024, help="rays per GPU per step")
     p.add_argument("--samples", type=int, nargs="+", default=[128, 128])
-    p.add_argument("--precision", choices=["f32", "split"], default="f32",
-                   help="MLP contraction arithmetic: fp32 MFMA, or fp32 operands as bf16x3 split MFMAs")
-    p.add_argument("--no-alt", action="store_true", help="skip the other precision mode's secondary measurement")
+    p.add_argument("--precision", choices=list(PRECISIONS), default="f32",
+                   help="MLP contraction arithmetic: fp32 MFMA, fp32 operands as bf16x3 split MFMAs (same 1e-5 "
+                        "parity), or the f16x2 perf mode (fp16 hi+lo, parity 2e-3)")
+    p.add_argument("--no-alt", action="store_true", help="skip the other precision modes' secondary measurements")
     p.add_argument("--dp", choices=["torch", "native"], default="torch",
                    help="N>1 gradient all-reduce: torch.distributed (RCCL) or the C ABI's nof_dp_* (RCCL)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -190,10 +196,10 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         native = NativeDP.init_rank(obj[0], world, rank, dev_idx)
 
-    def measure(split):
+    def measure(prec):
         """W untimed + K timed training steps of one precision mode; returns (s, timing, psnr)."""
         model = nof.AcceleratedMipNeRF(device=dev_idx, max_rays=n, num_samples=samples, seed=seed,
-                                       stream=stream, precision=1 if split else 0)
+                                       stream=stream, precision=PRECISIONS[prec])
         model.set_rng(seed, 0, rank * n)  # global ray ids: sharding never changes a sample
         opt = nof.AcceleratedAdamOptimizer(model.GetLayerSizes(), model.config)
         params = model.mlp.allParams
@@ -251,7 +257,7 @@ def main():
         model.close()
         return dt, timing, psnr, in_sync
 
-    def summarize(split, dt, timing):
+    def summarize(prec, dt, timing):
         ms_step = dt * 1e3 / a.steps
         M = [n * s for s in samples]
         flop = {"mlp_fwd": 2 * MACS_FWD * sum(M), "mlp_bwd": 2 * MACS_DX * sum(M), "wgrad": 2 * MACS_DW * sum(M)}
@@ -265,12 +271,12 @@ def main():
         achieved = fl_launch / (kernels[dom]["avg_launch_ms"] * 1e-3) / 1e12
         mlp_ms = sum(kernels[k]["ms_per_step"] for k in flop if k in kernels)
         mlp_tf = sum(flop.values()) / (mlp_ms * 1e-3) / 1e12
-        peak = PEAK_SPLIT_TFLOPS if split else PEAK_F32_TFLOPS
+        peak = PEAKS[prec]
         traffic = None
         tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(tfile):
             try:
-                traffic = json.load(open(tfile)).get(dom + ("_split" if split else ""))
+                traffic = json.load(open(tfile)).get(dom + ("" if prec == "f32" else "_" + prec))
             except (OSError, ValueError):
                 traffic = None
         return ms_step, kernels, {
@@ -280,20 +286,19 @@ def main():
             "mlp_all_kernels": {"achieved": round(mlp_tf, 2), "unit": "TFLOP/s", "frac": round(mlp_tf / peak, 4)},
         }
 
-    split = a.precision == "split"
-    dt, timing, psnr, in_sync = measure(split)
+    dt, timing, psnr, in_sync = measure(a.precision)
     rays_per_s = n * world * a.steps / dt
-    alt = None
+    alts = []
     if world == 1 and not a.no_alt:
-        alt = (not split,) + measure(not split)
+        alts = [(p,) + measure(p) for p in PRECISIONS if p != a.precision]
 
     result = None
     if rank == 0:
-        ms_step, kernels, roof = summarize(split, dt, timing)
+        ms_step, kernels, roof = summarize(a.precision, dt, timing)
         result = {
             "metric": METRIC, "value": round(rays_per_s, 1), "unit": "rays/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32 (bf16x3 split MFMA)" if split else "f32",
+            "vs_baseline": None, "dtype": DTYPES[a.precision],
             "data": "synthetic (Lego-shaped 800x800, 100 poses)",
             "config": {"workload": "BASELINE configs[1]: 1024-ray batches x 128+128 samples, 8x256 MLP fwd/bwd + Adam",
                        "rays_per_gpu": n, "global_batch": n * world, "samples": samples,
@@ -307,13 +312,14 @@ def main():
             result["params_in_sync"] = in_sync
             if backend != "nccl":
                 result["rehearsal"] = f"{backend}: {world} ranks on {torch.cuda.device_count()} GPU(s), not a scaling run"
-        if alt is not None:  # the other precision mode, same workload (parity-tested at the same tolerance)
-            asplit, adt, atiming, apsnr, _ = alt
-            ams, akernels, aroof = summarize(asplit, adt, atiming)
-            result["alt_precision"] = {
-                "precision": "split" if asplit else "f32", "value": round(n * a.steps / adt, 1), "unit": "rays/s",
-                "ms_per_step": round(ams, 4), **aroof,
-                "kernels": {k: v["avg_launch_ms"] for k, v in akernels.items()}, "psnr_fine": round(apsnr, 3)}
+        if alts:  # the other precision modes, same workload (split: same 1e-5 parity; f16x2: 2e-3)
+            result["alt_precision"] = []
+            for aprec, adt, atiming, apsnr, _ in alts:
+                ams, akernels, aroof = summarize(aprec, adt, atiming)
+                result["alt_precision"].append({
+                    "precision": aprec, "dtype": DTYPES[aprec], "value": round(n * a.steps / adt, 1),
+                    "unit": "rays/s", "ms_per_step": round(ams, 4), **aroof,
+                    "kernels": {k: v["avg_launch_ms"] for k, v in akernels.items()}, "psnr_fine": round(apsnr, 3)})
         if not a.no_integrator and world == 1:
             result["roofline_integrator"] = integrator_roofline(torch, nof, dev)
         if not a.no_cpu_baseline and world == 1:

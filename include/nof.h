@@ -58,12 +58,15 @@ typedef struct nof_config {
   int32_t precision;                      /* NOF_PRECISION_*: MLP contraction arithmetic (build extension) */
 } nof_config;
 
-/* MLP contraction arithmetic.  Both modes hold every operand and accumulator in fp32 and meet the
- * same fp32 parity tolerance; they differ only in how the MFMAs form products.
- *   F32       : v_mfma_f32_32x32x2_f32 (exact fp32 fmaf chains).
+/* MLP contraction arithmetic.  Every mode holds operands and accumulators in fp32 between the
+ * MFMAs; they differ in how the MFMAs form products.
+ *   F32       : v_mfma_f32_16x16x4_f32 (exact fp32 fmaf chains).  Parity: 1e-5.
  *   F32_SPLIT : each fp32 operand as three bf16 pieces (24 significand bits), six
- *               v_mfma_f32_32x32x16_bf16 per product, fp32 accumulation (~2.5x the F32 MFMA rate). */
-enum { NOF_PRECISION_F32 = 0, NOF_PRECISION_F32_SPLIT = 1 };
+ *               v_mfma_f32_32x32x16_bf16 per product, fp32 accumulation.  Same 1e-5 parity.
+ *   F16X2     : perf mode (BASELINE config 5 "fp16 on MFMA"): fp16 hi + lo pieces,
+ *               three v_mfma_f32_32x32x16_f16 per product, backward deltas power-of-2 scaled.
+ *               Parity: per-tensor relative L2 <= 2e-3. */
+enum { NOF_PRECISION_F32 = 0, NOF_PRECISION_F32_SPLIT = 1, NOF_PRECISION_F16X2 = 2 };
 
 void nof_config_default(nof_config* cfg);
 const char* nof_last_error(void);

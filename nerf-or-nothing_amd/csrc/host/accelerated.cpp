@@ -82,7 +82,9 @@ static void check_cfg(const nof_config& c) {
   if (c.net_depth != 8 || c.net_width != 256 || c.net_depth_condition != 1 || c.net_width_condition != 128 ||
       c.skip_layer != 4 || c.min_deg_point != 0 || c.max_deg_point != 16 || c.deg_view != 4)
     throw Error(NOF_ERR_UNSUPPORTED, "GPU path implements the reference network (8x256, 1x128, skip 4, PE 16/4)");
-  NOF_REQUIRE(c.precision == NOF_PRECISION_F32 || c.precision == NOF_PRECISION_F32_SPLIT, "unknown precision mode");
+  NOF_REQUIRE(c.precision == NOF_PRECISION_F32 || c.precision == NOF_PRECISION_F32_SPLIT ||
+                  c.precision == NOF_PRECISION_F16X2,
+              "unknown precision mode");
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -118,10 +120,14 @@ AcceleratedMLP::AcceleratedMLP(int deg_point, int deg_view, const nof_config& cf
   for (int l = 0; l < kLayers; ++l) { param_views_.push_back(params_.p + woff_[l]); grad_views_.push_back(grads_.p + woff_[l]); }
   for (int l = 0; l < kLayers; ++l) { param_views_.push_back(params_.p + boff_[l]); grad_views_.push_back(grads_.p + boff_[l]); }
 
-  split_ = cfg.precision == NOF_PRECISION_F32_SPLIT;
-  if (split_) {  // bf16 (hi, mid, lo) slices + the fp32 tails (mlp_common.h)
-    wimg_f_.alloc(nof::kFwdImageX3Floats + nof::kFwdTail);
-    wimg_b_.alloc(nof::kBwdImageX3Floats + nof::kBwdTail);
+  precision_ = cfg.precision;
+  if (precision_ == NOF_PRECISION_F32_SPLIT) {  // bf16 (hi, mid, lo) slices + the fp32 tails (mlp_common.h)
+    wimg_f_.alloc(nof::fwd_image_split_floats<1>() + nof::kFwdTail);
+    wimg_b_.alloc(nof::bwd_image_split_floats<1>() + nof::kBwdTail);
+  } else if (precision_ == NOF_PRECISION_F16X2) {  // f16 (hi, lo) slices + the fp32 tails
+    wimg_f_.alloc(nof::fwd_image_split_floats<2>() + nof::kFwdTail);
+    wimg_b_.alloc(nof::bwd_image_split_floats<2>() + nof::kBwdTail);
+    amax_.alloc(1);
   } else {
     wimg_f_.alloc(nof::kFwdImageFloats);
     wimg_b_.alloc(nof::kBwdImageFloats);
@@ -160,7 +166,8 @@ void AcceleratedMLP::pack_weights() {
   nof::PackArgs pa;
   for (int l = 0; l < kLayers; ++l) { pa.woff[l] = woff_[l]; pa.boff[l] = boff_[l]; }
   tb(kTPack);
-  if (split_) NOF_HIP(nof::launch_pack_weights_x3(params_.p, pa, wimg_f_.p, wimg_b_.p, st_));
+  if (precision_ != NOF_PRECISION_F32)
+    NOF_HIP(nof::launch_pack_weights_x3(params_.p, pa, wimg_f_.p, wimg_b_.p, precision_, st_));
   else NOF_HIP(nof::launch_pack_weights(params_.p, pa, wimg_f_.p, wimg_b_.p, st_));
   te(kTPack);
 }
@@ -168,7 +175,7 @@ void AcceleratedMLP::pack_weights() {
 void AcceleratedMLP::run_forward(int level, const nof::FwdArgs& a0) {
   Level& L = lv_[level];
   nof::FwdArgs a = a0;
-  a.split = split_ ? 1 : 0;
+  a.split = precision_;
   a.wimg = wimg_f_.p;
   a.act_in = L.act_in.p;
   a.act_h = L.act_h.p;
@@ -265,10 +272,11 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M) {
   std::vector<int64_t> cost(P.size());
   int64_t total = 0;
   for (size_t i = 0; i < P.size(); ++i) {
-    if (split_) {
+    if (precision_ != NOF_PRECISION_F32) {
       const int WC = nof::wgrad_x3_grid_cols();  // C/2 waves per SIMD
       const int RB = (P[i].ntr + 1) / 2, CB = (P[i].ntc + WC - 1) / WC;
-      cost[i] = std::max(RB * CB * WC / 2, P[i].ntr + P[i].ntc);
+      const int nprod = precision_ == NOF_PRECISION_F16X2 ? 3 : 6;
+      cost[i] = std::max(RB * CB * WC * nprod / 12, P[i].ntr + P[i].ntc);
     } else {
       int c2 = 0;
       P[i].shape = nof::wgrad_shape(P[i].ntr, P[i].ntc, &c2);
@@ -358,7 +366,11 @@ float* const* AcceleratedMLP::get_gradient(const float* color_grad, const float*
   Schedule& sc = schedule(level, L.M);
   nof::BwdArgs b{};
   b.M = L.M;
-  b.split = split_ ? 1 : 0;
+  b.split = precision_;
+  if (precision_ == NOF_PRECISION_F16X2) {
+    NOF_HIP(nof::launch_delta_amax(density_grad, color_grad, L.M, amax_.p, st_));
+    b.amax = amax_.p;
+  }
   b.dsigma = density_grad; b.drgb = color_grad; b.zhead = L.zhead.p;
   b.masks = L.masks.p;
   b.wimg_b = wimg_b_.p;
@@ -367,16 +379,17 @@ float* const* AcceleratedMLP::get_gradient(const float* color_grad, const float*
   NOF_HIP(nof::launch_mlp_bwd(b, st_));
   te(kTMlpBwd);
   tb(kTWgrad);
-  if (split_)
+  if (precision_ != NOF_PRECISION_F32)
     NOF_HIP(nof::launch_wgrad_x3(sc.probs.p, sc.items.p, sc.item_ptr.p, sc.num_wg, sc.slab_off.p, slabs_.p,
-                                 bias_slabs_.p, st_));
+                                 bias_slabs_.p, precision_, st_));
   else
     NOF_HIP(nof::launch_wgrad(sc.probs.p, sc.items.p, sc.item_ptr.p, sc.num_wg, sc.slab_off.p, slabs_.p,
                               bias_slabs_.p, st_));
   te(kTWgrad);
   tb(kTWgradReduce);
   NOF_HIP(nof::launch_wgrad_reduce(sc.outs.p, sc.nouts, sc.max_elems, sc.items.p, sc.probs.p, sc.slab_off.p,
-                                   slabs_.p, bias_slabs_.p, level > 0 ? 1 : 0, st_));
+                                   slabs_.p, bias_slabs_.p, level > 0 ? 1 : 0,
+                                   precision_ == NOF_PRECISION_F16X2 ? amax_.p : nullptr, st_));
   te(kTWgradReduce);
   return grad_views_.data();
 }

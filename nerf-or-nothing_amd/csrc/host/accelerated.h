@@ -142,7 +142,7 @@ class AcceleratedMLP {
   nof_config cfg_;
   hipStream_t st_;
   int num_cu_ = 256;
-  bool split_ = false;  // NOF_PRECISION_F32_SPLIT
+  int precision_ = 0;  // NOF_PRECISION_*
   size_t P_ = 0;
   std::array<int, kLayers> out_{}, in_{}, woff_{}, boff_{};
   DevBuf<float> params_, grads_, wimg_f_, wimg_b_;
@@ -150,6 +150,7 @@ class AcceleratedMLP {
   std::vector<Level> lv_;
   int max_M_ = 0;
   DevBuf<float> delta_, delta9x_, slabs_, bias_slabs_;
+  DevBuf<uint32_t> amax_;  // f16x2: bits of max |dsigma|, |drgb| of the level in flight (delta scale)
   size_t slab_cap_ = 0;
 };
 

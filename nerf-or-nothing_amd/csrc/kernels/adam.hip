@@ -123,54 +123,60 @@ __device__ inline float fwd_tail_value(const float* __restrict__ P, const PackAr
 __device__ inline float bwd_tail_value(const float* __restrict__ P, const PackArgs& pa, int t) {
   return t < kBwdTailW10 ? P[pa.woff[8] + t] : P[pa.woff[10] + (t - kBwdTailW10)];
 }
-__device__ inline __bf16 split_piece(float w, int piece) {
-  const float hi = (float)(__bf16)w;
-  if (piece == 0) return (__bf16)w;
-  const float r1 = w - hi;
-  const float mid = (float)(__bf16)r1;
-  if (piece == 1) return (__bf16)r1;
-  return (__bf16)(r1 - mid);
+// piece `piece` of w in split mode P (mlp_common.h: split2, same RNE conversions and residuals)
+template <int P>
+__device__ inline typename SplitMode<P>::V2 split_piece2(float w, int piece) {
+  typename SplitMode<P>::V2 o[SplitMode<P>::NP];
+  split2<P>(w, w, o);
+  typename SplitMode<P>::V2 r = o[0];
+#pragma unroll
+  for (int p = 1; p < SplitMode<P>::NP; ++p) r = piece == p ? o[p] : r;
+  return r;
 }
 
-constexpr int kX3SliceChunks = kX3SliceFloats / 4;  // 3072 fragments of 16 B
-
-__global__ void k_pack_weights_x3(const float* __restrict__ P, PackArgs pa, float* __restrict__ wf,
+template <int P>
+__global__ void k_pack_weights_x3(const float* __restrict__ P_, PackArgs pa, float* __restrict__ wf,
                                   float* __restrict__ wb) {
+  constexpr int NP = SplitMode<P>::NP;
+  constexpr int kChunks = split_slice_floats<P>() / 4;  // fragments of 16 B per slice
+  const float* __restrict__ Pp = P_;
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t nfc = (int64_t)kFwdSlices * kX3SliceChunks, nbc = (int64_t)kBwdSlices * kX3SliceChunks;
+  const int64_t nfc = (int64_t)kFwdSlices * kChunks, nbc = (int64_t)kBwdSlices * kChunks;
   if (gid < nfc + nbc) {
     const bool fwd = gid < nfc;
     const int64_t c = fwd ? gid : gid - nfc;
-    const int slice = (int)(c / kX3SliceChunks), q = (int)(c % kX3SliceChunks);
-    const int lane = q & 63, rest = q >> 6, piece = rest % 3, so = rest / 3, ot = so & 7, s = so >> 3;
+    const int slice = (int)(c / kChunks), q = (int)(c % kChunks);
+    const int lane = q & 63, rest = q >> 6, piece = rest % NP, so = rest / NP, ot = so & 7, s = so >> 3;
     const int h = lane >> 5, row = ot * 32 + (lane & 31);
     int l, base;
     if (fwd) fwd_slice(slice, l, base);
     else bwd_slice(slice, l, base);
     const int in = layer_in(l);
-    bf16x8 out;
+    typename SplitMode<P>::V8 out;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int kf = 16 * s + 8 * (j >> 2) + 4 * h + (j & 3);
       float w;
-      if (fwd) w = (row < layer_out(l) && base + kf < in) ? P[pa.woff[l] + (int64_t)row * in + base + kf] : 0.0f;
-      else w = P[pa.woff[l] + (int64_t)(base + kf) * in + row];
-      out[j] = split_piece(w, piece);
+      if (fwd) w = (row < layer_out(l) && base + kf < in) ? Pp[pa.woff[l] + (int64_t)row * in + base + kf] : 0.0f;
+      else w = Pp[pa.woff[l] + (int64_t)(base + kf) * in + row];
+      out[j] = split_piece2<P>(w, piece)[0];
     }
-    float* dst = (fwd ? wf : wb) + (size_t)slice * kX3SliceFloats + (size_t)q * 4;
-    *reinterpret_cast<bf16x8*>(dst) = out;
+    float* dst = (fwd ? wf : wb) + (size_t)slice * split_slice_floats<P>() + (size_t)q * 4;
+    *reinterpret_cast<typename SplitMode<P>::V8*>(dst) = out;
   } else {
     const int t = (int)(gid - nfc - nbc);
-    if (t < kFwdTail) wf[kFwdImageX3Floats + t] = fwd_tail_value(P, pa, t);
-    else if (t < kFwdTail + kBwdTail) wb[kBwdImageX3Floats + (t - kFwdTail)] = bwd_tail_value(P, pa, t - kFwdTail);
+    if (t < kFwdTail) wf[fwd_image_split_floats<P>() + t] = fwd_tail_value(Pp, pa, t);
+    else if (t < kFwdTail + kBwdTail)
+      wb[bwd_image_split_floats<P>() + (t - kFwdTail)] = bwd_tail_value(Pp, pa, t - kFwdTail);
   }
 }
-
 hipError_t launch_pack_weights_x3(const float* params, const PackArgs& pa, float* wimg_f, float* wimg_b,
-                                  hipStream_t st) {
-  const int64_t total = (int64_t)(kFwdSlices + kBwdSlices) * kX3SliceChunks + kFwdTail + kBwdTail;
-  hipLaunchKernelGGL(k_pack_weights_x3, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, params, pa, wimg_f,
-                     wimg_b);
+                                  int precision, hipStream_t st) {
+  const int chunks = precision == 2 ? split_slice_floats<2>() / 4 : split_slice_floats<1>() / 4;
+  const int64_t total = (int64_t)(kFwdSlices + kBwdSlices) * chunks + kFwdTail + kBwdTail;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (precision == 2) hipLaunchKernelGGL(k_pack_weights_x3<2>, grid, dim3(256), 0, st, params, pa, wimg_f, wimg_b);
+  else hipLaunchKernelGGL(k_pack_weights_x3<1>, grid, dim3(256), 0, st, params, pa, wimg_f, wimg_b);
   return hipGetLastError();
 }
 

@@ -37,7 +37,7 @@ hipError_t launch_output_gradient(int n, const float* C, const float* pix, const
 struct FwdArgs {
   int M, S, encoded;
   int no_store;                            // 1: inference only, skip the backward's side outputs
-  int split;                               // 1: split-bf16 image and MFMAs (mlp_common.h)
+  int split;                               // MLP precision: 0 fp32, 1 bf16x3 split, 2 f16x2 (mlp_common.h)
   const float *t, *origins, *dirs, *radii;  // fused-encoding inputs
   const float *enc_pos, *enc_dir;          // encoded inputs (API path): [M][96], [n][27]
   const float* wimg;                       // packed forward image (slices + tail)
@@ -53,14 +53,17 @@ hipError_t launch_mlp_fwd(const FwdArgs& a, hipStream_t st);
 
 struct BwdArgs {
   int M;
-  int split;
+  int split;                               // as FwdArgs::split
   const float *dsigma, *drgb, *zhead;
+  const uint32_t* amax;                    // split == 2: max |dsigma|, |drgb| bits (launch_delta_amax)
   const uint32_t* masks;
   const float* wimg_b;                     // packed backward image (slices + tail)
   float* delta;    // [8][M/32][256][32]
   float* delta9x;  // [M/32][160][32]
 };
 hipError_t launch_mlp_bwd(const BwdArgs& a, hipStream_t st);
+// f16x2 mode: *amax = bits of max(|dsigma|, |drgb|) over M samples (clears *amax first)
+hipError_t launch_delta_amax(const float* dsigma, const float* drgb, int M, uint32_t* amax, hipStream_t st);
 // fp32-precision kernels (v_mfma_f32_16x16x4_f32, two waves per SIMD): mlp_fwd16.hip / mlp_bwd16.hip
 hipError_t launch_mlp_fwd16(const FwdArgs& a, hipStream_t st);
 hipError_t launch_mlp_bwd16(const BwdArgs& a, hipStream_t st);
@@ -86,11 +89,13 @@ hipError_t launch_wgrad(const WgProblem* probs, const WgItem* items, const int* 
 // its busiest SIMD per 16 k-steps (2 per 32x32 tile-k-block at two waves per SIMD)
 int wgrad_shape(int ntr, int ntc, int* cost2);
 int wgrad_x3_grid_cols();  // columns of k_wgrad_x3's 2 x C wave grid (schedule cost model)
+// split-precision weight gradients: precision 1 (bf16x3) or 2 (f16x2)
 hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,
-                        const int64_t* slab_off, float* slabs, float* bias_slabs, hipStream_t st);
+                           const int64_t* slab_off, float* slabs, float* bias_slabs, int precision, hipStream_t st);
 hipError_t launch_wgrad_reduce(const WgOut* outs, int nouts, int max_elems, const WgItem* items,
                                const WgProblem* probs, const int64_t* slab_off, const float* slabs,
-                               const float* bias_slabs, int accumulate, hipStream_t st);
+                               const float* bias_slabs, int accumulate, const uint32_t* amax, hipStream_t st);
+// (amax != null: sums are multiplied by the inverse f16x2 delta scale, mlp_common.h)
 
 // ---- adam.hip ----------------------------------------------------------------------------------
 // ---- dataset.hip: device-resident record set -> SoA batch gather (+ optional loss-mult sum) ----
@@ -110,7 +115,8 @@ hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v, 
                        hipStream_t st);
 struct PackArgs { int woff[11]; int boff[11]; };
 hipError_t launch_pack_weights(const float* params, const PackArgs& pa, float* wimg_f, float* wimg_b, hipStream_t st);
+// split images: precision 1 (bf16 hi/mid/lo) or 2 (f16 hi/lo)
 hipError_t launch_pack_weights_x3(const float* params, const PackArgs& pa, float* wimg_f, float* wimg_b,
-                                  hipStream_t st);
+                                  int precision, hipStream_t st);
 
 }  // namespace nof

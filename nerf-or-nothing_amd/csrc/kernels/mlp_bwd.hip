@@ -8,6 +8,8 @@
 // block-swizzled [F][32] layout for the deterministic weight-gradient GEMMs (wgrad.hip).
 // Gradient routing per D11: dh7 = W8^T dz_s + W9[:, :256]^T delta9 ; dh3 = W4[:, :256]^T delta4.
 // Heads per MNcs:410-415 with the sigmoid' written as s(1-s) (overflow-safe, D28).
+#include <algorithm>
+
 #include "common.h"
 #include "launch.h"
 #include "mlp_common.h"
@@ -74,10 +76,10 @@ struct BwdEpi {
   }
 };
 
-template <bool X3>
+template <int P>  // precision (mlp_common.h)
 __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
-  __shared__ __attribute__((aligned(16))) float lds[ring_floats<X3>() + 256];
-  float* w8_lds = lds + ring_floats<X3>();
+  __shared__ __attribute__((aligned(16))) float lds[ring_floats<P>() + 256];
+  float* w8_lds = lds + ring_floats<P>();
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, j = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: block pointers stay in SGPRs
   const BlkStore bst(lane);
@@ -85,19 +87,25 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
   const int blk_raw = blockIdx.x * 4 + wave;
   const int blk = blk_raw < nblk ? blk_raw : nblk - 1;  // tail waves duplicate the last block
   const int m = blk * kBlk + j;
-  const float* tail = a.wimg_b + (size_t)kBwdSlices * slice_floats<X3>();
+  const float* tail = a.wimg_b + (size_t)kBwdSlices * slice_floats<P>();
   const size_t layer_stride = (size_t)nblk * kWidth * kBlk;
 
-  first_slice_dma<X3>(a.wimg_b, lds, tid);
+  first_slice_dma<P>(a.wimg_b, lds, tid);
 
   // ---- heads (MNcs:410-415) ------------------------------------------------------------
   const f32x4 zh = reinterpret_cast<const f32x4*>(a.zhead)[m];
-  const float dzs = a.dsigma[m] * sigmoid_f(zh[0] + kDensityBias);
+  float dzs = a.dsigma[m] * sigmoid_f(zh[0] + kDensityBias);
   float dzc[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const float s = sigmoid_f(zh[1 + c]);
     dzc[c] = a.drgb[(size_t)m * 3 + c] * (s * (1.0f - s)) * kRgbScale;
+  }
+  if constexpr (P == 2) {  // f16x2: deltas enter the fp16 pieces scaled by a power of two
+    const float sc = delta_scale(a.amax, false);
+    dzs *= sc;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) dzc[c] *= sc;
   }
   float* d9 = a.delta9x + (size_t)blk * kD9F * kBlk;  // uniform block base
   if (h == 0) {  // rows 128..131 = tile 4, registers 0..3 of lane half 0
@@ -151,20 +159,20 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
   // ---- dh7 = W9[:, :256]^T delta9 + w8 dz_s ; delta7 ---------------------------------------
   BwdEpi<true> e7(accA, bin, bst, lane);
   e7.begin(masks + ((size_t)blk * kMaskSlots + 7) * 256, delta_blk + 7 * layer_stride, lane, w8_lds, dzs);
-  dense_layer<X3, 4, 0, 8>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane);
+  dense_layer<P, 4, 0, 8>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane);
   e7.tile0();
   // ---- dh_{l-1} = W_l[:, :256]^T delta_l ; delta_{l-1}, l = 7..1 (l odd: A -> B) ------------
   BwdEpi<false> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
   eb.begin(masks + ((size_t)blk * kMaskSlots + 6) * 256, delta_blk + 6 * layer_stride, lane);
-  dense_layer<X3, 8, 0, 8>(bin, nullptr, accB, lds, cur, wsrc, false, tid, lane, e7);
+  dense_layer<P, 8, 0, 8>(bin, nullptr, accB, lds, cur, wsrc, false, tid, lane, e7);
   eb.tile0();
   static_assert(kDepth == 8, "bwd pairing assumes 8 trunk layers");
   for (int l = kDepth - 2; l >= 2; l -= 2) {
     ea.begin(masks + ((size_t)blk * kMaskSlots + l - 1) * 256, delta_blk + (l - 1) * layer_stride, lane);
-    dense_layer<X3, 8, 0, 8>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane, eb);
+    dense_layer<P, 8, 0, 8>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane, eb);
     ea.tile0();
     eb.begin(masks + ((size_t)blk * kMaskSlots + l - 2) * 256, delta_blk + (l - 2) * layer_stride, lane);
-    dense_layer<X3, 8, 0, 8>(bin, nullptr, accB, lds, cur, wsrc, l == 2, tid, lane, ea);
+    dense_layer<P, 8, 0, 8>(bin, nullptr, accB, lds, cur, wsrc, l == 2, tid, lane, ea);
     eb.tile0();
   }
   // delta0: nothing left to hide it under
@@ -174,13 +182,34 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
     for (int q = 0; q < 4; ++q) eb(t, q);
 }
 
+// amax of |dsigma|, |drgb| as float bits (non-negative floats order as unsigned ints); *amax must
+// be zero on entry (the launcher clears it on the stream first)
+__global__ void k_delta_amax(const float* __restrict__ dsigma, const float* __restrict__ drgb, int M,
+                             uint32_t* amax) {
+  float v = 0.0f;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 4 * M; i += gridDim.x * blockDim.x)
+    v = fmaxf(v, fabsf(i < M ? dsigma[i] : drgb[i - M]));
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(v));
+}
+
+hipError_t launch_delta_amax(const float* dsigma, const float* drgb, int M, uint32_t* amax, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(amax, 0, sizeof(uint32_t), st);
+  if (e != hipSuccess || M <= 0) return e;
+  const int blocks = std::min(1024, (4 * M + 255) / 256);
+  hipLaunchKernelGGL(k_delta_amax, dim3(blocks), dim3(256), 0, st, dsigma, drgb, M, amax);
+  return hipGetLastError();
+}
+
 hipError_t launch_mlp_bwd(const BwdArgs& a, hipStream_t st) {
   if (a.M <= 0) return hipSuccess;
   if (a.M % kBlk != 0) return hipErrorInvalidValue;
   const int nblk = a.M / kBlk;
-  if (a.split) hipLaunchKernelGGL(k_mlp_bwd<true>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
+  if (a.split == 1) hipLaunchKernelGGL(k_mlp_bwd<1>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
+  else if (a.split == 2) hipLaunchKernelGGL(k_mlp_bwd<2>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
 #ifdef NOF_F32_MFMA32
-  else hipLaunchKernelGGL(k_mlp_bwd<false>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
+  else hipLaunchKernelGGL(k_mlp_bwd<0>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
 #else
   else return launch_mlp_bwd16(a, st);
 #endif

@@ -96,21 +96,6 @@ template <int OT> constexpr int f32_parts_after_dma() {
   for (int q = 0; q < 4; ++q) n += (q * OT + 1 > 7) ? 1 : 0;
   return n;
 }
-// split layer (the 48-KB slice is 12 steps, checked below): kX3DmaPer DMA steps in each of the first
-// groups; parts in groups s OT + 1 and s OT + OT/2 + 1
-#ifndef NOF_X3_DMA_PER_GROUP
-#define NOF_X3_DMA_PER_GROUP 2
-#endif
-constexpr int kX3DmaPer = NOF_X3_DMA_PER_GROUP;                       // DMA steps per MFMA group
-constexpr int kX3DmaGroups = (12 + kX3DmaPer - 1) / kX3DmaPer;       // groups carrying DMA steps
-static_assert(kX3DmaGroups <= 8, "the OT = 4 layer has 8 MFMA groups per slice");
-template <int OT> constexpr int x3_parts_after_dma() {
-  int n = 0;
-  for (int s = 0; s < 2; ++s)
-    n += ((s * OT + 1 > kX3DmaGroups - 1) ? 1 : 0) + ((s * OT + OT / 2 + 1 > kX3DmaGroups - 1) ? 1 : 0);
-  return n;
-}
-
 // One dense layer: acc[ot] (ot < OT) = sum over NT_B slices with B from `bin` (registers) and
 // NT_I slices with B from the wave's IPE copy in LDS.  Consumes NT_B + NT_I slices of the
 // ring with one workgroup barrier each; the next slice's DMA is in flight during the MFMAs.
@@ -179,92 +164,146 @@ __device__ __forceinline__ void mlp_layer(const float (&bin)[8][16], const float
 }
 
 // ============================================================================================
-// Split mode (nof_config.precision = NOF_PRECISION_F32_SPLIT): every fp32 operand x is carried as
-// three bf16 pieces hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid) (24 significand
-// bits, fp32's exponent range, no scaling), and a product a.b as the six bf16 MFMAs whose terms
-// are >= 2^-16 of it (lo.hi, hi.lo, mid.mid, mid.hi, hi.mid, hi.hi) accumulated in fp32.  One
-// v_mfma_f32_32x32x16_bf16 does 8x the k of v_mfma_f32_32x32x2_f32 in half the cycles, so six of
-// them cost 3/8 of the fp32 MFMA time; measured error vs fp64 equals the fp32 MFMA's
-// (tools/probe/x3_probe.hip: rel L2 8.4e-7 vs 9.7e-7 at K = 4096).
+// Split modes: every fp32 operand x is carried as NP 16-bit pieces and a product a.b as the
+// NPROD 32x32x16 MFMAs of the piece pairs that matter, accumulated in fp32.  One 32x32x16 MFMA
+// does 8x the k of v_mfma_f32_32x32x2_f32 in half the cycles.
+//   P = 1 (NOF_PRECISION_F32_SPLIT, fp32-accurate): bf16 pieces hi = bf16(x), mid = bf16(x - hi),
+//     lo = bf16(x - hi - mid) (24 significand bits, fp32's exponent range, no scaling), six
+//     products (lo.hi, hi.lo, mid.mid, mid.hi, hi.mid, hi.hi: every term >= 2^-16 of the product).
+//     Measured error vs fp64 equals the fp32 MFMA's (tools/probe/x3_probe.hip: rel L2 8.4e-7 vs
+//     9.7e-7 at K = 4096).
+//   P = 2 (NOF_PRECISION_F16X2, the perf mode of SURVEY §8d): fp16 pieces hi = f16(x),
+//     lo = f16(x - hi) (22 significand bits inside fp16's range), three products (lo.hi, hi.lo,
+//     hi.hi).  Forward operands (weights ~0.1, activations O(1)) need no scaling; the backward
+//     deltas (O(1e-6) after the 1/sum(m) loss normalisation) are scaled by a power of two
+//     (k_delta_scale) before they reach the pieces and unscaled after the weight-gradient sums,
+//     so every fp32 step in between is exact.  tools/precision_study.py (f16x2s): gradients'
+//     per-tensor rel L2 vs fp64 median 7e-5, max 4e-4 (bound 2e-3).
 //
-// Fragment maps (32x32x16 bf16, verified by the probe): lane l = (h = l >> 5, x = l & 31) holds
-// A[row x][k = 8h + j] and B[k = 8h + j][col x], j = 0..7.  K-step s of an activation tile
+// Fragment maps (32x32x16 bf16/f16, verified by the probe): lane l = (h = l >> 5, x = l & 31)
+// holds A[row x][k = 8h + j] and B[k = 8h + j][col x], j = 0..7.  K-step s of an activation tile
 // (registers 8s..8s+7 of its accumulator) therefore carries feature 16s + 8(j >> 2) + 4h + (j & 3)
 // in element j, and the packed weight pieces follow that order.
 // ============================================================================================
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-struct Frag3 {
-  bf16x8 p[3];  // hi, mid, lo
+template <int P> struct SplitMode;
+template <> struct SplitMode<1> {
+  typedef bf16x8 V8;
+  typedef bf16x4 V4;
+  typedef bf16x2 V2;
+  static constexpr int NP = 3, NPROD = 6;
+  // product order (smallest terms first): pieces of A and B for product pp
+  static constexpr int pa(int pp) { return pp == 0 ? 2 : (pp == 2 || pp == 3) ? 1 : 0; }
+  static constexpr int pb(int pp) { return pp == 1 ? 2 : (pp == 2 || pp == 4) ? 1 : 0; }
+  static __device__ __forceinline__ f32x16 mfma(V8 a, V8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct SplitMode<2> {
+  typedef f16x8 V8;
+  typedef f16x4 V4;
+  typedef f16x2 V2;
+  static constexpr int NP = 2, NPROD = 3;
+  static constexpr int pa(int pp) { return pp == 0 ? 1 : 0; }
+  static constexpr int pb(int pp) { return pp == 1 ? 1 : 0; }
+  static __device__ __forceinline__ f32x16 mfma(V8 a, V8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
 };
 
-// split elements (i, i + 1) of a fragment: exact fp32 residuals, RNE conversions (v_cvt_pk_bf16_f32)
-__device__ __forceinline__ void split2(float x0, float x1, bf16x2& a, bf16x2& b, bf16x2& c) {
-  const f32x2 v = {x0, x1};
-  a = __builtin_convertvector(v, bf16x2);
-  const f32x2 r1 = v - __builtin_convertvector(a, f32x2);
-  b = __builtin_convertvector(r1, bf16x2);
-  const f32x2 r2 = r1 - __builtin_convertvector(b, f32x2);
-  c = __builtin_convertvector(r2, bf16x2);
+template <int P>
+struct Frag {
+  typename SplitMode<P>::V8 p[SplitMode<P>::NP];  // hi, (mid,) lo
+};
+
+// split elements (i, i + 1): exact fp32 residuals, RNE conversions (v_cvt_pk_bf16_f32 /
+// v_cvt_pk_f16_f32)
+template <int P>
+__device__ __forceinline__ void split2(float x0, float x1, typename SplitMode<P>::V2 (&o)[SplitMode<P>::NP]) {
+  typedef typename SplitMode<P>::V2 V2;
+  f32x2 r = {x0, x1};
+#pragma unroll
+  for (int p = 0; p < SplitMode<P>::NP; ++p) {
+    o[p] = __builtin_convertvector(r, V2);
+    if (p + 1 < SplitMode<P>::NP) r = r - __builtin_convertvector(o[p], f32x2);
+  }
 }
-__device__ __forceinline__ bf16x8 cat4(bf16x2 a, bf16x2 b, bf16x2 c, bf16x2 d) {
-  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-  const bf16x4 lo = __builtin_shufflevector(a, b, 0, 1, 2, 3);
-  const bf16x4 hi = __builtin_shufflevector(c, d, 0, 1, 2, 3);
+template <class V8, class V2>
+__device__ __forceinline__ V8 cat4(V2 a, V2 b, V2 c, V2 d) {
+  const auto lo = __builtin_shufflevector(a, b, 0, 1, 2, 3);
+  const auto hi = __builtin_shufflevector(c, d, 0, 1, 2, 3);
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
-__device__ __forceinline__ void split_pair(float x0, float x1, Frag3& f, int i) {
-  bf16x2 a, b, c;
-  split2(x0, x1, a, b, c);
-  f.p[0][i] = a[0]; f.p[0][i + 1] = a[1];
-  f.p[1][i] = b[0]; f.p[1][i + 1] = b[1];
-  f.p[2][i] = c[0]; f.p[2][i + 1] = c[1];
-}
-__device__ __forceinline__ void split8(const float (&v)[8], Frag3& f) {
-  bf16x2 a[4], b[4], c[4];
+template <int P>
+__device__ __forceinline__ void split_pair(float x0, float x1, Frag<P>& f, int i) {
+  typename SplitMode<P>::V2 o[SplitMode<P>::NP];
+  split2<P>(x0, x1, o);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) split2(v[2 * i], v[2 * i + 1], a[i], b[i], c[i]);
-  f.p[0] = cat4(a[0], a[1], a[2], a[3]);
-  f.p[1] = cat4(b[0], b[1], b[2], b[3]);
-  f.p[2] = cat4(c[0], c[1], c[2], c[3]);
+  for (int p = 0; p < SplitMode<P>::NP; ++p) { f.p[p][i] = o[p][0]; f.p[p][i + 1] = o[p][1]; }
 }
-__device__ __forceinline__ void split44(const f32x4& u, const f32x4& v, Frag3& f) {
-  const float e[8] = {u[0], u[1], u[2], u[3], v[0], v[1], v[2], v[3]};
-  split8(e, f);
+template <int P>
+__device__ __forceinline__ void split8(const float (&v)[8], Frag<P>& f) {
+  typedef typename SplitMode<P>::V2 V2;
+  constexpr int NP = SplitMode<P>::NP;
+  V2 o[4][NP];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) split2<P>(v[2 * i], v[2 * i + 1], o[i]);
+#pragma unroll
+  for (int p = 0; p < NP; ++p) f.p[p] = cat4<typename SplitMode<P>::V8>(o[0][p], o[1][p], o[2][p], o[3][p]);
 }
 
-// product order of mfma_x3 (smallest terms first): pieces of A and B for product pp
-__device__ __forceinline__ constexpr int x3_pa(int pp) { return pp == 0 ? 2 : (pp == 2 || pp == 3) ? 1 : 0; }
-__device__ __forceinline__ constexpr int x3_pb(int pp) { return pp == 1 ? 2 : (pp == 2 || pp == 4) ? 1 : 0; }
-
-__device__ __forceinline__ f32x16 mfma_x3(const Frag3& a, const Frag3& b, f32x16 c) {
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[2], b.p[0], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[2], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[1], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[0], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[1], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[0], c, 0, 0, 0);
+template <int P>
+__device__ __forceinline__ f32x16 mfma_split(const Frag<P>& a, const Frag<P>& b, f32x16 c) {
+  typedef SplitMode<P> M;
+#pragma unroll
+  for (int pp = 0; pp < M::NPROD; ++pp) c = M::mfma(a.p[M::pa(pp)], b.p[M::pb(pp)], c);
   return c;
 }
 
-// Split-mode weight slice: 32 input features (2 k-steps) x 256 rows (8 row tiles) x 3 pieces;
-// 16-B chunk ((s * 8 + ot) * 3 + piece) * 64 + lane holds lane's 8 bf16 of that fragment, so each
-// fragment is one conflict-free ds_read_b128 (1 KB contiguous per wave).  48 KB.
-constexpr int kX3SliceFloats = 2 * 8 * 3 * 64 * 4;
+// Split-mode weight slice: 32 input features (2 k-steps) x 256 rows (8 row tiles) x NP pieces;
+// 16-B chunk ((s * 8 + ot) * NP + piece) * 64 + lane holds lane's 8 pieces of that fragment, so
+// each fragment is one conflict-free ds_read_b128 (1 KB contiguous per wave).  48 KB (P = 1) or
+// 32 KB (P = 2).
+template <int P> constexpr int split_slice_floats() { return 2 * 8 * SplitMode<P>::NP * 64 * 4; }
+template <int P> constexpr int split_dma_steps() { return split_slice_floats<P>() / 4 / kMlpThreads; }
+constexpr int kX3SliceFloats = split_slice_floats<1>();
 constexpr size_t kFwdImageX3Floats = (size_t)kFwdSlices * kX3SliceFloats;  // + fwd tail (fp32)
 constexpr size_t kBwdImageX3Floats = (size_t)kBwdSlices * kX3SliceFloats;  // + bwd tail (fp32)
+template <int P> constexpr size_t fwd_image_split_floats() { return (size_t)kFwdSlices * split_slice_floats<P>(); }
+template <int P> constexpr size_t bwd_image_split_floats() { return (size_t)kBwdSlices * split_slice_floats<P>(); }
+static_assert(split_dma_steps<1>() == 12 && split_dma_steps<2>() == 8, "split slices = 12 / 8 DMA steps");
 
-static_assert(kX3SliceFloats / 4 / kMlpThreads == 12, "split slice = 12 DMA steps");
-__device__ __forceinline__ void slice_dma_x3(const float* __restrict__ src, float* dst, int tid) {
+template <int P>
+__device__ __forceinline__ void slice_dma_split(const float* __restrict__ src, float* dst, int tid) {
   const int wave = tid >> 6;
 #pragma unroll
-  for (int i = 0; i < kX3SliceFloats / 4 / kMlpThreads; ++i) {
+  for (int i = 0; i < split_dma_steps<P>(); ++i) {
     const int chunk = kMlpThreads * i + tid;
     __builtin_amdgcn_global_load_lds((gptr_t)(src + chunk * 4), (lptr_t)(dst + (kMlpThreads * i + 64 * wave) * 4),
                                      16, 0, 0);
   }
+}
+
+// split layer: kX3DmaPer DMA steps in each of the first groups; parts in groups s OT + 1 and
+// s OT + OT/2 + 1
+#ifndef NOF_X3_DMA_PER_GROUP
+#define NOF_X3_DMA_PER_GROUP 2
+#endif
+constexpr int kX3DmaPer = NOF_X3_DMA_PER_GROUP;  // DMA steps per MFMA group
+template <int P> constexpr int split_dma_groups() { return (split_dma_steps<P>() + kX3DmaPer - 1) / kX3DmaPer; }
+static_assert(split_dma_groups<1>() <= 8, "the OT = 4 layer has 8 MFMA groups per slice");
+template <int P, int OT> constexpr int split_parts_after_dma() {
+  int n = 0;
+  for (int s = 0; s < 2; ++s)
+    n += ((s * OT + 1 > split_dma_groups<P>() - 1) ? 1 : 0) + ((s * OT + OT / 2 + 1 > split_dma_groups<P>() - 1) ? 1 : 0);
+  return n;
 }
 
 // raw fp32 B values of k-step kk of a split-mode layer: tiles t < NT_B from the register-resident
@@ -287,29 +326,32 @@ __device__ __forceinline__ void x3_b_values(const float (&bin)[8][16], const flo
 }
 
 // Split-mode dense layer: same contract as mlp_layer (slices of the split image, one barrier per
-// slice).  Per (k-step, row tile): three ds_read_b128 (issued one group ahead) and six MFMAs; the
+// slice).  Per (k-step, row tile): NP ds_read_b128 (issued one group ahead) and NPROD MFMAs; the
 // next k-step's B fragment is split pair by pair in the shadow of the current k-step's MFMAs.
 // Epilogue parts: k-step s of slice t runs epi(t + 1, 2s) and epi(t + 1, 2s + 1), so the first half
 // of tile t + 1 is in `bin` before k-step 1 of slice t splits it as the next B fragment.
-template <int NT_B, int NT_I, int OT, class Epi>
-__device__ __forceinline__ void mlp_layer_x3(const float (&bin)[8][16], const float* ipe_lds, f32x16 (&acc)[8],
-                                             float* lds, int& cur, const float*& wsrc, bool last_in_schedule,
-                                             int tid, int lane, Epi& epi) {
+template <int P, int NT_B, int NT_I, int OT, class Epi>
+__device__ __forceinline__ void mlp_layer_split(const float (&bin)[8][16], const float* ipe_lds, f32x16 (&acc)[8],
+                                                float* lds, int& cur, const float*& wsrc, bool last_in_schedule,
+                                                int tid, int lane, Epi& epi) {
+  typedef typename SplitMode<P>::V8 V8;
+  constexpr int NP = SplitMode<P>::NP;
+  constexpr int SF = split_slice_floats<P>();
   constexpr int NK = 2 * (NT_B + NT_I);
   constexpr int PER = OT / 4;  // row-tile groups per split pair
-  Frag3 b_cur, b_nxt;
+  Frag<P> b_cur, b_nxt;
   {
     float v[8];
     x3_b_values<NT_B>(bin, ipe_lds, 0, lane, v);
-    split8(v, b_cur);
+    split8<P>(v, b_cur);
   }
 #pragma unroll
   for (int t = 0; t < NT_B + NT_I; ++t) {
     const bool has_next = !(last_in_schedule && t == NT_B + NT_I - 1);
-    const bf16x8* W = reinterpret_cast<const bf16x8*>(lds + cur * kX3SliceFloats) + lane;
-    Frag3 a_cur;
+    const V8* W = reinterpret_cast<const V8*>(lds + cur * SF) + lane;
+    Frag<P> a_cur;
 #pragma unroll
-    for (int p = 0; p < 3; ++p) a_cur.p[p] = W[p * 64];
+    for (int p = 0; p < NP; ++p) a_cur.p[p] = W[p * 64];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int kk = 2 * t + s;
@@ -317,8 +359,9 @@ __device__ __forceinline__ void mlp_layer_x3(const float (&bin)[8][16], const fl
       if (kk + 1 < NK) x3_b_values<NT_B>(bin, ipe_lds, kk + 1, lane, vn);
 #pragma unroll
       for (int ot = 0; ot < OT; ++ot) {
-        asm volatile("" ::"v"(a_cur.p[0]), "v"(a_cur.p[1]), "v"(a_cur.p[2]));  // wait here, before the next reads
-        Frag3 a_nxt = a_cur;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) asm volatile("" ::"v"(a_cur.p[p]));  // wait here, before the next reads
+        Frag<P> a_nxt = a_cur;
         const bool more = !(s == 1 && ot == OT - 1);
 #ifdef NOF_DIAG_NO_AREAD
         if (more && t == 0) {
@@ -328,22 +371,22 @@ __device__ __forceinline__ void mlp_layer_x3(const float (&bin)[8][16], const fl
           const int s2 = ot == OT - 1 ? s + 1 : s;
           const int ot2 = ot == OT - 1 ? 0 : ot + 1;
 #pragma unroll
-          for (int p = 0; p < 3; ++p) a_nxt.p[p] = W[((s2 * 8 + ot2) * 3 + p) * 64];
+          for (int p = 0; p < NP; ++p) a_nxt.p[p] = W[((s2 * 8 + ot2) * NP + p) * 64];
         }
 #ifndef NOF_DIAG_NO_DMA
-        if (has_next && s * OT + ot < kX3DmaGroups) {
+        if (has_next && s * OT + ot < split_dma_groups<P>()) {
 #pragma unroll
           for (int u = 0; u < kX3DmaPer; ++u) {
             const int st = kX3DmaPer * (s * OT + ot) + u;
-            if (st < 12) slice_dma_step(wsrc + kX3SliceFloats, lds + (cur ^ 1) * kX3SliceFloats, tid, st);
+            if (st < split_dma_steps<P>()) slice_dma_step(wsrc + SF, lds + (cur ^ 1) * SF, tid, st);
           }
         }
 #endif
         __builtin_amdgcn_sched_barrier(0);
-        acc[ot] = mfma_x3(a_cur, b_cur, kk == 0 ? f32x16{} : acc[ot]);
+        acc[ot] = mfma_split<P>(a_cur, b_cur, kk == 0 ? f32x16{} : acc[ot]);
         if (kk + 1 < NK && ot % PER == 0) {
           const int i = 2 * (ot / PER);
-          split_pair(vn[i], vn[i + 1], b_nxt, i);
+          split_pair<P>(vn[i], vn[i + 1], b_nxt, i);
         }
         if (t + 1 < NT_B && (ot == 1 || ot == OT / 2 + 1)) epi(t + 1, 2 * s + (ot == 1 ? 0 : 1));
         __builtin_amdgcn_sched_barrier(0);
@@ -351,36 +394,52 @@ __device__ __forceinline__ void mlp_layer_x3(const float (&bin)[8][16], const fl
       }
       b_cur = b_nxt;
     }
-    slice_barrier(t + 1 < NT_B ? x3_parts_after_dma<OT>() * Epi::kVmPerPart : 0);
+    slice_barrier(t + 1 < NT_B ? split_parts_after_dma<P, OT>() * Epi::kVmPerPart : 0);
     cur ^= 1;
 #ifndef NOF_DIAG_DMA_SAME
-    wsrc += kX3SliceFloats;
+    wsrc += SF;
 #endif
   }
 }
 
-// mode dispatch for the fused kernels
-template <bool X3, int NT_B, int NT_I, int OT, class Epi>
+// f16x2 backward-delta scaling: amax = max |x| over the incoming dsigma / drgb (float bits, written
+// by k_delta_amax), scale = 2^(kDeltaTop - floor(log2 amax)) so the largest head delta lands in
+// [2^8, 2^9) — 2^7 below fp16's max for the growth through the layers, and 2^-24 absolute
+// resolution of the lo piece is then 2^-32 of the tensor's max.  Power of two: every fp32 op on
+// scaled values is exact, and k_wgrad_reduce multiplies the sums by the inverse.
+constexpr int kDeltaTop = 8;
+__device__ __forceinline__ float delta_scale(const uint32_t* amax_bits, bool inverse) {
+  const float amax = __uint_as_float(*amax_bits);
+  if (!(amax > 0.0f) || !(amax < __builtin_huge_valf())) return 1.0f;
+  int e;
+  (void)frexpf(amax, &e);  // amax = m 2^e, m in [0.5, 1)
+  const int k = min(max(kDeltaTop - (e - 1), -100), 100);
+  return ldexpf(1.0f, inverse ? -k : k);
+}
+
+// mode dispatch for the fused kernels: P = 0 fp32 (32x32x2 fp32 MFMA), 1 bf16x3, 2 f16x2
+template <int P, int NT_B, int NT_I, int OT, class Epi>
 __device__ __forceinline__ void dense_layer(const float (&bin)[8][16], const float* ipe_lds, f32x16 (&acc)[8],
                                             float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
                                             int lane, Epi& epi) {
-  if constexpr (X3) mlp_layer_x3<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi);
+  if constexpr (P > 0)
+    mlp_layer_split<P, NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi);
   else mlp_layer<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi);
 }
-template <bool X3, int NT_B, int NT_I, int OT>
+template <int P, int NT_B, int NT_I, int OT>
 __device__ __forceinline__ void dense_layer(const float (&bin)[8][16], const float* ipe_lds, f32x16 (&acc)[8],
                                             float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
                                             int lane) {
   NoEpi none;
-  dense_layer<X3, NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, none);
+  dense_layer<P, NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, none);
 }
-template <bool X3>
+template <int P>
 __device__ __forceinline__ void first_slice_dma(const float* src, float* dst, int tid) {
-  if constexpr (X3) slice_dma_x3(src, dst, tid);
+  if constexpr (P > 0) slice_dma_split<P>(src, dst, tid);
   else slice_dma(src, dst, tid);
 }
-template <bool X3> constexpr int ring_floats() { return 2 * (X3 ? kX3SliceFloats : kSliceFloats); }
-template <bool X3> constexpr int slice_floats() { return X3 ? kX3SliceFloats : kSliceFloats; }
+template <int P> constexpr int slice_floats() { return P > 0 ? split_slice_floats<P>() : kSliceFloats; }
+template <int P> constexpr int ring_floats() { return 2 * slice_floats<P>(); }
 
 // Stores of accumulator tiles into a chunk-swizzled [F][32] block (common.h) with no per-store
 // VALU: the wave-uniform block base lives in SGPRs (+ 4 KB per 32-feature tile, a scalar add), the

@@ -142,9 +142,9 @@ struct FwdEpi {
   }
 };
 
-template <bool X3, bool store>  // store: side outputs for the backward pass (off for inference)
+template <int P, bool store>  // P: precision (mlp_common.h); store: side outputs for the backward pass (off for inference)
 __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
-  constexpr int kRing = ring_floats<X3>();
+  constexpr int kRing = ring_floats<P>();
   constexpr int kBiasLds = 8 * 256 + 256;
   __shared__ __attribute__((aligned(16))) float lds[kRing + 4 * kIpeLdsFloats + 4 * 128 + kBiasLds];
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, j = lane & 31;
@@ -156,9 +156,9 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
   const int ray = m0 / a.S;
   const int s0 = m0 - ray * a.S;
   const int m = m0 + j;
-  const float* tail = a.wimg + (size_t)kFwdSlices * slice_floats<X3>();
+  const float* tail = a.wimg + (size_t)kFwdSlices * slice_floats<P>();
 
-  first_slice_dma<X3>(a.wimg, lds, tid);  // first slice in flight while the encodings are computed
+  first_slice_dma<P>(a.wimg, lds, tid);  // first slice in flight while the encodings are computed
 
   // ---- encodings: 48 IPE features per lane in B-operand order ----------------------------
   float ipe[3][16];
@@ -243,25 +243,25 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
   // ---- trunk: layer l writes acc(l odd ? B : A) ------------------------------------------
   FwdEpi<store, false> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
   ea.begin(biases, act_h_blk, mask_ptr(a.masks, blk, 0), lane);
-  dense_layer<X3, 0, 3, 8>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane);
+  dense_layer<P, 0, 3, 8>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane);
   ea.tile0();
   for (int l = 1; l < kDepth - 1; l += 2) {
     eb.begin(biases + l * 256, act_h_blk + l * layer_stride, mask_ptr(a.masks, blk, l), lane);
-    dense_layer<X3, 8, 0, 8>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea);
+    dense_layer<P, 8, 0, 8>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea);
     eb.tile0();
     ea.begin(biases + (l + 1) * 256, act_h_blk + (l + 1) * layer_stride, mask_ptr(a.masks, blk, l + 1), lane);
-    if (l + 1 == kSkip) dense_layer<X3, 8, 3, 8>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, eb);
-    else dense_layer<X3, 8, 0, 8>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, eb);
+    if (l + 1 == kSkip) dense_layer<P, 8, 3, 8>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, eb);
+    else dense_layer<P, 8, 0, 8>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, eb);
     ea.tile0();
   }
   static_assert(kDepth == 8 && kSkip % 2 == 0, "trunk pairing assumes 8 layers and an even skip layer");
   FwdEpi<store, true> e7(accB, bin, bst, lane);  // + density head (layer 8): z_s = w8 . h7 + b8
   e7.begin(biases + 7 * 256, act_h_blk + 7 * layer_stride, mask_ptr(a.masks, blk, 7), lane, bias_lds + 8 * 256);
-  dense_layer<X3, 8, 0, 8>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea);
+  dense_layer<P, 8, 0, 8>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea);
   e7.tile0();
 
   // ---- view layer 9: relu(W9[:, :256] h7 + dirbias); h7 tiles 1..7 finish in its shadow -------
-  dense_layer<X3, 8, 0, 4>(bin, ipe_lds, accA, lds, cur, wsrc, true, tid, lane, e7);
+  dense_layer<P, 8, 0, 4>(bin, ipe_lds, accA, lds, cur, wsrc, true, tid, lane, e7);
   float zs = e7.zs;
   zs += __shfl_xor(zs, 32, 64);
   zs += tail[kFwdTailBias + 8 * 256];
@@ -299,13 +299,16 @@ hipError_t launch_mlp_fwd(const FwdArgs& a, hipStream_t st) {
   if (a.M % kBlk != 0 || a.S % kBlk != 0) return hipErrorInvalidValue;
   const int nblk = a.M / kBlk;
   const dim3 grid((nblk + 3) / 4), block(kMlpThreads);
-  if (a.split) {
-    if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd<true, false>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((k_mlp_fwd<true, true>), grid, block, 0, st, a);
+  if (a.split == 1) {
+    if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd<1, false>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((k_mlp_fwd<1, true>), grid, block, 0, st, a);
+  } else if (a.split == 2) {
+    if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd<2, false>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((k_mlp_fwd<2, true>), grid, block, 0, st, a);
   } else {
 #ifdef NOF_F32_MFMA32  // the 32x32x2, one-wave-per-SIMD fp32 kernels (diagnostic builds only)
-    if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd<false, false>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((k_mlp_fwd<false, true>), grid, block, 0, st, a);
+    if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd<0, false>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((k_mlp_fwd<0, true>), grid, block, 0, st, a);
 #else
     return launch_mlp_fwd16(a, st);
 #endif

@@ -232,8 +232,9 @@ __global__ __launch_bounds__(kWgThreads, 1) void k_wgrad(const WgProblem* __rest
 constexpr int kX3WC = NOF_X3_WC;                  // wave-grid columns (2 rows): 4 -> 8 waves, 2 per SIMD
 constexpr int kWgX3Threads = 64 * 2 * kX3WC;
 constexpr int kX3RowsPerC = kWgX3Threads / 4;      // concatenated rows one loader chunk index covers
-constexpr int kX3Frag = 3 * 8 * 64 * 4;  // floats per operand fragment image: [piece][tile][lane][16 B]
-constexpr int kX3Lds = 2 * 2 * kX3Frag;   // 96 KB
+// floats per operand fragment image: [piece][tile][lane][16 B]; LDS = 2 images x 2 operands
+template <int P> constexpr int x3_frag() { return SplitMode<P>::NP * 8 * 64 * 4; }
+template <int P> constexpr int x3_lds() { return 2 * 2 * x3_frag<P>(); }  // 96 KB (bf16x3), 64 KB (f16x2)
 
 template <int N>
 struct X3Raw {
@@ -250,9 +251,15 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // grid's problem has at most 64 (RB + CB) rows).  A 16-row group of one wave never straddles the
 // A/B boundary (both are multiples of 32 rows), so operand choice is wave-uniform and no chunk is
 // wasted on rows outside the problem (only the last chunk can fall past the end: skipped).
-template <int RB, int CB>
+template <int PM, int RB, int CB>
 __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& P, float* lds, int tid, int wave,
                                            float* slabs, float* bias_slabs, const int64_t* slab_off) {
+  typedef SplitMode<PM> SM;
+  typedef typename SM::V8 V8;
+  typedef typename SM::V4 V4;
+  typedef typename SM::V2 V2;
+  constexpr int NP = SM::NP;
+  constexpr int kX3Frag = x3_frag<PM>();
   // chunks per thread: the grid's largest problem has 2 RB + kX3WC CB row tiles of 128 chunks
   constexpr int NCH = ((2 * RB + kX3WC * CB) * 128 + kWgX3Threads - 1) / kWgX3Threads;
   // opaque thread index: the lane-derived offsets of the instantiations are recomputed per item
@@ -308,15 +315,13 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
   // chunk lc of row (t, xr) = samples 4 lc .. 4 lc + 3 = elements 4 (lc & 1) .. +3 of fragment lane
   // (h = lc >> 1, xr): one 8-B piece per (piece, row)
   auto put = [&](float* img, int row, const f32x4& v) {
-    bf16x2 a0, b0, c0_, a1, b1, c1;
-    split2(v[0], v[1], a0, b0, c0_);
-    split2(v[2], v[3], a1, b1, c1);
-    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    V2 e0[NP], e1[NP];
+    split2<PM>(v[0], v[1], e0);
+    split2<PM>(v[2], v[3], e1);
     const int t = row >> 5, xr = row & 31;
-    bf16x4* dst = reinterpret_cast<bf16x4*>(img) + (((t * 64 + (lc >> 1) * 32 + xr) * 2) + (lc & 1));
-    dst[0] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3);
-    dst[8 * 64 * 2] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3);
-    dst[2 * 8 * 64 * 2] = __builtin_shufflevector(c0_, c1, 0, 1, 2, 3);
+    V4* dst = reinterpret_cast<V4*>(img) + (((t * 64 + (lc >> 1) * 32 + xr) * 2) + (lc & 1));
+#pragma unroll
+    for (int p = 0; p < NP; ++p) dst[p * 8 * 64 * 2] = __builtin_shufflevector(e0[p], e1[p], 0, 1, 2, 3);
   };
   // chunk c -> image `buf` (A or B half); live = false (the last step's clamped duplicate) keeps it
   // out of the bias sums
@@ -340,9 +345,9 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
   // nobody reads rather than branching.
   auto step = [&](int k, const X3Raw<NCH>& nx) {
     const bool live = k + 1 < K;
-    const bf16x8* FA = reinterpret_cast<const bf16x8*>(lds + (k & 1) * 2 * kX3Frag) + (lane & 63);
-    const bf16x8* FB = FA + kX3Frag / 4;
-    Frag3 fb[CB], fa;
+    const V8* FA = reinterpret_cast<const V8*>(lds + (k & 1) * 2 * kX3Frag) + (lane & 63);
+    const V8* FB = FA + kX3Frag / 4;
+    Frag<PM> fb[CB], fa;
 #ifdef NOF_WG_SPLIT_FRONT
 #pragma unroll
     for (int c = 0; c < NCH; ++c) split_chunk(nx, (k + 1) & 1, c, live);
@@ -350,13 +355,13 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
     // first row group's fragments in the order its MFMAs consume them (lo.hi, hi.lo, mid.mid, ...):
     // the first MFMAs start after two reads instead of after all of them
 #pragma unroll
-    for (int pp = 0; pp < 6; ++pp) {
-      const int pa = x3_pa(pp), pb = x3_pb(pp);
+    for (int pp = 0; pp < SM::NPROD; ++pp) {
+      const int pa = SM::pa(pp), pb = SM::pb(pp);
       bool a_new = true, b_new = true;
 #pragma unroll
       for (int q = 0; q < pp; ++q) {
-        a_new = a_new && x3_pa(q) != pa;
-        b_new = b_new && x3_pb(q) != pb;
+        a_new = a_new && SM::pa(q) != pa;
+        b_new = b_new && SM::pb(q) != pb;
       }
       if (a_new) fa.p[pa] = FA[(pa * 8 + rowt[0]) * 64];
       if (b_new) {
@@ -366,23 +371,23 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
     }
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
-      Frag3 fn = fa;
+      Frag<PM> fn = fa;
       if (r + 1 < RB) {
 #pragma unroll
-        for (int p = 0; p < 3; ++p) fn.p[p] = FA[(p * 8 + rowt[r + 1]) * 64];
+        for (int p = 0; p < NP; ++p) fn.p[p] = FA[(p * 8 + rowt[r + 1]) * 64];
       }
 #pragma unroll
-      for (int pp = 0; pp < 6; ++pp) {
+      for (int pp = 0; pp < SM::NPROD; ++pp) {
 #ifndef NOF_DIAG_X3_NOMFMA
 #pragma unroll
         for (int c = 0; c < CB; ++c)
-          acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa.p[x3_pa(pp)], fb[c].p[x3_pb(pp)], acc[r][c], 0, 0, 0);
+          acc[r][c] = SM::mfma(fa.p[SM::pa(pp)], fb[c].p[SM::pb(pp)], acc[r][c]);
 #endif
 #ifndef NOF_WG_SPLIT_FRONT
         // chunks [NCH r / RB, NCH (r + 1) / RB): one after each MFMA group, the rest after the last
         const int i0 = (NCH * r) / RB, i1 = (NCH * (r + 1)) / RB;
 #pragma unroll
-        for (int i = i0 + pp; i < (pp == 5 ? i1 : min(i0 + pp + 1, i1)); ++i)
+        for (int i = i0 + pp; i < (pp == SM::NPROD - 1 ? i1 : min(i0 + pp + 1, i1)); ++i)
 #ifdef NOF_DIAG_X3_NOSPLIT
           if (nx.v[0][0] == 12345.0f)
 #endif
@@ -441,6 +446,7 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
   __syncthreads();  // images are reused by the next item
 }
 
+template <int PM>
 __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_x3(const WgProblem* __restrict__ probs,
                                                               const WgItem* __restrict__ items,
                                                               const int* __restrict__ item_ptr,
@@ -456,20 +462,20 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_x3(const WgProblem* _
     const int RB = (P.ntr + 1) >> 1, CB = (P.ntc + kX3WC - 1) / kX3WC;  // 2 x kX3WC wave grid
     if constexpr (kX3WC == 2) {
       switch (RB * 10 + CB) {
-        case 11: wg_item_x3<1, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-        case 12: wg_item_x3<1, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-        case 21: wg_item_x3<2, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-        case 34: wg_item_x3<3, 4>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-        case 42: wg_item_x3<4, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-        default: wg_item_x3<4, 4>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        case 11: wg_item_x3<PM, 1, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        case 12: wg_item_x3<PM, 1, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        case 21: wg_item_x3<PM, 2, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        case 34: wg_item_x3<PM, 3, 4>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        case 42: wg_item_x3<PM, 4, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        default: wg_item_x3<PM, 4, 4>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
       }
     } else {
       switch (RB * 10 + CB) {
-        case 11: wg_item_x3<1, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-        case 21: wg_item_x3<2, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-        case 32: wg_item_x3<3, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-        case 41: wg_item_x3<4, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-        default: wg_item_x3<4, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        case 11: wg_item_x3<PM, 1, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        case 21: wg_item_x3<PM, 2, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        case 32: wg_item_x3<PM, 3, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        case 41: wg_item_x3<PM, 4, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+        default: wg_item_x3<PM, 4, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
       }
     }
   }
@@ -497,26 +503,35 @@ int wgrad_shape(int ntr, int ntc, int* cost2) {
   return best;
 }
 
-hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,
-                           const int64_t* slab_off, float* slabs, float* bias_slabs, hipStream_t st) {
-  if (num_wg <= 0) return hipSuccess;
-  const size_t shm = sizeof(float) * kX3Lds;  // 96 KB
+template <int P>
+static hipError_t launch_wgrad_split(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,
+                                     const int64_t* slab_off, float* slabs, float* bias_slabs, hipStream_t st) {
+  const size_t shm = sizeof(float) * x3_lds<P>();
   static bool attr = false;
   if (!attr) {
     const hipError_t e =
-        hipFuncSetAttribute((const void*)k_wgrad_x3, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+        hipFuncSetAttribute((const void*)k_wgrad_x3<P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL(k_wgrad_x3, dim3(num_wg), dim3(kWgX3Threads), shm, st, probs, items, item_ptr, slab_off, slabs,
-                     bias_slabs);
+  hipLaunchKernelGGL(k_wgrad_x3<P>, dim3(num_wg), dim3(kWgX3Threads), shm, st, probs, items, item_ptr, slab_off,
+                     slabs, bias_slabs);
   return hipGetLastError();
+}
+
+hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,
+                           const int64_t* slab_off, float* slabs, float* bias_slabs, int precision, hipStream_t st) {
+  if (num_wg <= 0) return hipSuccess;
+  if (precision == 2) return launch_wgrad_split<2>(probs, items, item_ptr, num_wg, slab_off, slabs, bias_slabs, st);
+  return launch_wgrad_split<1>(probs, items, item_ptr, num_wg, slab_off, slabs, bias_slabs, st);
 }
 
 __global__ void k_wgrad_reduce(const WgOut* __restrict__ outs, const WgItem* __restrict__ items,
                                const WgProblem* __restrict__ probs, const int64_t* __restrict__ slab_off,
-                               const float* __restrict__ slabs, const float* __restrict__ bias_slabs, int accumulate) {
+                               const float* __restrict__ slabs, const float* __restrict__ bias_slabs, int accumulate,
+                               const uint32_t* __restrict__ amax) {
   const WgOut o = outs[blockIdx.y];
+  const float inv = amax ? delta_scale(amax, true) : 1.0f;  // f16x2: undo the delta scaling (exact)
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int ld = probs[o.prob].ntc * 32;
   if (e < o.nrows * o.ncols) {
@@ -524,12 +539,14 @@ __global__ void k_wgrad_reduce(const WgOut* __restrict__ outs, const WgItem* __r
     const size_t off = (size_t)(o.row_off + rr) * ld + o.col_off + cc;
     float s = 0.0f;
     for (int k = 0; k < o.nitems; ++k) s += slabs[slab_off[items[o.item0 + k].slab] + off];
+    s *= inv;
     float* dst = o.dst + (size_t)rr * o.ld + o.dst_col + cc;
     *dst = accumulate ? *dst + s : s;
   }
   if (o.bias_dst && e < o.nrows) {
     float s = 0.0f;
     for (int k = 0; k < o.nitems; ++k) s += bias_slabs[(size_t)items[o.item0 + k].slab * 256 + o.row_off + e];
+    s *= inv;
     o.bias_dst[e] = accumulate ? o.bias_dst[e] + s : s;
   }
 }
@@ -551,10 +568,10 @@ hipError_t launch_wgrad(const WgProblem* probs, const WgItem* items, const int* 
 
 hipError_t launch_wgrad_reduce(const WgOut* outs, int nouts, int max_elems, const WgItem* items,
                                const WgProblem* probs, const int64_t* slab_off, const float* slabs,
-                               const float* bias_slabs, int accumulate, hipStream_t st) {
+                               const float* bias_slabs, int accumulate, const uint32_t* amax, hipStream_t st) {
   if (nouts <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_wgrad_reduce, dim3((max_elems + 255) / 256, nouts), dim3(256), 0, st, outs, items, probs,
-                     slab_off, slabs, bias_slabs, accumulate);
+                     slab_off, slabs, bias_slabs, accumulate, amax);
   return hipGetLastError();
 }
 

@@ -24,7 +24,7 @@ class NofError(RuntimeError):
         self.status = status
 
 
-NOF_PRECISION_F32, NOF_PRECISION_F32_SPLIT = 0, 1
+NOF_PRECISION_F32, NOF_PRECISION_F32_SPLIT, NOF_PRECISION_F16X2 = 0, 1, 2
 
 
 class nof_config(C.Structure):

@@ -11,6 +11,9 @@ from conftest import rel_l2
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-5
+# per-tensor relative L2 bound per precision mode: fp32 and the bf16x3 split mode are
+# fp32-accurate; the f16x2 perf mode is bounded at 2e-3
+TOLS = {0: 1e-5, 1: 1e-5, 2: 2e-3}
 
 
 def _device_rays(r, dev):
@@ -26,11 +29,11 @@ def _run_gpu(model, r, dev, msum=None):
     return model.get_gradient_device(n, d["o"], d["d"], d["radius"], d["near"], d["far"], d["lossmult"], d["pix"], msum)
 
 
-PRECISIONS = [0, 1]  # NOF_PRECISION_F32, NOF_PRECISION_F32_SPLIT: same fp32 tolerance for both
+PRECISIONS = [0, 1, 2]  # NOF_PRECISION_F32, _F32_SPLIT (both 1e-5), _F16X2 (perf mode, 2e-3)
 
 
 # blender = configs 2/3 shapes (64+128 = config 3); llff = config 5's NDC forward-facing rays at
-# 256 samples per level (its fp16-activation variant is covered by split mode: see DESIGN.md §3)
+# 256 samples per level (config 5 runs fp16 on MFMA: precision 2)
 @pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("kind,n,samples", [("blender", 16, (64, 64)), ("blender", 8, (128, 128)),
                                             ("blender", 6, (64, 128)), ("llff", 3, (256, 256))])
@@ -65,22 +68,26 @@ def test_step_parity(gpu, oracle, kind, n, samples, precision):
                       t_override={1: lv[1]["t"]}, relu_mask=masks, nthreads=16)
     ref_free = oracle.step(oracle.Spec(), params, r, samples=samples, seed=seed, step_idx=step, ray_base=ray_base,
                            t_override={1: lv[1]["t"]}, nthreads=16, want=("sigma",))
+    tol = TOLS[precision]
     for l in range(len(samples)):  # the masks only differ at ties: forward outputs agree either way
-        assert rel_l2(lv[l]["density"], ref_free["sigma"][l]) < TOL
+        assert rel_l2(lv[l]["density"], ref_free["sigma"][l]) < tol
     for l in range(len(samples)):
-        assert rel_l2(lv[l]["density"], ref["sigma"][l]) < TOL, f"density level {l}"
-        assert rel_l2(lv[l]["rgb"], ref["rgb"][l]) < TOL, f"rgb level {l}"
-        assert rel_l2(lv[l]["weights"], ref["w"][l]) < TOL, f"weights level {l}"
-        assert rel_l2(lv[l]["comp_rgb"], ref["C"][l]) < TOL, f"comp_rgb level {l}"
-        assert rel_l2(lv[l]["density_grad"], ref["dsigma"][l]) < TOL, f"dsigma level {l}"
-        assert rel_l2(lv[l]["rgb_grad"], ref["drgb"][l]) < TOL, f"drgb level {l}"
+        assert rel_l2(lv[l]["density"], ref["sigma"][l]) < tol, f"density level {l}"
+        assert rel_l2(lv[l]["rgb"], ref["rgb"][l]) < tol, f"rgb level {l}"
+        assert rel_l2(lv[l]["weights"], ref["w"][l]) < tol, f"weights level {l}"
+        assert rel_l2(lv[l]["comp_rgb"], ref["C"][l]) < tol, f"comp_rgb level {l}"
+        assert rel_l2(lv[l]["density_grad"], ref["dsigma"][l]) < tol, f"dsigma level {l}"
+        assert rel_l2(lv[l]["rgb_grad"], ref["drgb"][l]) < tol, f"drgb level {l}"
     sizes = oracle.layer_sizes(oracle.Spec())
     off = 0
+    errs = []
     for i, s in enumerate(sizes):
         e = rel_l2(G[off:off + s], ref["grads"][off:off + s])
-        assert e < TOL, f"gradient tensor {i}: rel L2 {e:.3g}"
+        errs.append(e)
+        assert e < tol, f"gradient tensor {i}: rel L2 {e:.3g}"
         off += s
-    assert abs(model.loss() - ref["loss"]) <= 1e-5 * abs(ref["loss"])
+    print(f"precision {precision}: gradient rel L2 max {max(errs):.2e} median {np.median(errs):.2e}")
+    assert abs(model.loss() - ref["loss"]) <= tol * abs(ref["loss"])
     model.close()
 
 

@@ -78,7 +78,7 @@ def test_dataset_file_equals_host(gpu, tmp_path):
         nof.RayDataset(tmp_path / "bad.bin")
 
 
-@pytest.mark.parametrize("precision", [0, 1])
+@pytest.mark.parametrize("precision", [0, 1, 2])
 def test_checkpoint_resume_bit_exact(gpu, tmp_path, precision):
     import torch
     import nof
@@ -118,3 +118,27 @@ def test_trainer_prints_fine_loss(gpu, capsys):
     out = capsys.readouterr().out
     assert "Step 2/1000000, Loss:" in out and "Step 4/1000000, Loss:" in out
     assert np.isfinite(tr.last_loss) and tr.last_loss > 0
+
+
+def test_perf_mode_psnr_matches_f32(gpu):
+    """the f16x2 perf mode trains to within 0.1 dB PSNR of the fp32 mode after a fixed
+    number of steps (same init, same batches; config-2 shaped rays at 64+64 samples)."""
+    import nof
+    from nof.train import Trainer
+
+    ds = nof.RayDataset(records=_records(20000, 21))
+    psnr = {}
+    for prec in (0, 2):
+        tr = Trainer(ds, batch_size=256, seed=31, print_every=0, num_samples=(64, 64), precision=prec,
+                     lr_delay_steps=0)
+        losses = []
+        for k in range(300):
+            tr.step()
+            if k == 0 or k >= 280:
+                losses.append(tr.model.loss())  # both levels' weighted loss of this step's batch
+        psnr[prec] = -10.0 * np.log10(np.mean(losses[1:]))
+        psnr[("first", prec)] = -10.0 * np.log10(losses[0])
+        tr.model.close()
+    print("psnr", psnr)
+    assert psnr[0] > psnr[("first", 0)] + 0.5  # it learns
+    assert abs(psnr[2] - psnr[0]) < 0.1

@@ -53,6 +53,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--rays", type=int, default=1024, help="rays per GPU per step")
     p.add_argument("--samples", type=int, nargs="+", default=[128, 128])
+    p.add_argument("--scene", choices=["blender", "llff"], default="blender",
+                   help="synthetic ray distribution: Lego-shaped 800x800 views (configs 2-4) or forward-facing "
+                        "LLFF NDC rays (config 5: --scene llff --rays 512 --samples 256 256 --precision f16x2)")
     p.add_argument("--precision", choices=list(PRECISIONS), default="f32",
                    help="MLP contraction arithmetic: fp32 MFMA, fp32 operands as bf16x3 split MFMAs (same 1e-5 "
                         "parity), or the f16x2 perf mode (fp16 hi+lo, parity 2e-3)")
@@ -140,6 +143,14 @@ def integrator_roofline(torch, nof, dev, n=1 << 20, S=128, reps=5):
             "workload": f"{n} rays x {S} samples, render fwd+bwd", "kernels": out}
 
 
+def workload_name(a):
+    if a.scene == "llff":
+        return "BASELINE configs[4] per-GPU shape" if (a.rays, a.samples) == (512, [256, 256]) else "LLFF-shaped"
+    if (a.rays, a.samples) == (1024, [128, 128]):
+        return "BASELINE configs[1]"
+    return "BASELINE configs[2]" if a.samples == [64, 128] else "Lego-shaped"
+
+
 def main():
     a = parse()
     import torch
@@ -184,7 +195,7 @@ def main():
     # pre-staged synthetic batches (views of a 100-pose Lego-shaped scene; shard = disjoint views)
     pool = []
     for i in range(4):
-        r = synth.blender_rays(n, seed=1000 * rank + i)
+        r = (synth.llff_rays if a.scene == "llff" else synth.blender_rays)(n, seed=1000 * rank + i)
         pool.append({k: torch.from_numpy(v).to(dev) for k, v in r.items()})
     msum_global = float(n * world)  # lossmult = 1 everywhere: sum over all shards (D14, DP-global)
 
@@ -299,8 +310,10 @@ def main():
             "metric": METRIC, "value": round(rays_per_s, 1), "unit": "rays/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": DTYPES[a.precision],
-            "data": "synthetic (Lego-shaped 800x800, 100 poses)",
-            "config": {"workload": "BASELINE configs[1]: 1024-ray batches x 128+128 samples, 8x256 MLP fwd/bwd + Adam",
+            "data": "synthetic (Lego-shaped 800x800, 100 poses)" if a.scene == "blender"
+                    else "synthetic (forward-facing LLFF-shaped 800x800, NDC)",
+            "config": {"workload": f"{workload_name(a)}: {n}-ray batches x {'+'.join(map(str, samples))} samples, "
+                                   "8x256 MLP fwd/bwd + Adam",
                        "rays_per_gpu": n, "global_batch": n * world, "samples": samples,
                        "parallelism": f"dp{world}", "precision": a.precision,
                        "allreduce": a.dp if world > 1 else None},

@@ -244,20 +244,25 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M) {
   struct OutSpec { int prob, row_off, nrows, col_off, ncols; float* dst; int ld, dst_col; float* bias; };
   std::vector<OutSpec> os;
   float* G = grads_.p;
+  // operand blocks hold fp16 in the f16x2 mode (mlp_common.h ActOut): element offsets in halves there
+  const bool half = precision_ == NOF_PRECISION_F16X2;
+  auto at = [&](float* base, size_t off) -> const float* {
+    return half ? reinterpret_cast<const float*>(reinterpret_cast<const uint16_t*>(base) + off) : base + off;
+  };
   auto Wg = [&](int l) { return G + woff_[l]; };
   auto Bg = [&](int l) { return G + boff_[l]; };
   int p;
   p = prob(delta_.p, 256, 0, 8, L.act_in.p, nof::kInF, 0, 3);
   os.push_back({p, 0, 256, 0, 96, Wg(0), 96, 0, Bg(0)});
   for (int l = 1; l < 8; ++l) {
-    p = prob(delta_.p + l * ls, 256, 0, 8, L.act_h.p + (l - 1) * ls, 256, 0, 8);
+    p = prob(at(delta_.p, l * ls), 256, 0, 8, at(L.act_h.p, (l - 1) * ls), 256, 0, 8);
     os.push_back({p, 0, 256, 0, 256, Wg(l), in_[l], 0, Bg(l)});
     if (l == 4) {
-      p = prob(delta_.p + l * ls, 256, 0, 8, L.act_in.p, nof::kInF, 0, 3);
+      p = prob(at(delta_.p, l * ls), 256, 0, 8, L.act_in.p, nof::kInF, 0, 3);
       os.push_back({p, 0, 256, 0, 96, Wg(4), in_[4], 256, nullptr});
     }
   }
-  p = prob(delta9x_.p, nof::kD9F, 0, 5, L.act_h.p + 7 * ls, 256, 0, 8);
+  p = prob(delta9x_.p, nof::kD9F, 0, 5, at(L.act_h.p, 7 * ls), 256, 0, 8);
   os.push_back({p, 0, 128, 0, 256, Wg(9), in_[9], 0, Bg(9)});
   os.push_back({p, 128, 1, 0, 256, Wg(8), in_[8], 0, Bg(8)});
   p = prob(delta9x_.p, nof::kD9F, 0, 4, L.act_in.p, nof::kInF, 96, 1);
@@ -275,7 +280,7 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M) {
     if (precision_ != NOF_PRECISION_F32) {
       const int WC = nof::wgrad_x3_grid_cols();  // C/2 waves per SIMD
       const int RB = (P[i].ntr + 1) / 2, CB = (P[i].ntc + WC - 1) / WC;
-      const int nprod = precision_ == NOF_PRECISION_F16X2 ? 3 : 6;
+      const int nprod = precision_ == NOF_PRECISION_F16X2 ? 1 : 6;  // k_wgrad_h: one f16 MFMA per product
       cost[i] = std::max(RB * CB * WC * nprod / 12, P[i].ntr + P[i].ntc);
     } else {
       int c2 = 0;

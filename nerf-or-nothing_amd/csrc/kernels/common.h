@@ -32,6 +32,10 @@ constexpr int kBwdSlices = 4 + 8 * 7;                      // 60: L9 | L7..L1
 // one whole 128-B line, and the weight-gradient GEMMs read 4 consecutive samples of a row per
 // lane (ds_read_b128) with the 8 lanes of each LDS phase on 8 distinct 16-B bank groups.
 __host__ __device__ inline int blk_off(int f, int s) { return f * kBlk + ((((s >> 2) ^ (f & 7)) << 2) | (s & 3)); }
+// fp16 activation / delta blocks of the f16x2 mode: [F][32] halves, row f = 64 B of 4 16-B chunks
+// (chunk c = samples 8c..8c+7 = one 32x32x16 MFMA fragment lane), stored at chunk c ^ ((f >> 2) & 3)
+// so that the weight-gradient kernel's fragment ds_read_b128 are bank-conflict-free.  Offset in halves.
+__host__ __device__ inline int blkh_off(int f, int s) { return f * kBlk + ((((s >> 3) ^ ((f >> 2) & 3)) << 3) | (s & 7)); }
 
 // Packed weight slice [rows][32]: logical 16-B chunk c of row r stored at c ^ ((r >> 1) & 7),
 // making the ds_read_b128 operand fetches of the MFMA A operand bank-conflict-free.

@@ -19,8 +19,9 @@ namespace nof {
 // delta = mask ? acc (+ w8 * dzs) : 0 -> B operand + delta block, run a quarter tile per call inside
 // the next layer's MFMA stream (see FwdEpi in mlp_fwd.hip): part (t, q) handles registers 4q..4q+3 of tile t; w8 values are loaded one part
 // ahead; the layer's ReLU mask word is loaded by begin(), a layer ahead of its first use.
-template <bool kDensity>
+template <bool kDensity, bool kHalf>
 struct BwdEpi {
+  typedef typename ActOut<kHalf>::T AT;
 #ifndef NOF_DIAG_NO_ACT_STORE
   static constexpr int kVmPerPart = 4;
 #else
@@ -28,17 +29,17 @@ struct BwdEpi {
 #endif
   const f32x16 (&acc)[8];
   float (&bin)[8][16];
-  const BlkStore& bst;
+  const ActOut<kHalf>& ao;
   const int h;
   const float* w8;  // LDS, + 4h
   float dzs;
-  float* dst_blk;
+  AT* dst_blk;
   uint4 mk;
   f32x4 wnext;
 
-  __device__ __forceinline__ BwdEpi(const f32x16 (&acc_)[8], float (&bin_)[8][16], const BlkStore& bst_, int lane)
-      : acc(acc_), bin(bin_), bst(bst_), h(lane >> 5) {}
-  __device__ __forceinline__ void begin(const uint32_t* mask, float* dst_blk_, int lane, const float* w8_ = nullptr,
+  __device__ __forceinline__ BwdEpi(const f32x16 (&acc_)[8], float (&bin_)[8][16], const ActOut<kHalf>& ao_, int lane)
+      : acc(acc_), bin(bin_), ao(ao_), h(lane >> 5) {}
+  __device__ __forceinline__ void begin(const uint32_t* mask, AT* dst_blk_, int lane, const float* w8_ = nullptr,
                                         float dzs_ = 0.0f) {
     mk = reinterpret_cast<const uint4*>(mask)[lane];
     dst_blk = dst_blk_;
@@ -57,7 +58,7 @@ struct BwdEpi {
       w4 = wnext;
       if (!(t == 7 && q == 3)) wnext = *reinterpret_cast<const f32x4*>(w8 + 32 * t + 8 * q + 8);
     }
-    float* tile = dst_blk + t * 32 * kBlk;
+    AT* tile = dst_blk + t * 32 * kBlk;
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const int r = 4 * q + jj;
@@ -66,7 +67,7 @@ struct BwdEpi {
       v = mask_bit(mk, t, r) ? v : 0.0f;
       bin[t][r] = v;
 #ifndef NOF_DIAG_NO_ACT_STORE
-      blk_store_at(tile, bst, 0, r, v);
+      ao.put(tile, r, v);
 #endif
     }
   }
@@ -82,7 +83,9 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
   float* w8_lds = lds + ring_floats<P>();
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, j = lane & 31;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: block pointers stay in SGPRs
-  const BlkStore bst(lane);
+  constexpr bool kH = P == 2;  // f16x2: fp16 delta blocks (the weight-gradient operands)
+  typedef typename ActOut<kH>::T AT;
+  const ActOut<kH> ao(lane);
   const int nblk = a.M / kBlk;
   const int blk_raw = blockIdx.x * 4 + wave;
   const int blk = blk_raw < nblk ? blk_raw : nblk - 1;  // tail waves duplicate the last block
@@ -107,12 +110,12 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) dzc[c] *= sc;
   }
-  float* d9 = a.delta9x + (size_t)blk * kD9F * kBlk;  // uniform block base
+  AT* d9 = reinterpret_cast<AT*>(a.delta9x) + (size_t)blk * kD9F * kBlk;  // uniform block base
   if (h == 0) {  // rows 128..131 = tile 4, registers 0..3 of lane half 0
-    blk_store<4, 0>(d9, bst, dzs);
-    blk_store<4, 1>(d9, bst, dzc[0]);
-    blk_store<4, 2>(d9, bst, dzc[1]);
-    blk_store<4, 3>(d9, bst, dzc[2]);
+    ao.put(d9 + 4 * 32 * kBlk, 0, dzs);
+    ao.put(d9 + 4 * 32 * kBlk, 1, dzc[0]);
+    ao.put(d9 + 4 * 32 * kBlk, 2, dzc[1]);
+    ao.put(d9 + 4 * 32 * kBlk, 3, dzc[2]);
   }
   // ---- delta9 = (W10^T dz_rgb) * relu'(layer 9) ------------------------------------------
   float bin[8][16];
@@ -137,15 +140,9 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
       }
 #pragma unroll
     for (int ot = 0; ot < 4; ++ot) {
-      float* tile = d9 + ot * 32 * kBlk;
-      blk_store<0, 0>(tile, bst, bin[ot][0]);   blk_store<0, 1>(tile, bst, bin[ot][1]);
-      blk_store<0, 2>(tile, bst, bin[ot][2]);   blk_store<0, 3>(tile, bst, bin[ot][3]);
-      blk_store<0, 4>(tile, bst, bin[ot][4]);   blk_store<0, 5>(tile, bst, bin[ot][5]);
-      blk_store<0, 6>(tile, bst, bin[ot][6]);   blk_store<0, 7>(tile, bst, bin[ot][7]);
-      blk_store<0, 8>(tile, bst, bin[ot][8]);   blk_store<0, 9>(tile, bst, bin[ot][9]);
-      blk_store<0, 10>(tile, bst, bin[ot][10]); blk_store<0, 11>(tile, bst, bin[ot][11]);
-      blk_store<0, 12>(tile, bst, bin[ot][12]); blk_store<0, 13>(tile, bst, bin[ot][13]);
-      blk_store<0, 14>(tile, bst, bin[ot][14]); blk_store<0, 15>(tile, bst, bin[ot][15]);
+      AT* tile = d9 + ot * 32 * kBlk;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ao.put(tile, r, bin[ot][r]);
     }
   }
   if (tid < 64) reinterpret_cast<f32x4*>(w8_lds)[tid] = reinterpret_cast<const f32x4*>(tail + kBwdTailW8)[tid];
@@ -155,14 +152,14 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
   const float* wsrc = a.wimg_b;
   f32x16 accA[8], accB[8];  // ping-pong, as in the forward
   const uint32_t* masks = a.masks;
-  float* delta_blk = a.delta + (size_t)blk * kWidth * kBlk;
+  AT* delta_blk = reinterpret_cast<AT*>(a.delta) + (size_t)blk * kWidth * kBlk;
   // ---- dh7 = W9[:, :256]^T delta9 + w8 dz_s ; delta7 ---------------------------------------
-  BwdEpi<true> e7(accA, bin, bst, lane);
+  BwdEpi<true, kH> e7(accA, bin, ao, lane);
   e7.begin(masks + ((size_t)blk * kMaskSlots + 7) * 256, delta_blk + 7 * layer_stride, lane, w8_lds, dzs);
   dense_layer<P, 4, 0, 8>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane);
   e7.tile0();
   // ---- dh_{l-1} = W_l[:, :256]^T delta_l ; delta_{l-1}, l = 7..1 (l odd: A -> B) ------------
-  BwdEpi<false> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
+  BwdEpi<false, kH> ea(accA, bin, ao, lane), eb(accB, bin, ao, lane);
   eb.begin(masks + ((size_t)blk * kMaskSlots + 6) * 256, delta_blk + 6 * layer_stride, lane);
   dense_layer<P, 8, 0, 8>(bin, nullptr, accB, lds, cur, wsrc, false, tid, lane, e7);
   eb.tile0();

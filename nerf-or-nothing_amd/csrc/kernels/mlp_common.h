@@ -291,13 +291,18 @@ __device__ __forceinline__ void slice_dma_split(const float* __restrict__ src, f
   }
 }
 
-// split layer: kX3DmaPer DMA steps in each of the first groups; parts in groups s OT + 1 and
+// split layer: split_dma_per<P>() DMA steps in each of the first groups; parts in groups s OT + 1 and
 // s OT + OT/2 + 1
 #ifndef NOF_X3_DMA_PER_GROUP
 #define NOF_X3_DMA_PER_GROUP 2
 #endif
-constexpr int kX3DmaPer = NOF_X3_DMA_PER_GROUP;  // DMA steps per MFMA group
-template <int P> constexpr int split_dma_groups() { return (split_dma_steps<P>() + kX3DmaPer - 1) / kX3DmaPer; }
+#ifndef NOF_F16_DMA_PER_GROUP
+#define NOF_F16_DMA_PER_GROUP 2
+#endif
+template <int P> constexpr int split_dma_per() { return P == 1 ? NOF_X3_DMA_PER_GROUP : NOF_F16_DMA_PER_GROUP; }
+template <int P> constexpr int split_dma_groups() {
+  return (split_dma_steps<P>() + split_dma_per<P>() - 1) / split_dma_per<P>();
+}
 static_assert(split_dma_groups<1>() <= 8, "the OT = 4 layer has 8 MFMA groups per slice");
 template <int P, int OT> constexpr int split_parts_after_dma() {
   int n = 0;
@@ -376,8 +381,8 @@ __device__ __forceinline__ void mlp_layer_split(const float (&bin)[8][16], const
 #ifndef NOF_DIAG_NO_DMA
         if (has_next && s * OT + ot < split_dma_groups<P>()) {
 #pragma unroll
-          for (int u = 0; u < kX3DmaPer; ++u) {
-            const int st = kX3DmaPer * (s * OT + ot) + u;
+          for (int u = 0; u < split_dma_per<P>(); ++u) {
+            const int st = split_dma_per<P>() * (s * OT + ot) + u;
             if (st < split_dma_steps<P>()) slice_dma_step(wsrc + SF, lds + (cur ^ 1) * SF, tid, st);
           }
         }
@@ -470,6 +475,45 @@ __device__ __forceinline__ void blk_store_at(float* sbase, const BlkStore& bs, i
   gchar* p = (gchar*)sbase + ot * 4096 + (size_t)bs.voff[r & 3] + (8 * (r >> 2) + (r & 3)) * 128;
   *(gfloat*)p = v;
 }
+
+// fp16 counterpart (f16x2 mode, common.h blkh_off): element (f, j) of lane (h, j) register r of tile
+// ot: f = 32 ot + 8 (r >> 2) + 4h + (r & 3), so (f >> 2) & 3 = 2 ((r >> 2) & 1) + h and
+//   byte(f, j) = 2048 ot + 512 (r >> 2) + 64 (r & 3) + 256 h + ((((j >> 3) ^ (2 ((r >> 2) & 1) + h)) << 4) | ((j & 7) << 1)):
+// two lane offsets (by (r >> 2) & 1), the rest immediate (<= 1728 B past the tile base).
+struct BlkStoreH {
+  uint32_t voff[2];
+  __device__ __forceinline__ explicit BlkStoreH(int lane) {
+    const int h = lane >> 5, j = lane & 31;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) voff[q] = 256u * h + ((((j >> 3) ^ (2 * q + h)) << 4) | ((j & 7) << 1));
+  }
+};
+__device__ __forceinline__ void blkh_store_at(_Float16* tile_base, const BlkStoreH& bs, int r, float v) {
+  typedef __attribute__((address_space(1))) char gchar;
+  typedef __attribute__((address_space(1))) _Float16 ghalf;
+  gchar* p = (gchar*)tile_base + (size_t)bs.voff[(r >> 2) & 1] + 512 * (r >> 2) + 64 * (r & 3);
+  *(ghalf*)p = (_Float16)v;
+}
+constexpr int kTileHalves = 32 * kBlk;  // one 32-feature tile of an fp16 block (2 KB)
+
+// Activation / delta block writer of the 32x32-accumulator kernels: fp32 chunk-swizzled blocks
+// (f32 / bf16x3 modes) or fp16 blocks (f16x2 mode).  Both hold 32 x kBlk elements per 32-feature
+// tile, so block and tile pointer arithmetic is the same in elements of T.
+template <bool kHalf> struct ActOut;
+template <> struct ActOut<false> {
+  typedef float T;
+  BlkStore bs;
+  __device__ __forceinline__ explicit ActOut(int lane) : bs(lane) {}
+  __device__ __forceinline__ void put(T* tile, int r, float v) const { blk_store_at(tile, bs, 0, r, v); }
+};
+template <> struct ActOut<true> {
+  typedef _Float16 T;
+  BlkStoreH bs;
+  __device__ __forceinline__ explicit ActOut(int lane) : bs(lane) {}
+  __device__ __forceinline__ void put(T* tile, int r, float v) const { blkh_store_at(tile, bs, r, v); }
+};
+template <bool kHalf>
+__device__ __forceinline__ int act_off(int f, int s) { return kHalf ? blkh_off(f, s) : blk_off(f, s); }
 
 // feature index held by register r of accumulator tile ot in lane half h
 __device__ __forceinline__ int tile_feature(int ot, int r, int h) { return ot * 32 + 8 * (r >> 2) + 4 * h + (r & 3); }

@@ -20,10 +20,10 @@ namespace nof {
 // bias + ReLU epilogue on OT accumulator tiles -> next layer's B operand, act block, mask.
 // No per-lane guards: a tail wave past the last block is clamped onto that block and
 // recomputes bit-identical values, so its duplicate stores are benign.
-template <int OT, bool store>
+template <int OT, bool store, bool kHalf>
 __device__ __forceinline__ void fwd_epilogue(const f32x16 (&acc)[8], float (&bin)[8][16], const float* bias,
-                                             float* __restrict__ act_blk, uint32_t* __restrict__ mask_dst, int lane,
-                                             const BlkStore& bst) {
+                                             typename ActOut<kHalf>::T* __restrict__ act_blk,
+                                             uint32_t* __restrict__ mask_dst, int lane, const ActOut<kHalf>& ao) {
   const int h = lane >> 5;
   uint32_t mw[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
@@ -44,15 +44,9 @@ __device__ __forceinline__ void fwd_epilogue(const f32x16 (&acc)[8], float (&bin
     }
 #ifndef NOF_DIAG_NO_ACT_STORE
     if constexpr (store) {
-      float* tile = act_blk + ot * 32 * kBlk;  // uniform: one scalar add per tile
-      blk_store<0, 0>(tile, bst, bin[ot][0]);   blk_store<0, 1>(tile, bst, bin[ot][1]);
-      blk_store<0, 2>(tile, bst, bin[ot][2]);   blk_store<0, 3>(tile, bst, bin[ot][3]);
-      blk_store<0, 4>(tile, bst, bin[ot][4]);   blk_store<0, 5>(tile, bst, bin[ot][5]);
-      blk_store<0, 6>(tile, bst, bin[ot][6]);   blk_store<0, 7>(tile, bst, bin[ot][7]);
-      blk_store<0, 8>(tile, bst, bin[ot][8]);   blk_store<0, 9>(tile, bst, bin[ot][9]);
-      blk_store<0, 10>(tile, bst, bin[ot][10]); blk_store<0, 11>(tile, bst, bin[ot][11]);
-      blk_store<0, 12>(tile, bst, bin[ot][12]); blk_store<0, 13>(tile, bst, bin[ot][13]);
-      blk_store<0, 14>(tile, bst, bin[ot][14]); blk_store<0, 15>(tile, bst, bin[ot][15]);
+      typename ActOut<kHalf>::T* tile = act_blk + ot * 32 * kBlk;  // uniform: one scalar add per tile
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ao.put(tile, r, bin[ot][r]);
     }
 #endif
   }
@@ -67,8 +61,9 @@ __device__ __forceinline__ void fwd_epilogue(const f32x16 (&acc)[8], float (&bin
 // values are loaded one part ahead (part (t, q) uses features 32t + 8q + 4h.., the next part
 // always sits 8 further); biases and w8 come from the workgroup's LDS copy, so the only vector-memory
 // ops of a part are its stores.  kDensity folds the density head (w8 . h7) into layer 7's epilogue.
-template <bool store, bool kDensity>
+template <bool store, bool kDensity, bool kHalf>
 struct FwdEpi {
+  typedef typename ActOut<kHalf>::T AT;
 #ifndef NOF_DIAG_NO_ACT_STORE
   static constexpr int kVmPerPart = store ? 4 : 0;
 #else
@@ -76,19 +71,19 @@ struct FwdEpi {
 #endif
   const f32x16 (&acc)[8];
   float (&bin)[8][16];
-  const BlkStore& bst;
+  const ActOut<kHalf>& ao;
   const int h;
   const float* bias;  // LDS, + 4h
   const float* w8;    // LDS, + 4h
-  float* act_blk;
+  AT* act_blk;
   uint4* mask_dst;    // + lane
   uint32_t mw[4];
   f32x4 bnext, wnext;
   float zs;
 
-  __device__ __forceinline__ FwdEpi(const f32x16 (&acc_)[8], float (&bin_)[8][16], const BlkStore& bst_, int lane)
-      : acc(acc_), bin(bin_), bst(bst_), h(lane >> 5) {}
-  __device__ __forceinline__ void begin(const float* bias_, float* act_blk_, uint32_t* mask_, int lane,
+  __device__ __forceinline__ FwdEpi(const f32x16 (&acc_)[8], float (&bin_)[8][16], const ActOut<kHalf>& ao_, int lane)
+      : acc(acc_), bin(bin_), ao(ao_), h(lane >> 5) {}
+  __device__ __forceinline__ void begin(const float* bias_, AT* act_blk_, uint32_t* mask_, int lane,
                                         const float* w8_ = nullptr) {
     bias = bias_ + 4 * h;
     act_blk = act_blk_;
@@ -125,9 +120,9 @@ struct FwdEpi {
     }
 #ifndef NOF_DIAG_NO_ACT_STORE
     if constexpr (store) {
-      float* tile = act_blk + t * 32 * kBlk;
+      AT* tile = act_blk + t * 32 * kBlk;
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) blk_store_at(tile, bst, 0, 4 * q + jj, bin[t][4 * q + jj]);
+      for (int jj = 0; jj < 4; ++jj) ao.put(tile, 4 * q + jj, bin[t][4 * q + jj]);
     }
 #endif
     if (!more) {
@@ -188,19 +183,21 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
 #pragma unroll
   for (int k = 0; k < kDirIn; ++k) pe[k] = a.encoded ? a.enc_dir[(size_t)ray * kDirIn + k] : dir_feature(k, d3);
 
-  float* act_in_blk = a.act_in + (size_t)blk * kInF * kBlk;
+  constexpr bool kH = P == 2;  // f16x2: fp16 activation blocks (the weight-gradient operands)
+  typedef typename ActOut<kH>::T AT;
+  AT* act_in_blk = reinterpret_cast<AT*>(a.act_in) + (size_t)blk * kInF * kBlk;
   if constexpr (store) {
 #pragma unroll
     for (int tp = 0; tp < 3; ++tp)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) act_in_blk[blk_off(tile_feature(tp, r, h), j)] = ipe[tp][r];
+      for (int r = 0; r < 16; ++r) act_in_blk[act_off<kH>(tile_feature(tp, r, h), j)] = (AT)ipe[tp][r];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {  // view PE rows 96..122, zero rows 123..127
       const int k = 16 * h + i;
       float v = 0.0f;
 #pragma unroll
       for (int kk = 0; kk < kDirIn; ++kk) v = (kk == k) ? pe[kk] : v;
-      act_in_blk[blk_off(kPosIn + k, j)] = v;
+      act_in_blk[act_off<kH>(kPosIn + k, j)] = (AT)v;
     }
   }
   // view-direction part of layer 9 folded into a per-ray bias: b9 + W9[:, 256:283] . PE(d)
@@ -231,17 +228,17 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
   }
   __syncthreads();
 
-  const BlkStore bst(lane);
+  const ActOut<kH> ao(lane);
   int cur = 0;
   const float* wsrc = a.wimg;
   f32x16 accA[8], accB[8];  // ping-pong: layer l accumulates into one set while l - 1's epilogue drains the other
   float bin[8][16];
   const size_t layer_stride = (size_t)nblk * kWidth * kBlk;
   const float* biases = bias_lds;
-  float* act_h_blk = a.act_h + (size_t)blk * kWidth * kBlk;
+  AT* act_h_blk = reinterpret_cast<AT*>(a.act_h) + (size_t)blk * kWidth * kBlk;
 
   // ---- trunk: layer l writes acc(l odd ? B : A) ------------------------------------------
-  FwdEpi<store, false> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
+  FwdEpi<store, false, kH> ea(accA, bin, ao, lane), eb(accB, bin, ao, lane);
   ea.begin(biases, act_h_blk, mask_ptr(a.masks, blk, 0), lane);
   dense_layer<P, 0, 3, 8>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane);
   ea.tile0();
@@ -255,7 +252,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
     ea.tile0();
   }
   static_assert(kDepth == 8 && kSkip % 2 == 0, "trunk pairing assumes 8 layers and an even skip layer");
-  FwdEpi<store, true> e7(accB, bin, bst, lane);  // + density head (layer 8): z_s = w8 . h7 + b8
+  FwdEpi<store, true, kH> e7(accB, bin, ao, lane);  // + density head (layer 8): z_s = w8 . h7 + b8
   e7.begin(biases + 7 * 256, act_h_blk + 7 * layer_stride, mask_ptr(a.masks, blk, 7), lane, bias_lds + 8 * 256);
   dense_layer<P, 8, 0, 8>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea);
   e7.tile0();
@@ -265,8 +262,8 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
   float zs = e7.zs;
   zs += __shfl_xor(zs, 32, 64);
   zs += tail[kFwdTailBias + 8 * 256];
-  fwd_epilogue<4, store>(accA, bin, dirb, a.act_h9 + (size_t)blk * kWidthCond * kBlk, mask_ptr(a.masks, blk, 8), lane,
-                         bst);
+  fwd_epilogue<4, store, kH>(accA, bin, dirb, reinterpret_cast<AT*>(a.act_h9) + (size_t)blk * kWidthCond * kBlk,
+                             mask_ptr(a.masks, blk, 8), lane, ao);
 
   // ---- RGB head (layer 10) ------------------------------------------------------------
   float zc[3] = {0.0f, 0.0f, 0.0f};

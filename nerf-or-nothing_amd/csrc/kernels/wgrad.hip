@@ -481,6 +481,146 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_x3(const WgProblem* _
   }
 }
 
+// ---- f16x2 mode: fp16 operand blocks (common.h blkh_off), one 32x32x16 f16 MFMA per product -------
+// The forward / backward of the f16x2 mode write activations and (power-of-2 scaled) deltas as fp16
+// blocks, so every operand is already an MFMA fragment image: this launch is a pure stream of
+// 2-KB tiles (32 feature rows x 32 samples) from HBM into an NS-stage LDS ring by LDS-DMA
+// (global_load_lds_dwordx4, 1 KB contiguous per wave-instruction), NS - 2 blocks in flight behind a
+// counted vmcnt, and ds_read_b128 fragment reads (conflict-free through the blkh_off chunk XOR).
+// Same 2 x kX3WC wave grid and item schedule as k_wgrad_x3; MFMA time is ~1/4 of the stream time.
+constexpr int kWhStages = 4;
+constexpr int kWhStageHalves = 16 * 32 * kBlk;             // up to 16 tiles (8 A + 8 B) of 2 KB
+constexpr int kWhLds = kWhStages * kWhStageHalves * 2;      // bytes: 128 KB
+
+// s_waitcnt vmcnt(n) alone (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14)
+template <int N> __device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+template <int RB, int CB>
+__device__ __forceinline__ void wg_item_h(const WgItem& item, const WgProblem& P, _Float16* lds, int tid, int wave,
+                                          float* slabs, float* bias_slabs, const int64_t* slab_off) {
+  constexpr int ND = ((2 * RB + kX3WC * CB) * 128 + kWgX3Threads - 1) / kWgX3Threads;  // DMA instrs / block
+  int tq = tid;
+  asm volatile("" : "+v"(tq));
+  const int lane = tq & 63;
+  const int h = lane >> 5, x = lane & 31;
+  const int wr = wave / kX3WC, wc = wave % kX3WC;
+  const int r0 = wr * RB, c0 = wc * CB;
+  const bool active = r0 < P.ntr && c0 < P.ntc;  // wave-uniform
+  int rowt[RB], colt[CB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) rowt[r] = min(r0 + r, P.ntr - 1);
+#pragma unroll
+  for (int c = 0; c < CB; ++c) colt[c] = min(c0 + c, P.ntc - 1);
+  const int T = P.ntr + P.ntc;  // tiles per block
+  const size_t strideA = (size_t)P.FA * kBlk * 2, strideB = (size_t)P.FB * kBlk * 2;  // bytes per block
+  const char* baseA = reinterpret_cast<const char*>(P.A) + (size_t)item.kb0 * strideA + (size_t)P.a_row0 * kBlk * 2;
+  const char* baseB = reinterpret_cast<const char*>(P.B) + (size_t)item.kb0 * strideB + (size_t)P.b_col0 * kBlk * 2;
+  const int K = item.kb1 - item.kb0;
+  // DMA of block k (clamped to K - 1: a duplicate lands in a stage nobody reads before it is refilled)
+  auto dma = [&](int k) {
+    k = min(k, K - 1);
+    _Float16* stage = lds + (k % kWhStages) * kWhStageHalves;
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+      const int cw = min(i * kWgX3Threads + wave * 64, T * 128 - 64);  // wave's first 16-B chunk (uniform)
+      const int tt = cw >> 7;                                            // tile (uniform)
+      const char* src = (tt < P.ntr ? baseA + (size_t)k * strideA + tt * 2048
+                                    : baseB + (size_t)k * strideB + (tt - P.ntr) * 2048) + (cw & 127) * 16 + lane * 16;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(stage + cw * 8), 16, 0, 0);
+    }
+  };
+  f32x16 acc[RB][CB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r)
+#pragma unroll
+    for (int c = 0; c < CB; ++c) acc[r][c] = f32x16{};
+  float bsum[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) bsum[r] = 0.0f;
+  const int swz = (x >> 2) & 3;
+#pragma unroll
+  for (int k = 0; k < kWhStages - 1; ++k) dma(k);
+  for (int k = 0; k < K; ++k) {
+    wait_vmcnt<(kWhStages - 2) * ND>();  // block k landed (this wave's part); k + 1 .. k + NS - 2 in flight
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave's part; stage k - 1 read out
+    dma(k + kWhStages - 1);  // into stage (k - 1) % NS
+    const f16x8* st = reinterpret_cast<const f16x8*>(lds + (k % kWhStages) * kWhStageHalves);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int co = x * 4 + ((2 * ks + h) ^ swz);  // 16-B chunk of row x within a tile
+      f16x8 fa[RB], fb[CB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) fa[r] = st[rowt[r] * 128 + co];
+#pragma unroll
+      for (int c = 0; c < CB; ++c) fb[c] = st[(P.ntr + colt[c]) * 128 + co];
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int c = 0; c < CB; ++c) acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[r], fb[c], acc[r][c], 0, 0, 0);
+      if (wc == 0) {  // bias partials: row sums of delta (uniform branch)
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          float s = 0.0f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s += (float)fa[r][j];
+          bsum[r] += s;
+        }
+      }
+    }
+  }
+  wait_vmcnt<0>();  // retire the clamped tail DMAs before the ring is reused
+  if (active) {
+    float* slab = slabs + slab_off[item.slab];
+    const int ld_ = P.ntc * 32;
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int c = 0; c < CB; ++c) {
+        if (r0 + r < P.ntr && c0 + c < P.ntc) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int row = rowt[r] * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            slab[(size_t)row * ld_ + colt[c] * 32 + x] = acc[r][c][e];
+          }
+        }
+      }
+  }
+  if (wc == 0) {
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const float v = bsum[r] + __shfl_xor(bsum[r], 32, 64);
+      if (r0 + r < P.ntr && h == 0) bias_slabs[(size_t)item.slab * 256 + rowt[r] * 32 + x] = v;
+    }
+  }
+  __syncthreads();  // the ring is reused by the next item
+}
+
+__global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_h(const WgProblem* __restrict__ probs,
+                                                             const WgItem* __restrict__ items,
+                                                             const int* __restrict__ item_ptr,
+                                                             const int64_t* __restrict__ slab_off, float* slabs,
+                                                             float* bias_slabs) {
+  extern __shared__ __attribute__((aligned(16))) _Float16 ldsh[];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int it0 = item_ptr[blockIdx.x], it1 = item_ptr[blockIdx.x + 1];
+  static_assert(kX3WC == 4, "k_wgrad_h instantiates the 2 x 4 wave grid's shapes");
+  for (int it = it0; it < it1; ++it) {
+    const WgItem item = items[it];
+    const WgProblem P = probs[item.prob];
+    switch (((P.ntr + 1) >> 1) * 10 + (P.ntc + kX3WC - 1) / kX3WC) {
+      case 11: wg_item_h<1, 1>(item, P, ldsh, tid, wave, slabs, bias_slabs, slab_off); break;
+      case 21: wg_item_h<2, 1>(item, P, ldsh, tid, wave, slabs, bias_slabs, slab_off); break;
+      case 32: wg_item_h<3, 2>(item, P, ldsh, tid, wave, slabs, bias_slabs, slab_off); break;
+      case 41: wg_item_h<4, 1>(item, P, ldsh, tid, wave, slabs, bias_slabs, slab_off); break;
+      default: wg_item_h<4, 2>(item, P, ldsh, tid, wave, slabs, bias_slabs, slab_off); break;
+    }
+  }
+}
+
 int wgrad_x3_grid_cols() { return kX3WC; }
 
 int wgrad_shape(int ntr, int ntc, int* cost2) {
@@ -522,7 +662,17 @@ static hipError_t launch_wgrad_split(const WgProblem* probs, const WgItem* items
 hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,
                            const int64_t* slab_off, float* slabs, float* bias_slabs, int precision, hipStream_t st) {
   if (num_wg <= 0) return hipSuccess;
-  if (precision == 2) return launch_wgrad_split<2>(probs, items, item_ptr, num_wg, slab_off, slabs, bias_slabs, st);
+  if (precision == 2) {  // fp16 operand blocks (k_wgrad_h)
+    static bool attr = false;
+    if (!attr) {
+      const hipError_t e = hipFuncSetAttribute((const void*)k_wgrad_h, hipFuncAttributeMaxDynamicSharedMemorySize, kWhLds);
+      if (e != hipSuccess) return e;
+      attr = true;
+    }
+    hipLaunchKernelGGL(k_wgrad_h, dim3(num_wg), dim3(kWgX3Threads), kWhLds, st, probs, items, item_ptr, slab_off,
+                       slabs, bias_slabs);
+    return hipGetLastError();
+  }
   return launch_wgrad_split<1>(probs, items, item_ptr, num_wg, slab_off, slabs, bias_slabs, st);
 }
 

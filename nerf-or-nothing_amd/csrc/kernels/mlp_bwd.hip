@@ -35,7 +35,7 @@ struct BwdEpi {
   float dzs;
   AT* dst_blk;
   uint4 mk;
-  f32x4 wnext;
+  f32x4 wnext, wcur;
 
   __device__ __forceinline__ BwdEpi(const f32x16 (&acc_)[8], float (&bin_)[8][16], const ActOut<kHalf>& ao_, int lane)
       : acc(acc_), bin(bin_), ao(ao_), h(lane >> 5) {}
@@ -49,27 +49,29 @@ struct BwdEpi {
       wnext = *reinterpret_cast<const f32x4*>(w8);
     }
   }
-  __device__ __forceinline__ void operator()(int t, int q) {
+  // register r of tile t (one or two per MFMA group in the split layers); w8 loaded one part ahead
+  __device__ __forceinline__ void reg(int t, int r) {
 #ifdef NOF_DIAG_NO_EPI
     return;
 #endif
-    f32x4 w4;
+    const int q = r >> 2, jj = r & 3;
     if constexpr (kDensity) {
-      w4 = wnext;
-      if (!(t == 7 && q == 3)) wnext = *reinterpret_cast<const f32x4*>(w8 + 32 * t + 8 * q + 8);
+      if (jj == 0) {
+        wcur = wnext;
+        if (!(t == 7 && q == 3)) wnext = *reinterpret_cast<const f32x4*>(w8 + 32 * t + 8 * q + 8);
+      }
     }
-    AT* tile = dst_blk + t * 32 * kBlk;
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int r = 4 * q + jj;
-      float v = acc[t][r];
-      if constexpr (kDensity) v += w4[jj] * dzs;
-      v = mask_bit(mk, t, r) ? v : 0.0f;
-      bin[t][r] = v;
+    float v = acc[t][r];
+    if constexpr (kDensity) v += wcur[jj] * dzs;
+    v = mask_bit(mk, t, r) ? v : 0.0f;
+    bin[t][r] = v;
 #ifndef NOF_DIAG_NO_ACT_STORE
-      ao.put(tile, r, v);
+    ao.put(dst_blk + t * 32 * kBlk, r, v);
 #endif
-    }
+  }
+  __device__ __forceinline__ void operator()(int t, int q) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) reg(t, 4 * q + jj);
   }
   __device__ __forceinline__ void tile0() {
 #pragma unroll
@@ -188,13 +190,17 @@ __global__ void k_delta_amax(const float* __restrict__ dsigma, const float* __re
     v = fmaxf(v, fabsf(i < M ? dsigma[i] : drgb[i - M]));
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  if ((threadIdx.x & 63) == 0) atomicMax(amax, __float_as_uint(v));
+  __shared__ float wmax[4];  // one atomic per block: 4096 same-address atomics serialise (~10 ns each)
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicMax(amax, __float_as_uint(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]))));
 }
 
 hipError_t launch_delta_amax(const float* dsigma, const float* drgb, int M, uint32_t* amax, hipStream_t st) {
   hipError_t e = hipMemsetAsync(amax, 0, sizeof(uint32_t), st);
   if (e != hipSuccess || M <= 0) return e;
-  const int blocks = std::min(1024, (4 * M + 255) / 256);
+  const int blocks = std::min(256, (4 * M + 255) / 256);
   hipLaunchKernelGGL(k_delta_amax, dim3(blocks), dim3(256), 0, st, dsigma, drgb, M, amax);
   return hipGetLastError();
 }

@@ -70,6 +70,7 @@ constexpr int kIpeLdsFloats = 3 * 4 * 64 * 4;
 struct NoEpi {
   static constexpr int kVmPerPart = 0;
   __device__ __forceinline__ void operator()(int, int) {}
+  __device__ __forceinline__ void reg(int, int) {}
 };
 
 // End-of-slice barrier.  This wave's DMA of the next slice must have landed before any wave reads
@@ -304,12 +305,9 @@ template <int P> constexpr int split_dma_groups() {
   return (split_dma_steps<P>() + split_dma_per<P>() - 1) / split_dma_per<P>();
 }
 static_assert(split_dma_groups<1>() <= 8, "the OT = 4 layer has 8 MFMA groups per slice");
-template <int P, int OT> constexpr int split_parts_after_dma() {
-  int n = 0;
-  for (int s = 0; s < 2; ++s)
-    n += ((s * OT + 1 > split_dma_groups<P>() - 1) ? 1 : 0) + ((s * OT + OT / 2 + 1 > split_dma_groups<P>() - 1) ? 1 : 0);
-  return n;
-}
+// epilogue registers run after the slice's last DMA step (groups past the last DMA group; counted
+// low, which only waits longer): 8 / OT registers per MFMA group
+template <int P, int OT> constexpr int split_regs_after_dma() { return (2 * OT - split_dma_groups<P>()) * (8 / OT); }
 
 // raw fp32 B values of k-step kk of a split-mode layer: tiles t < NT_B from the register-resident
 // activations, the rest from the wave's IPE copy in LDS ([tp][q][lane][4] floats)
@@ -333,8 +331,9 @@ __device__ __forceinline__ void x3_b_values(const float (&bin)[8][16], const flo
 // Split-mode dense layer: same contract as mlp_layer (slices of the split image, one barrier per
 // slice).  Per (k-step, row tile): NP ds_read_b128 (issued one group ahead) and NPROD MFMAs; the
 // next k-step's B fragment is split pair by pair in the shadow of the current k-step's MFMAs.
-// Epilogue parts: k-step s of slice t runs epi(t + 1, 2s) and epi(t + 1, 2s + 1), so the first half
-// of tile t + 1 is in `bin` before k-step 1 of slice t splits it as the next B fragment.
+// Epilogue: each MFMA group of k-step s of slice t finishes 8 / OT registers of tile t + 1 (registers
+// 8s .. 8s + 7 over the k-step), so the first half of tile t + 1 is in `bin` before k-step 1 of
+// slice t splits it as the next B fragment, and the epilogue's VALU work is spread evenly.
 template <int P, int NT_B, int NT_I, int OT, class Epi>
 __device__ __forceinline__ void mlp_layer_split(const float (&bin)[8][16], const float* ipe_lds, f32x16 (&acc)[8],
                                                 float* lds, int& cur, const float*& wsrc, bool last_in_schedule,
@@ -393,13 +392,16 @@ __device__ __forceinline__ void mlp_layer_split(const float (&bin)[8][16], const
           const int i = 2 * (ot / PER);
           split_pair<P>(vn[i], vn[i + 1], b_nxt, i);
         }
-        if (t + 1 < NT_B && (ot == 1 || ot == OT / 2 + 1)) epi(t + 1, 2 * s + (ot == 1 ? 0 : 1));
+        if (t + 1 < NT_B) {  // registers 8s + (8 / OT) ot .. of tile t + 1: the first half before k-step 1 splits it
+#pragma unroll
+          for (int u = 0; u < 8 / OT; ++u) epi.reg(t + 1, 8 * s + (8 / OT) * ot + u);
+        }
         __builtin_amdgcn_sched_barrier(0);
         a_cur = a_nxt;
       }
       b_cur = b_nxt;
     }
-    slice_barrier(t + 1 < NT_B ? split_parts_after_dma<P, OT>() * Epi::kVmPerPart : 0);
+    slice_barrier(t + 1 < NT_B ? split_regs_after_dma<P, OT>() * (Epi::kVmPerPart / 4) : 0);
     cur ^= 1;
 #ifndef NOF_DIAG_DMA_SAME
     wsrc += SF;

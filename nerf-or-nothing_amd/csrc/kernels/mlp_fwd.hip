@@ -78,7 +78,7 @@ struct FwdEpi {
   AT* act_blk;
   uint4* mask_dst;    // + lane
   uint32_t mw[4];
-  f32x4 bnext, wnext;
+  f32x4 bnext, wnext, bcur, wcur;
   float zs;
 
   __device__ __forceinline__ FwdEpi(const f32x16 (&acc_)[8], float (&bin_)[8][16], const ActOut<kHalf>& ao_, int lane)
@@ -96,40 +96,40 @@ struct FwdEpi {
       zs = 0.0f;
     }
   }
-  __device__ __forceinline__ void operator()(int t, int q) {
+  // register r of tile t (the split layers run one or two registers per MFMA group, spreading the
+  // epilogue's VALU work evenly over the slice); bias / w8 values are loaded one part (4 registers) ahead
+  __device__ __forceinline__ void reg(int t, int r) {
 #ifdef NOF_DIAG_NO_EPI
     return;
 #endif
+    const int q = r >> 2, jj = r & 3;
     const int fo = 32 * t + 8 * q;
-    const f32x4 b4 = bnext;
     const bool more = !(t == 7 && q == 3);
-    if (more) bnext = *reinterpret_cast<const f32x4*>(bias + fo + 8);
-    f32x4 w4;
-    if constexpr (kDensity) {
-      w4 = wnext;
-      if (more) wnext = *reinterpret_cast<const f32x4*>(w8 + fo + 8);
+    if (jj == 0) {
+      bcur = bnext;
+      if (more) bnext = *reinterpret_cast<const f32x4*>(bias + fo + 8);
+      if constexpr (kDensity) {
+        wcur = wnext;
+        if (more) wnext = *reinterpret_cast<const f32x4*>(w8 + fo + 8);
+      }
     }
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int r = 4 * q + jj;
-      const float z = acc[t][r] + b4[jj];
-      const float hv = z > 0.0f ? z : 0.0f;
-      bin[t][r] = hv;
-      mw[t >> 1] = (mw[t >> 1] << 1) | (hv > 0.0f ? 1u : 0u);
-      if constexpr (kDensity) zs += w4[jj] * hv;
-    }
+    const float z = acc[t][r] + bcur[jj];
+    const float hv = z > 0.0f ? z : 0.0f;
+    bin[t][r] = hv;
+    mw[t >> 1] = (mw[t >> 1] << 1) | (hv > 0.0f ? 1u : 0u);
+    if constexpr (kDensity) zs += wcur[jj] * hv;
 #ifndef NOF_DIAG_NO_ACT_STORE
-    if constexpr (store) {
-      AT* tile = act_blk + t * 32 * kBlk;
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) ao.put(tile, 4 * q + jj, bin[t][4 * q + jj]);
-    }
+    if constexpr (store) ao.put(act_blk + t * 32 * kBlk, r, hv);
 #endif
-    if (!more) {
+    if (!more && jj == 3) {
       uint4 mv;
       mv.x = mw[0]; mv.y = mw[1]; mv.z = mw[2]; mv.w = mw[3];
       if constexpr (store) *mask_dst = mv;
     }
+  }
+  __device__ __forceinline__ void operator()(int t, int q) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) reg(t, 4 * q + jj);
   }
   __device__ __forceinline__ void tile0() {
 #pragma unroll

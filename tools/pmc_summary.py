@@ -7,7 +7,7 @@ coalesced streaming read on gfx950 (MI355X_MICROARCH.md, HBM section), WRITE_SIZ
 import csv, collections, json, os, shutil, sys
 
 src, tag = sys.argv[1], sys.argv[2]
-suffix = sys.argv[3] if len(sys.argv) > 3 else ""  # "_split" for the split-precision kernels
+suffix = sys.argv[3] if len(sys.argv) > 3 else ""  # "_split" / "_f16x2" for the other precision modes
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 dst = os.path.join(root, "profiles")
 os.makedirs(dst, exist_ok=True)
@@ -40,6 +40,8 @@ json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
 names = {"k_mlp_fwd16<true>": "mlp_fwd", "k_mlp_bwd16": "mlp_bwd", "k_wgrad": "wgrad",
          "k_mlp_fwd<false, true>": "mlp_fwd", "k_mlp_bwd<false>": "mlp_bwd",  # NOF_F32_MFMA32 builds
          "k_mlp_fwd<true, true>": "mlp_fwd_split", "k_mlp_bwd<true>": "mlp_bwd_split", "k_wgrad_x3": "wgrad_split",
+         "k_mlp_fwd<1, true>": "mlp_fwd_split", "k_mlp_bwd<1>": "mlp_bwd_split", "k_wgrad_x3<1>": "wgrad_split",
+         "k_mlp_fwd<2, true>": "mlp_fwd_f16x2", "k_mlp_bwd<2>": "mlp_bwd_f16x2", "k_wgrad_h": "wgrad_f16x2",
          "k_render_fwd<2>": "render_fwd" + suffix, "k_render_bwd<2>": "render_bwd" + suffix}
 tfile = os.path.join(dst, "pmc_traffic.json")
 traffic = json.load(open(tfile)) if os.path.exists(tfile) else {}

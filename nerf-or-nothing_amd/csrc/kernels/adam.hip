@@ -146,8 +146,12 @@ __global__ void k_pack_weights_x3(const float* __restrict__ P_, PackArgs pa, flo
     const bool fwd = gid < nfc;
     const int64_t c = fwd ? gid : gid - nfc;
     const int slice = (int)(c / kChunks), q = (int)(c % kChunks);
-    const int lane = q & 63, rest = q >> 6, piece = rest % NP, so = rest / NP, ot = so & 7, s = so >> 3;
-    const int h = lane >> 5, row = ot * 32 + (lane & 31);
+    const int lane = q & 63, rest = q >> 6, piece = rest % NP, so = rest / NP;
+    // P = 1 (32x32x16 fragments, mlp_common.h): so = 8 s + ot, lane (h, x): row 32 ot + x,
+    //   element j = column 16 s + 8 (j >> 2) + 4h + (j & 3);
+    // P = 2 (16x16x32 fragments, mlp16.h mlp_layer16h): so = row tile rt, lane (g, x): row 16 rt + x,
+    //   element j = column 16 (j >> 2) + 4g + (j & 3)
+    const int row = P == 2 ? 16 * so + (lane & 15) : (so & 7) * 32 + (lane & 31);
     int l, base;
     if (fwd) fwd_slice(slice, l, base);
     else bwd_slice(slice, l, base);
@@ -155,7 +159,8 @@ __global__ void k_pack_weights_x3(const float* __restrict__ P_, PackArgs pa, flo
     typename SplitMode<P>::V8 out;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int kf = 16 * s + 8 * (j >> 2) + 4 * h + (j & 3);
+      const int kf = P == 2 ? 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3)
+                            : 16 * (so >> 3) + 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3);
       float w;
       if (fwd) w = (row < layer_out(l) && base + kf < in) ? Pp[pa.woff[l] + (int64_t)row * in + base + kf] : 0.0f;
       else w = Pp[pa.woff[l] + (int64_t)(base + kf) * in + row];

@@ -83,6 +83,27 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t blk_rsrc(float* blk) {
   return __builtin_amdgcn_make_buffer_rsrc(blk, (short)0, 0x7fffffff, 0x00020000);
 }
 
+// fp16 counterpart (f16x2 mode, common.h blkh_off): byte(f, s) = 64 f + ((((s >> 3) ^ ((f >> 2) & 3)) << 4) |
+// ((s & 7) << 1)) with f = 16t + 4g + r, s = 16 half + j, so (f >> 2) & 3 = g and the lane part does not
+// depend on (t, r): one voffset, 1024 t in soffset, 64 r immediate.
+struct BlkStore16H {
+  uint32_t voff;
+  __device__ __forceinline__ BlkStore16H(int lane, int half) {
+    const int g = lane >> 4, j = lane & 15;
+    voff = 256u * g + ((((2 * half + (j >> 3)) ^ g) << 4) | ((j & 7) << 1));
+  }
+  __device__ __forceinline__ void store(__amdgpu_buffer_rsrc_t blk, int t, int r, float v) const {
+    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)v), blk, (int)voff + 64 * r,
+                                          1024 * t, 0);
+  }
+};
+template <int P> struct Store16 { typedef BlkStore16 T; typedef float E; };
+template <> struct Store16<2> { typedef BlkStore16H T; typedef _Float16 E; };
+template <class E>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t blk_rsrc_t(E* blk) {
+  return __builtin_amdgcn_make_buffer_rsrc(blk, (short)0, 0x7fffffff, 0x00020000);
+}
+
 // ReLU masks of the 16-sample kernels: per 32-sample block and slot (trunk layers 0..7, view layer
 // 9) 1 KB = [half][64 lanes][uint2]; bit of (tile t, register r) at position 31 - ((t & 7) 4 + r) of
 // word t >> 3 (shift-accumulated in tile order).
@@ -180,12 +201,92 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
     wsrc += kSliceFloats;
   }
 }
-template <int NT_B, int NT_I, int OT>
-__device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16],
-                                            float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
-                                            int lane) {
+// f16x2 mode on v_mfma_f32_16x16x32_f16 (same two-waves-per-SIMD structure).  One slice (32 input
+// features = input tiles 2t, 2t + 1) is ONE k-step: lane (g, j) supplies B[k = 8g + i][col j], and
+// k = 8g + i is taken to be feature 16 (2t + (i >> 2)) + 4g + (i & 3) — the registers bin[2t][0..3],
+// bin[2t + 1][0..3] as they stand, split once per slice into fp16 hi / lo.  The packed slice
+// (k_pack_weights_x3<2>) holds, per 16-row tile rt and piece p, the 16-B A fragment of lane (g, j):
+// W[16 rt + j][base + 16 (i >> 2) + 4g + (i & 3)], i = 0..7 (chunk (2 rt + p) 64 + lane: one
+// contiguous ds_read_b128 per fragment).  A group = one row-tile pair x 3 products (lo.hi, hi.lo,
+// hi.hi) interleaved over the pair's two accumulators; the next pair's fragments are read one group
+// ahead; the 4 DMA steps of slice t + 2 ride groups 0..3; epilogue tiles 2t + 2, 2t + 3 run after them.
+template <int NT_B, int NT_I, int OT, class Epi>
+__device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16],
+                                             float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
+                                             int lane, Epi& epi) {
+  typedef SplitMode<2> SM;
+  static_assert(OT % 2 == 0 && OT <= 16, "row tiles come in pairs");
+  constexpr int NG = OT / 2;  // groups per slice
+  constexpr int kE1 = NG > 4 ? 4 : NG - 1;
+  constexpr int kE2 = NG > 6 ? 6 : NG - 1;
+#pragma unroll
+  for (int t = 0; t < NT_B + NT_I; ++t) {
+    const bool dma = !(last_in_schedule && t + 2 >= NT_B + NT_I);  // slice t + 2 exists
+    const int nxt2 = cur == 0 ? 2 : cur - 1;                         // (cur + 2) % 3
+    const f16x8* W = reinterpret_cast<const f16x8*>(lds + cur * kSliceFloats) + lane;
+    float v[8];
+    if (t < NT_B) {
+      const int tb = t < NT_B ? 2 * t : 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = bin[tb + (i >> 2)][i & 3];
+    } else {
+      const int ti = t >= NT_B ? 2 * (t - NT_B) : 0;
+      const f32x4 u0 = *reinterpret_cast<const f32x4*>(ipe_lds + (ti * 64 + lane) * 4);
+      const f32x4 u1 = *reinterpret_cast<const f32x4*>(ipe_lds + ((ti + 1) * 64 + lane) * 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { v[i] = u0[i]; v[4 + i] = u1[i]; }
+    }
+    Frag<2> b;
+    split8<2>(v, b);
+    Frag<2> a0, a1;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) { a0.p[p] = W[p * 64]; a1.p[p] = W[(2 + p) * 64]; }
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      asm volatile("" ::"v"(a0.p[0]), "v"(a0.p[1]), "v"(a1.p[0]), "v"(a1.p[1]));  // this group's reads land here
+      Frag<2> n0 = a0, n1 = a1;
+      if (q + 1 < NG) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          n0.p[p] = W[((2 * q + 2) * 2 + p) * 64];
+          n1.p[p] = W[((2 * q + 3) * 2 + p) * 64];
+        }
+      }
+#ifndef NOF_DIAG_NO_DMA
+      if (dma && q < 4) slice16_dma_step(wsrc + 2 * kSliceFloats, lds + nxt2 * kSliceFloats, tid, q);
+#endif
+      __builtin_amdgcn_sched_barrier(0);
+      const bool first = t == 0;
+#pragma unroll
+      for (int pp = 0; pp < SM::NPROD; ++pp) {
+        acc[2 * q] = SM::mfma16(a0.p[SM::pa(pp)], b.p[SM::pb(pp)], (first && pp == 0) ? f32x4{} : acc[2 * q]);
+        acc[2 * q + 1] = SM::mfma16(a1.p[SM::pa(pp)], b.p[SM::pb(pp)], (first && pp == 0) ? f32x4{} : acc[2 * q + 1]);
+      }
+      if (t + 1 < NT_B && q == kE1) epi(2 * t + 2);
+      if (t + 1 < NT_B && q == kE2) epi(2 * t + 3);
+      __builtin_amdgcn_sched_barrier(0);
+      a0 = n0;
+      a1 = n1;
+    }
+    slice_barrier((dma ? 4 : 0) + (t + 1 < NT_B ? 2 * Epi::kVmPerPart : 0));
+    cur = cur == 2 ? 0 : cur + 1;
+    wsrc += kSliceFloats;
+  }
+}
+
+// precision dispatch: P = 0 fp32 16x16x4, P = 2 f16x2 16x16x32
+template <int P, int NT_B, int NT_I, int OT, class Epi>
+__device__ __forceinline__ void layer16(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16], float* lds,
+                                        int& cur, const float*& wsrc, bool last_in_schedule, int tid, int lane,
+                                        Epi& epi) {
+  if constexpr (P == 2) mlp_layer16h<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi);
+  else mlp_layer16<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi);
+}
+template <int P, int NT_B, int NT_I, int OT>
+__device__ __forceinline__ void layer16(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16], float* lds,
+                                        int& cur, const float*& wsrc, bool last_in_schedule, int tid, int lane) {
   NoEpi16 none;
-  mlp_layer16<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, none);
+  layer16<P, NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, none);
 }
 
 }  // namespace nof

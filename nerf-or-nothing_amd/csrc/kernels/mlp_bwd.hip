@@ -210,7 +210,11 @@ hipError_t launch_mlp_bwd(const BwdArgs& a, hipStream_t st) {
   if (a.M % kBlk != 0) return hipErrorInvalidValue;
   const int nblk = a.M / kBlk;
   if (a.split == 1) hipLaunchKernelGGL(k_mlp_bwd<1>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
+#ifdef NOF_F16_MFMA32
   else if (a.split == 2) hipLaunchKernelGGL(k_mlp_bwd<2>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
+#else
+  else if (a.split == 2) return launch_mlp_bwd16(a, st);
+#endif
 #ifdef NOF_F32_MFMA32
   else hipLaunchKernelGGL(k_mlp_bwd<0>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
 #else

@@ -17,12 +17,12 @@ namespace nof {
 
 // delta = mask ? acc (+ w8 * dz_s) : 0 -> B operand + delta block, one tile per call inside the
 // next layer's MFMA stream; w8 values loaded one tile ahead.
-template <bool kDensity>
+template <bool kDensity, class ST>
 struct BwdEpi16 {
   static constexpr int kVmPerPart = 4;
   const f32x4 (&acc)[16];
   float (&bin)[16][4];
-  const BlkStore16& bst;
+  const ST& bst;
   const int g;
   const float* w8;  // LDS, + 4g
   float dzs;
@@ -30,12 +30,12 @@ struct BwdEpi16 {
   uint2 mk;
   f32x4 wnext;
 
-  __device__ __forceinline__ BwdEpi16(const f32x4 (&acc_)[16], float (&bin_)[16][4], const BlkStore16& bst_, int lane)
+  __device__ __forceinline__ BwdEpi16(const f32x4 (&acc_)[16], float (&bin_)[16][4], const ST& bst_, int lane)
       : acc(acc_), bin(bin_), bst(bst_), g(lane >> 4) {}
-  __device__ __forceinline__ void begin(const uint2* mask, float* dst_blk_, const float* w8_ = nullptr,
-                                        float dzs_ = 0.0f) {
+  template <class E>
+  __device__ __forceinline__ void begin(const uint2* mask, E* dst_blk_, const float* w8_ = nullptr, float dzs_ = 0.0f) {
     mk = *mask;
-    dst_blk = blk_rsrc(dst_blk_);
+    dst_blk = blk_rsrc_t(dst_blk_);
     if constexpr (kDensity) {
       w8 = w8_ + 4 * g;
       dzs = dzs_;
@@ -63,13 +63,17 @@ struct BwdEpi16 {
   }
 };
 
+// P: 0 = fp32, 2 = f16x2 (16x16x32 f16, power-of-2 scaled deltas stored as fp16 blocks)
+template <int P>
 __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
+  typedef typename Store16<P>::T ST;
+  typedef typename Store16<P>::E AE;
   __shared__ __attribute__((aligned(16))) float lds[kRing16Floats + 256];
   float* w8_lds = lds + kRing16Floats;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: block pointers stay in SGPRs
   const int half = wave & 1;
-  const BlkStore16 bst(lane, half);
+  const ST bst(lane, half);
   const int nblk = a.M / kBlk;
   const int blk_raw = blockIdx.x * 4 + (wave >> 1);
   const int blk = blk_raw < nblk ? blk_raw : nblk - 1;  // tail waves duplicate the last block
@@ -82,14 +86,20 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
 
   // ---- heads (MNcs:410-415) ------------------------------------------------------------
   const f32x4 zh = reinterpret_cast<const f32x4*>(a.zhead)[m];
-  const float dzs = a.dsigma[m] * sigmoid_f(zh[0] + kDensityBias);
+  float dzs = a.dsigma[m] * sigmoid_f(zh[0] + kDensityBias);
   float dzc[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const float s = sigmoid_f(zh[1 + c]);
     dzc[c] = a.drgb[(size_t)m * 3 + c] * (s * (1.0f - s)) * kRgbScale;
   }
-  const __amdgpu_buffer_rsrc_t d9 = blk_rsrc(a.delta9x + (size_t)blk * kD9F * kBlk);  // uniform block base
+  if constexpr (P == 2) {  // f16x2: deltas enter the fp16 pieces scaled by a power of two
+    const float sc = delta_scale(a.amax, false);
+    dzs *= sc;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) dzc[c] *= sc;
+  }
+  const __amdgpu_buffer_rsrc_t d9 = blk_rsrc_t(reinterpret_cast<AE*>(a.delta9x) + (size_t)blk * kD9F * kBlk);
   // rows 128..143 = tile 8: dz_sigma, dz_rgb in lane group 0, zeros above
 #pragma unroll
   for (int r = 0; r < 4; ++r) bst.store(d9, 8, r, g == 0 ? (r == 0 ? dzs : dzc[r - 1]) : 0.0f);
@@ -119,24 +129,24 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
   int cur = 0;
   const float* wsrc = a.wimg_b;
   f32x4 accA[16], accB[16];  // ping-pong, as in the forward
-  float* delta_blk = a.delta + (size_t)blk * kWidth * kBlk;
+  AE* delta_blk = reinterpret_cast<AE*>(a.delta) + (size_t)blk * kWidth * kBlk;
   // ---- dh7 = W9[:, :256]^T delta9 + w8 dz_s ; delta7 ---------------------------------------
-  BwdEpi16<true> e7(accA, bin, bst, lane);
+  BwdEpi16<true, ST> e7(accA, bin, bst, lane);
   e7.begin(mask16_ptr(masks, blk, 7, half, lane), delta_blk + 7 * layer_stride, w8_lds, dzs);
-  mlp_layer16<4, 0, 16>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane);
+  layer16<P, 4, 0, 16>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane);
   e7.tile01();
   // ---- dh_{l-1} = W_l[:, :256]^T delta_l ; delta_{l-1}, l = 7..1 (l odd: A -> B) ------------
-  BwdEpi16<false> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
+  BwdEpi16<false, ST> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
   eb.begin(mask16_ptr(masks, blk, 6, half, lane), delta_blk + 6 * layer_stride);
-  mlp_layer16<8, 0, 16>(bin, nullptr, accB, lds, cur, wsrc, false, tid, lane, e7);
+  layer16<P, 8, 0, 16>(bin, nullptr, accB, lds, cur, wsrc, false, tid, lane, e7);
   eb.tile01();
   static_assert(kDepth == 8, "bwd pairing assumes 8 trunk layers");
   for (int l = kDepth - 2; l >= 2; l -= 2) {
     ea.begin(mask16_ptr(masks, blk, l - 1, half, lane), delta_blk + (l - 1) * layer_stride);
-    mlp_layer16<8, 0, 16>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane, eb);
+    layer16<P, 8, 0, 16>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane, eb);
     ea.tile01();
     eb.begin(mask16_ptr(masks, blk, l - 2, half, lane), delta_blk + (l - 2) * layer_stride);
-    mlp_layer16<8, 0, 16>(bin, nullptr, accB, lds, cur, wsrc, l == 2, tid, lane, ea);
+    layer16<P, 8, 0, 16>(bin, nullptr, accB, lds, cur, wsrc, l == 2, tid, lane, ea);
     eb.tile01();
   }
   // delta0: nothing left to hide it under
@@ -146,7 +156,8 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
 
 hipError_t launch_mlp_bwd16(const BwdArgs& a, hipStream_t st) {
   const int nblk = a.M / kBlk;
-  hipLaunchKernelGGL(k_mlp_bwd16, dim3((nblk + 3) / 4), dim3(kMlp16Threads), 0, st, a);
+  if (a.split == 2) hipLaunchKernelGGL(k_mlp_bwd16<2>, dim3((nblk + 3) / 4), dim3(kMlp16Threads), 0, st, a);
+  else hipLaunchKernelGGL(k_mlp_bwd16<0>, dim3((nblk + 3) / 4), dim3(kMlp16Threads), 0, st, a);
   return hipGetLastError();
 }
 

@@ -206,6 +206,9 @@ template <> struct SplitMode<1> {
   static __device__ __forceinline__ f32x16 mfma(V8 a, V8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
   }
+  static __device__ __forceinline__ f32x4 mfma16(V8 a, V8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
 };
 template <> struct SplitMode<2> {
   typedef f16x8 V8;
@@ -216,6 +219,9 @@ template <> struct SplitMode<2> {
   static constexpr int pb(int pp) { return pp == 1 ? 1 : 0; }
   static __device__ __forceinline__ f32x16 mfma(V8 a, V8 b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ f32x4 mfma16(V8 a, V8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
   }
 };
 

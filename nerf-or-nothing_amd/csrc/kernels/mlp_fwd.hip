@@ -300,8 +300,12 @@ hipError_t launch_mlp_fwd(const FwdArgs& a, hipStream_t st) {
     if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd<1, false>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((k_mlp_fwd<1, true>), grid, block, 0, st, a);
   } else if (a.split == 2) {
+#ifdef NOF_F16_MFMA32  // the 32x32x16, one-wave-per-SIMD f16x2 kernels (diagnostic builds only)
     if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd<2, false>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((k_mlp_fwd<2, true>), grid, block, 0, st, a);
+#else
+    return launch_mlp_fwd16(a, st);
+#endif
   } else {
 #ifdef NOF_F32_MFMA32  // the 32x32x2, one-wave-per-SIMD fp32 kernels (diagnostic builds only)
     if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd<0, false>), grid, block, 0, st, a);

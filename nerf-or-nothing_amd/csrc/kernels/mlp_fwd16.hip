@@ -22,7 +22,7 @@ namespace nof {
 // come from the workgroup's LDS copy, loaded one tile ahead.  kDensity folds the density head
 // (z_s = w8 . h7) into layer 7's epilogue.  A tail wave clamped onto the last block recomputes
 // bit-identical values, so its duplicate stores are benign.
-template <bool store, bool kDensity, int NT>
+template <bool store, bool kDensity, int NT, class ST>
 struct FwdEpi16 {
 #ifndef NOF_DIAG_NO_ACT_STORE
   static constexpr int kVmPerPart = store ? 4 : 0;
@@ -31,7 +31,7 @@ struct FwdEpi16 {
 #endif
   const f32x4 (&acc)[16];
   float (&bin)[16][4];
-  const BlkStore16& bst;
+  const ST& bst;
   const int g;
   const float* bias;  // LDS, + 4g
   const float* w8;    // LDS, + 4g
@@ -41,12 +41,12 @@ struct FwdEpi16 {
   f32x4 bnext, wnext;
   float zs;
 
-  __device__ __forceinline__ FwdEpi16(const f32x4 (&acc_)[16], float (&bin_)[16][4], const BlkStore16& bst_, int lane)
+  __device__ __forceinline__ FwdEpi16(const f32x4 (&acc_)[16], float (&bin_)[16][4], const ST& bst_, int lane)
       : acc(acc_), bin(bin_), bst(bst_), g(lane >> 4) {}
-  __device__ __forceinline__ void begin(const float* bias_, float* act_blk_, uint2* mask_dst_,
-                                        const float* w8_ = nullptr) {
+  template <class E>
+  __device__ __forceinline__ void begin(const float* bias_, E* act_blk_, uint2* mask_dst_, const float* w8_ = nullptr) {
     bias = bias_ + 4 * g;
-    act_blk = blk_rsrc(act_blk_);
+    act_blk = blk_rsrc_t(act_blk_);
     mask_dst = mask_dst_;
     mw[0] = mw[1] = 0u;
     bnext = *reinterpret_cast<const f32x4*>(bias);
@@ -85,8 +85,11 @@ struct FwdEpi16 {
   }
 };
 
-template <bool store>  // store: side outputs for the backward pass (off for inference)
+// P: 0 = fp32 (16x16x4 fp32 MFMA, fp32 activation blocks), 2 = f16x2 (16x16x32 f16, fp16 blocks)
+template <int P, bool store>  // store: side outputs for the backward pass (off for inference)
 __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
+  typedef typename Store16<P>::T ST;
+  typedef typename Store16<P>::E AE;
   constexpr int kRing = kRing16Floats;
   constexpr int kBiasLds = 8 * 256 + 256;
   __shared__ __attribute__((aligned(16))) float lds[kRing + 8 * kIpe16Floats + 8 * 128 + kBiasLds];
@@ -132,9 +135,9 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
 #pragma unroll
   for (int k = 0; k < kDirIn; ++k) pe[k] = a.encoded ? a.enc_dir[(size_t)ray * kDirIn + k] : dir_feature(k, d3);
 
-  const BlkStore16 bst(lane, half);
+  const ST bst(lane, half);
   if constexpr (store) {
-    const __amdgpu_buffer_rsrc_t act_in_rs = blk_rsrc(a.act_in + (size_t)blk * kInF * kBlk);
+    const __amdgpu_buffer_rsrc_t act_in_rs = blk_rsrc_t(reinterpret_cast<AE*>(a.act_in) + (size_t)blk * kInF * kBlk);
 #pragma unroll
     for (int t = 0; t < 6; ++t)
 #pragma unroll
@@ -181,37 +184,37 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
   float bin[16][4];
   const size_t layer_stride = (size_t)nblk * kWidth * kBlk;
   const float* biases = bias_lds;
-  float* act_h_blk = a.act_h + (size_t)blk * kWidth * kBlk;
+  AE* act_h_blk = reinterpret_cast<AE*>(a.act_h) + (size_t)blk * kWidth * kBlk;
 
   // ---- trunk: layer l writes acc(l odd ? B : A) ------------------------------------------
-  FwdEpi16<store, false, 16> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
+  FwdEpi16<store, false, 16, ST> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
   ea.begin(biases, act_h_blk, mask16_ptr(a.masks, blk, 0, half, lane));
-  mlp_layer16<0, 3, 16>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane);
+  layer16<P, 0, 3, 16>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane);
   ea.tile01();
   for (int l = 1; l < kDepth - 1; l += 2) {
     eb.begin(biases + l * 256, act_h_blk + l * layer_stride, mask16_ptr(a.masks, blk, l, half, lane));
-    mlp_layer16<8, 0, 16>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea);
+    layer16<P, 8, 0, 16>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea);
     eb.tile01();
     ea.begin(biases + (l + 1) * 256, act_h_blk + (l + 1) * layer_stride, mask16_ptr(a.masks, blk, l + 1, half, lane));
-    if (l + 1 == kSkip) mlp_layer16<8, 3, 16>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, eb);
-    else mlp_layer16<8, 0, 16>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, eb);
+    if (l + 1 == kSkip) layer16<P, 8, 3, 16>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, eb);
+    else layer16<P, 8, 0, 16>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, eb);
     ea.tile01();
   }
   static_assert(kDepth == 8 && kSkip % 2 == 0, "trunk pairing assumes 8 layers and an even skip layer");
-  FwdEpi16<store, true, 16> e7(accB, bin, bst, lane);  // + density head (layer 8): z_s = w8 . h7 + b8
+  FwdEpi16<store, true, 16, ST> e7(accB, bin, bst, lane);  // + density head (layer 8): z_s = w8 . h7 + b8
   e7.begin(biases + 7 * 256, act_h_blk + 7 * layer_stride, mask16_ptr(a.masks, blk, 7, half, lane),
            bias_lds + 8 * 256);
-  mlp_layer16<8, 0, 16>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea);
+  layer16<P, 8, 0, 16>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea);
   e7.tile01();
 
   // ---- view layer 9: relu(W9[:, :256] h7 + dirbias); h7 tiles 2..15 finish in its shadow -------
-  mlp_layer16<8, 0, 8>(bin, ipe_lds, accA, lds, cur, wsrc, true, tid, lane, e7);
+  layer16<P, 8, 0, 8>(bin, ipe_lds, accA, lds, cur, wsrc, true, tid, lane, e7);
   float zs = e7.zs;
   zs += __shfl_xor(zs, 16, 64);
   zs += __shfl_xor(zs, 32, 64);
   zs += tail[kFwdTailBias + 8 * 256];
-  FwdEpi16<store, false, 8> e9(accA, bin, bst, lane);
-  e9.begin(dirb, a.act_h9 + (size_t)blk * kWidthCond * kBlk, mask16_ptr(a.masks, blk, 8, half, lane));
+  FwdEpi16<store, false, 8, ST> e9(accA, bin, bst, lane);
+  e9.begin(dirb, reinterpret_cast<AE*>(a.act_h9) + (size_t)blk * kWidthCond * kBlk, mask16_ptr(a.masks, blk, 8, half, lane));
 #pragma unroll
   for (int t = 0; t < 8; ++t) e9(t);
 
@@ -243,8 +246,13 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
 hipError_t launch_mlp_fwd16(const FwdArgs& a, hipStream_t st) {
   const int nblk = a.M / kBlk;
   const dim3 grid((nblk + 3) / 4), block(kMlp16Threads);
-  if (a.no_store) hipLaunchKernelGGL(k_mlp_fwd16<false>, grid, block, 0, st, a);
-  else hipLaunchKernelGGL(k_mlp_fwd16<true>, grid, block, 0, st, a);
+  if (a.split == 2) {
+    if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd16<2, false>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((k_mlp_fwd16<2, true>), grid, block, 0, st, a);
+  } else {
+    if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd16<0, false>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((k_mlp_fwd16<0, true>), grid, block, 0, st, a);
+  }
   return hipGetLastError();
 }
 

@@ -253,7 +253,11 @@ __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const fl
         }
       }
 #ifndef NOF_DIAG_NO_DMA
+#ifdef NOF_H16_DMA_SPREAD  // DMA steps in every other group
+      if (dma && (q & 1) == 0 && q / 2 < 4) slice16_dma_step(wsrc + 2 * kSliceFloats, lds + nxt2 * kSliceFloats, tid, q / 2);
+#else
       if (dma && q < 4) slice16_dma_step(wsrc + 2 * kSliceFloats, lds + nxt2 * kSliceFloats, tid, q);
+#endif
 #endif
       __builtin_amdgcn_sched_barrier(0);
       const bool first = t == 0;

@@ -488,7 +488,10 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_x3(const WgProblem* _
 // (global_load_lds_dwordx4, 1 KB contiguous per wave-instruction), NS - 2 blocks in flight behind a
 // counted vmcnt, and ds_read_b128 fragment reads (conflict-free through the blkh_off chunk XOR).
 // Same 2 x kX3WC wave grid and item schedule as k_wgrad_x3; MFMA time is ~1/4 of the stream time.
-constexpr int kWhStages = 4;
+#ifndef NOF_WH_STAGES
+#define NOF_WH_STAGES 4
+#endif
+constexpr int kWhStages = NOF_WH_STAGES;
 constexpr int kWhStageHalves = 16 * 32 * kBlk;             // up to 16 tiles (8 A + 8 B) of 2 KB
 constexpr int kWhLds = kWhStages * kWhStageHalves * 2;      // bytes: 128 KB
 

@@ -270,55 +270,58 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M) {
   p = prob(delta9x_.p, nof::kD9F, 128, 1, L.act_h9.p, 128, 0, 4);
   os.push_back({p, 1, 3, 0, 128, Wg(10), in_[10], 0, Bg(10)});
 
-  // cost per k-block (wgrad.hip): MFMA time of the busiest SIMD vs staging bytes (4 KB per 32-row
-  // operand block).  fp32: 2 x 4 waves of RB x CB tiles, ~16 KB per MFMA round keeps a CU under its
-  // HBM share.  split: 2 x C waves (C/2 per SIMD) of RB x CB tiles, six bf16 MFMAs per product — a
-  // 32-row block of loads costs about one tile's MFMAs at the CU's HBM share.
+  // cost per k-block, calibrated against per-item timings (NOF_DIAG_WG_TIME builds,
+  // tools/diag_item_time.py).  fp32 (k_wgrad, MFMA-bound): wgrad_block_cost.  f16x2 (k_wgrad_h, an
+  // HBM stream): the bytes, 10 (ntr + ntc) — 1.57 / 1.11 / 1.28 / 0.49 us per block measured for the
+  // 16 / 11 / 13 / 5-tile problems — and the one-column (4,1) problem 0.60 us (two active waves and
+  // the bias sums on them: +12).  split (k_wgrad_x3): MFMA rounds of 2 x C waves vs the loads.
   std::vector<int64_t> cost(P.size());
-  int64_t total = 0;
   for (size_t i = 0; i < P.size(); ++i) {
-    if (precision_ != NOF_PRECISION_F32) {
+    if (precision_ == NOF_PRECISION_F16X2) {
+      cost[i] = 10 * (P[i].ntr + P[i].ntc) + (P[i].ntc == 1 ? 12 : 0);
+    } else if (precision_ != NOF_PRECISION_F32) {
       const int WC = nof::wgrad_x3_grid_cols();  // C/2 waves per SIMD
       const int RB = (P[i].ntr + 1) / 2, CB = (P[i].ntc + WC - 1) / WC;
-      const int nprod = precision_ == NOF_PRECISION_F16X2 ? 1 : 6;  // k_wgrad_h: one f16 MFMA per product
-      cost[i] = std::max(RB * CB * WC * nprod / 12, P[i].ntr + P[i].ntc);
+      cost[i] = std::max(RB * CB * WC / 2, P[i].ntr + P[i].ntc);
     } else {
-      int c2 = 0;
-      P[i].shape = nof::wgrad_shape(P[i].ntr, P[i].ntc, &c2);
-      cost[i] = std::max(c2, (P[i].ntr + P[i].ntc + 1) / 2);
+      cost[i] = nof::wgrad_block_cost(P[i].ntr, P[i].ntc, &P[i].shape);
     }
-    total += cost[i] * nblk;
   }
+  // Workgroup w takes the problem-major sequence of (problem, k-block) between the cumulative-cost
+  // marks w * total / G and (w + 1) * total / G, each rounded to the nearest block: no workgroup is
+  // off by more than one block and no rounding accumulates onto the last one (the greedy fill this
+  // replaces closed every workgroup short and left the sum of the shortfalls to the last: measured
+  // workgroup ends 229-324 us for a 253-us mean).
+  std::vector<int64_t> cum(P.size() + 1, 0);
+  for (size_t i = 0; i < P.size(); ++i) cum[i + 1] = cum[i] + cost[i] * nblk;
+  const int64_t total = cum.back();
   const int G_wg = num_cu_;
-  const int64_t per = (total + G_wg - 1) / G_wg;
+  auto mark = [&](int w) {  // global block index of the cut before workgroup w
+    if (w >= G_wg) return (int64_t)P.size() * nblk;
+    const double x = (double)total * w / G_wg;
+    size_t pi = 0;
+    while (pi + 1 < P.size() && (double)cum[pi + 1] <= x) ++pi;
+    const int64_t kb = std::min<int64_t>(nblk, std::llround((x - (double)cum[pi]) / (double)cost[pi]));
+    return (int64_t)pi * nblk + kb;
+  };
   std::vector<nof::WgItem> items;
   std::vector<int> item_wg;
-  std::vector<int> first_item(P.size()), nitems(P.size());
-  int wg = 0;
-  int64_t used = 0;
-  for (size_t pi = 0; pi < P.size(); ++pi) {
-    first_item[pi] = (int)items.size();
-    int kb = 0;
-    while (kb < nblk) {
-      int64_t take;
-      if (wg == G_wg - 1) {
-        take = nblk - kb;
-      } else {
-        take = std::min<int64_t>(nblk - kb, (per - used) / cost[pi]);
-        if (take == 0) {
-          if (used > 0) { ++wg; used = 0; continue; }  // finish this workgroup instead of a 1-block sliver
-          take = 1;
-        }
-      }
+  std::vector<int> first_item(P.size(), -1), nitems(P.size(), 0);
+  for (int w = 0; w < G_wg; ++w) {
+    int64_t g0 = mark(w);
+    const int64_t g1 = std::max(g0, mark(w + 1));
+    while (g0 < g1) {  // split the workgroup's range at problem boundaries
+      const int pi = (int)(g0 / nblk);
+      const int kb0 = (int)(g0 - (int64_t)pi * nblk);
+      const int kb1 = (int)std::min<int64_t>(nblk, g1 - (int64_t)pi * nblk);
       nof::WgItem itm;
-      itm.prob = (int)pi; itm.kb0 = kb; itm.kb1 = kb + (int)take; itm.slab = (int)items.size();
+      itm.prob = pi; itm.kb0 = kb0; itm.kb1 = kb1; itm.slab = (int)items.size();
+      if (first_item[pi] < 0) first_item[pi] = (int)items.size();
+      nitems[pi]++;
       items.push_back(itm);
-      item_wg.push_back(wg);
-      used += take * cost[pi];
-      kb += (int)take;
-      if (used >= per && wg < G_wg - 1) { ++wg; used = 0; }
+      item_wg.push_back(w);
+      g0 = (int64_t)pi * nblk + kb1;
     }
-    nitems[pi] = (int)items.size() - first_item[pi];
   }
   const int nwg = std::min(G_wg, item_wg.empty() ? 0 : item_wg.back() + 1);
   std::vector<int> item_ptr(nwg + 1, 0);

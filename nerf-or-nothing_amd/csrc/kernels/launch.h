@@ -88,6 +88,9 @@ hipError_t launch_wgrad(const WgProblem* probs, const WgItem* items, const int* 
 // fp32 k_wgrad: the cheapest wave-grid shape for an ntr x ntc tile problem; *cost2 = MFMA tiles of
 // its busiest SIMD per 16 k-steps (2 per 32x32 tile-k-block at two waves per SIMD)
 int wgrad_shape(int ntr, int ntc, int* cost2);
+// fp32 k_wgrad: calibrated time of one k-block of an ntr x ntc tile problem (1600 = an (8,8) block);
+// *shape = the wave-grid shape it runs with
+int wgrad_block_cost(int ntr, int ntc, int* shape);
 int wgrad_x3_grid_cols();  // columns of k_wgrad_x3's 2 x C wave grid (schedule cost model)
 // split-precision weight gradients: precision 1 (bf16x3) or 2 (f16x2)
 hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,

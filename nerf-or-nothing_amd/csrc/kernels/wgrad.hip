@@ -187,15 +187,50 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
   __syncthreads();  // LDS ring reused by the next item
 }
 
+#ifdef NOF_DIAG_WG_TIME  // per-workgroup wall-clock start/end of the last k_wgrad / k_wgrad_h launch
+__device__ unsigned long long g_wg_times[2][1024][2];
+#define NOF_WG_T0(k) const unsigned long long wg_t0_ = wall_clock64();
+#define NOF_WG_T1(k)                                                                   \
+  __syncthreads();                                                                     \
+  if (threadIdx.x == 0 && blockIdx.x < 1024) {                                         \
+    g_wg_times[k][blockIdx.x][0] = wg_t0_;                                             \
+    g_wg_times[k][blockIdx.x][1] = wall_clock64();                                     \
+  }
+__device__ unsigned long long g_item_times[2][4096][4];  // t0, t1, problem, k-blocks
+#define NOF_IT_T0(k) const unsigned long long it_t0_ = wall_clock64();
+#define NOF_IT_T1(k)                                                                 \
+  if (threadIdx.x == 0 && it < 4096) {                                               \
+    g_item_times[k][it][0] = it_t0_;                                                 \
+    g_item_times[k][it][1] = wall_clock64();                                         \
+    g_item_times[k][it][2] = item.prob | (blockIdx.x << 16);                         \
+    g_item_times[k][it][3] = item.kb1 - item.kb0;                                    \
+  }
+extern "C" int nof_diag_item_times(unsigned long long* host, int kernel) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_item_times), sizeof(unsigned long long) * 16384,
+                                  sizeof(unsigned long long) * 16384 * kernel, hipMemcpyDeviceToHost);
+}
+extern "C" int nof_diag_wg_times(unsigned long long* host, int kernel) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wg_times), sizeof(unsigned long long) * 2048,
+                                  sizeof(unsigned long long) * 2048 * kernel, hipMemcpyDeviceToHost);
+}
+#else
+#define NOF_WG_T0(k)
+#define NOF_WG_T1(k)
+#define NOF_IT_T0(k)
+#define NOF_IT_T1(k)
+#endif
+
 __global__ __launch_bounds__(kWgThreads, 1) void k_wgrad(const WgProblem* __restrict__ probs,
                                                          const WgItem* __restrict__ items,
                                                          const int* __restrict__ item_ptr,
                                                          const int64_t* __restrict__ slab_off, float* slabs,
                                                          float* bias_slabs) {
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [2 buffers][A | B] x kWgHalf
+  NOF_WG_T0(0)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int it0 = item_ptr[blockIdx.x], it1 = item_ptr[blockIdx.x + 1];
   for (int it = it0; it < it1; ++it) {
+    NOF_IT_T0(0)
     const WgItem item = items[it];
     const WgProblem P = probs[item.prob];
     switch (P.shape) {  // kWgShapes
@@ -208,7 +243,9 @@ __global__ __launch_bounds__(kWgThreads, 1) void k_wgrad(const WgProblem* __rest
       default: NOF_WG_CASE(5)
 #undef NOF_WG_CASE
     }
+    NOF_IT_T1(0)
   }
+  NOF_WG_T1(0)
 }
 
 // ---- split mode (mlp_common.h): bf16x3 operands, six bf16 MFMAs per 32x32x16 product -----------
@@ -607,11 +644,13 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_h(const WgProblem* __
                                                              const int64_t* __restrict__ slab_off, float* slabs,
                                                              float* bias_slabs) {
   extern __shared__ __attribute__((aligned(16))) _Float16 ldsh[];
+  NOF_WG_T0(1)
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int it0 = item_ptr[blockIdx.x], it1 = item_ptr[blockIdx.x + 1];
   static_assert(kX3WC == 4, "k_wgrad_h instantiates the 2 x 4 wave grid's shapes");
   for (int it = it0; it < it1; ++it) {
+    NOF_IT_T0(1)
     const WgItem item = items[it];
     const WgProblem P = probs[item.prob];
     switch (((P.ntr + 1) >> 1) * 10 + (P.ntc + kX3WC - 1) / kX3WC) {
@@ -621,7 +660,9 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_h(const WgProblem* __
       case 41: wg_item_h<4, 1>(item, P, ldsh, tid, wave, slabs, bias_slabs, slab_off); break;
       default: wg_item_h<4, 2>(item, P, ldsh, tid, wave, slabs, bias_slabs, slab_off); break;
     }
+    NOF_IT_T1(1)
   }
+  NOF_WG_T1(1)
 }
 
 int wgrad_x3_grid_cols() { return kX3WC; }
@@ -644,6 +685,18 @@ int wgrad_shape(int ntr, int ntc, int* cost2) {
   }
   if (cost2) *cost2 = best_cost;
   return best;
+}
+
+// Calibrated k_wgrad cost of one k-block (per-item timings of NOF_DIAG_WG_TIME builds,
+// tools/diag_item_time.py: 7.82 / 3.08 / 4.99 / 1.00 us per block for the (8,8) / (8,3) / (5,8) /
+// (4,1),(1,4) tile problems): the busiest SIMD's MFMA tiles, 2-5 % dearer per tile for the narrow
+// shapes (more fragment reads per MFMA), or the staging latency that bounds the 1-tile-wide problems.
+int wgrad_block_cost(int ntr, int ntc, int* shape) {
+  int c2 = 0;
+  *shape = wgrad_shape(ntr, ntc, &c2);
+  const int tiles = kWgShapes[*shape].rb * kWgShapes[*shape].cb;
+  const int f = tiles >= 8 ? 100 : (tiles >= 5 ? 102 : 105);
+  return std::max(c2 * f, 35 * (ntr + ntc + 1));
 }
 
 template <int P>

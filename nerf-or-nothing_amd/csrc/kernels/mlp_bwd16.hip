@@ -15,6 +15,24 @@
 
 namespace nof {
 
+#ifdef NOF_DIAG_WG_TIME  // per-workgroup wall-clock start/end of the last launch
+__device__ unsigned long long g_bwd_times[4096][2];
+extern "C" int nof_diag_bwd_times(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bwd_times), sizeof(g_bwd_times), 0, hipMemcpyDeviceToHost);
+}
+#define NOF_MT0 const unsigned long long mt0_ = wall_clock64();
+#define NOF_MT1                                                                         \
+  __syncthreads();                                                                      \
+  if (threadIdx.x == 0 && blockIdx.x < 4096) {                                          \
+    g_bwd_times[blockIdx.x][0] = mt0_;                                                \
+    g_bwd_times[blockIdx.x][1] = wall_clock64();                                      \
+  }
+#else
+#define NOF_MT0
+#define NOF_MT1
+#endif
+
+
 // delta = mask ? acc (+ w8 * dz_s) : 0 -> B operand + delta block, one tile per call inside the
 // next layer's MFMA stream; w8 values loaded one tile ahead.
 template <bool kDensity, class ST>
@@ -68,6 +86,7 @@ template <int P>
 __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
   typedef typename Store16<P>::T ST;
   typedef typename Store16<P>::E AE;
+  NOF_MT0
   __shared__ __attribute__((aligned(16))) float lds[kRing16Floats + 256];
   float* w8_lds = lds + kRing16Floats;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
@@ -152,6 +171,7 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
   // delta0: nothing left to hide it under
 #pragma unroll
   for (int t = 2; t < 16; ++t) eb(t);
+  NOF_MT1
 }
 
 hipError_t launch_mlp_bwd16(const BwdArgs& a, hipStream_t st) {

@@ -17,6 +17,24 @@
 
 namespace nof {
 
+#ifdef NOF_DIAG_WG_TIME  // per-workgroup wall-clock start/end of the last launch
+__device__ unsigned long long g_fwd_times[4096][2];
+extern "C" int nof_diag_fwd_times(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd_times), sizeof(g_fwd_times), 0, hipMemcpyDeviceToHost);
+}
+#define NOF_MT0 const unsigned long long mt0_ = wall_clock64();
+#define NOF_MT1                                                                         \
+  __syncthreads();                                                                      \
+  if (threadIdx.x == 0 && blockIdx.x < 4096) {                                          \
+    g_fwd_times[blockIdx.x][0] = mt0_;                                                \
+    g_fwd_times[blockIdx.x][1] = wall_clock64();                                      \
+  }
+#else
+#define NOF_MT0
+#define NOF_MT1
+#endif
+
+
 // bias + ReLU epilogue of one accumulator tile -> next layer's B operand, act block, mask bits;
 // NT tiles per layer, run in tile order (the mask words are shift-accumulated).  Biases (and w8)
 // come from the workgroup's LDS copy, loaded one tile ahead.  kDensity folds the density head
@@ -90,6 +108,7 @@ template <int P, bool store>  // store: side outputs for the backward pass (off 
 __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
   typedef typename Store16<P>::T ST;
   typedef typename Store16<P>::E AE;
+  NOF_MT0
   constexpr int kRing = kRing16Floats;
   constexpr int kBiasLds = 8 * 256 + 256;
   __shared__ __attribute__((aligned(16))) float lds[kRing + 8 * kIpe16Floats + 8 * 128 + kBiasLds];
@@ -241,6 +260,7 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
     zh[0] = zs; zh[1] = zc[0]; zh[2] = zc[1]; zh[3] = zc[2];
     if constexpr (store) reinterpret_cast<f32x4*>(a.zhead)[m] = zh;
   }
+  NOF_MT1
 }
 
 hipError_t launch_mlp_fwd16(const FwdArgs& a, hipStream_t st) {

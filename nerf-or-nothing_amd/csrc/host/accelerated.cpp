@@ -274,7 +274,9 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M) {
   // tools/diag_item_time.py).  fp32 (k_wgrad, MFMA-bound): wgrad_block_cost.  f16x2 (k_wgrad_h, an
   // HBM stream): the bytes, 10 (ntr + ntc) — 1.57 / 1.11 / 1.28 / 0.49 us per block measured for the
   // 16 / 11 / 13 / 5-tile problems — and the one-column (4,1) problem 0.60 us (two active waves and
-  // the bias sums on them: +12).  split (k_wgrad_x3): MFMA rounds of 2 x C waves vs the loads.
+  // the bias sums on them: +12).  split (k_wgrad_x3): 10 RB CB (every wave's MFMA tiles, clamped
+  // duplicates included) + 5 (ntr + ntc) (loads and splits) — 5.01 / 3.00 / 3.87 / 1.47 / 1.15 us
+  // measured for the (8,8) / (8,3) / (5,8) / (4,1) / (1,4) problems = 160 / 96 / 124 / 47 / 37.
   std::vector<int64_t> cost(P.size());
   for (size_t i = 0; i < P.size(); ++i) {
     if (precision_ == NOF_PRECISION_F16X2) {
@@ -282,7 +284,7 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M) {
     } else if (precision_ != NOF_PRECISION_F32) {
       const int WC = nof::wgrad_x3_grid_cols();  // C/2 waves per SIMD
       const int RB = (P[i].ntr + 1) / 2, CB = (P[i].ntc + WC - 1) / WC;
-      cost[i] = std::max(RB * CB * WC / 2, P[i].ntr + P[i].ntc);
+      cost[i] = 10 * RB * CB + 5 * (P[i].ntr + P[i].ntc);
     } else {
       cost[i] = nof::wgrad_block_cost(P[i].ntr, P[i].ntc, &P[i].shape);
     }

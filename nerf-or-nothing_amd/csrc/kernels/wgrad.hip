@@ -492,8 +492,10 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_x3(const WgProblem* _
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  NOF_WG_T0(1)
   const int it0 = item_ptr[blockIdx.x], it1 = item_ptr[blockIdx.x + 1];
   for (int it = it0; it < it1; ++it) {
+    NOF_IT_T0(1)
     const WgItem item = items[it];
     const WgProblem P = probs[item.prob];
     const int RB = (P.ntr + 1) >> 1, CB = (P.ntc + kX3WC - 1) / kX3WC;  // 2 x kX3WC wave grid
@@ -515,7 +517,9 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_x3(const WgProblem* _
         default: wg_item_x3<PM, 4, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
       }
     }
+    NOF_IT_T1(1)
   }
+  NOF_WG_T1(1)
 }
 
 // ---- f16x2 mode: fp16 operand blocks (common.h blkh_off), one 32x32x16 f16 MFMA per product -------

@@ -20,7 +20,7 @@ for _ in range(3):
 torch.cuda.synchronize()
 lib = nof.lib()
 ib = (C.c_ulonglong * 16384)()
-assert lib.nof_diag_item_times(ib, 1 if prec == 2 else 0) == 0
+assert lib.nof_diag_item_times(ib, 0 if prec == 0 else 1) == 0
 it = np.frombuffer(ib, dtype=np.uint64).reshape(4096, 4).astype(np.int64)
 it = it[it[:, 1] > 0]
 prob, wg = it[:, 2] & 0xFFFF, it[:, 2] >> 16

@@ -18,7 +18,7 @@ for _ in range(3):
 torch.cuda.synchronize()
 lib = nof.lib()
 buf = (C.c_ulonglong * 2048)()
-assert lib.nof_diag_wg_times(buf, 1 if prec == 2 else 0) == 0
+assert lib.nof_diag_wg_times(buf, 0 if prec == 0 else 1) == 0
 t = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 2).astype(np.int64)
 t = t[t[:, 1] > 0]
 t0 = t[:, 0].min()

@@ -128,10 +128,13 @@ struct NoEpi16 {
 // input tiles x OT/2 row-tile pairs = OT MFMA groups of 8 (two accumulators interleaved: the
 // 16x16x4 dependent latency is 40 cycles against a 32-cycle issue), each group's two A operands
 // read one group ahead; the 4 DMA steps of slice t + 2 ride groups 0..3; one barrier per slice.
+// cinit (LDS, + 4g; null: zero) is the accumulators' initial value — the layer's bias enters as
+// the C operand of each tile's first MFMA instead of as a VALU add in the epilogue (the fp32
+// MFMA and the VALU share the issue port: every epilogue instruction is MFMA time).
 template <int NT_B, int NT_I, int OT, class Epi>
 __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16],
                                             float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
-                                            int lane, Epi& epi) {
+                                            int lane, Epi& epi, const float* cinit) {
   static_assert(OT % 2 == 0 && OT <= 16, "row tiles come in pairs");
   constexpr int NG = OT;  // groups per slice: 2 input tiles x OT / 2 pairs
 #ifndef NOF_EPI16_G1
@@ -153,6 +156,9 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
       return *reinterpret_cast<const f32x4*>(W + (2 * p + which) * 16 * 32 + (((4 * tt + g) ^ swz) << 2));
     };
     f32x4 a0 = aread(0, 0), a1 = aread(0, 1);
+    auto cread = [&](int p, int which) { return *reinterpret_cast<const f32x4*>(cinit + 16 * (2 * p + which)); };
+    f32x4 c0 = {}, c1 = {};  // initial accumulators of the group's pair (slice 0, first input tile)
+    if (t == 0 && cinit) { c0 = cread(0, 0); c1 = cread(0, 1); }
 #pragma unroll
     for (int q = 0; q < NG; ++q) {
       const int tt = q / (OT / 2), p = q % (OT / 2);
@@ -164,8 +170,8 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
         const int ti = (t >= NT_B) ? 2 * (t - NT_B) + tt : 0;
         b4 = *reinterpret_cast<const f32x4*>(ipe_lds + (ti * 64 + lane) * 4);
       }
-      asm volatile("" ::"v"(a0), "v"(a1));  // this group's reads land here, before the next ones issue
-      f32x4 n0 = a0, n1 = a1;
+      asm volatile("" ::"v"(a0), "v"(a1), "v"(c0), "v"(c1));  // this group's reads land here, before the next ones issue
+      f32x4 n0 = a0, n1 = a1, m0 = c0, m1 = c1;
 #ifdef NOF_DIAG_NO_AREAD
       if (q + 1 < NG && t == 0) {
 #else
@@ -174,6 +180,7 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
         n0 = aread(q + 1, 0);
         n1 = aread(q + 1, 1);
       }
+      if (t == 0 && cinit && q + 1 < OT / 2) { m0 = cread(q + 1, 0); m1 = cread(q + 1, 1); }
 #ifndef NOF_DIAG_NO_DMA
       if (dma && q < 4) slice16_dma_step(wsrc + 2 * kSliceFloats, lds + nxt2 * kSliceFloats, tid, q);
 #endif
@@ -183,8 +190,8 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
       const bool first = t == 0 && tt == 0;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        acc[2 * p] = mfma16(a0[r], b4[r], (first && r == 0) ? f32x4{} : acc[2 * p]);
-        acc[2 * p + 1] = mfma16(a1[r], b4[r], (first && r == 0) ? f32x4{} : acc[2 * p + 1]);
+        acc[2 * p] = mfma16(a0[r], b4[r], (first && r == 0) ? c0 : acc[2 * p]);
+        acc[2 * p + 1] = mfma16(a1[r], b4[r], (first && r == 0) ? c1 : acc[2 * p + 1]);
       }
       if (t + 1 < NT_B && q == kEpiGroup1) epi(2 * t + 2);
       if (t + 1 < NT_B && q == kEpiGroup2) epi(2 * t + 3);
@@ -193,6 +200,8 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
 #endif
       a0 = n0;
       a1 = n1;
+      c0 = m0;
+      c1 = m1;
     }
     // slice t + 1 (issued during slice t - 1) must have landed; everything issued during this
     // slice (the DMA of t + 2, both epilogue parts' stores) may stay in flight
@@ -213,7 +222,7 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
 template <int NT_B, int NT_I, int OT, class Epi>
 __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16],
                                              float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
-                                             int lane, Epi& epi) {
+                                             int lane, Epi& epi, const float* cinit) {
   typedef SplitMode<2> SM;
   static_assert(OT % 2 == 0 && OT <= 16, "row tiles come in pairs");
   constexpr int NG = OT / 2;  // groups per slice
@@ -241,10 +250,15 @@ __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const fl
     Frag<2> a0, a1;
 #pragma unroll
     for (int p = 0; p < 2; ++p) { a0.p[p] = W[p * 64]; a1.p[p] = W[(2 + p) * 64]; }
+    auto cread = [&](int rt) { return *reinterpret_cast<const f32x4*>(cinit + 16 * rt); };
+    f32x4 c0 = {}, c1 = {};  // initial accumulators of the group's pair (slice 0): bias or 0
+    if (t == 0 && cinit) { c0 = cread(0); c1 = cread(1); }
 #pragma unroll
     for (int q = 0; q < NG; ++q) {
-      asm volatile("" ::"v"(a0.p[0]), "v"(a0.p[1]), "v"(a1.p[0]), "v"(a1.p[1]));  // this group's reads land here
+      asm volatile("" ::"v"(a0.p[0]), "v"(a0.p[1]), "v"(a1.p[0]), "v"(a1.p[1]), "v"(c0), "v"(c1));
       Frag<2> n0 = a0, n1 = a1;
+      f32x4 m0 = c0, m1 = c1;
+      if (t == 0 && cinit && q + 1 < NG) { m0 = cread(2 * q + 2); m1 = cread(2 * q + 3); }
       if (q + 1 < NG) {
 #pragma unroll
         for (int p = 0; p < 2; ++p) {
@@ -263,14 +277,16 @@ __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const fl
       const bool first = t == 0;
 #pragma unroll
       for (int pp = 0; pp < SM::NPROD; ++pp) {
-        acc[2 * q] = SM::mfma16(a0.p[SM::pa(pp)], b.p[SM::pb(pp)], (first && pp == 0) ? f32x4{} : acc[2 * q]);
-        acc[2 * q + 1] = SM::mfma16(a1.p[SM::pa(pp)], b.p[SM::pb(pp)], (first && pp == 0) ? f32x4{} : acc[2 * q + 1]);
+        acc[2 * q] = SM::mfma16(a0.p[SM::pa(pp)], b.p[SM::pb(pp)], (first && pp == 0) ? c0 : acc[2 * q]);
+        acc[2 * q + 1] = SM::mfma16(a1.p[SM::pa(pp)], b.p[SM::pb(pp)], (first && pp == 0) ? c1 : acc[2 * q + 1]);
       }
       if (t + 1 < NT_B && q == kE1) epi(2 * t + 2);
       if (t + 1 < NT_B && q == kE2) epi(2 * t + 3);
       __builtin_amdgcn_sched_barrier(0);
       a0 = n0;
       a1 = n1;
+      c0 = m0;
+      c1 = m1;
     }
     slice_barrier((dma ? 4 : 0) + (t + 1 < NT_B ? 2 * Epi::kVmPerPart : 0));
     cur = cur == 2 ? 0 : cur + 1;
@@ -282,15 +298,17 @@ __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const fl
 template <int P, int NT_B, int NT_I, int OT, class Epi>
 __device__ __forceinline__ void layer16(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16], float* lds,
                                         int& cur, const float*& wsrc, bool last_in_schedule, int tid, int lane,
-                                        Epi& epi) {
-  if constexpr (P == 2) mlp_layer16h<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi);
-  else mlp_layer16<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi);
+                                        Epi& epi, const float* cinit = nullptr) {
+  if constexpr (P == 2)
+    mlp_layer16h<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi, cinit);
+  else mlp_layer16<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi, cinit);
 }
 template <int P, int NT_B, int NT_I, int OT>
 __device__ __forceinline__ void layer16(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16], float* lds,
-                                        int& cur, const float*& wsrc, bool last_in_schedule, int tid, int lane) {
+                                        int& cur, const float*& wsrc, bool last_in_schedule, int tid, int lane,
+                                        const float* cinit = nullptr) {
   NoEpi16 none;
-  layer16<P, NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, none);
+  layer16<P, NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, none, cinit);
 }
 
 }  // namespace nof

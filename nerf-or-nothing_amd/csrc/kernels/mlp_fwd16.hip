@@ -35,9 +35,9 @@ extern "C" int nof_diag_fwd_times(unsigned long long* host) {
 #endif
 
 
-// bias + ReLU epilogue of one accumulator tile -> next layer's B operand, act block, mask bits;
-// NT tiles per layer, run in tile order (the mask words are shift-accumulated).  Biases (and w8)
-// come from the workgroup's LDS copy, loaded one tile ahead.  kDensity folds the density head
+// ReLU epilogue of one accumulator tile (the bias is already in it: the layer's first MFMAs take it
+// as C) -> next layer's B operand, act block, mask bits; NT tiles per layer, run in tile order (the
+// mask words are shift-accumulated).  w8 comes from the workgroup's LDS copy, loaded one tile ahead.  kDensity folds the density head
 // (z_s = w8 . h7) into layer 7's epilogue.  A tail wave clamped onto the last block recomputes
 // bit-identical values, so its duplicate stores are benign.
 template <bool store, bool kDensity, int NT, class ST>
@@ -51,23 +51,20 @@ struct FwdEpi16 {
   float (&bin)[16][4];
   const ST& bst;
   const int g;
-  const float* bias;  // LDS, + 4g
   const float* w8;    // LDS, + 4g
   __amdgpu_buffer_rsrc_t act_blk;
   uint2* mask_dst;
   uint32_t mw[2];
-  f32x4 bnext, wnext;
+  f32x4 wnext;
   float zs;
 
   __device__ __forceinline__ FwdEpi16(const f32x4 (&acc_)[16], float (&bin_)[16][4], const ST& bst_, int lane)
       : acc(acc_), bin(bin_), bst(bst_), g(lane >> 4) {}
   template <class E>
-  __device__ __forceinline__ void begin(const float* bias_, E* act_blk_, uint2* mask_dst_, const float* w8_ = nullptr) {
-    bias = bias_ + 4 * g;
+  __device__ __forceinline__ void begin(E* act_blk_, uint2* mask_dst_, const float* w8_ = nullptr) {
     act_blk = blk_rsrc_t(act_blk_);
     mask_dst = mask_dst_;
     mw[0] = mw[1] = 0u;
-    bnext = *reinterpret_cast<const f32x4*>(bias);
     if constexpr (kDensity) {
       w8 = w8_ + 4 * g;
       wnext = *reinterpret_cast<const f32x4*>(w8);
@@ -75,9 +72,7 @@ struct FwdEpi16 {
     }
   }
   __device__ __forceinline__ void operator()(int t) {
-    const f32x4 b4 = bnext;
     const bool more = t + 1 < NT;
-    if (more) bnext = *reinterpret_cast<const f32x4*>(bias + 16 * (t + 1));
     f32x4 w4;
     if constexpr (kDensity) {
       w4 = wnext;
@@ -85,7 +80,7 @@ struct FwdEpi16 {
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float z = acc[t][r] + b4[r];
+      const float z = acc[t][r];
       const float hv = z > 0.0f ? z : 0.0f;
       bin[t][r] = hv;
       mw[t >> 3] = (mw[t >> 3] << 1) | (hv > 0.0f ? 1u : 0u);
@@ -150,9 +145,13 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) ipe[t][r] = a.enc_pos[(size_t)m * kPosIn + feat16(t, g, r)];
   }
+  // view PE of the wave's ray: lane k < 27 evaluates feature k once, every lane reads the 27 values
+  // back as wave-uniform scalars (27 accurate sin/cos per lane otherwise, MFMA-idle prologue time)
+  const int kl = lane < kDirIn ? lane : 0;
+  const float pe_l = a.encoded ? a.enc_dir[(size_t)ray * kDirIn + kl] : dir_feature(kl, d3);
   float pe[kDirIn];
 #pragma unroll
-  for (int k = 0; k < kDirIn; ++k) pe[k] = a.encoded ? a.enc_dir[(size_t)ray * kDirIn + k] : dir_feature(k, d3);
+  for (int k = 0; k < kDirIn; ++k) pe[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pe_l), k));
 
   const ST bst(lane, half);
   if constexpr (store) {
@@ -207,33 +206,34 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
 
   // ---- trunk: layer l writes acc(l odd ? B : A) ------------------------------------------
   FwdEpi16<store, false, 16, ST> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
-  ea.begin(biases, act_h_blk, mask16_ptr(a.masks, blk, 0, half, lane));
-  layer16<P, 0, 3, 16>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane);
+  const float* bias_g = biases + 4 * g;  // the lane group's bias slot (the layers' initial accumulators)
+  ea.begin(act_h_blk, mask16_ptr(a.masks, blk, 0, half, lane));
+  layer16<P, 0, 3, 16>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, bias_g);
   ea.tile01();
   for (int l = 1; l < kDepth - 1; l += 2) {
-    eb.begin(biases + l * 256, act_h_blk + l * layer_stride, mask16_ptr(a.masks, blk, l, half, lane));
-    layer16<P, 8, 0, 16>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea);
+    eb.begin(act_h_blk + l * layer_stride, mask16_ptr(a.masks, blk, l, half, lane));
+    layer16<P, 8, 0, 16>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea, bias_g + l * 256);
     eb.tile01();
-    ea.begin(biases + (l + 1) * 256, act_h_blk + (l + 1) * layer_stride, mask16_ptr(a.masks, blk, l + 1, half, lane));
-    if (l + 1 == kSkip) layer16<P, 8, 3, 16>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, eb);
-    else layer16<P, 8, 0, 16>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, eb);
+    ea.begin(act_h_blk + (l + 1) * layer_stride, mask16_ptr(a.masks, blk, l + 1, half, lane));
+    if (l + 1 == kSkip)
+      layer16<P, 8, 3, 16>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, eb, bias_g + (l + 1) * 256);
+    else layer16<P, 8, 0, 16>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, eb, bias_g + (l + 1) * 256);
     ea.tile01();
   }
   static_assert(kDepth == 8 && kSkip % 2 == 0, "trunk pairing assumes 8 layers and an even skip layer");
   FwdEpi16<store, true, 16, ST> e7(accB, bin, bst, lane);  // + density head (layer 8): z_s = w8 . h7 + b8
-  e7.begin(biases + 7 * 256, act_h_blk + 7 * layer_stride, mask16_ptr(a.masks, blk, 7, half, lane),
-           bias_lds + 8 * 256);
-  layer16<P, 8, 0, 16>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea);
+  e7.begin(act_h_blk + 7 * layer_stride, mask16_ptr(a.masks, blk, 7, half, lane), bias_lds + 8 * 256);
+  layer16<P, 8, 0, 16>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea, bias_g + 7 * 256);
   e7.tile01();
 
   // ---- view layer 9: relu(W9[:, :256] h7 + dirbias); h7 tiles 2..15 finish in its shadow -------
-  layer16<P, 8, 0, 8>(bin, ipe_lds, accA, lds, cur, wsrc, true, tid, lane, e7);
+  layer16<P, 8, 0, 8>(bin, ipe_lds, accA, lds, cur, wsrc, true, tid, lane, e7, dirb + 4 * g);
   float zs = e7.zs;
   zs += __shfl_xor(zs, 16, 64);
   zs += __shfl_xor(zs, 32, 64);
   zs += tail[kFwdTailBias + 8 * 256];
   FwdEpi16<store, false, 8, ST> e9(accA, bin, bst, lane);
-  e9.begin(dirb, reinterpret_cast<AE*>(a.act_h9) + (size_t)blk * kWidthCond * kBlk, mask16_ptr(a.masks, blk, 8, half, lane));
+  e9.begin(reinterpret_cast<AE*>(a.act_h9) + (size_t)blk * kWidthCond * kBlk, mask16_ptr(a.masks, blk, 8, half, lane));
 #pragma unroll
   for (int t = 0; t < 8; ++t) e9(t);
 

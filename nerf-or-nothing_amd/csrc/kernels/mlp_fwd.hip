@@ -179,9 +179,12 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) ipe[tp][r] = a.enc_pos[(size_t)m * kPosIn + tile_feature(tp, r, h)];
   }
+  // view PE of the wave's ray: lane k < 27 evaluates feature k once (wave-uniform scalars after)
+  const int kl = lane < kDirIn ? lane : 0;
+  const float pe_l = a.encoded ? a.enc_dir[(size_t)ray * kDirIn + kl] : dir_feature(kl, d3);
   float pe[kDirIn];
 #pragma unroll
-  for (int k = 0; k < kDirIn; ++k) pe[k] = a.encoded ? a.enc_dir[(size_t)ray * kDirIn + k] : dir_feature(k, d3);
+  for (int k = 0; k < kDirIn; ++k) pe[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pe_l), k));
 
   constexpr bool kH = P == 2;  // f16x2: fp16 activation blocks (the weight-gradient operands)
   typedef typename ActOut<kH>::T AT;

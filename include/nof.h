@@ -312,6 +312,9 @@ nof_status nof_kernel_adam(int64_t n, float* params, const float* grads, float* 
 #define NOF_NUM_TIMERS 8
 /* timer ids: 0 pack, 1 sample, 2 mlp_fwd, 3 render_fwd, 4 render_bwd, 5 mlp_bwd, 6 wgrad, 7 wgrad_reduce */
 nof_status nof_mipnerf_enable_timing(nof_mipnerf* h, int32_t enable);
+/* only the timers whose bit is set in mask (bit i = timer id i); 0 disables.  Each timed launch is
+ * bracketed by two hipEventRecords on the stream, which cost the launch sequence a few us each */
+nof_status nof_mipnerf_enable_timing_mask(nof_mipnerf* h, uint32_t mask);
 /* synchronises; returns summed milliseconds and launch counts per timer id since the last read */
 nof_status nof_mipnerf_read_timing(nof_mipnerf* h, float* ms, int32_t* launches, int32_t cap);
 

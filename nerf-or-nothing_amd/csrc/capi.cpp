@@ -240,7 +240,10 @@ nof_status nof_image_metrics(const float* img0, const float* img1, int32_t width
   });
 }
 nof_status nof_mipnerf_enable_timing(nof_mipnerf* h, int32_t enable) {
-  return guard([&] { ARG(h); h->impl->timer.enable(enable != 0, h->impl->mlp->stream()); });
+  return guard([&] { ARG(h); h->impl->timer.enable(enable != 0 ? 0xFFu : 0u, h->impl->mlp->stream()); });
+}
+nof_status nof_mipnerf_enable_timing_mask(nof_mipnerf* h, uint32_t mask) {
+  return guard([&] { ARG(h); h->impl->timer.enable(mask, h->impl->mlp->stream()); });
 }
 nof_status nof_mipnerf_read_timing(nof_mipnerf* h, float* ms, int32_t* launches, int32_t cap) {
   return guard([&] { ARG(h && ms && launches); h->impl->timer.read(ms, launches, cap); });

@@ -15,8 +15,8 @@ using nof::kBlk;
 // ------------------------------------------------------------------------------------------------
 // KernelTimer
 // ------------------------------------------------------------------------------------------------
-void KernelTimer::enable(bool on, hipStream_t st) {
-  on_ = on;
+void KernelTimer::enable(uint32_t mask, hipStream_t st) {
+  mask_ = mask;
   st_ = st;
   used_ = 0;
   recs_.clear();
@@ -30,12 +30,12 @@ hipEvent_t KernelTimer::get() {
   return pool_[used_++];
 }
 void KernelTimer::begin(int id) {
-  if (!on_) return;
+  if (!((mask_ >> id) & 1u)) return;
   open_[id] = get();
   NOF_HIP(hipEventRecord(open_[id], st_));
 }
 void KernelTimer::end(int id) {
-  if (!on_ || !open_[id]) return;
+  if (!((mask_ >> id) & 1u) || !open_[id]) return;
   hipEvent_t b = get();
   NOF_HIP(hipEventRecord(b, st_));
   recs_.push_back({id, open_[id], b});

@@ -65,8 +65,8 @@ struct DevBuf {
 // Per-kernel-class hipEvent timing on one stream.
 class KernelTimer {
  public:
-  void enable(bool on, hipStream_t st);
-  bool on() const { return on_; }
+  void enable(uint32_t mask, hipStream_t st);  // bit i: timer id i
+  bool on() const { return mask_ != 0; }
   void begin(int id);
   void end(int id);
   void read(float* ms, int* launches, int cap);  // synchronises
@@ -74,7 +74,7 @@ class KernelTimer {
 
  private:
   hipEvent_t get();
-  bool on_ = false;
+  uint32_t mask_ = 0;
   hipStream_t st_ = nullptr;
   std::vector<hipEvent_t> pool_;
   size_t used_ = 0;

@@ -104,6 +104,7 @@ SIGNATURES = {
     "nof_checkpoint_save": [C.c_char_p, P, P],
     "nof_checkpoint_load": [C.c_char_p, P, P],
     "nof_mipnerf_enable_timing": [P, I32],
+    "nof_mipnerf_enable_timing_mask": [P, C.c_uint32],
     "nof_mipnerf_read_timing": [P, C.POINTER(F), C.POINTER(I32), I32],
     "nof_mlp_get_output": [P, P, P, I32, I32, I32, C.POINTER(U64), C.POINTER(U64)],
     "nof_mlp_get_gradient": [P, P, P, I32, C.POINTER(PP)],

@@ -257,8 +257,13 @@ class AcceleratedMipNeRF:
                     o[k].append(v)
         return [{k: np.concatenate(v) for k, v in o.items()} for o in outs]
 
-    def enable_timing(self, on: bool = True):
-        call("nof_mipnerf_enable_timing", self._h, int(on))
+    def enable_timing(self, on: bool = True, timers=None):
+        """hipEvent timing of every kernel class, or only of the named ones (L.TIMER_NAMES)."""
+        if timers is None:
+            call("nof_mipnerf_enable_timing", self._h, int(on))
+        else:
+            mask = sum(1 << L.TIMER_NAMES.index(t) for t in timers) if on else 0
+            call("nof_mipnerf_enable_timing_mask", self._h, C.c_uint32(mask))
 
     def read_timing(self) -> dict:
         ms = (C.c_float * L.NOF_NUM_TIMERS)()

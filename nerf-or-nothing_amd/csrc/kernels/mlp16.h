@@ -182,7 +182,17 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
       }
       if (t == 0 && cinit && q + 1 < OT / 2) { m0 = cread(q + 1, 0); m1 = cread(q + 1, 1); }
 #ifndef NOF_DIAG_NO_DMA
-      if (dma && q < 4) slice16_dma_step(wsrc + 2 * kSliceFloats, lds + nxt2 * kSliceFloats, tid, q);
+#ifndef NOF_DMA16_STRIDE
+#define NOF_DMA16_STRIDE 1
+#endif
+#ifndef NOF_DMA16_G0
+#define NOF_DMA16_G0 0
+#endif
+      // DMA step i in group kG0 + i * kDS (i < 4; groups 0..3 where the layer has too few groups)
+      constexpr bool kFit = NOF_DMA16_G0 + 3 * NOF_DMA16_STRIDE < NG;
+      constexpr int kG0 = kFit ? NOF_DMA16_G0 : 0, kDS = kFit ? NOF_DMA16_STRIDE : 1;
+      if (dma && q >= kG0 && (q - kG0) % kDS == 0 && (q - kG0) / kDS < 4)
+        slice16_dma_step(wsrc + 2 * kSliceFloats, lds + nxt2 * kSliceFloats, tid, (q - kG0) / kDS);
 #endif
 #ifndef NOF_NO_SCHED_BARRIER
       __builtin_amdgcn_sched_barrier(0);

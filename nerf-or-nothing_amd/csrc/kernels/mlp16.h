@@ -113,6 +113,15 @@ __device__ __forceinline__ uint2* mask16_ptr(uint32_t* masks, int blk, int slot,
 __device__ __forceinline__ bool mask16_bit(const uint2& m, int t, int r) {
   return ((t >> 3 ? m.y : m.x) >> (31 - ((t & 7) * 4 + r))) & 1u;
 }
+// v where the ReLU bit of (t, r) is set, else +0.0 (the same bits as mask16_bit ? v : 0.0f): the bit
+// sign-extended to a full word (v_bfe_i32) ANDed with v — two VALU ops instead of and/cmp/cndmask
+// (inline asm: the compiler folds the plain C form back into and/cmp/cndmask)
+__device__ __forceinline__ float mask16_apply(const uint2& m, int t, int r, float v) {
+  const uint32_t w = t >> 3 ? m.y : m.x;
+  uint32_t all;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(all) : "v"(w), "n"(31 - ((t & 7) * 4 + r)));
+  return __uint_as_float(__float_as_uint(v) & all);
+}
 
 // Epilogue hook of mlp_layer16: epi(tile) finishes one accumulator tile of the PREVIOUS layer
 // (4 registers) into `bin`; tiles 2t + 2 and 2t + 3 run during slice t (in MFMA groups 1 and

@@ -70,7 +70,7 @@ struct BwdEpi16 {
     for (int r = 0; r < 4; ++r) {
       float v = acc[t][r];
       if constexpr (kDensity) v += w4[r] * dzs;
-      v = mask16_bit(mk, t, r) ? v : 0.0f;
+      v = mask16_apply(mk, t, r, v);
       bin[t][r] = v;
       bst.store(dst_blk, t, r, v);
     }
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float v = (wa[r] * dzc[0] + wb[r] * dzc[1]) + wc[r] * dzc[2];
-        v = mask16_bit(mk, t, r) ? v : 0.0f;
+        v = mask16_apply(mk, t, r, v);
         bin[t][r] = v;
         bst.store(d9, t, r, v);
       }

@@ -20,8 +20,27 @@ __device__ unsigned long long g_bwd_times[4096][2];
 extern "C" int nof_diag_bwd_times(unsigned long long* host) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bwd_times), sizeof(g_bwd_times), 0, hipMemcpyDeviceToHost);
 }
-#define NOF_MT0 const unsigned long long mt0_ = wall_clock64();
+#ifdef NOF_DIAG_BAR_TIME
+__device__ unsigned long long g_bwd_bar[4096][8][3];  // per wave: vmcnt-wait, barrier, lifetime (cycles)
+extern "C" int nof_diag_bwd_bar(unsigned long long* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bwd_bar), sizeof(g_bwd_bar), 0, hipMemcpyDeviceToHost);
+}
+#define NOF_BT0                                                                          \
+  const unsigned long long btk0_ = __builtin_amdgcn_s_memtime();                          \
+  if ((threadIdx.x & 63) == 0) { bar_acc()[threadIdx.x >> 6][0] = 0; bar_acc()[threadIdx.x >> 6][1] = 0; }
+#define NOF_BT1                                                                          \
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096) {                                    \
+    g_bwd_bar[blockIdx.x][threadIdx.x >> 6][0] = bar_acc()[threadIdx.x >> 6][0];        \
+    g_bwd_bar[blockIdx.x][threadIdx.x >> 6][1] = bar_acc()[threadIdx.x >> 6][1];        \
+    g_bwd_bar[blockIdx.x][threadIdx.x >> 6][2] = __builtin_amdgcn_s_memtime() - btk0_;  \
+  }
+#else
+#define NOF_BT0
+#define NOF_BT1
+#endif
+#define NOF_MT0 const unsigned long long mt0_ = wall_clock64(); NOF_BT0
 #define NOF_MT1                                                                         \
+  NOF_BT1                                                                               \
   __syncthreads();                                                                      \
   if (threadIdx.x == 0 && blockIdx.x < 4096) {                                          \
     g_bwd_times[blockIdx.x][0] = mt0_;                                                \

@@ -78,7 +78,29 @@ struct NoEpi {
 // retires in issue order, so waiting down to <= n_after outstanding retires the DMA) may stay in
 // flight — __syncthreads() would wait for them too (or, with no wait of its own, leave the DMA
 // unretired).  lgkmcnt(0): this slice's ds_reads are done before the next DMA overwrites the slot.
+#ifdef NOF_DIAG_BAR_TIME  // per-wave cycles spent in the slice barriers' vmcnt wait and s_barrier
+__device__ __forceinline__ unsigned long long (&bar_acc())[16][2] {
+  static __shared__ unsigned long long acc[16][2];
+  return acc;
+}
+#endif
 __device__ __forceinline__ void slice_barrier(int n_after) {
+#ifdef NOF_DIAG_BAR_TIME
+  const unsigned long long bt0 = __builtin_amdgcn_s_memtime();
+  if (n_after >= 16) asm volatile("s_waitcnt vmcnt(16)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+  else if (n_after >= 12) asm volatile("s_waitcnt vmcnt(12)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+  else if (n_after >= 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+  else if (n_after >= 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+  const unsigned long long bt1 = __builtin_amdgcn_s_memtime();
+  asm volatile("s_barrier" ::: "memory");
+  const unsigned long long bt2 = __builtin_amdgcn_s_memtime();
+  if ((threadIdx.x & 63) == 0) {
+    bar_acc()[threadIdx.x >> 6][0] += bt1 - bt0;
+    bar_acc()[threadIdx.x >> 6][1] += bt2 - bt1;
+  }
+  return;
+#endif
 #if defined(NOF_DIAG_DMA_NOWAIT)
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #elif !defined(NOF_DIAG_NO_BARRIER)

@@ -46,15 +46,33 @@ __device__ __forceinline__ void slice16_dma(const float* __restrict__ src, float
   for (int i = 0; i < 4; ++i) slice16_dma_step(src, dst, tid, i);
 }
 
-// Weight ring: 3 slots, the DMA of slice t + 2 issued during slice t (a full slice of L2 latency
-// to land), so the end-of-slice barrier only waits for slice t + 1, issued a slice earlier; the
-// DMA and epilogue stores issued during slice t itself stay in flight (counted vmcnt).
-constexpr int kRing16Slots = 3;
-constexpr int kRing16Floats = kRing16Slots * kSliceFloats;
+// Weight ring, 3 slots (f16x2): the DMA of slice t + 2 issued during slice t (a full slice of L2
+// latency to land), so the end-of-slice barrier only waits for slice t + 1, issued a slice earlier;
+// the DMA and epilogue stores issued during slice t itself stay in flight (counted vmcnt).
+// fp32: 4 slots and ONE barrier per two slices (after odd global slices).  Slice t still DMAs
+// slice t + 2, now into the slot of t - 2, which every wave left before the barrier that ended
+// slice t - 1 or t - 2; the barrier after odd t retires the DMAs of t + 1 and t + 2.  Half the
+// barriers let the two waves of a SIMD drift by up to two slices before the leader waits (they
+// spent 12-13 % of their life at the per-slice barrier, tools/diag_bar_time.py).  The 128-KB ring
+// leaves no room for the forward's per-wave IPE copy, which then stays in 24 registers.
+#ifndef NOF_RING16_FP32_SLOTS
+#define NOF_RING16_FP32_SLOTS 4
+#endif
+static_assert(NOF_RING16_FP32_SLOTS == 3 || NOF_RING16_FP32_SLOTS == 4, "fp32 ring: 3 or 4 slots");
+template <int P> constexpr int ring16_slots() { return P == 0 ? NOF_RING16_FP32_SLOTS : 3; }
+template <int P> constexpr int ring16_floats() { return ring16_slots<P>() * kSliceFloats; }
 // prologue: slices 0 and 1 into slots 0 and 1 (retired by the prologue's __syncthreads)
 __device__ __forceinline__ void ring16_prologue(const float* __restrict__ img, float* lds, int tid) {
   slice16_dma(img, lds, tid);
   slice16_dma(img + kSliceFloats, lds + kSliceFloats, tid);
+}
+// Static priority for the second-dispatched half of the workgroup (waves 4..7, the partner of wave
+// w - 4 on its SIMD), which otherwise loses issue arbitration by age on every slice
+// (MI355X_MICROARCH.md, two waves per SIMD, item 4).  Off unless built with NOF_PRIO16.
+__device__ __forceinline__ void prio16_younger_half() {
+#ifdef NOF_PRIO16
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
 }
 
 // Feature held by register r of tile t in lane group g.
@@ -140,11 +158,13 @@ struct NoEpi16 {
 // cinit (LDS, + 4g; null: zero) is the accumulators' initial value — the layer's bias enters as
 // the C operand of each tile's first MFMA instead of as a VALU add in the epilogue (the fp32
 // MFMA and the VALU share the issue port: every epilogue instruction is MFMA time).
+// ipe: with the 4-slot ring the wave's IPE registers (float[6][4], flattened), else its LDS copy.
 template <int NT_B, int NT_I, int OT, class Epi>
-__device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16],
+__device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const float* ipe, f32x4 (&acc)[16],
                                             float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
                                             int lane, Epi& epi, const float* cinit) {
   static_assert(OT % 2 == 0 && OT <= 16, "row tiles come in pairs");
+  constexpr int kSlots = ring16_slots<0>();
   constexpr int NG = OT;  // groups per slice: 2 input tiles x OT / 2 pairs
 #ifndef NOF_EPI16_G1
 #define NOF_EPI16_G1 4
@@ -157,7 +177,7 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
 #pragma unroll
   for (int t = 0; t < NT_B + NT_I; ++t) {
     const bool dma = !(last_in_schedule && t + 2 >= NT_B + NT_I);  // slice t + 2 exists
-    const int nxt2 = cur == 0 ? 2 : cur - 1;                         // (cur + 2) % 3
+    const int nxt2 = kSlots == 4 ? ((cur + 2) & 3) : (cur == 0 ? 2 : cur - 1);  // (cur + 2) % slots
     const float* W = lds + cur * kSliceFloats + row * 32;
     // group q = tt * (OT / 2) + p: input tile tt of the slice, row tiles 2p, 2p + 1
     auto aread = [&](int q, int which) {
@@ -177,7 +197,9 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
         b4[0] = bin[tb][0]; b4[1] = bin[tb][1]; b4[2] = bin[tb][2]; b4[3] = bin[tb][3];
       } else {
         const int ti = (t >= NT_B) ? 2 * (t - NT_B) + tt : 0;
-        b4 = *reinterpret_cast<const f32x4*>(ipe_lds + (ti * 64 + lane) * 4);
+        if constexpr (kSlots == 4) {
+          b4[0] = ipe[4 * ti]; b4[1] = ipe[4 * ti + 1]; b4[2] = ipe[4 * ti + 2]; b4[3] = ipe[4 * ti + 3];
+        } else b4 = *reinterpret_cast<const f32x4*>(ipe + (ti * 64 + lane) * 4);
       }
       asm volatile("" ::"v"(a0), "v"(a1), "v"(c0), "v"(c1));  // this group's reads land here, before the next ones issue
       f32x4 n0 = a0, n1 = a1, m0 = c0, m1 = c1;
@@ -222,10 +244,17 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
       c0 = m0;
       c1 = m1;
     }
-    // slice t + 1 (issued during slice t - 1) must have landed; everything issued during this
-    // slice (the DMA of t + 2, both epilogue parts' stores) may stay in flight
-    slice_barrier((dma ? 4 : 0) + (t + 1 < NT_B ? 2 * Epi::kVmPerPart : 0));
-    cur = cur == 2 ? 0 : cur + 1;
+    if constexpr (kSlots == 4) {
+      // after odd global slices (slot parity = slice parity): slices t + 1 and t + 2 must have
+      // landed, so only the epilogue stores issued after this slice's DMA may stay in flight
+      if (cur & 1) slice_barrier(t + 1 < NT_B ? 2 * Epi::kVmPerPart : 0);
+      cur = (cur + 1) & 3;
+    } else {
+      // slice t + 1 (issued during slice t - 1) must have landed; everything issued during this
+      // slice (the DMA of t + 2, both epilogue parts' stores) may stay in flight
+      slice_barrier((dma ? 4 : 0) + (t + 1 < NT_B ? 2 * Epi::kVmPerPart : 0));
+      cur = cur == 2 ? 0 : cur + 1;
+    }
     wsrc += kSliceFloats;
   }
 }

@@ -106,8 +106,8 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
   typedef typename Store16<P>::T ST;
   typedef typename Store16<P>::E AE;
   NOF_MT0
-  __shared__ __attribute__((aligned(16))) float lds[kRing16Floats + 256];
-  float* w8_lds = lds + kRing16Floats;
+  __shared__ __attribute__((aligned(16))) float lds[ring16_floats<P>() + 256];
+  float* w8_lds = lds + ring16_floats<P>();
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: block pointers stay in SGPRs
   const int half = wave & 1;
@@ -163,6 +163,7 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
   }
   if (tid < 64) reinterpret_cast<f32x4*>(w8_lds)[tid] = reinterpret_cast<const f32x4*>(tail + kBwdTailW8)[tid];
   __syncthreads();
+  prio16_younger_half();
 
   int cur = 0;
   const float* wsrc = a.wimg_b;

@@ -6,8 +6,9 @@
 // one launch per level.  Semantics per MLP.CallCached (MLPcs:112-136) and the C# heads
 // (MNcs:307-309, D23): sigma = softplus(z_s - 1), rgb = sigmoid(z_c) * 1.002 - 0.001.
 //
-// Per wave (16 samples of one ray): the 24 IPE features of its lanes computed in registers and
-// parked in LDS (B operand of layer 0 and of the skip layer), then 11 layers with activations
+// Per wave (16 samples of one ray): the 24 IPE features of its lanes computed in registers (the B
+// operand of layer 0 and of the skip layer: kept in registers beside the fp32 4-slot weight ring,
+// parked in LDS in f16x2 mode), then 11 layers with activations
 // resident in registers.  Side outputs for the backward pass: every layer's activations in the
 // block-swizzled [F][32] layout (weight-gradient GEMMs), packed ReLU masks (dX chain), raw heads.
 #include "common.h"
@@ -123,9 +124,11 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
   typedef typename Store16<P>::T ST;
   typedef typename Store16<P>::E AE;
   NOF_MT0
-  constexpr int kRing = kRing16Floats;
+  constexpr int kRing = ring16_floats<P>();
+  constexpr bool kIpeReg = ring16_slots<P>() == 4;  // 4-slot ring: IPE B values stay in registers
+  constexpr int kIpeLds = kIpeReg ? 0 : 8 * kIpe16Floats;
   constexpr int kBiasLds = 8 * 256 + 256;
-  __shared__ __attribute__((aligned(16))) float lds[kRing + 8 * kIpe16Floats + 8 * 128 + kBiasLds];
+  __shared__ __attribute__((aligned(16))) float lds[kRing + kIpeLds + 8 * 128 + kBiasLds];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: block pointers stay in SGPRs
   const int half = wave & 1;
@@ -190,16 +193,21 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
         bst.store(act_in_rs, t, r, v);
       }
   }
-  float* ipe_lds = lds + kRing + wave * kIpe16Floats;
+  // B operand of layer 0 and the skip layer: the registers themselves, or the wave's LDS copy
+  const float* ipe_b = &ipe[0][0];
+  if constexpr (!kIpeReg) {
+    float* ipe_lds = lds + kRing + wave * kIpe16Floats;
 #pragma unroll
-  for (int t = 0; t < 6; ++t) {
-    f32x4 v;
-    v[0] = ipe[t][0]; v[1] = ipe[t][1]; v[2] = ipe[t][2]; v[3] = ipe[t][3];
-    *reinterpret_cast<f32x4*>(ipe_lds + (t * 64 + lane) * 4) = v;
+    for (int t = 0; t < 6; ++t) {
+      f32x4 v;
+      v[0] = ipe[t][0]; v[1] = ipe[t][1]; v[2] = ipe[t][2]; v[3] = ipe[t][3];
+      *reinterpret_cast<f32x4*>(ipe_lds + (t * 64 + lane) * 4) = v;
+    }
+    ipe_b = ipe_lds;
   }
   // view-direction part of layer 9 folded into a per-ray bias: b9 + W9[:, 256:283] . PE(d)
-  float* dirb = lds + kRing + 8 * kIpe16Floats + wave * 128;
-  float* bias_lds = lds + kRing + 8 * kIpe16Floats + 8 * 128;  // trunk biases (layers 0..7) and w8
+  float* dirb = lds + kRing + kIpeLds + wave * 128;
+  float* bias_lds = lds + kRing + kIpeLds + 8 * 128;  // trunk biases (layers 0..7) and w8
   for (int i = tid; i < kBiasLds / 4; i += kMlp16Threads) {
     const float* src = i < 512 ? tail + kFwdTailBias + 4 * i : tail + kFwdTailW8 + 4 * (i - 512);
     *reinterpret_cast<f32x4*>(bias_lds + 4 * i) = *reinterpret_cast<const f32x4*>(src);
@@ -214,6 +222,7 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
     dirb[o] = s;
   }
   __syncthreads();
+  prio16_younger_half();
 
   int cur = 0;
   const float* wsrc = a.wimg;
@@ -227,26 +236,26 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
   FwdEpi16<store, false, 16, ST> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
   const float* bias_g = biases + 4 * g;  // the lane group's bias slot (the layers' initial accumulators)
   ea.begin(act_h_blk, mask16_ptr(a.masks, blk, 0, half, lane));
-  layer16<P, 0, 3, 16>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, bias_g);
+  layer16<P, 0, 3, 16>(bin, ipe_b, accA, lds, cur, wsrc, false, tid, lane, bias_g);
   ea.tile01();
   for (int l = 1; l < kDepth - 1; l += 2) {
     eb.begin(act_h_blk + l * layer_stride, mask16_ptr(a.masks, blk, l, half, lane));
-    layer16<P, 8, 0, 16>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea, bias_g + l * 256);
+    layer16<P, 8, 0, 16>(bin, ipe_b, accB, lds, cur, wsrc, false, tid, lane, ea, bias_g + l * 256);
     eb.tile01();
     ea.begin(act_h_blk + (l + 1) * layer_stride, mask16_ptr(a.masks, blk, l + 1, half, lane));
     if (l + 1 == kSkip)
-      layer16<P, 8, 3, 16>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, eb, bias_g + (l + 1) * 256);
-    else layer16<P, 8, 0, 16>(bin, ipe_lds, accA, lds, cur, wsrc, false, tid, lane, eb, bias_g + (l + 1) * 256);
+      layer16<P, 8, 3, 16>(bin, ipe_b, accA, lds, cur, wsrc, false, tid, lane, eb, bias_g + (l + 1) * 256);
+    else layer16<P, 8, 0, 16>(bin, ipe_b, accA, lds, cur, wsrc, false, tid, lane, eb, bias_g + (l + 1) * 256);
     ea.tile01();
   }
   static_assert(kDepth == 8 && kSkip % 2 == 0, "trunk pairing assumes 8 layers and an even skip layer");
   FwdEpi16<store, true, 16, ST> e7(accB, bin, bst, lane);  // + density head (layer 8): z_s = w8 . h7 + b8
   e7.begin(act_h_blk + 7 * layer_stride, mask16_ptr(a.masks, blk, 7, half, lane), bias_lds + 8 * 256);
-  layer16<P, 8, 0, 16>(bin, ipe_lds, accB, lds, cur, wsrc, false, tid, lane, ea, bias_g + 7 * 256);
+  layer16<P, 8, 0, 16>(bin, ipe_b, accB, lds, cur, wsrc, false, tid, lane, ea, bias_g + 7 * 256);
   e7.tile01();
 
   // ---- view layer 9: relu(W9[:, :256] h7 + dirbias); h7 tiles 2..15 finish in its shadow -------
-  layer16<P, 8, 0, 8>(bin, ipe_lds, accA, lds, cur, wsrc, true, tid, lane, e7, dirb + 4 * g);
+  layer16<P, 8, 0, 8>(bin, ipe_b, accA, lds, cur, wsrc, true, tid, lane, e7, dirb + 4 * g);
   float zs = e7.zs;
   zs += __shfl_xor(zs, 16, 64);
   zs += __shfl_xor(zs, 32, 64);

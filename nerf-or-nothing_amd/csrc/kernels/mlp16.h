@@ -58,8 +58,12 @@ __device__ __forceinline__ void slice16_dma(const float* __restrict__ src, float
 #ifndef NOF_RING16_FP32_SLOTS
 #define NOF_RING16_FP32_SLOTS 4
 #endif
+#ifndef NOF_RING16_F16_SLOTS  // f16x2 16x16 kernels: 4 slots measured 0.3 % (fwd) / 1.3 % (bwd) slower —
+#define NOF_RING16_F16_SLOTS 3  // they are bound by the weight stream, and 4 slots push both to 256 VGPRs
+#endif
 static_assert(NOF_RING16_FP32_SLOTS == 3 || NOF_RING16_FP32_SLOTS == 4, "fp32 ring: 3 or 4 slots");
-template <int P> constexpr int ring16_slots() { return P == 0 ? NOF_RING16_FP32_SLOTS : 3; }
+static_assert(NOF_RING16_F16_SLOTS == 3 || NOF_RING16_F16_SLOTS == 4, "f16x2 ring: 3 or 4 slots");
+template <int P> constexpr int ring16_slots() { return P == 0 ? NOF_RING16_FP32_SLOTS : NOF_RING16_F16_SLOTS; }
 template <int P> constexpr int ring16_floats() { return ring16_slots<P>() * kSliceFloats; }
 // prologue: slices 0 and 1 into slots 0 and 1 (retired by the prologue's __syncthreads)
 __device__ __forceinline__ void ring16_prologue(const float* __restrict__ img, float* lds, int tid) {
@@ -273,13 +277,14 @@ __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const fl
                                              int lane, Epi& epi, const float* cinit) {
   typedef SplitMode<2> SM;
   static_assert(OT % 2 == 0 && OT <= 16, "row tiles come in pairs");
+  constexpr int kSlots = ring16_slots<2>();
   constexpr int NG = OT / 2;  // groups per slice
   constexpr int kE1 = NG > 4 ? 4 : NG - 1;
   constexpr int kE2 = NG > 6 ? 6 : NG - 1;
 #pragma unroll
   for (int t = 0; t < NT_B + NT_I; ++t) {
     const bool dma = !(last_in_schedule && t + 2 >= NT_B + NT_I);  // slice t + 2 exists
-    const int nxt2 = cur == 0 ? 2 : cur - 1;                         // (cur + 2) % 3
+    const int nxt2 = kSlots == 4 ? ((cur + 2) & 3) : (cur == 0 ? 2 : cur - 1);  // (cur + 2) % slots
     const f16x8* W = reinterpret_cast<const f16x8*>(lds + cur * kSliceFloats) + lane;
     float v[8];
     if (t < NT_B) {
@@ -288,10 +293,15 @@ __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const fl
       for (int i = 0; i < 8; ++i) v[i] = bin[tb + (i >> 2)][i & 3];
     } else {
       const int ti = t >= NT_B ? 2 * (t - NT_B) : 0;
-      const f32x4 u0 = *reinterpret_cast<const f32x4*>(ipe_lds + (ti * 64 + lane) * 4);
-      const f32x4 u1 = *reinterpret_cast<const f32x4*>(ipe_lds + ((ti + 1) * 64 + lane) * 4);
+      if constexpr (kSlots == 4) {  // the wave's IPE registers
 #pragma unroll
-      for (int i = 0; i < 4; ++i) { v[i] = u0[i]; v[4 + i] = u1[i]; }
+        for (int i = 0; i < 8; ++i) v[i] = ipe_lds[4 * ti + i];
+      } else {
+        const f32x4 u0 = *reinterpret_cast<const f32x4*>(ipe_lds + (ti * 64 + lane) * 4);
+        const f32x4 u1 = *reinterpret_cast<const f32x4*>(ipe_lds + ((ti + 1) * 64 + lane) * 4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { v[i] = u0[i]; v[4 + i] = u1[i]; }
+      }
     }
     Frag<2> b;
     split8<2>(v, b);
@@ -336,8 +346,13 @@ __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const fl
       c0 = m0;
       c1 = m1;
     }
-    slice_barrier((dma ? 4 : 0) + (t + 1 < NT_B ? 2 * Epi::kVmPerPart : 0));
-    cur = cur == 2 ? 0 : cur + 1;
+    if constexpr (kSlots == 4) {  // one barrier per two slices, as mlp_layer16
+      if (cur & 1) slice_barrier(t + 1 < NT_B ? 2 * Epi::kVmPerPart : 0);
+      cur = (cur + 1) & 3;
+    } else {
+      slice_barrier((dma ? 4 : 0) + (t + 1 < NT_B ? 2 * Epi::kVmPerPart : 0));
+      cur = cur == 2 ? 0 : cur + 1;
+    }
     wsrc += kSliceFloats;
   }
 }

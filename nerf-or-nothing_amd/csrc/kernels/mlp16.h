@@ -163,7 +163,9 @@ struct NoEpi16 {
 // the C operand of each tile's first MFMA instead of as a VALU add in the epilogue (the fp32
 // MFMA and the VALU share the issue port: every epilogue instruction is MFMA time).
 // ipe: with the 4-slot ring the wave's IPE registers (float[6][4], flattened), else its LDS copy.
-template <int NT_B, int NT_I, int OT, class Epi>
+// AH: A operands read AH groups ahead (2: the wave still issues back-to-back MFMAs when its partner
+// waits at the barrier and the ds_reads take longer than one group; costs 8 VGPRs).
+template <int NT_B, int NT_I, int OT, int AH, class Epi>
 __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const float* ipe, f32x4 (&acc)[16],
                                             float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
                                             int lane, Epi& epi, const float* cinit) {
@@ -188,7 +190,10 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
       const int tt = q / (OT / 2), p = q % (OT / 2);
       return *reinterpret_cast<const f32x4*>(W + (2 * p + which) * 16 * 32 + (((4 * tt + g) ^ swz) << 2));
     };
+    static_assert(AH == 1 || AH == 2, "operand read-ahead: 1 or 2 groups");
     f32x4 a0 = aread(0, 0), a1 = aread(0, 1);
+    f32x4 p0 = a0, p1 = a1;  // AH == 2: group 1's operands, in flight
+    if constexpr (AH == 2) { p0 = aread(1, 0); p1 = aread(1, 1); }
     auto cread = [&](int p, int which) { return *reinterpret_cast<const f32x4*>(cinit + 16 * (2 * p + which)); };
     f32x4 c0 = {}, c1 = {};  // initial accumulators of the group's pair (slice 0, first input tile)
     if (t == 0 && cinit) { c0 = cread(0, 0); c1 = cread(0, 1); }
@@ -210,10 +215,10 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
 #ifdef NOF_DIAG_NO_AREAD
       if (q + 1 < NG && t == 0) {
 #else
-      if (q + 1 < NG) {
+      if (q + AH < NG) {
 #endif
-        n0 = aread(q + 1, 0);
-        n1 = aread(q + 1, 1);
+        n0 = aread(q + AH, 0);
+        n1 = aread(q + AH, 1);
       }
       if (t == 0 && cinit && q + 1 < OT / 2) { m0 = cread(q + 1, 0); m1 = cread(q + 1, 1); }
 #ifndef NOF_DIAG_NO_DMA
@@ -243,8 +248,12 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
 #ifndef NOF_NO_SCHED_BARRIER
       __builtin_amdgcn_sched_barrier(0);
 #endif
-      a0 = n0;
-      a1 = n1;
+      if constexpr (AH == 2) {
+        a0 = p0; a1 = p1;
+        p0 = n0; p1 = n1;
+      } else {
+        a0 = n0; a1 = n1;
+      }
       c0 = m0;
       c1 = m1;
     }
@@ -358,20 +367,20 @@ __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const fl
 }
 
 // precision dispatch: P = 0 fp32 16x16x4, P = 2 f16x2 16x16x32
-template <int P, int NT_B, int NT_I, int OT, class Epi>
+template <int P, int NT_B, int NT_I, int OT, int AH = 1, class Epi>
 __device__ __forceinline__ void layer16(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16], float* lds,
                                         int& cur, const float*& wsrc, bool last_in_schedule, int tid, int lane,
                                         Epi& epi, const float* cinit = nullptr) {
   if constexpr (P == 2)
     mlp_layer16h<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi, cinit);
-  else mlp_layer16<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi, cinit);
+  else mlp_layer16<NT_B, NT_I, OT, AH>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi, cinit);
 }
-template <int P, int NT_B, int NT_I, int OT>
+template <int P, int NT_B, int NT_I, int OT, int AH = 1>
 __device__ __forceinline__ void layer16(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16], float* lds,
                                         int& cur, const float*& wsrc, bool last_in_schedule, int tid, int lane,
                                         const float* cinit = nullptr) {
   NoEpi16 none;
-  layer16<P, NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, none, cinit);
+  layer16<P, NT_B, NT_I, OT, AH>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, none, cinit);
 }
 
 }  // namespace nof

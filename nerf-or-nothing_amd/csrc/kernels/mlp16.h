@@ -65,6 +65,20 @@ static_assert(NOF_RING16_FP32_SLOTS == 3 || NOF_RING16_FP32_SLOTS == 4, "fp32 ri
 static_assert(NOF_RING16_F16_SLOTS == 3 || NOF_RING16_F16_SLOTS == 4, "f16x2 ring: 3 or 4 slots");
 template <int P> constexpr int ring16_slots() { return P == 0 ? NOF_RING16_FP32_SLOTS : NOF_RING16_F16_SLOTS; }
 template <int P> constexpr int ring16_floats() { return ring16_slots<P>() * kSliceFloats; }
+// fp32 accumulator chains per MFMA stream (2: mlp_layer16, 4: mlp_layer16w), per kernel.  Four
+// chains measured no faster in the kernels (fwd 1.118 -> 1.128 ms with the 3-slot ring it needs,
+// bwd 0.957 -> 0.960): the two-chain issue limit of the probe does not bind there.
+#ifndef NOF_FWD16_CHAINS
+#define NOF_FWD16_CHAINS 2
+#endif
+#ifndef NOF_BWD16_CHAINS
+#define NOF_BWD16_CHAINS 2
+#endif
+// the forward's four-chain layers need the 8 VGPRs its IPE registers take: 3-slot ring, IPE in LDS
+#ifndef NOF_FWD16_FP32_SLOTS
+#define NOF_FWD16_FP32_SLOTS (NOF_FWD16_CHAINS == 4 ? 3 : NOF_RING16_FP32_SLOTS)
+#endif
+template <int P> constexpr int fwd16_slots() { return P == 0 ? NOF_FWD16_FP32_SLOTS : NOF_RING16_F16_SLOTS; }
 // prologue: slices 0 and 1 into slots 0 and 1 (retired by the prologue's __syncthreads)
 __device__ __forceinline__ void ring16_prologue(const float* __restrict__ img, float* lds, int tid) {
   slice16_dma(img, lds, tid);
@@ -165,12 +179,11 @@ struct NoEpi16 {
 // ipe: with the 4-slot ring the wave's IPE registers (float[6][4], flattened), else its LDS copy.
 // AH: A operands read AH groups ahead (2: the wave still issues back-to-back MFMAs when its partner
 // waits at the barrier and the ds_reads take longer than one group; costs 8 VGPRs).
-template <int NT_B, int NT_I, int OT, int AH, class Epi>
+template <int NT_B, int NT_I, int OT, int AH, int kSlots, class Epi>
 __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const float* ipe, f32x4 (&acc)[16],
                                             float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
                                             int lane, Epi& epi, const float* cinit) {
   static_assert(OT % 2 == 0 && OT <= 16, "row tiles come in pairs");
-  constexpr int kSlots = ring16_slots<0>();
   constexpr int NG = OT;  // groups per slice: 2 input tiles x OT / 2 pairs
 #ifndef NOF_EPI16_G1
 #define NOF_EPI16_G1 4
@@ -265,6 +278,100 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
     } else {
       // slice t + 1 (issued during slice t - 1) must have landed; everything issued during this
       // slice (the DMA of t + 2, both epilogue parts' stores) may stay in flight
+      slice_barrier((dma ? 4 : 0) + (t + 1 < NT_B ? 2 * Epi::kVmPerPart : 0));
+      cur = cur == 2 ? 0 : cur + 1;
+    }
+    wsrc += kSliceFloats;
+  }
+}
+// Four-chain variant of mlp_layer16 ("staggered windows").  v_mfma_f32_16x16x4_f32 sustains only
+// 138-141 TF/s on two interleaved accumulator chains, against 148-154 TF/s on eight
+// (tools/probe/mfma_rate.hip, random operands, 1 or 2 waves per SIMD: the partner wave does not fill
+// the dependency bubbles).  Window w of a slice runs the r = 2, 3 k-steps of group w - 1 beside the
+// r = 0, 1 k-steps of group w: four accumulators, each one's consecutive MFMAs four issues apart.
+// Operand pairs of three groups rotate (w - 1 finishing, w starting, w + 1 in flight: one window of
+// latency, as the two-chain loop's one group): 8 more VGPRs.  Same DMA steps (windows 0..3),
+// epilogue tiles (after windows kEpiGroup1, kEpiGroup2) and barriers as mlp_layer16.
+template <int NT_B, int NT_I, int OT, int kSlots, class Epi>
+__device__ __forceinline__ void mlp_layer16w(const float (&bin)[16][4], const float* ipe, f32x4 (&acc)[16],
+                                             float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
+                                             int lane, Epi& epi, const float* cinit) {
+  static_assert(OT % 2 == 0 && OT <= 16, "row tiles come in pairs");
+  constexpr int NG = OT;  // groups per slice: 2 input tiles x OT / 2 pairs
+  constexpr int kEpiGroup1 = NOF_EPI16_G1;
+  constexpr int kEpiGroup2 = (NG / 2 + NOF_EPI16_G1 < NG) ? NG / 2 + NOF_EPI16_G1 : NG - 1;
+  const int g = lane >> 4;
+  const int row = lane & 15;
+  const int swz = (row >> 1) & 7;
+#pragma unroll
+  for (int t = 0; t < NT_B + NT_I; ++t) {
+    const bool dma = !(last_in_schedule && t + 2 >= NT_B + NT_I);  // slice t + 2 exists
+    const int nxt2 = kSlots == 4 ? ((cur + 2) & 3) : (cur == 0 ? 2 : cur - 1);  // (cur + 2) % slots
+    const float* W = lds + cur * kSliceFloats + row * 32;
+    auto aread = [&](int q, int which) {
+      const int tt = q / (OT / 2), p = q % (OT / 2);
+      return *reinterpret_cast<const f32x4*>(W + (2 * p + which) * 16 * 32 + (((4 * tt + g) ^ swz) << 2));
+    };
+    // B operand k-step r of group q (input tile tt = q / (OT / 2) of the slice)
+    auto bval = [&](int q, int r) -> float {
+      const int tt = q / (OT / 2);
+      if (t < NT_B) return bin[(t < NT_B) ? 2 * t + tt : 0][r];
+      const int ti = (t >= NT_B) ? 2 * (t - NT_B) + tt : 0;
+      if constexpr (kSlots == 4) return ipe[4 * ti + r];
+      else return ipe[(ti * 64 + lane) * 4 + r];
+    };
+    auto cread = [&](int p, int which) { return *reinterpret_cast<const f32x4*>(cinit + 16 * (2 * p + which)); };
+    f32x4 PA[3], PB[3];  // operand pairs of groups q, by q % 3
+    f32x4 CA[2], CB[2];  // initial accumulators (bias) of groups q < OT / 2 of slice 0, by q % 2
+    PA[0] = aread(0, 0);
+    PB[0] = aread(0, 1);
+    CA[0] = CB[0] = CA[1] = CB[1] = f32x4{};
+    if (t == 0 && cinit) { CA[0] = cread(0, 0); CB[0] = cread(0, 1); }
+#pragma unroll
+    for (int w = 0; w <= NG; ++w) {
+      if (w < NG) asm volatile("" ::"v"(PA[w % 3]), "v"(PB[w % 3]), "v"(CA[w % 2]), "v"(CB[w % 2]));
+      if (w + 1 < NG) {
+        PA[(w + 1) % 3] = aread(w + 1, 0);
+        PB[(w + 1) % 3] = aread(w + 1, 1);
+        if (t == 0 && cinit && w + 1 < OT / 2) { CA[(w + 1) % 2] = cread(w + 1, 0); CB[(w + 1) % 2] = cread(w + 1, 1); }
+      }
+#ifndef NOF_DIAG_NO_DMA
+      constexpr bool kFit = NOF_DMA16_G0 + 3 * NOF_DMA16_STRIDE < NG;
+      constexpr int kG0 = kFit ? NOF_DMA16_G0 : 0, kDS = kFit ? NOF_DMA16_STRIDE : 1;
+      if (dma && w < NG && w >= kG0 && (w - kG0) % kDS == 0 && (w - kG0) / kDS < 4)
+        slice16_dma_step(wsrc + 2 * kSliceFloats, lds + nxt2 * kSliceFloats, tid, (w - kG0) / kDS);
+#endif
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (w >= 1) {  // group w - 1, k-step h + 2
+          const int q = w - 1, p = q % (OT / 2);
+          const float b = bval(q, h + 2);
+          acc[2 * p] = mfma16(PA[q % 3][h + 2], b, acc[2 * p]);
+        }
+        if (w < NG) {  // group w, k-step h
+          const int q = w, p = q % (OT / 2);
+          const bool first = t == 0 && q < OT / 2 && h == 0;
+          acc[2 * p] = mfma16(PA[q % 3][h], bval(q, h), first ? CA[q % 2] : acc[2 * p]);
+        }
+        if (w >= 1) {
+          const int q = w - 1, p = q % (OT / 2);
+          acc[2 * p + 1] = mfma16(PB[q % 3][h + 2], bval(q, h + 2), acc[2 * p + 1]);
+        }
+        if (w < NG) {
+          const int q = w, p = q % (OT / 2);
+          const bool first = t == 0 && q < OT / 2 && h == 0;
+          acc[2 * p + 1] = mfma16(PB[q % 3][h], bval(q, h), first ? CB[q % 2] : acc[2 * p + 1]);
+        }
+      }
+      if (t + 1 < NT_B && w == kEpiGroup1) epi(2 * t + 2);
+      if (t + 1 < NT_B && w == kEpiGroup2) epi(2 * t + 3);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (kSlots == 4) {
+      if (cur & 1) slice_barrier(t + 1 < NT_B ? 2 * Epi::kVmPerPart : 0);
+      cur = (cur + 1) & 3;
+    } else {
       slice_barrier((dma ? 4 : 0) + (t + 1 < NT_B ? 2 * Epi::kVmPerPart : 0));
       cur = cur == 2 ? 0 : cur + 1;
     }
@@ -367,20 +474,24 @@ __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const fl
 }
 
 // precision dispatch: P = 0 fp32 16x16x4, P = 2 f16x2 16x16x32
-template <int P, int NT_B, int NT_I, int OT, int AH = 1, class Epi>
+// fp32: CH = 2 (mlp_layer16, AH-group operand read-ahead) or 4 accumulator chains (mlp_layer16w);
+// R = ring slots of the calling kernel
+template <int P, int NT_B, int NT_I, int OT, int AH = 1, int R = ring16_slots<P>(), int CH = 2, class Epi>
 __device__ __forceinline__ void layer16(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16], float* lds,
                                         int& cur, const float*& wsrc, bool last_in_schedule, int tid, int lane,
                                         Epi& epi, const float* cinit = nullptr) {
   if constexpr (P == 2)
     mlp_layer16h<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi, cinit);
-  else mlp_layer16<NT_B, NT_I, OT, AH>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi, cinit);
+  else if constexpr (CH == 4)
+    mlp_layer16w<NT_B, NT_I, OT, R>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi, cinit);
+  else mlp_layer16<NT_B, NT_I, OT, AH, R>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi, cinit);
 }
-template <int P, int NT_B, int NT_I, int OT, int AH = 1>
+template <int P, int NT_B, int NT_I, int OT, int AH = 1, int R = ring16_slots<P>(), int CH = 2>
 __device__ __forceinline__ void layer16(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16], float* lds,
                                         int& cur, const float*& wsrc, bool last_in_schedule, int tid, int lane,
                                         const float* cinit = nullptr) {
   NoEpi16 none;
-  layer16<P, NT_B, NT_I, OT, AH>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, none, cinit);
+  layer16<P, NT_B, NT_I, OT, AH, R, CH>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, none, cinit);
 }
 
 }  // namespace nof

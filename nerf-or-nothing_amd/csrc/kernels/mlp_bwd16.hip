@@ -178,20 +178,20 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
   // ---- dh7 = W9[:, :256]^T delta9 + w8 dz_s ; delta7 ---------------------------------------
   BwdEpi16<true, ST> e7(accA, bin, bst, lane);
   e7.begin(mask16_ptr(masks, blk, 7, half, lane), delta_blk + 7 * layer_stride, w8_lds, dzs);
-  layer16<P, 4, 0, 16, kBwdAhead16>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane);
+  layer16<P, 4, 0, 16, kBwdAhead16, ring16_slots<P>(), NOF_BWD16_CHAINS>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane);
   e7.tile01();
   // ---- dh_{l-1} = W_l[:, :256]^T delta_l ; delta_{l-1}, l = 7..1 (l odd: A -> B) ------------
   BwdEpi16<false, ST> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
   eb.begin(mask16_ptr(masks, blk, 6, half, lane), delta_blk + 6 * layer_stride);
-  layer16<P, 8, 0, 16, kBwdAhead16>(bin, nullptr, accB, lds, cur, wsrc, false, tid, lane, e7);
+  layer16<P, 8, 0, 16, kBwdAhead16, ring16_slots<P>(), NOF_BWD16_CHAINS>(bin, nullptr, accB, lds, cur, wsrc, false, tid, lane, e7);
   eb.tile01();
   static_assert(kDepth == 8, "bwd pairing assumes 8 trunk layers");
   for (int l = kDepth - 2; l >= 2; l -= 2) {
     ea.begin(mask16_ptr(masks, blk, l - 1, half, lane), delta_blk + (l - 1) * layer_stride);
-    layer16<P, 8, 0, 16, kBwdAhead16>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane, eb);
+    layer16<P, 8, 0, 16, kBwdAhead16, ring16_slots<P>(), NOF_BWD16_CHAINS>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane, eb);
     ea.tile01();
     eb.begin(mask16_ptr(masks, blk, l - 2, half, lane), delta_blk + (l - 2) * layer_stride);
-    layer16<P, 8, 0, 16, kBwdAhead16>(bin, nullptr, accB, lds, cur, wsrc, l == 2, tid, lane, ea);
+    layer16<P, 8, 0, 16, kBwdAhead16, ring16_slots<P>(), NOF_BWD16_CHAINS>(bin, nullptr, accB, lds, cur, wsrc, l == 2, tid, lane, ea);
     eb.tile01();
   }
   // delta0: nothing left to hide it under

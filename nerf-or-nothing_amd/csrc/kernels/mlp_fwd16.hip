@@ -130,8 +130,8 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
   typedef typename Store16<P>::T ST;
   typedef typename Store16<P>::E AE;
   NOF_MT0
-  constexpr int kRing = ring16_floats<P>();
-  constexpr bool kIpeReg = ring16_slots<P>() == 4;  // 4-slot ring: IPE B values stay in registers
+  constexpr int kRing = fwd16_slots<P>() * kSliceFloats;
+  constexpr bool kIpeReg = fwd16_slots<P>() == 4;  // 4-slot ring: IPE B values stay in registers
   constexpr int kIpeLds = kIpeReg ? 0 : 8 * kIpe16Floats;
   constexpr int kBiasLds = 8 * 256 + 256;
   __shared__ __attribute__((aligned(16))) float lds[kRing + kIpeLds + 8 * 128 + kBiasLds];
@@ -242,26 +242,26 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
   FwdEpi16<store, false, 16, ST> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
   const float* bias_g = biases + 4 * g;  // the lane group's bias slot (the layers' initial accumulators)
   ea.begin(act_h_blk, mask16_ptr(a.masks, blk, 0, half, lane));
-  layer16<P, 0, 3, 16, kFwdAhead16>(bin, ipe_b, accA, lds, cur, wsrc, false, tid, lane, bias_g);
+  layer16<P, 0, 3, 16, kFwdAhead16, fwd16_slots<P>(), NOF_FWD16_CHAINS>(bin, ipe_b, accA, lds, cur, wsrc, false, tid, lane, bias_g);
   ea.tile01();
   for (int l = 1; l < kDepth - 1; l += 2) {
     eb.begin(act_h_blk + l * layer_stride, mask16_ptr(a.masks, blk, l, half, lane));
-    layer16<P, 8, 0, 16, kFwdAhead16>(bin, ipe_b, accB, lds, cur, wsrc, false, tid, lane, ea, bias_g + l * 256);
+    layer16<P, 8, 0, 16, kFwdAhead16, fwd16_slots<P>(), NOF_FWD16_CHAINS>(bin, ipe_b, accB, lds, cur, wsrc, false, tid, lane, ea, bias_g + l * 256);
     eb.tile01();
     ea.begin(act_h_blk + (l + 1) * layer_stride, mask16_ptr(a.masks, blk, l + 1, half, lane));
     if (l + 1 == kSkip)
-      layer16<P, 8, 3, 16, kFwdAhead16>(bin, ipe_b, accA, lds, cur, wsrc, false, tid, lane, eb, bias_g + (l + 1) * 256);
-    else layer16<P, 8, 0, 16, kFwdAhead16>(bin, ipe_b, accA, lds, cur, wsrc, false, tid, lane, eb, bias_g + (l + 1) * 256);
+      layer16<P, 8, 3, 16, kFwdAhead16, fwd16_slots<P>(), NOF_FWD16_CHAINS>(bin, ipe_b, accA, lds, cur, wsrc, false, tid, lane, eb, bias_g + (l + 1) * 256);
+    else layer16<P, 8, 0, 16, kFwdAhead16, fwd16_slots<P>(), NOF_FWD16_CHAINS>(bin, ipe_b, accA, lds, cur, wsrc, false, tid, lane, eb, bias_g + (l + 1) * 256);
     ea.tile01();
   }
   static_assert(kDepth == 8 && kSkip % 2 == 0, "trunk pairing assumes 8 layers and an even skip layer");
   FwdEpi16<store, true, 16, ST> e7(accB, bin, bst, lane);  // + density head (layer 8): z_s = w8 . h7 + b8
   e7.begin(act_h_blk + 7 * layer_stride, mask16_ptr(a.masks, blk, 7, half, lane), bias_lds + 8 * 256);
-  layer16<P, 8, 0, 16, kFwdAhead16>(bin, ipe_b, accB, lds, cur, wsrc, false, tid, lane, ea, bias_g + 7 * 256);
+  layer16<P, 8, 0, 16, kFwdAhead16, fwd16_slots<P>(), NOF_FWD16_CHAINS>(bin, ipe_b, accB, lds, cur, wsrc, false, tid, lane, ea, bias_g + 7 * 256);
   e7.tile01();
 
   // ---- view layer 9: relu(W9[:, :256] h7 + dirbias); h7 tiles 2..15 finish in its shadow -------
-  layer16<P, 8, 0, 8, kFwdAhead16>(bin, ipe_b, accA, lds, cur, wsrc, true, tid, lane, e7, dirb + 4 * g);
+  layer16<P, 8, 0, 8, kFwdAhead16, fwd16_slots<P>(), NOF_FWD16_CHAINS>(bin, ipe_b, accA, lds, cur, wsrc, true, tid, lane, e7, dirb + 4 * g);
   float zs = e7.zs;
   zs += __shfl_xor(zs, 16, 64);
   zs += __shfl_xor(zs, 32, 64);

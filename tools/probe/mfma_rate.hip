@@ -5,6 +5,7 @@
 // chip actually sustains at the clock it holds under that stream.
 #include <hip/hip_runtime.h>
 #include <cstdio>
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
@@ -112,6 +113,32 @@ __global__ __launch_bounds__(512) void k_f32_rand(const unsigned* rnd, float* ou
   for (int i = 0; i < NACC; ++i) s += acc[i][0] + acc[i][15];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
+// v_mfma_f32_16x16x4_f32 — the shape of the fp32 16x16 MLP kernels (mlp16.h): NACC independent
+// accumulators per wave (the kernels interleave 2), random operands
+template <int NACC>
+__global__ __launch_bounds__(512) void k_f32_16_rand(const unsigned* rnd, float* out, int iters) {
+  f32x4 acc[NACC];
+#pragma unroll
+  for (int i = 0; i < NACC; ++i) acc[i] = f32x4{};
+  float a[4], b[4];
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    a[j] = __builtin_bit_cast(float, rnd[j * 64 + l] & 0xBFFFFFFFu);
+    b[j] = __builtin_bit_cast(float, rnd[(4 + j) * 64 + l] & 0xBFFFFFFFu);
+  }
+  for (int it = 0; it < iters; it += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0; i < NACC; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[(u + i) & 3], b[(u + 2 * i) & 3], acc[i], 0, 0, 0);
+  }
+  float s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < NACC; ++i) s += acc[i][0] + acc[i][3];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
 
 template <typename K>
 static double run_rand(K kern, const unsigned* rnd, int threads, int iters, int nacc, double flop_per_mfma, float* d) {
@@ -150,6 +177,9 @@ int main() {
          run_rand(k_f32_rand<8>, r, 512, it / 2, 8, 4096.0, d));
   printf("random data: bf16 8 acc 1 w/SIMD %.1f, 2 w/SIMD %.1f TF/s\n", run_rand(k_bf16_rand<8>, r, 256, it, 8, 32768.0, d),
          run_rand(k_bf16_rand<8>, r, 512, it / 2, 8, 32768.0, d));
+  printf("random data: fp32 16x16x4, 2 acc: 1 w/SIMD %.1f, 2 w/SIMD %.1f TF/s; 8 acc: 1 w/SIMD %.1f, 2 w/SIMD %.1f TF/s\n",
+         run_rand(k_f32_16_rand<2>, r, 256, it, 2, 2048.0, d), run_rand(k_f32_16_rand<2>, r, 512, it / 2, 2, 2048.0, d),
+         run_rand(k_f32_16_rand<8>, r, 256, it, 8, 2048.0, d), run_rand(k_f32_16_rand<8>, r, 512, it / 2, 8, 2048.0, d));
   (void)hipFree(r);
   (void)hipFree(d);
   return 0;

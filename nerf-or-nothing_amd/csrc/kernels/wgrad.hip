@@ -747,8 +747,22 @@ __global__ void k_wgrad_reduce(const WgOut* __restrict__ outs, const WgItem* __r
   if (e < o.nrows * o.ncols) {
     const int rr = e / o.ncols, cc = e - rr * o.ncols;
     const size_t off = (size_t)(o.row_off + rr) * ld + o.col_off + cc;
+    // item slab offsets are workgroup-uniform (scalar loads); kU slab values in flight per step,
+    // summed in item order (the same bits as one at a time)
+#ifndef NOF_REDUCE_UNROLL
+#define NOF_REDUCE_UNROLL 8
+#endif
+    constexpr int kU = NOF_REDUCE_UNROLL;
     float s = 0.0f;
-    for (int k = 0; k < o.nitems; ++k) s += slabs[slab_off[items[o.item0 + k].slab] + off];
+    int k = 0;
+    for (; k + kU <= o.nitems; k += kU) {
+      float v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) v[u] = slabs[slab_off[items[o.item0 + k + u].slab] + off];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) s += v[u];
+    }
+    for (; k < o.nitems; ++k) s += slabs[slab_off[items[o.item0 + k].slab] + off];
     s *= inv;
     float* dst = o.dst + (size_t)rr * o.ld + o.dst_col + cc;
     *dst = accumulate ? *dst + s : s;

@@ -228,6 +228,9 @@ __global__ __launch_bounds__(kWgThreads, 1) void k_wgrad(const WgProblem* __rest
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [2 buffers][A | B] x kWgHalf
   NOF_WG_T0(0)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef NOF_WG_PRIO  // static younger-half priority (MI355X_MICROARCH.md item 4): measured 3.8 % slower, off
+  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
   const int it0 = item_ptr[blockIdx.x], it1 = item_ptr[blockIdx.x + 1];
   for (int it = it0; it < it1; ++it) {
     NOF_IT_T0(0)

@@ -53,44 +53,16 @@ __device__ __forceinline__ void slice16_dma(const float* __restrict__ src, float
 // slice t + 2, now into the slot of t - 2, which every wave left before the barrier that ended
 // slice t - 1 or t - 2; the barrier after odd t retires the DMAs of t + 1 and t + 2.  Half the
 // barriers let the two waves of a SIMD drift by up to two slices before the leader waits (they
-// spent 12-13 % of their life at the per-slice barrier, tools/diag_bar_time.py).  The 128-KB ring
-// leaves no room for the forward's per-wave IPE copy, which then stays in 24 registers.
-#ifndef NOF_RING16_FP32_SLOTS
-#define NOF_RING16_FP32_SLOTS 4
-#endif
-#ifndef NOF_RING16_F16_SLOTS  // f16x2 16x16 kernels: 4 slots measured 0.3 % (fwd) / 1.3 % (bwd) slower —
-#define NOF_RING16_F16_SLOTS 3  // they are bound by the weight stream, and 4 slots push both to 256 VGPRs
-#endif
-static_assert(NOF_RING16_FP32_SLOTS == 3 || NOF_RING16_FP32_SLOTS == 4, "fp32 ring: 3 or 4 slots");
-static_assert(NOF_RING16_F16_SLOTS == 3 || NOF_RING16_F16_SLOTS == 4, "f16x2 ring: 3 or 4 slots");
-template <int P> constexpr int ring16_slots() { return P == 0 ? NOF_RING16_FP32_SLOTS : NOF_RING16_F16_SLOTS; }
+// spent 12-13 % of their life at the per-slice barrier of the 3-slot ring).  The 128-KB ring
+// leaves no room for the forward's per-wave IPE copy, which then stays in 24 registers.  (f16x2:
+// 4 slots measured 0.3 % / 1.3 % slower — bound by the weight stream, and they push both kernels
+// to 256 VGPRs.)
+template <int P> constexpr int ring16_slots() { return P == 0 ? 4 : 3; }
 template <int P> constexpr int ring16_floats() { return ring16_slots<P>() * kSliceFloats; }
-// fp32 accumulator chains per MFMA stream (2: mlp_layer16, 4: mlp_layer16w), per kernel.  Four
-// chains measured no faster in the kernels (fwd 1.118 -> 1.128 ms with the 3-slot ring it needs,
-// bwd 0.957 -> 0.960): the two-chain issue limit of the probe does not bind there.
-#ifndef NOF_FWD16_CHAINS
-#define NOF_FWD16_CHAINS 2
-#endif
-#ifndef NOF_BWD16_CHAINS
-#define NOF_BWD16_CHAINS 2
-#endif
-// the forward's four-chain layers need the 8 VGPRs its IPE registers take: 3-slot ring, IPE in LDS
-#ifndef NOF_FWD16_FP32_SLOTS
-#define NOF_FWD16_FP32_SLOTS (NOF_FWD16_CHAINS == 4 ? 3 : NOF_RING16_FP32_SLOTS)
-#endif
-template <int P> constexpr int fwd16_slots() { return P == 0 ? NOF_FWD16_FP32_SLOTS : NOF_RING16_F16_SLOTS; }
 // prologue: slices 0 and 1 into slots 0 and 1 (retired by the prologue's __syncthreads)
 __device__ __forceinline__ void ring16_prologue(const float* __restrict__ img, float* lds, int tid) {
   slice16_dma(img, lds, tid);
   slice16_dma(img + kSliceFloats, lds + kSliceFloats, tid);
-}
-// Static priority for the second-dispatched half of the workgroup (waves 4..7, the partner of wave
-// w - 4 on its SIMD), which otherwise loses issue arbitration by age on every slice
-// (MI355X_MICROARCH.md, two waves per SIMD, item 4).  Off unless built with NOF_PRIO16.
-__device__ __forceinline__ void prio16_younger_half() {
-#ifdef NOF_PRIO16
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
-#endif
 }
 
 // Feature held by register r of tile t in lane group g.
@@ -169,27 +141,24 @@ struct NoEpi16 {
 };
 
 // One dense layer: acc[ot] (ot < OT) = sum over NT_B slices with B from `bin` (registers, tiles
-// 2t, 2t + 1 of slice t) and NT_I slices with B from the wave's IPE copy in LDS.  Per slice: 2
-// input tiles x OT/2 row-tile pairs = OT MFMA groups of 8 (two accumulators interleaved: the
-// 16x16x4 dependent latency is 40 cycles against a 32-cycle issue), each group's two A operands
-// read one group ahead; the 4 DMA steps of slice t + 2 ride groups 0..3; one barrier per slice.
-// cinit (LDS, + 4g; null: zero) is the accumulators' initial value — the layer's bias enters as
-// the C operand of each tile's first MFMA instead of as a VALU add in the epilogue (the fp32
-// MFMA and the VALU share the issue port: every epilogue instruction is MFMA time).
-// ipe: with the 4-slot ring the wave's IPE registers (float[6][4], flattened), else its LDS copy.
-// AH: A operands read AH groups ahead (2: the wave still issues back-to-back MFMAs when its partner
-// waits at the barrier and the ds_reads take longer than one group; costs 8 VGPRs).
-template <int NT_B, int NT_I, int OT, int AH, int kSlots, class Epi>
+// 2t, 2t + 1 of slice t) and NT_I slices with B from the wave's IPE values.  Per slice: 2 input
+// tiles x OT/2 row-tile pairs = OT MFMA groups of 8 (two accumulators interleaved: the 16x16x4
+// dependent latency is 40 cycles against a 32-cycle issue), each group's two A operands read one
+// group ahead; the 4 DMA steps of slice t + 2 ride groups 0..3.  cinit (LDS, + 4g; null: zero) is
+// the accumulators' initial value — the layer's bias enters as the C operand of each tile's first
+// MFMA instead of as a VALU add in the epilogue (the fp32 MFMA and the VALU share the issue port:
+// every epilogue instruction is MFMA time).  ipe: with the 4-slot ring the wave's IPE registers
+// (float[6][4], flattened), else its LDS copy.  Measured and not kept (git history): four
+// accumulator chains, two-group operand read-ahead, a static younger-half priority, other
+// DMA / epilogue placements — all neutral or slower.
+template <int NT_B, int NT_I, int OT, int kSlots, class Epi>
 __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const float* ipe, f32x4 (&acc)[16],
                                             float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
                                             int lane, Epi& epi, const float* cinit) {
   static_assert(OT % 2 == 0 && OT <= 16, "row tiles come in pairs");
   constexpr int NG = OT;  // groups per slice: 2 input tiles x OT / 2 pairs
-#ifndef NOF_EPI16_G1
-#define NOF_EPI16_G1 4
-#endif
-  constexpr int kEpiGroup1 = NOF_EPI16_G1;
-  constexpr int kEpiGroup2 = (NG / 2 + NOF_EPI16_G1 < NG) ? NG / 2 + NOF_EPI16_G1 : NG - 1;
+  constexpr int kEpiGroup1 = 4;  // epilogue tiles after the DMA steps (groups 1 / 9: 2.5 % slower)
+  constexpr int kEpiGroup2 = (NG / 2 + 4 < NG) ? NG / 2 + 4 : NG - 1;
   const int g = lane >> 4;
   const int row = lane & 15;
   const int swz = (row >> 1) & 7;
@@ -203,10 +172,7 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
       const int tt = q / (OT / 2), p = q % (OT / 2);
       return *reinterpret_cast<const f32x4*>(W + (2 * p + which) * 16 * 32 + (((4 * tt + g) ^ swz) << 2));
     };
-    static_assert(AH == 1 || AH == 2, "operand read-ahead: 1 or 2 groups");
     f32x4 a0 = aread(0, 0), a1 = aread(0, 1);
-    f32x4 p0 = a0, p1 = a1;  // AH == 2: group 1's operands, in flight
-    if constexpr (AH == 2) { p0 = aread(1, 0); p1 = aread(1, 1); }
     auto cread = [&](int p, int which) { return *reinterpret_cast<const f32x4*>(cinit + 16 * (2 * p + which)); };
     f32x4 c0 = {}, c1 = {};  // initial accumulators of the group's pair (slice 0, first input tile)
     if (t == 0 && cinit) { c0 = cread(0, 0); c1 = cread(0, 1); }
@@ -225,31 +191,13 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
       }
       asm volatile("" ::"v"(a0), "v"(a1), "v"(c0), "v"(c1));  // this group's reads land here, before the next ones issue
       f32x4 n0 = a0, n1 = a1, m0 = c0, m1 = c1;
-#ifdef NOF_DIAG_NO_AREAD
-      if (q + 1 < NG && t == 0) {
-#else
-      if (q + AH < NG) {
-#endif
-        n0 = aread(q + AH, 0);
-        n1 = aread(q + AH, 1);
+      if (q + 1 < NG) {
+        n0 = aread(q + 1, 0);
+        n1 = aread(q + 1, 1);
       }
       if (t == 0 && cinit && q + 1 < OT / 2) { m0 = cread(q + 1, 0); m1 = cread(q + 1, 1); }
-#ifndef NOF_DIAG_NO_DMA
-#ifndef NOF_DMA16_STRIDE
-#define NOF_DMA16_STRIDE 1
-#endif
-#ifndef NOF_DMA16_G0
-#define NOF_DMA16_G0 0
-#endif
-      // DMA step i in group kG0 + i * kDS (i < 4; groups 0..3 where the layer has too few groups)
-      constexpr bool kFit = NOF_DMA16_G0 + 3 * NOF_DMA16_STRIDE < NG;
-      constexpr int kG0 = kFit ? NOF_DMA16_G0 : 0, kDS = kFit ? NOF_DMA16_STRIDE : 1;
-      if (dma && q >= kG0 && (q - kG0) % kDS == 0 && (q - kG0) / kDS < 4)
-        slice16_dma_step(wsrc + 2 * kSliceFloats, lds + nxt2 * kSliceFloats, tid, (q - kG0) / kDS);
-#endif
-#ifndef NOF_NO_SCHED_BARRIER
+      if (dma && q < 4) slice16_dma_step(wsrc + 2 * kSliceFloats, lds + nxt2 * kSliceFloats, tid, q);
       __builtin_amdgcn_sched_barrier(0);
-#endif
       const bool first = t == 0 && tt == 0;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -258,15 +206,9 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
       }
       if (t + 1 < NT_B && q == kEpiGroup1) epi(2 * t + 2);
       if (t + 1 < NT_B && q == kEpiGroup2) epi(2 * t + 3);
-#ifndef NOF_NO_SCHED_BARRIER
       __builtin_amdgcn_sched_barrier(0);
-#endif
-      if constexpr (AH == 2) {
-        a0 = p0; a1 = p1;
-        p0 = n0; p1 = n1;
-      } else {
-        a0 = n0; a1 = n1;
-      }
+      a0 = n0;
+      a1 = n1;
       c0 = m0;
       c1 = m1;
     }
@@ -278,100 +220,6 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
     } else {
       // slice t + 1 (issued during slice t - 1) must have landed; everything issued during this
       // slice (the DMA of t + 2, both epilogue parts' stores) may stay in flight
-      slice_barrier((dma ? 4 : 0) + (t + 1 < NT_B ? 2 * Epi::kVmPerPart : 0));
-      cur = cur == 2 ? 0 : cur + 1;
-    }
-    wsrc += kSliceFloats;
-  }
-}
-// Four-chain variant of mlp_layer16 ("staggered windows").  v_mfma_f32_16x16x4_f32 sustains only
-// 138-141 TF/s on two interleaved accumulator chains, against 148-154 TF/s on eight
-// (tools/probe/mfma_rate.hip, random operands, 1 or 2 waves per SIMD: the partner wave does not fill
-// the dependency bubbles).  Window w of a slice runs the r = 2, 3 k-steps of group w - 1 beside the
-// r = 0, 1 k-steps of group w: four accumulators, each one's consecutive MFMAs four issues apart.
-// Operand pairs of three groups rotate (w - 1 finishing, w starting, w + 1 in flight: one window of
-// latency, as the two-chain loop's one group): 8 more VGPRs.  Same DMA steps (windows 0..3),
-// epilogue tiles (after windows kEpiGroup1, kEpiGroup2) and barriers as mlp_layer16.
-template <int NT_B, int NT_I, int OT, int kSlots, class Epi>
-__device__ __forceinline__ void mlp_layer16w(const float (&bin)[16][4], const float* ipe, f32x4 (&acc)[16],
-                                             float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
-                                             int lane, Epi& epi, const float* cinit) {
-  static_assert(OT % 2 == 0 && OT <= 16, "row tiles come in pairs");
-  constexpr int NG = OT;  // groups per slice: 2 input tiles x OT / 2 pairs
-  constexpr int kEpiGroup1 = NOF_EPI16_G1;
-  constexpr int kEpiGroup2 = (NG / 2 + NOF_EPI16_G1 < NG) ? NG / 2 + NOF_EPI16_G1 : NG - 1;
-  const int g = lane >> 4;
-  const int row = lane & 15;
-  const int swz = (row >> 1) & 7;
-#pragma unroll
-  for (int t = 0; t < NT_B + NT_I; ++t) {
-    const bool dma = !(last_in_schedule && t + 2 >= NT_B + NT_I);  // slice t + 2 exists
-    const int nxt2 = kSlots == 4 ? ((cur + 2) & 3) : (cur == 0 ? 2 : cur - 1);  // (cur + 2) % slots
-    const float* W = lds + cur * kSliceFloats + row * 32;
-    auto aread = [&](int q, int which) {
-      const int tt = q / (OT / 2), p = q % (OT / 2);
-      return *reinterpret_cast<const f32x4*>(W + (2 * p + which) * 16 * 32 + (((4 * tt + g) ^ swz) << 2));
-    };
-    // B operand k-step r of group q (input tile tt = q / (OT / 2) of the slice)
-    auto bval = [&](int q, int r) -> float {
-      const int tt = q / (OT / 2);
-      if (t < NT_B) return bin[(t < NT_B) ? 2 * t + tt : 0][r];
-      const int ti = (t >= NT_B) ? 2 * (t - NT_B) + tt : 0;
-      if constexpr (kSlots == 4) return ipe[4 * ti + r];
-      else return ipe[(ti * 64 + lane) * 4 + r];
-    };
-    auto cread = [&](int p, int which) { return *reinterpret_cast<const f32x4*>(cinit + 16 * (2 * p + which)); };
-    f32x4 PA[3], PB[3];  // operand pairs of groups q, by q % 3
-    f32x4 CA[2], CB[2];  // initial accumulators (bias) of groups q < OT / 2 of slice 0, by q % 2
-    PA[0] = aread(0, 0);
-    PB[0] = aread(0, 1);
-    CA[0] = CB[0] = CA[1] = CB[1] = f32x4{};
-    if (t == 0 && cinit) { CA[0] = cread(0, 0); CB[0] = cread(0, 1); }
-#pragma unroll
-    for (int w = 0; w <= NG; ++w) {
-      if (w < NG) asm volatile("" ::"v"(PA[w % 3]), "v"(PB[w % 3]), "v"(CA[w % 2]), "v"(CB[w % 2]));
-      if (w + 1 < NG) {
-        PA[(w + 1) % 3] = aread(w + 1, 0);
-        PB[(w + 1) % 3] = aread(w + 1, 1);
-        if (t == 0 && cinit && w + 1 < OT / 2) { CA[(w + 1) % 2] = cread(w + 1, 0); CB[(w + 1) % 2] = cread(w + 1, 1); }
-      }
-#ifndef NOF_DIAG_NO_DMA
-      constexpr bool kFit = NOF_DMA16_G0 + 3 * NOF_DMA16_STRIDE < NG;
-      constexpr int kG0 = kFit ? NOF_DMA16_G0 : 0, kDS = kFit ? NOF_DMA16_STRIDE : 1;
-      if (dma && w < NG && w >= kG0 && (w - kG0) % kDS == 0 && (w - kG0) / kDS < 4)
-        slice16_dma_step(wsrc + 2 * kSliceFloats, lds + nxt2 * kSliceFloats, tid, (w - kG0) / kDS);
-#endif
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (w >= 1) {  // group w - 1, k-step h + 2
-          const int q = w - 1, p = q % (OT / 2);
-          const float b = bval(q, h + 2);
-          acc[2 * p] = mfma16(PA[q % 3][h + 2], b, acc[2 * p]);
-        }
-        if (w < NG) {  // group w, k-step h
-          const int q = w, p = q % (OT / 2);
-          const bool first = t == 0 && q < OT / 2 && h == 0;
-          acc[2 * p] = mfma16(PA[q % 3][h], bval(q, h), first ? CA[q % 2] : acc[2 * p]);
-        }
-        if (w >= 1) {
-          const int q = w - 1, p = q % (OT / 2);
-          acc[2 * p + 1] = mfma16(PB[q % 3][h + 2], bval(q, h + 2), acc[2 * p + 1]);
-        }
-        if (w < NG) {
-          const int q = w, p = q % (OT / 2);
-          const bool first = t == 0 && q < OT / 2 && h == 0;
-          acc[2 * p + 1] = mfma16(PB[q % 3][h], bval(q, h), first ? CB[q % 2] : acc[2 * p + 1]);
-        }
-      }
-      if (t + 1 < NT_B && w == kEpiGroup1) epi(2 * t + 2);
-      if (t + 1 < NT_B && w == kEpiGroup2) epi(2 * t + 3);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if constexpr (kSlots == 4) {
-      if (cur & 1) slice_barrier(t + 1 < NT_B ? 2 * Epi::kVmPerPart : 0);
-      cur = (cur + 1) & 3;
-    } else {
       slice_barrier((dma ? 4 : 0) + (t + 1 < NT_B ? 2 * Epi::kVmPerPart : 0));
       cur = cur == 2 ? 0 : cur + 1;
     }
@@ -440,13 +288,7 @@ __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const fl
           n1.p[p] = W[((2 * q + 3) * 2 + p) * 64];
         }
       }
-#ifndef NOF_DIAG_NO_DMA
-#ifdef NOF_H16_DMA_SPREAD  // DMA steps in every other group
-      if (dma && (q & 1) == 0 && q / 2 < 4) slice16_dma_step(wsrc + 2 * kSliceFloats, lds + nxt2 * kSliceFloats, tid, q / 2);
-#else
       if (dma && q < 4) slice16_dma_step(wsrc + 2 * kSliceFloats, lds + nxt2 * kSliceFloats, tid, q);
-#endif
-#endif
       __builtin_amdgcn_sched_barrier(0);
       const bool first = t == 0;
 #pragma unroll
@@ -474,24 +316,22 @@ __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const fl
 }
 
 // precision dispatch: P = 0 fp32 16x16x4, P = 2 f16x2 16x16x32
-// fp32: CH = 2 (mlp_layer16, AH-group operand read-ahead) or 4 accumulator chains (mlp_layer16w);
-// R = ring slots of the calling kernel
-template <int P, int NT_B, int NT_I, int OT, int AH = 1, int R = ring16_slots<P>(), int CH = 2, class Epi>
+template <int P, int NT_B, int NT_I, int OT, class Epi>
 __device__ __forceinline__ void layer16(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16], float* lds,
                                         int& cur, const float*& wsrc, bool last_in_schedule, int tid, int lane,
                                         Epi& epi, const float* cinit = nullptr) {
   if constexpr (P == 2)
     mlp_layer16h<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi, cinit);
-  else if constexpr (CH == 4)
-    mlp_layer16w<NT_B, NT_I, OT, R>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi, cinit);
-  else mlp_layer16<NT_B, NT_I, OT, AH, R>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi, cinit);
+  else
+    mlp_layer16<NT_B, NT_I, OT, ring16_slots<P>()>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane,
+                                                   epi, cinit);
 }
-template <int P, int NT_B, int NT_I, int OT, int AH = 1, int R = ring16_slots<P>(), int CH = 2>
+template <int P, int NT_B, int NT_I, int OT>
 __device__ __forceinline__ void layer16(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16], float* lds,
                                         int& cur, const float*& wsrc, bool last_in_schedule, int tid, int lane,
                                         const float* cinit = nullptr) {
   NoEpi16 none;
-  layer16<P, NT_B, NT_I, OT, AH, R, CH>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, none, cinit);
+  layer16<P, NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, none, cinit);
 }
 
 }  // namespace nof

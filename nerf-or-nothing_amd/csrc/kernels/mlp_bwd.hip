@@ -22,11 +22,7 @@ namespace nof {
 template <bool kDensity, bool kHalf>
 struct BwdEpi {
   typedef typename ActOut<kHalf>::T AT;
-#ifndef NOF_DIAG_NO_ACT_STORE
   static constexpr int kVmPerPart = 4;
-#else
-  static constexpr int kVmPerPart = 0;
-#endif
   const f32x16 (&acc)[8];
   float (&bin)[8][16];
   const ActOut<kHalf>& ao;
@@ -51,9 +47,6 @@ struct BwdEpi {
   }
   // register r of tile t (one or two per MFMA group in the split layers); w8 loaded one part ahead
   __device__ __forceinline__ void reg(int t, int r) {
-#ifdef NOF_DIAG_NO_EPI
-    return;
-#endif
     const int q = r >> 2, jj = r & 3;
     if constexpr (kDensity) {
       if (jj == 0) {
@@ -65,9 +58,7 @@ struct BwdEpi {
     if constexpr (kDensity) v += wcur[jj] * dzs;
     v = mask_bit(mk, t, r) ? v : 0.0f;
     bin[t][r] = v;
-#ifndef NOF_DIAG_NO_ACT_STORE
     ao.put(dst_blk + t * 32 * kBlk, r, v);
-#endif
   }
   __device__ __forceinline__ void operator()(int t, int q) {
 #pragma unroll
@@ -209,17 +200,8 @@ hipError_t launch_mlp_bwd(const BwdArgs& a, hipStream_t st) {
   if (a.M <= 0) return hipSuccess;
   if (a.M % kBlk != 0) return hipErrorInvalidValue;
   const int nblk = a.M / kBlk;
-  if (a.split == 1) hipLaunchKernelGGL(k_mlp_bwd<1>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
-#ifdef NOF_F16_MFMA32
-  else if (a.split == 2) hipLaunchKernelGGL(k_mlp_bwd<2>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
-#else
-  else if (a.split == 2) return launch_mlp_bwd16(a, st);
-#endif
-#ifdef NOF_F32_MFMA32
-  else hipLaunchKernelGGL(k_mlp_bwd<0>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
-#else
-  else return launch_mlp_bwd16(a, st);
-#endif
+  if (a.split != 1) return launch_mlp_bwd16(a, st);  // fp32 and f16x2: the 16x16 kernels (mlp_bwd16.hip)
+  hipLaunchKernelGGL(k_mlp_bwd<1>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
   return hipGetLastError();
 }
 

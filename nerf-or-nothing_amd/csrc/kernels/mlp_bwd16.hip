@@ -15,42 +15,6 @@
 
 namespace nof {
 
-#ifdef NOF_DIAG_WG_TIME  // per-workgroup wall-clock start/end of the last launch
-__device__ unsigned long long g_bwd_times[4096][2];
-extern "C" int nof_diag_bwd_times(unsigned long long* host) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bwd_times), sizeof(g_bwd_times), 0, hipMemcpyDeviceToHost);
-}
-#ifdef NOF_DIAG_BAR_TIME
-__device__ unsigned long long g_bwd_bar[4096][8][3];  // per wave: vmcnt-wait, barrier, lifetime (cycles)
-extern "C" int nof_diag_bwd_bar(unsigned long long* host) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bwd_bar), sizeof(g_bwd_bar), 0, hipMemcpyDeviceToHost);
-}
-#define NOF_BT0                                                                          \
-  const unsigned long long btk0_ = __builtin_amdgcn_s_memtime();                          \
-  if ((threadIdx.x & 63) == 0) { bar_acc()[threadIdx.x >> 6][0] = 0; bar_acc()[threadIdx.x >> 6][1] = 0; }
-#define NOF_BT1                                                                          \
-  if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096) {                                    \
-    g_bwd_bar[blockIdx.x][threadIdx.x >> 6][0] = bar_acc()[threadIdx.x >> 6][0];        \
-    g_bwd_bar[blockIdx.x][threadIdx.x >> 6][1] = bar_acc()[threadIdx.x >> 6][1];        \
-    g_bwd_bar[blockIdx.x][threadIdx.x >> 6][2] = __builtin_amdgcn_s_memtime() - btk0_;  \
-  }
-#else
-#define NOF_BT0
-#define NOF_BT1
-#endif
-#define NOF_MT0 const unsigned long long mt0_ = wall_clock64(); NOF_BT0
-#define NOF_MT1                                                                         \
-  NOF_BT1                                                                               \
-  __syncthreads();                                                                      \
-  if (threadIdx.x == 0 && blockIdx.x < 4096) {                                          \
-    g_bwd_times[blockIdx.x][0] = mt0_;                                                \
-    g_bwd_times[blockIdx.x][1] = wall_clock64();                                      \
-  }
-#else
-#define NOF_MT0
-#define NOF_MT1
-#endif
-
 
 // delta = mask ? acc (+ w8 * dz_s) : 0 -> B operand + delta block, one tile per call inside the
 // next layer's MFMA stream; w8 values loaded one tile ahead.
@@ -100,18 +64,11 @@ struct BwdEpi16 {
   }
 };
 
-// A-operand read-ahead of the dX chain (mlp16.h mlp_layer16): 2 groups (253 VGPRs) measured 0.4 % slower
-#ifndef NOF_BWD16_AHEAD
-#define NOF_BWD16_AHEAD 1
-#endif
-constexpr int kBwdAhead16 = NOF_BWD16_AHEAD;
-
 // P: 0 = fp32, 2 = f16x2 (16x16x32 f16, power-of-2 scaled deltas stored as fp16 blocks)
 template <int P>
 __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
   typedef typename Store16<P>::T ST;
   typedef typename Store16<P>::E AE;
-  NOF_MT0
   __shared__ __attribute__((aligned(16))) float lds[ring16_floats<P>() + 256];
   float* w8_lds = lds + ring16_floats<P>();
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;
@@ -169,7 +126,6 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
   }
   if (tid < 64) reinterpret_cast<f32x4*>(w8_lds)[tid] = reinterpret_cast<const f32x4*>(tail + kBwdTailW8)[tid];
   __syncthreads();
-  prio16_younger_half();
 
   int cur = 0;
   const float* wsrc = a.wimg_b;
@@ -178,26 +134,25 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
   // ---- dh7 = W9[:, :256]^T delta9 + w8 dz_s ; delta7 ---------------------------------------
   BwdEpi16<true, ST> e7(accA, bin, bst, lane);
   e7.begin(mask16_ptr(masks, blk, 7, half, lane), delta_blk + 7 * layer_stride, w8_lds, dzs);
-  layer16<P, 4, 0, 16, kBwdAhead16, ring16_slots<P>(), NOF_BWD16_CHAINS>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane);
+  layer16<P, 4, 0, 16>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane);
   e7.tile01();
   // ---- dh_{l-1} = W_l[:, :256]^T delta_l ; delta_{l-1}, l = 7..1 (l odd: A -> B) ------------
   BwdEpi16<false, ST> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
   eb.begin(mask16_ptr(masks, blk, 6, half, lane), delta_blk + 6 * layer_stride);
-  layer16<P, 8, 0, 16, kBwdAhead16, ring16_slots<P>(), NOF_BWD16_CHAINS>(bin, nullptr, accB, lds, cur, wsrc, false, tid, lane, e7);
+  layer16<P, 8, 0, 16>(bin, nullptr, accB, lds, cur, wsrc, false, tid, lane, e7);
   eb.tile01();
   static_assert(kDepth == 8, "bwd pairing assumes 8 trunk layers");
   for (int l = kDepth - 2; l >= 2; l -= 2) {
     ea.begin(mask16_ptr(masks, blk, l - 1, half, lane), delta_blk + (l - 1) * layer_stride);
-    layer16<P, 8, 0, 16, kBwdAhead16, ring16_slots<P>(), NOF_BWD16_CHAINS>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane, eb);
+    layer16<P, 8, 0, 16>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane, eb);
     ea.tile01();
     eb.begin(mask16_ptr(masks, blk, l - 2, half, lane), delta_blk + (l - 2) * layer_stride);
-    layer16<P, 8, 0, 16, kBwdAhead16, ring16_slots<P>(), NOF_BWD16_CHAINS>(bin, nullptr, accB, lds, cur, wsrc, l == 2, tid, lane, ea);
+    layer16<P, 8, 0, 16>(bin, nullptr, accB, lds, cur, wsrc, l == 2, tid, lane, ea);
     eb.tile01();
   }
   // delta0: nothing left to hide it under
 #pragma unroll
   for (int t = 2; t < 16; ++t) eb(t);
-  NOF_MT1
 }
 
 hipError_t launch_mlp_bwd16(const BwdArgs& a, hipStream_t st) {

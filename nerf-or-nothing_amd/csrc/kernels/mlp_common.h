@@ -1,11 +1,13 @@
-// The fused per-sample MLP on gfx950 — shared machinery of the forward and backward kernels.
+// The fused per-sample MLP on gfx950 — shared machinery of the split-mode (bf16x3) forward and
+// backward kernels (the fp32 and f16x2 modes run the 16x16 kernels of mlp16.h, which reuse the
+// packed slices, the slice barrier and the split helpers defined here).
 //
 // Work decomposition: one wave64 owns one block of 32 consecutive samples and keeps that
 // block's whole activation vector in registers across ALL layers: a 256-feature x 32-sample
-// tile is 8 MFMA accumulator tiles (f32x16) = 128 registers per lane.  The 32x32x2 fp32 MFMA
-// leaves layer l's output with the feature index in the registers and the sample on the lane,
-// which is exactly the B-operand layout the next layer's MFMA needs (k = feature pair
-// (r, r+4) per register r), so activations never leave the register file between layers.
+// tile is 8 MFMA accumulator tiles (f32x16) = 128 registers per lane.  The 32x32 MFMA leaves
+// layer l's output with the feature index in the registers and the sample on the lane, which is
+// exactly the B-operand layout the next layer's MFMA needs, so activations never leave the
+// register file between layers.
 //
 // Weights stream through LDS: the 4 waves of a workgroup share a double-buffered ring of
 // 32-KB "slices" (256 output rows x 32 input columns, fp32, chunk-XOR-swizzled so each lane's
@@ -23,27 +25,12 @@ constexpr int kMlpThreads = 256;  // 4 waves = 4 sample blocks
 typedef const __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
 
-// Copy one 32-KB packed slice global -> LDS with LDS-DMA (global_load_lds_dwordx4): no staging
-// VGPRs.  Thread tid moves 16-B chunks tid + 256 i; each wave-instruction lands 1 KB contiguous
-// (LDS destination = wave-uniform base + lane * 16).  Retired by the vmcnt(0) that the next
-// __syncthreads() emits.
-__device__ __forceinline__ void slice_dma(const float* __restrict__ src, float* dst, int tid) {
-  const int wave = tid >> 6;
-#pragma unroll
-  for (int i = 0; i < kSliceFloats / 4 / kMlpThreads; ++i) {
-    const int chunk = kMlpThreads * i + tid;
-    __builtin_amdgcn_global_load_lds((gptr_t)(src + chunk * 4), (lptr_t)(dst + (kMlpThreads * i + 64 * wave) * 4),
-                                     16, 0, 0);
-  }
-}
-
-// Step i of a slice DMA (either precision: thread tid moves 16-B chunk 256 i + tid).  The fused
-// layers spread a slice's steps over the first MFMA groups of the previous slice instead of
-// issuing them as one burst, which would queue 4 waves x 8-12 requests on the CU's texture unit
-// and stall every wave's MFMA issue behind it.
-#ifndef NOF_DMA_GLOBAL
-// buffer_load_dwordx4 ... lds: the slice base lives in the (scalar) buffer descriptor, the step in
-// soffset and the lane's 16 B in a constant voffset, so a step costs no per-lane address math.
+// Step i of a slice DMA (thread tid moves 16-B chunk 256 i + tid).  The fused layers spread a
+// slice's steps over the first MFMA groups of the previous slice instead of issuing them as one
+// burst, which would queue 4 waves x 8-12 requests on the CU's texture unit and stall every wave's
+// MFMA issue behind it.  buffer_load_dwordx4 ... lds: the slice base lives in the (scalar) buffer
+// descriptor, the step in soffset and the lane's 16 B in a constant voffset, so a step costs no
+// per-lane address math.
 __device__ __forceinline__ void slice_dma_step(const float* __restrict__ src, float* dst, int tid, int i) {
   const int wave = tid >> 6;
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), (short)0,
@@ -51,14 +38,6 @@ __device__ __forceinline__ void slice_dma_step(const float* __restrict__ src, fl
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lptr_t)(dst + (kMlpThreads * i + 64 * wave) * 4), 16, tid * 16,
                                            i * kMlpThreads * 16, 0, 0);
 }
-#else
-__device__ __forceinline__ void slice_dma_step(const float* __restrict__ src, float* dst, int tid, int i) {
-  const int wave = tid >> 6;
-  const int chunk = kMlpThreads * i + tid;
-  __builtin_amdgcn_global_load_lds((gptr_t)(src + chunk * 4), (lptr_t)(dst + (kMlpThreads * i + 64 * wave) * 4), 16,
-                                   0, 0);
-}
-#endif
 
 // Per-wave LDS copy of the 48 IPE B-operands: [tp][q][lane][4] floats (12 KB / wave).
 constexpr int kIpeLdsFloats = 3 * 4 * 64 * 4;
@@ -78,112 +57,12 @@ struct NoEpi {
 // retires in issue order, so waiting down to <= n_after outstanding retires the DMA) may stay in
 // flight — __syncthreads() would wait for them too (or, with no wait of its own, leave the DMA
 // unretired).  lgkmcnt(0): this slice's ds_reads are done before the next DMA overwrites the slot.
-#ifdef NOF_DIAG_BAR_TIME  // per-wave cycles spent in the slice barriers' vmcnt wait and s_barrier
-__device__ __forceinline__ unsigned long long (&bar_acc())[16][2] {
-  static __shared__ unsigned long long acc[16][2];
-  return acc;
-}
-#endif
 __device__ __forceinline__ void slice_barrier(int n_after) {
-#ifdef NOF_DIAG_BAR_TIME
-  const unsigned long long bt0 = __builtin_amdgcn_s_memtime();
-  if (n_after >= 16) asm volatile("s_waitcnt vmcnt(16)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-  else if (n_after >= 12) asm volatile("s_waitcnt vmcnt(12)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-  else if (n_after >= 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-  else if (n_after >= 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-  const unsigned long long bt1 = __builtin_amdgcn_s_memtime();
-  asm volatile("s_barrier" ::: "memory");
-  const unsigned long long bt2 = __builtin_amdgcn_s_memtime();
-  if ((threadIdx.x & 63) == 0) {
-    bar_acc()[threadIdx.x >> 6][0] += bt1 - bt0;
-    bar_acc()[threadIdx.x >> 6][1] += bt2 - bt1;
-  }
-  return;
-#endif
-#if defined(NOF_DIAG_DMA_NOWAIT)
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#elif !defined(NOF_DIAG_NO_BARRIER)
   if (n_after >= 16) asm volatile("s_waitcnt vmcnt(16)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   else if (n_after >= 12) asm volatile("s_waitcnt vmcnt(12)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   else if (n_after >= 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   else if (n_after >= 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
-}
-
-static_assert(kSliceFloats / 4 / kMlpThreads == 8, "fp32 slice = 8 DMA steps");
-// fp32 layer: slice DMA steps in MFMA groups 0..7; epilogue part q in group q OT + 1
-template <int OT> constexpr int f32_parts_after_dma() {
-  int n = 0;
-  for (int q = 0; q < 4; ++q) n += (q * OT + 1 > 7) ? 1 : 0;
-  return n;
-}
-// One dense layer: acc[ot] (ot < OT) = sum over NT_B slices with B from `bin` (registers) and
-// NT_I slices with B from the wave's IPE copy in LDS.  Consumes NT_B + NT_I slices of the
-// ring with one workgroup barrier each; the next slice's DMA is in flight during the MFMAs.
-// The first MFMA of each accumulator takes C = 0 (inline constant) instead of a zeroing pass.
-template <int NT_B, int NT_I, int OT, class Epi>
-__device__ __forceinline__ void mlp_layer(const float (&bin)[8][16], const float* ipe_lds, f32x16 (&acc)[8],
-                                          float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
-                                          int lane, Epi& epi) {
-  const int h = lane >> 5;
-  const int row = lane & 31;
-  const int swz = (row >> 1) & 7;
-#pragma unroll
-  for (int t = 0; t < NT_B + NT_I; ++t) {
-    const bool has_next = !(last_in_schedule && t == NT_B + NT_I - 1);
-    const float* W = lds + cur * kSliceFloats + row * 32;
-    // A operands of (q, ot) are read one group ahead so the ds_read latency hides under the
-    // previous group's 4 MFMAs (left alone, hipcc serialises read -> lgkmcnt(0) -> MFMA).
-    f32x4 a_cur = *reinterpret_cast<const f32x4*>(W + ((h ^ swz) << 2));
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      f32x4 b4;
-      if (t < NT_B) {
-        const int tb = (t < NT_B) ? t : 0;
-        b4[0] = bin[tb][4 * q]; b4[1] = bin[tb][4 * q + 1]; b4[2] = bin[tb][4 * q + 2]; b4[3] = bin[tb][4 * q + 3];
-      } else {
-        const int ti = (t >= NT_B) ? (t - NT_B) : 0;
-        b4 = *reinterpret_cast<const f32x4*>(ipe_lds + ((ti * 4 + q) * 64 + lane) * 4);
-      }
-#pragma unroll
-      for (int ot = 0; ot < OT; ++ot) {
-        // Touch a_cur first: the waitcnt for its read (issued one group earlier) lands here, before
-        // the next read is issued. hipcc models LDS-DMA as an lgkm event too, so it only ever emits
-        // lgkmcnt(0); waiting after issuing the next read would expose that read's full latency.
-        asm volatile("" ::"v"(a_cur));
-        f32x4 a_nxt = a_cur;
-        const bool more = !(q == 3 && ot == OT - 1);
-#ifdef NOF_DIAG_NO_AREAD
-        if (more && t == 0) {
-#else
-        if (more) {
-#endif
-          const int q2 = ot == OT - 1 ? q + 1 : q;
-          const int ot2 = ot == OT - 1 ? 0 : ot + 1;
-          a_nxt = *reinterpret_cast<const f32x4*>(W + ot2 * 32 * 32 + (((2 * q2 + h) ^ swz) << 2));
-        }
-#ifndef NOF_DIAG_NO_DMA
-        if (has_next && q * OT + ot < 8)
-          slice_dma_step(wsrc + kSliceFloats, lds + (cur ^ 1) * kSliceFloats, tid, q * OT + ot);
-#endif
-        __builtin_amdgcn_sched_barrier(0);  // keep the next group's read above this group's MFMAs
-        if (t == 0 && q == 0) acc[ot] = mfma32(a_cur[0], b4[0], f32x16{});
-        else acc[ot] = mfma32(a_cur[0], b4[0], acc[ot]);
-#pragma unroll
-        for (int jj = 1; jj < 4; ++jj) acc[ot] = mfma32(a_cur[jj], b4[jj], acc[ot]);
-        if (t + 1 < NT_B && ot == 1) epi(t + 1, q);
-        __builtin_amdgcn_sched_barrier(0);
-        a_cur = a_nxt;
-      }
-    }
-    slice_barrier(t + 1 < NT_B ? f32_parts_after_dma<OT>() * Epi::kVmPerPart : 0);
-    cur ^= 1;
-#ifndef NOF_DIAG_DMA_SAME
-    wsrc += kSliceFloats;
-#endif
-  }
 }
 
 // ============================================================================================
@@ -322,13 +201,7 @@ __device__ __forceinline__ void slice_dma_split(const float* __restrict__ src, f
 
 // split layer: split_dma_per<P>() DMA steps in each of the first groups; parts in groups s OT + 1 and
 // s OT + OT/2 + 1
-#ifndef NOF_X3_DMA_PER_GROUP
-#define NOF_X3_DMA_PER_GROUP 2
-#endif
-#ifndef NOF_F16_DMA_PER_GROUP
-#define NOF_F16_DMA_PER_GROUP 2
-#endif
-template <int P> constexpr int split_dma_per() { return P == 1 ? NOF_X3_DMA_PER_GROUP : NOF_F16_DMA_PER_GROUP; }
+template <int P> constexpr int split_dma_per() { return 2; }
 template <int P> constexpr int split_dma_groups() {
   return (split_dma_steps<P>() + split_dma_per<P>() - 1) / split_dma_per<P>();
 }
@@ -356,8 +229,8 @@ __device__ __forceinline__ void x3_b_values(const float (&bin)[8][16], const flo
   }
 }
 
-// Split-mode dense layer: same contract as mlp_layer (slices of the split image, one barrier per
-// slice).  Per (k-step, row tile): NP ds_read_b128 (issued one group ahead) and NPROD MFMAs; the
+// Split-mode dense layer: acc[ot] (ot < OT) = sum over NT_B slices with B from `bin` (registers)
+// and NT_I slices with B from the wave's IPE copy in LDS, one barrier per slice of the split image.  Per (k-step, row tile): NP ds_read_b128 (issued one group ahead) and NPROD MFMAs; the
 // next k-step's B fragment is split pair by pair in the shadow of the current k-step's MFMAs.
 // Epilogue: each MFMA group of k-step s of slice t finishes 8 / OT registers of tile t + 1 (registers
 // 8s .. 8s + 7 over the k-step), so the first half of tile t + 1 is in `bin` before k-step 1 of
@@ -395,17 +268,12 @@ __device__ __forceinline__ void mlp_layer_split(const float (&bin)[8][16], const
         for (int p = 0; p < NP; ++p) asm volatile("" ::"v"(a_cur.p[p]));  // wait here, before the next reads
         Frag<P> a_nxt = a_cur;
         const bool more = !(s == 1 && ot == OT - 1);
-#ifdef NOF_DIAG_NO_AREAD
-        if (more && t == 0) {
-#else
         if (more) {
-#endif
           const int s2 = ot == OT - 1 ? s + 1 : s;
           const int ot2 = ot == OT - 1 ? 0 : ot + 1;
 #pragma unroll
           for (int p = 0; p < NP; ++p) a_nxt.p[p] = W[((s2 * 8 + ot2) * NP + p) * 64];
         }
-#ifndef NOF_DIAG_NO_DMA
         if (has_next && s * OT + ot < split_dma_groups<P>()) {
 #pragma unroll
           for (int u = 0; u < split_dma_per<P>(); ++u) {
@@ -413,7 +281,6 @@ __device__ __forceinline__ void mlp_layer_split(const float (&bin)[8][16], const
             if (st < split_dma_steps<P>()) slice_dma_step(wsrc + SF, lds + (cur ^ 1) * SF, tid, st);
           }
         }
-#endif
         __builtin_amdgcn_sched_barrier(0);
         acc[ot] = mfma_split<P>(a_cur, b_cur, kk == 0 ? f32x16{} : acc[ot]);
         if (kk + 1 < NK && ot % PER == 0) {
@@ -431,9 +298,7 @@ __device__ __forceinline__ void mlp_layer_split(const float (&bin)[8][16], const
     }
     slice_barrier(t + 1 < NT_B ? split_regs_after_dma<P, OT>() * (Epi::kVmPerPart / 4) : 0);
     cur ^= 1;
-#ifndef NOF_DIAG_DMA_SAME
     wsrc += SF;
-#endif
   }
 }
 
@@ -452,14 +317,13 @@ __device__ __forceinline__ float delta_scale(const uint32_t* amax_bits, bool inv
   return ldexpf(1.0f, inverse ? -k : k);
 }
 
-// mode dispatch for the fused kernels: P = 0 fp32 (32x32x2 fp32 MFMA), 1 bf16x3, 2 f16x2
+// the split-mode (P = 1) fused kernels' layer, with or without an epilogue hook
 template <int P, int NT_B, int NT_I, int OT, class Epi>
 __device__ __forceinline__ void dense_layer(const float (&bin)[8][16], const float* ipe_lds, f32x16 (&acc)[8],
                                             float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
                                             int lane, Epi& epi) {
-  if constexpr (P > 0)
-    mlp_layer_split<P, NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi);
-  else mlp_layer<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi);
+  static_assert(P == 1, "the 32x32 kernels run the split mode only (fp32 / f16x2: mlp16.h)");
+  mlp_layer_split<P, NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi);
 }
 template <int P, int NT_B, int NT_I, int OT>
 __device__ __forceinline__ void dense_layer(const float (&bin)[8][16], const float* ipe_lds, f32x16 (&acc)[8],
@@ -470,8 +334,7 @@ __device__ __forceinline__ void dense_layer(const float (&bin)[8][16], const flo
 }
 template <int P>
 __device__ __forceinline__ void first_slice_dma(const float* src, float* dst, int tid) {
-  if constexpr (P > 0) slice_dma_split<P>(src, dst, tid);
-  else slice_dma(src, dst, tid);
+  slice_dma_split<P>(src, dst, tid);
 }
 template <int P> constexpr int slice_floats() { return P > 0 ? split_slice_floats<P>() : kSliceFloats; }
 template <int P> constexpr int ring_floats() { return 2 * slice_floats<P>(); }
@@ -506,29 +369,8 @@ __device__ __forceinline__ void blk_store_at(float* sbase, const BlkStore& bs, i
   *(gfloat*)p = v;
 }
 
-// fp16 counterpart (f16x2 mode, common.h blkh_off): element (f, j) of lane (h, j) register r of tile
-// ot: f = 32 ot + 8 (r >> 2) + 4h + (r & 3), so (f >> 2) & 3 = 2 ((r >> 2) & 1) + h and
-//   byte(f, j) = 2048 ot + 512 (r >> 2) + 64 (r & 3) + 256 h + ((((j >> 3) ^ (2 ((r >> 2) & 1) + h)) << 4) | ((j & 7) << 1)):
-// two lane offsets (by (r >> 2) & 1), the rest immediate (<= 1728 B past the tile base).
-struct BlkStoreH {
-  uint32_t voff[2];
-  __device__ __forceinline__ explicit BlkStoreH(int lane) {
-    const int h = lane >> 5, j = lane & 31;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) voff[q] = 256u * h + ((((j >> 3) ^ (2 * q + h)) << 4) | ((j & 7) << 1));
-  }
-};
-__device__ __forceinline__ void blkh_store_at(_Float16* tile_base, const BlkStoreH& bs, int r, float v) {
-  typedef __attribute__((address_space(1))) char gchar;
-  typedef __attribute__((address_space(1))) _Float16 ghalf;
-  gchar* p = (gchar*)tile_base + (size_t)bs.voff[(r >> 2) & 1] + 512 * (r >> 2) + 64 * (r & 3);
-  *(ghalf*)p = (_Float16)v;
-}
-constexpr int kTileHalves = 32 * kBlk;  // one 32-feature tile of an fp16 block (2 KB)
-
-// Activation / delta block writer of the 32x32-accumulator kernels: fp32 chunk-swizzled blocks
-// (f32 / bf16x3 modes) or fp16 blocks (f16x2 mode).  Both hold 32 x kBlk elements per 32-feature
-// tile, so block and tile pointer arithmetic is the same in elements of T.
+// Activation / delta block writer of the 32x32-accumulator (split-mode) kernels: fp32
+// chunk-swizzled blocks.
 template <bool kHalf> struct ActOut;
 template <> struct ActOut<false> {
   typedef float T;
@@ -536,14 +378,8 @@ template <> struct ActOut<false> {
   __device__ __forceinline__ explicit ActOut(int lane) : bs(lane) {}
   __device__ __forceinline__ void put(T* tile, int r, float v) const { blk_store_at(tile, bs, 0, r, v); }
 };
-template <> struct ActOut<true> {
-  typedef _Float16 T;
-  BlkStoreH bs;
-  __device__ __forceinline__ explicit ActOut(int lane) : bs(lane) {}
-  __device__ __forceinline__ void put(T* tile, int r, float v) const { blkh_store_at(tile, bs, r, v); }
-};
 template <bool kHalf>
-__device__ __forceinline__ int act_off(int f, int s) { return kHalf ? blkh_off(f, s) : blk_off(f, s); }
+__device__ __forceinline__ int act_off(int f, int s) { static_assert(!kHalf, "fp32 blocks"); return blk_off(f, s); }
 
 // feature index held by register r of accumulator tile ot in lane half h
 __device__ __forceinline__ int tile_feature(int ot, int r, int h) { return ot * 32 + 8 * (r >> 2) + 4 * h + (r & 3); }

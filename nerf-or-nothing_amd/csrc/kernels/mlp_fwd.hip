@@ -42,13 +42,11 @@ __device__ __forceinline__ void fwd_epilogue(const f32x16 (&acc)[8], float (&bin
         mw[ot >> 1] = (mw[ot >> 1] << 1) | (hv > 0.0f ? 1u : 0u);
       }
     }
-#ifndef NOF_DIAG_NO_ACT_STORE
     if constexpr (store) {
       typename ActOut<kHalf>::T* tile = act_blk + ot * 32 * kBlk;  // uniform: one scalar add per tile
 #pragma unroll
       for (int r = 0; r < 16; ++r) ao.put(tile, r, bin[ot][r]);
     }
-#endif
   }
   uint4 mv;
   mv.x = mw[0]; mv.y = mw[1]; mv.z = mw[2]; mv.w = mw[3];
@@ -64,11 +62,7 @@ __device__ __forceinline__ void fwd_epilogue(const f32x16 (&acc)[8], float (&bin
 template <bool store, bool kDensity, bool kHalf>
 struct FwdEpi {
   typedef typename ActOut<kHalf>::T AT;
-#ifndef NOF_DIAG_NO_ACT_STORE
   static constexpr int kVmPerPart = store ? 4 : 0;
-#else
-  static constexpr int kVmPerPart = 0;
-#endif
   const f32x16 (&acc)[8];
   float (&bin)[8][16];
   const ActOut<kHalf>& ao;
@@ -99,9 +93,6 @@ struct FwdEpi {
   // register r of tile t (the split layers run one or two registers per MFMA group, spreading the
   // epilogue's VALU work evenly over the slice); bias / w8 values are loaded one part (4 registers) ahead
   __device__ __forceinline__ void reg(int t, int r) {
-#ifdef NOF_DIAG_NO_EPI
-    return;
-#endif
     const int q = r >> 2, jj = r & 3;
     const int fo = 32 * t + 8 * q;
     const bool more = !(t == 7 && q == 3);
@@ -118,9 +109,7 @@ struct FwdEpi {
     bin[t][r] = hv;
     mw[t >> 1] = (mw[t >> 1] << 1) | (hv > 0.0f ? 1u : 0u);
     if constexpr (kDensity) zs += wcur[jj] * hv;
-#ifndef NOF_DIAG_NO_ACT_STORE
     if constexpr (store) ao.put(act_blk + t * 32 * kBlk, r, hv);
-#endif
     if (!more && jj == 3) {
       uint4 mv;
       mv.x = mw[0]; mv.y = mw[1]; mv.z = mw[2]; mv.w = mw[3];
@@ -168,11 +157,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
     for (int tp = 0; tp < 3; ++tp)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-#ifndef NOF_DIAG_NO_IPE
         ipe[tp][r] = ipe_feature(tile_feature(tp, r, h), mean, cov);
-#else
-        ipe[tp][r] = mean[r % 3] * (float)tile_feature(tp, r, h) + cov[r % 3];
-#endif
   } else {
 #pragma unroll
     for (int tp = 0; tp < 3; ++tp)
@@ -299,24 +284,9 @@ hipError_t launch_mlp_fwd(const FwdArgs& a, hipStream_t st) {
   if (a.M % kBlk != 0 || a.S % kBlk != 0) return hipErrorInvalidValue;
   const int nblk = a.M / kBlk;
   const dim3 grid((nblk + 3) / 4), block(kMlpThreads);
-  if (a.split == 1) {
-    if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd<1, false>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((k_mlp_fwd<1, true>), grid, block, 0, st, a);
-  } else if (a.split == 2) {
-#ifdef NOF_F16_MFMA32  // the 32x32x16, one-wave-per-SIMD f16x2 kernels (diagnostic builds only)
-    if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd<2, false>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((k_mlp_fwd<2, true>), grid, block, 0, st, a);
-#else
-    return launch_mlp_fwd16(a, st);
-#endif
-  } else {
-#ifdef NOF_F32_MFMA32  // the 32x32x2, one-wave-per-SIMD fp32 kernels (diagnostic builds only)
-    if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd<0, false>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((k_mlp_fwd<0, true>), grid, block, 0, st, a);
-#else
-    return launch_mlp_fwd16(a, st);
-#endif
-  }
+  if (a.split != 1) return launch_mlp_fwd16(a, st);  // fp32 and f16x2: the 16x16 kernels (mlp_fwd16.hip)
+  if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd<1, false>), grid, block, 0, st, a);
+  else hipLaunchKernelGGL((k_mlp_fwd<1, true>), grid, block, 0, st, a);
   return hipGetLastError();
 }
 

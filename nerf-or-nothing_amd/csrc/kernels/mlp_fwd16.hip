@@ -18,42 +18,6 @@
 
 namespace nof {
 
-#ifdef NOF_DIAG_WG_TIME  // per-workgroup wall-clock start/end of the last launch
-__device__ unsigned long long g_fwd_times[4096][2];
-extern "C" int nof_diag_fwd_times(unsigned long long* host) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd_times), sizeof(g_fwd_times), 0, hipMemcpyDeviceToHost);
-}
-#ifdef NOF_DIAG_BAR_TIME
-__device__ unsigned long long g_fwd_bar[4096][8][3];  // per wave: vmcnt-wait, barrier, lifetime (cycles)
-extern "C" int nof_diag_fwd_bar(unsigned long long* host) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fwd_bar), sizeof(g_fwd_bar), 0, hipMemcpyDeviceToHost);
-}
-#define NOF_BT0                                                                          \
-  const unsigned long long btk0_ = __builtin_amdgcn_s_memtime();                          \
-  if ((threadIdx.x & 63) == 0) { bar_acc()[threadIdx.x >> 6][0] = 0; bar_acc()[threadIdx.x >> 6][1] = 0; }
-#define NOF_BT1                                                                          \
-  if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096) {                                    \
-    g_fwd_bar[blockIdx.x][threadIdx.x >> 6][0] = bar_acc()[threadIdx.x >> 6][0];        \
-    g_fwd_bar[blockIdx.x][threadIdx.x >> 6][1] = bar_acc()[threadIdx.x >> 6][1];        \
-    g_fwd_bar[blockIdx.x][threadIdx.x >> 6][2] = __builtin_amdgcn_s_memtime() - btk0_;  \
-  }
-#else
-#define NOF_BT0
-#define NOF_BT1
-#endif
-#define NOF_MT0 const unsigned long long mt0_ = wall_clock64(); NOF_BT0
-#define NOF_MT1                                                                         \
-  NOF_BT1                                                                               \
-  __syncthreads();                                                                      \
-  if (threadIdx.x == 0 && blockIdx.x < 4096) {                                          \
-    g_fwd_times[blockIdx.x][0] = mt0_;                                                \
-    g_fwd_times[blockIdx.x][1] = wall_clock64();                                      \
-  }
-#else
-#define NOF_MT0
-#define NOF_MT1
-#endif
-
 
 // ReLU epilogue of one accumulator tile (the bias is already in it: the layer's first MFMAs take it
 // as C) -> next layer's B operand, act block, mask bits; NT tiles per layer, run in tile order (the
@@ -62,11 +26,7 @@ extern "C" int nof_diag_fwd_bar(unsigned long long* host) {
 // bit-identical values, so its duplicate stores are benign.
 template <bool store, bool kDensity, int NT, class ST>
 struct FwdEpi16 {
-#ifndef NOF_DIAG_NO_ACT_STORE
   static constexpr int kVmPerPart = store ? 4 : 0;
-#else
-  static constexpr int kVmPerPart = 0;
-#endif
   const f32x4 (&acc)[16];
   float (&bin)[16][4];
   const ST& bst;
@@ -118,20 +78,13 @@ struct FwdEpi16 {
   }
 };
 
-// A-operand read-ahead (mlp16.h mlp_layer16): 2 groups spill 12 VGPRs in the store variant, 1.1 % slower
-#ifndef NOF_FWD16_AHEAD
-#define NOF_FWD16_AHEAD 1
-#endif
-constexpr int kFwdAhead16 = NOF_FWD16_AHEAD;
-
 // P: 0 = fp32 (16x16x4 fp32 MFMA, fp32 activation blocks), 2 = f16x2 (16x16x32 f16, fp16 blocks)
 template <int P, bool store>  // store: side outputs for the backward pass (off for inference)
 __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
   typedef typename Store16<P>::T ST;
   typedef typename Store16<P>::E AE;
-  NOF_MT0
-  constexpr int kRing = fwd16_slots<P>() * kSliceFloats;
-  constexpr bool kIpeReg = fwd16_slots<P>() == 4;  // 4-slot ring: IPE B values stay in registers
+  constexpr int kRing = ring16_slots<P>() * kSliceFloats;
+  constexpr bool kIpeReg = ring16_slots<P>() == 4;  // 4-slot ring: IPE B values stay in registers
   constexpr int kIpeLds = kIpeReg ? 0 : 8 * kIpe16Floats;
   constexpr int kBiasLds = 8 * 256 + 256;
   __shared__ __attribute__((aligned(16))) float lds[kRing + kIpeLds + 8 * 128 + kBiasLds];
@@ -162,11 +115,7 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
     for (int t = 0; t < 6; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-#ifndef NOF_DIAG_NO_IPE
         ipe[t][r] = ipe_feature(feat16(t, g, r), mean, cov);
-#else
-        ipe[t][r] = mean[r % 3] * (float)feat16(t, g, r) + cov[r % 3];
-#endif
   } else {
 #pragma unroll
     for (int t = 0; t < 6; ++t)
@@ -228,7 +177,6 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
     dirb[o] = s;
   }
   __syncthreads();
-  prio16_younger_half();
 
   int cur = 0;
   const float* wsrc = a.wimg;
@@ -242,26 +190,26 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
   FwdEpi16<store, false, 16, ST> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
   const float* bias_g = biases + 4 * g;  // the lane group's bias slot (the layers' initial accumulators)
   ea.begin(act_h_blk, mask16_ptr(a.masks, blk, 0, half, lane));
-  layer16<P, 0, 3, 16, kFwdAhead16, fwd16_slots<P>(), NOF_FWD16_CHAINS>(bin, ipe_b, accA, lds, cur, wsrc, false, tid, lane, bias_g);
+  layer16<P, 0, 3, 16>(bin, ipe_b, accA, lds, cur, wsrc, false, tid, lane, bias_g);
   ea.tile01();
   for (int l = 1; l < kDepth - 1; l += 2) {
     eb.begin(act_h_blk + l * layer_stride, mask16_ptr(a.masks, blk, l, half, lane));
-    layer16<P, 8, 0, 16, kFwdAhead16, fwd16_slots<P>(), NOF_FWD16_CHAINS>(bin, ipe_b, accB, lds, cur, wsrc, false, tid, lane, ea, bias_g + l * 256);
+    layer16<P, 8, 0, 16>(bin, ipe_b, accB, lds, cur, wsrc, false, tid, lane, ea, bias_g + l * 256);
     eb.tile01();
     ea.begin(act_h_blk + (l + 1) * layer_stride, mask16_ptr(a.masks, blk, l + 1, half, lane));
     if (l + 1 == kSkip)
-      layer16<P, 8, 3, 16, kFwdAhead16, fwd16_slots<P>(), NOF_FWD16_CHAINS>(bin, ipe_b, accA, lds, cur, wsrc, false, tid, lane, eb, bias_g + (l + 1) * 256);
-    else layer16<P, 8, 0, 16, kFwdAhead16, fwd16_slots<P>(), NOF_FWD16_CHAINS>(bin, ipe_b, accA, lds, cur, wsrc, false, tid, lane, eb, bias_g + (l + 1) * 256);
+      layer16<P, 8, 3, 16>(bin, ipe_b, accA, lds, cur, wsrc, false, tid, lane, eb, bias_g + (l + 1) * 256);
+    else layer16<P, 8, 0, 16>(bin, ipe_b, accA, lds, cur, wsrc, false, tid, lane, eb, bias_g + (l + 1) * 256);
     ea.tile01();
   }
   static_assert(kDepth == 8 && kSkip % 2 == 0, "trunk pairing assumes 8 layers and an even skip layer");
   FwdEpi16<store, true, 16, ST> e7(accB, bin, bst, lane);  // + density head (layer 8): z_s = w8 . h7 + b8
   e7.begin(act_h_blk + 7 * layer_stride, mask16_ptr(a.masks, blk, 7, half, lane), bias_lds + 8 * 256);
-  layer16<P, 8, 0, 16, kFwdAhead16, fwd16_slots<P>(), NOF_FWD16_CHAINS>(bin, ipe_b, accB, lds, cur, wsrc, false, tid, lane, ea, bias_g + 7 * 256);
+  layer16<P, 8, 0, 16>(bin, ipe_b, accB, lds, cur, wsrc, false, tid, lane, ea, bias_g + 7 * 256);
   e7.tile01();
 
   // ---- view layer 9: relu(W9[:, :256] h7 + dirbias); h7 tiles 2..15 finish in its shadow -------
-  layer16<P, 8, 0, 8, kFwdAhead16, fwd16_slots<P>(), NOF_FWD16_CHAINS>(bin, ipe_b, accA, lds, cur, wsrc, true, tid, lane, e7, dirb + 4 * g);
+  layer16<P, 8, 0, 8>(bin, ipe_b, accA, lds, cur, wsrc, true, tid, lane, e7, dirb + 4 * g);
   float zs = e7.zs;
   zs += __shfl_xor(zs, 16, 64);
   zs += __shfl_xor(zs, 32, 64);
@@ -294,7 +242,6 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
     zh[0] = zs; zh[1] = zc[0]; zh[2] = zc[1]; zh[3] = zc[2];
     if constexpr (store) reinterpret_cast<f32x4*>(a.zhead)[m] = zh;
   }
-  NOF_MT1
 }
 
 hipError_t launch_mlp_fwd16(const FwdArgs& a, hipStream_t st) {

@@ -121,11 +121,7 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
 #pragma unroll
       for (int cc = 0; cc < 4; ++cc) {
         f32x4 an[RB], bn[CB];
-#ifdef NOF_DIAG_WG_NOREAD
-        if (cc < 3 && kb < 0) {
-#else
         if (cc < 3) {
-#endif
           const int ch = ((2 * (cc + 1) + h) ^ xs) << 2;
 #pragma unroll
           for (int r = 0; r < RB; ++r) an[r] = *reinterpret_cast<const f32x4*>(LA + aoff[r] + ch);
@@ -140,9 +136,7 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
           for (int r = 0; r < RB; ++r)
 #pragma unroll
             for (int c = 0; c < CB; ++c) acc[r][c] = mfma32(a[r][i], b[c][i], acc[r][c]);
-#ifndef NOF_DIAG_WG_NODMA
           if (cc * 4 + i < NJ) dma_step(kbn, nxt, cc * 4 + i);
-#endif
         }
         if (cc < 3) {
 #pragma unroll
@@ -155,9 +149,7 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
 #pragma unroll
       for (int j = 0; j < NJ; ++j) dma_step(kbn, nxt, j);
     }
-#ifndef NOF_DIAG_WG_NOBAR
     __syncthreads();
-#endif
     cur ^= 1;
   }
   if (active) {
@@ -228,9 +220,6 @@ __global__ __launch_bounds__(kWgThreads, 1) void k_wgrad(const WgProblem* __rest
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [2 buffers][A | B] x kWgHalf
   NOF_WG_T0(0)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#ifdef NOF_WG_PRIO  // static younger-half priority (MI355X_MICROARCH.md item 4): measured 3.8 % slower, off
-  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-#endif
   const int it0 = item_ptr[blockIdx.x], it1 = item_ptr[blockIdx.x + 1];
   for (int it = it0; it < it1; ++it) {
     NOF_IT_T0(0)
@@ -252,9 +241,9 @@ __global__ __launch_bounds__(kWgThreads, 1) void k_wgrad(const WgProblem* __rest
 }
 
 // ---- split mode (mlp_common.h): bf16x3 operands, six bf16 MFMAs per 32x32x16 product -----------
-// 4 waves, one per SIMD, on a 2 x 2 grid: wave (wr, wc) owns row tiles [wr RB, wr RB + RB) x col
-// tiles [wc CB, wc CB + CB) (up to 4 x 4 tiles = 256 accumulator registers), so the whole MFMA
-// stream of a CU runs from one wave per SIMD and each fragment read feeds RB or CB products.
+// 8 waves, two per SIMD, on a 2 x 4 grid: wave (wr, wc) owns row tiles [wr RB, wr RB + RB) x col
+// tiles [wc CB, wc CB + CB) (up to 4 x 2 tiles = 128 accumulator registers), so one wave's load or
+// barrier wait is its SIMD partner's MFMA time and each fragment read feeds RB or CB products.
 // Per 16-sample k-step (the 64-B half of every feature row of a chunk-swizzled block, common.h):
 //   * every thread loads up to 8 16-B chunks (16 rows x 64 contiguous bytes per wave-instruction)
 //     straight into registers, two k-steps ahead: two register sets rotate
@@ -266,10 +255,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void k_wgrad(const WgProblem* __rest
 //     previous k-step, whose fragments are one conflict-free ds_read_b128 each;
 //   * one bare barrier per k-step (lgkmcnt(0) + s_barrier: __syncthreads' release fence would
 //     wait for the loads in flight).
-#ifndef NOF_X3_WC
-#define NOF_X3_WC 4
-#endif
-constexpr int kX3WC = NOF_X3_WC;                  // wave-grid columns (2 rows): 4 -> 8 waves, 2 per SIMD
+constexpr int kX3WC = 4;  // wave-grid columns (2 rows): 8 waves, 2 per SIMD (a 2 x 2 grid at one wave per SIMD: 9 % slower)
 constexpr int kWgX3Threads = 64 * 2 * kX3WC;
 constexpr int kX3RowsPerC = kWgX3Threads / 4;      // concatenated rows one loader chunk index covers
 // floats per operand fragment image: [piece][tile][lane][16 B]; LDS = 2 images x 2 operands
@@ -337,9 +323,6 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
   }
   typedef const __attribute__((address_space(1))) f32x4 gf4;
   auto load = [&](int k, X3Raw<NCH>& q) {  // global (not flat) loads: flat_load would count in lgkmcnt
-#ifdef NOF_DIAG_X3_SAMEK
-    k &= 1;
-#endif
     const char* A = reinterpret_cast<const char*>(baseA + (size_t)(k >> 1) * strideA);
     const char* B = reinterpret_cast<const char*>(baseB + (size_t)(k >> 1) * strideB);
     const uint32_t par = (uint32_t)(k & 1) << 6;
@@ -388,10 +371,6 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
     const V8* FA = reinterpret_cast<const V8*>(lds + (k & 1) * 2 * kX3Frag) + (lane & 63);
     const V8* FB = FA + kX3Frag / 4;
     Frag<PM> fb[CB], fa;
-#ifdef NOF_WG_SPLIT_FRONT
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) split_chunk(nx, (k + 1) & 1, c, live);
-#endif
     // first row group's fragments in the order its MFMAs consume them (lo.hi, hi.lo, mid.mid, ...):
     // the first MFMAs start after two reads instead of after all of them
 #pragma unroll
@@ -418,21 +397,14 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
       }
 #pragma unroll
       for (int pp = 0; pp < SM::NPROD; ++pp) {
-#ifndef NOF_DIAG_X3_NOMFMA
 #pragma unroll
         for (int c = 0; c < CB; ++c)
           acc[r][c] = SM::mfma(fa.p[SM::pa(pp)], fb[c].p[SM::pb(pp)], acc[r][c]);
-#endif
-#ifndef NOF_WG_SPLIT_FRONT
         // chunks [NCH r / RB, NCH (r + 1) / RB): one after each MFMA group, the rest after the last
         const int i0 = (NCH * r) / RB, i1 = (NCH * (r + 1)) / RB;
 #pragma unroll
         for (int i = i0 + pp; i < (pp == SM::NPROD - 1 ? i1 : min(i0 + pp + 1, i1)); ++i)
-#ifdef NOF_DIAG_X3_NOSPLIT
-          if (nx.v[0][0] == 12345.0f)
-#endif
-            split_chunk(nx, (k + 1) & 1, i, live);
-#endif
+          split_chunk(nx, (k + 1) & 1, i, live);
       }
       fa = fn;
     }
@@ -502,23 +474,12 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_x3(const WgProblem* _
     const WgItem item = items[it];
     const WgProblem P = probs[item.prob];
     const int RB = (P.ntr + 1) >> 1, CB = (P.ntc + kX3WC - 1) / kX3WC;  // 2 x kX3WC wave grid
-    if constexpr (kX3WC == 2) {
-      switch (RB * 10 + CB) {
-        case 11: wg_item_x3<PM, 1, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-        case 12: wg_item_x3<PM, 1, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-        case 21: wg_item_x3<PM, 2, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-        case 34: wg_item_x3<PM, 3, 4>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-        case 42: wg_item_x3<PM, 4, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-        default: wg_item_x3<PM, 4, 4>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-      }
-    } else {
-      switch (RB * 10 + CB) {
-        case 11: wg_item_x3<PM, 1, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-        case 21: wg_item_x3<PM, 2, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-        case 32: wg_item_x3<PM, 3, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-        case 41: wg_item_x3<PM, 4, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-        default: wg_item_x3<PM, 4, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
-      }
+    switch (RB * 10 + CB) {
+      case 11: wg_item_x3<PM, 1, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+      case 21: wg_item_x3<PM, 2, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+      case 32: wg_item_x3<PM, 3, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+      case 41: wg_item_x3<PM, 4, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
+      default: wg_item_x3<PM, 4, 2>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
     }
     NOF_IT_T1(1)
   }
@@ -532,10 +493,7 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_x3(const WgProblem* _
 // (global_load_lds_dwordx4, 1 KB contiguous per wave-instruction), NS - 2 blocks in flight behind a
 // counted vmcnt, and ds_read_b128 fragment reads (conflict-free through the blkh_off chunk XOR).
 // Same 2 x kX3WC wave grid and item schedule as k_wgrad_x3; MFMA time is ~1/4 of the stream time.
-#ifndef NOF_WH_STAGES
-#define NOF_WH_STAGES 4
-#endif
-constexpr int kWhStages = NOF_WH_STAGES;
+constexpr int kWhStages = 4;
 constexpr int kWhStageHalves = 16 * 32 * kBlk;             // up to 16 tiles (8 A + 8 B) of 2 KB
 constexpr int kWhLds = kWhStages * kWhStageHalves * 2;      // bytes: 128 KB
 
@@ -752,10 +710,7 @@ __global__ void k_wgrad_reduce(const WgOut* __restrict__ outs, const WgItem* __r
     const size_t off = (size_t)(o.row_off + rr) * ld + o.col_off + cc;
     // item slab offsets are workgroup-uniform (scalar loads); kU slab values in flight per step,
     // summed in item order (the same bits as one at a time)
-#ifndef NOF_REDUCE_UNROLL
-#define NOF_REDUCE_UNROLL 8
-#endif
-    constexpr int kU = NOF_REDUCE_UNROLL;
+    constexpr int kU = 8;
     float s = 0.0f;
     int k = 0;
     for (; k + kU <= o.nitems; k += kU) {

@@ -40,7 +40,6 @@ json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
 names = {"k_mlp_fwd16<true>": "mlp_fwd", "k_mlp_bwd16": "mlp_bwd", "k_wgrad": "wgrad",
          "k_mlp_fwd16<0, true>": "mlp_fwd", "k_mlp_bwd16<0>": "mlp_bwd",
          "k_mlp_fwd16<2, true>": "mlp_fwd_f16x2", "k_mlp_bwd16<2>": "mlp_bwd_f16x2",
-         "k_mlp_fwd<false, true>": "mlp_fwd", "k_mlp_bwd<false>": "mlp_bwd",  # NOF_F32_MFMA32 builds
          "k_mlp_fwd<true, true>": "mlp_fwd_split", "k_mlp_bwd<true>": "mlp_bwd_split", "k_wgrad_x3": "wgrad_split",
          "k_mlp_fwd<1, true>": "mlp_fwd_split", "k_mlp_bwd<1>": "mlp_bwd_split", "k_wgrad_x3<1>": "wgrad_split",
          "k_mlp_fwd<2, true>": "mlp_fwd_f16x2", "k_mlp_bwd<2>": "mlp_bwd_f16x2", "k_wgrad_h": "wgrad_f16x2",

@@ -257,6 +257,7 @@ struct SampleCache {
   std::vector<std::vector<uint8_t>> act;  // act[l]: ReLU active flags of layer l
   T zs;
   T zc[3];
+  int flips = 0;  // adopted ReLU decisions that differ from this sample's own z > 0
 };
 
 template <class T>
@@ -272,14 +273,19 @@ static void dense(const float* Wt, const float* b, int out, int in, const T* x, 
 // `mask` (optional, test hook): [D*W + Dc*Wc] ReLU decisions to use instead of z > 0, so a
 // GPU run can be compared on identical activation patterns (an fp32 vs fp64 pre-activation at
 // ~0 otherwise flips a unit and shifts every gradient below it).
+// Returns how many of the adopted decisions differ from the oracle's own z > 0 (0 without a mask).
 template <class T>
-static void relu_apply(std::vector<T>& z, std::vector<uint8_t>& act, const uint8_t* mask) {
+static int relu_apply(std::vector<T>& z, std::vector<uint8_t>& act, const uint8_t* mask) {
   act.resize(z.size());
+  int flips = 0;
   for (size_t o = 0; o < z.size(); ++o) {
-    const bool a = mask ? mask[o] != 0 : z[o] > T(0);
+    const bool own = z[o] > T(0);
+    const bool a = mask ? mask[o] != 0 : own;
+    flips += a != own;
     act[o] = a;
     z[o] = a ? z[o] : T(0);
   }
+  return flips;
 }
 
 template <class T>
@@ -287,6 +293,7 @@ static void mlp_forward_sample(const Spec& sp, const float* P, const T* enc, con
                                const uint8_t* mask = nullptr) {
   const int L = sp.L, D = sp.D, Dc = sp.Dc;
   c.in.resize(L); c.outv.resize(L); c.act.resize(L);
+  c.flips = 0;
   std::vector<T> h(enc, enc + sp.pos_in);
   for (int l = 0; l < D; ++l) {
     std::vector<T>& x = c.in[l];
@@ -294,7 +301,7 @@ static void mlp_forward_sample(const Spec& sp, const float* P, const T* enc, con
     if (l % sp.skip == 0 && l > 0) x.insert(x.end(), enc, enc + sp.pos_in);   // MLPcs:95
     std::vector<T> z(sp.out[l]);
     dense<T>(P + sp.woff[l], P + sp.boff[l], sp.out[l], sp.in[l], x.data(), z.data());
-    relu_apply<T>(z, c.act[l], mask ? mask + (size_t)l * sp.W : nullptr);
+    c.flips += relu_apply<T>(z, c.act[l], mask ? mask + (size_t)l * sp.W : nullptr);
     c.outv[l] = z;
     h = z;
   }
@@ -307,7 +314,7 @@ static void mlp_forward_sample(const Spec& sp, const float* P, const T* enc, con
     c.in[l] = x;
     std::vector<T> z(sp.out[l]);
     dense<T>(P + sp.woff[l], P + sp.boff[l], sp.out[l], sp.in[l], x.data(), z.data());
-    relu_apply<T>(z, c.act[l], mask ? mask + (size_t)D * sp.W + (size_t)i * sp.Wc : nullptr);
+    c.flips += relu_apply<T>(z, c.act[l], mask ? mask + (size_t)D * sp.W + (size_t)i * sp.Wc : nullptr);
     c.outv[l] = z;
     x = z;
   }
@@ -427,6 +434,7 @@ struct StepIO {
   void* grads;             // T  [P] (overwritten)
   void* loss;              // T  scalar
   int nthreads;
+  int64_t* mask_flips;     // [level] adopted ReLU decisions != the oracle's own (optional)
 };
 
 template <class T>
@@ -440,6 +448,7 @@ static void step(const Spec& sp, const float* P, const StepIO& io) {
 #endif
   std::vector<std::vector<T>> Gp(nth, std::vector<T>(io.grads ? sp.P : 0, T(0)));
   std::vector<T> lossp(nth, T(0));
+  std::vector<std::vector<int64_t>> flipsp(nth, std::vector<int64_t>(NL, 0));
 #pragma omp parallel for num_threads(nth) schedule(dynamic, 1)
   for (int r = 0; r < n; ++r) {
 #ifdef _OPENMP
@@ -478,6 +487,7 @@ static void step(const Spec& sp, const float* P, const StepIO& io) {
                                 ? io.relu_mask[lv] + ((size_t)r * S + k) * ((size_t)sp.D * sp.W + (size_t)sp.Dc * sp.Wc)
                                 : nullptr;
         mlp_forward_sample<T>(sp, P, enc.data(), dpe.data(), c, mk);
+        flipsp[tid][lv] += c.flips;
         zs[lv][k] = c.zs;
         sig[lv][k] = softplus<T>(c.zs + (T)kDensityBias);                       // MNcs:309
         for (int j = 0; j < 3; ++j) {
@@ -526,6 +536,8 @@ static void step(const Spec& sp, const float* P, const StepIO& io) {
     for (size_t i = 0; i < sp.P; ++i) { T s = T(0); for (int t = 0; t < nth; ++t) s += Gp[t][i]; G[i] = s; }
   }
   if (io.loss) { T s = T(0); for (int t = 0; t < nth; ++t) s += lossp[t]; *(T*)io.loss = s; }
+  if (io.mask_flips)
+    for (int lv = 0; lv < NL; ++lv) { int64_t s = 0; for (int t = 0; t < nth; ++t) s += flipsp[t][lv]; io.mask_flips[lv] = s; }
 }
 
 }  // namespace orc
@@ -640,6 +652,7 @@ struct orc_step_args {
   float* const* t_out; void* const* w_out; void* const* C_out; void* const* sigma_out; void* const* rgb_out;
   void* const* dsigma_out; void* const* drgb_out; void* grads; void* loss;
   int32_t nthreads;
+  int64_t* mask_flips;
 };
 
 static StepIO cvt(const orc_step_args* a) {
@@ -651,6 +664,7 @@ static StepIO cvt(const orc_step_args* a) {
   io.t_override = a->t_override; io.relu_mask = a->relu_mask; io.t_out = a->t_out; io.w_out = a->w_out; io.C_out = a->C_out; io.sigma_out = a->sigma_out;
   io.rgb_out = a->rgb_out; io.dsigma_out = a->dsigma_out; io.drgb_out = a->drgb_out; io.grads = a->grads; io.loss = a->loss;
   io.nthreads = a->nthreads;
+  io.mask_flips = a->mask_flips;
   return io;
 }
 

@@ -40,6 +40,7 @@ class OrcStepArgs(C.Structure):
         ("sigma_out", C.POINTER(C.c_void_p)), ("rgb_out", C.POINTER(C.c_void_p)),
         ("dsigma_out", C.POINTER(C.c_void_p)), ("drgb_out", C.POINTER(C.c_void_p)),
         ("grads", C.c_void_p), ("loss", C.c_void_p), ("nthreads", C.c_int32),
+        ("mask_flips", C.c_void_p),
     ]
 
 
@@ -242,7 +243,8 @@ def step(spec: Spec, P, rays: dict, samples=(128, 128), seed=0, step_idx=0, ray_
     ``rays``: dict of float32 arrays o[n,3], d[n,3], radius[n], near[n], far[n], lossmult[n], pix[n,3].
     ``t_override``: optional {level: t[n, S_l+1]} replacing resampled t-values for level >= 1.
     ``relu_mask``: optional {level: uint8 [n, S_l, D*W + Dc*Wc]} ReLU decisions to use instead of z > 0.
-    Returns a dict of per-level lists plus ``grads`` [P] and ``loss``.
+    Returns a dict of per-level lists plus ``grads`` [P], ``loss`` and ``mask_flips`` (per level, the
+    adopted decisions that differ from the oracle's own z > 0; zeros without ``relu_mask``).
     """
     P = _f32(P)
     n = rays["o"].shape[0]
@@ -299,10 +301,14 @@ def step(spec: Spec, P, rays: dict, samples=(128, 128), seed=0, step_idx=0, ray_
     args.grads = G.ctypes.data if G is not None else None
     args.loss = loss.ctypes.data
     args.nthreads = nthreads if nthreads else (os.cpu_count() or 1)
+    flips = np.zeros(NL, np.int64)
+    args.mask_flips = flips.ctypes.data
     fn = lib().orc_step_f64 if dtype == np.float64 else lib().orc_step_f32
     fn(C.byref(spec.c()), P, C.byref(args))
     keep["grads"] = G
     keep["loss"] = float(loss[0])
+    # relu_mask given: per level, how many adopted decisions differ from the oracle's own z > 0
+    keep["mask_flips"] = [int(x) for x in flips]
     return keep
 
 

@@ -76,6 +76,33 @@ def test_sample_pdf_bitexact(gpu, oracle, S_in, S_out):
     assert np.array_equal(t.cpu().numpy(), rt)
 
 
+def test_samplers_config1_size(gpu, oracle):
+    """BASELINE configs[0]'s sampling at its stated size (one 400x400 view, 4096 rays x 64+64): the
+    GPU samplers are network-independent, so they run the configuration the HIP MLP does not."""
+    import torch
+    import nof
+    from nof import synth
+
+    n, S, seed = 4096, 64, 0x5EED0001
+    r = synth.blender_rays(n, width=400, height=400, num_views=1, seed=1)
+    t0 = empty((n, S + 1), gpu)
+    nof._lib.call("nof_kernel_sample_stratified", n, S, T(r["near"], gpu).data_ptr(), T(r["far"], gpu).data_ptr(), 1,
+                  seed, 0, 0, 0, t0.data_ptr(), None)
+    sync()
+    ref0 = oracle.sample_stratified(r["near"], r["far"], S, True, seed, 0, 0, 0)
+    assert np.array_equal(t0.cpu().numpy(), ref0)
+    w = np.random.default_rng(4).random((n, S), dtype=np.float32) ** 4
+    w[::97] = 0.0  # all-zero rays: the padding-only path
+    t1 = empty((n, S + 1), gpu)
+    idx = empty((n, S + 1), gpu, dtype=torch.int32)
+    nof._lib.call("nof_kernel_sample_pdf", n, S, T(ref0, gpu).data_ptr(), T(w, gpu).data_ptr(), S, 0.01, 1, seed, 0,
+                  1, 0, t1.data_ptr(), idx.data_ptr(), None)
+    sync()
+    rt, ridx = oracle.sample_pdf(ref0, w, S, 0.01, True, seed, 0, 1, 0)
+    assert np.array_equal(idx.cpu().numpy(), ridx)
+    assert np.array_equal(t1.cpu().numpy(), rt)
+
+
 def test_cast_bitexact_and_encode(gpu, oracle):
     import nof
 

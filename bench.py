@@ -3,11 +3,16 @@
 One step = both levels forward (stratified + hierarchical sampling, fused frustum/IPE/8x256 MLP,
 integrator) + fused loss gradient + both levels backward (integrator adjoint, MLP dX chain,
 weight-gradient GEMMs) + (N>1) RCCL all-reduce of the flat gradient arena + fused Adam.
-Workload = BASELINE.json configs[1]: Lego-shaped synthetic 800x800 batches, 1024 rays per GPU,
-128 + 128 samples, 8x256 MLP, fp32.  Inputs are pre-staged in HBM before the timed region.
+Workload at N=1 = BASELINE.json configs[1]: Lego-shaped synthetic 800x800 batches of 1024 rays,
+128 + 128 samples, 8x256 MLP, fp32.  At N>1 the default is configs[3]: a 65536-ray global batch
+sharded over the N GPUs (strong scaling; each shard micro-batched in 8192-ray calls accumulated
+into one gradient), with the N=1 line also carrying the same 65536-ray batch on one GPU
+(`config4_1gpu`), the denominator of SURVEY §8(e)'s scaling ratio.  Inputs are pre-staged in HBM
+before the timed region.
 
     python bench.py [--gpus N --steps K --warmup W]                      (N = 1)
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+    python bench.py --gpus N --single-process                            (one process, N devices)
 
 Rank 0 prints ONE JSON line.  `roofline` covers the dominant kernel, timed live with hipEvents
 on the library's stream inside the timed region; `cpu_baseline` times the oracle's faithful
@@ -51,7 +56,16 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--rays", type=int, default=1024, help="rays per GPU per step")
+    p.add_argument("--global-batch", type=int, default=None,
+                   help="rays per step over all GPUs (default: 1024 at N=1 = configs[1]; 65536 at N>1 = configs[3], "
+                        "strong scaling; LLFF: 512 per GPU = configs[4]'s per-GPU shape)")
+    p.add_argument("--rays", type=int, default=None, help="rays per GPU per step (weak scaling: global = N x rays)")
+    p.add_argument("--micro-batch", type=int, default=8192,
+                   help="rays per get_gradient call; a larger shard is micro-batched and accumulated")
+    p.add_argument("--single-process", action="store_true",
+                   help="one process drives --gpus devices (nof_dp_init_all, grouped all-reduce) instead of one "
+                        "process per GPU")
+    p.add_argument("--no-config4", action="store_true", help="skip the N=1 configs[3] (65536-ray) measurement")
     p.add_argument("--samples", type=int, nargs="+", default=[128, 128])
     p.add_argument("--scene", choices=["blender", "llff"], default="blender",
                    help="synthetic ray distribution: Lego-shaped 800x800 views (configs 2-4) or forward-facing "
@@ -64,32 +78,27 @@ def parse():
                    help="N>1 gradient all-reduce: torch.distributed (RCCL) or the C ABI's nof_dp_* (RCCL)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-integrator", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline work")
-    return p.parse_args()
+    p.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU-baseline work (both legs)")
+    a = p.parse_args()
+    if a.rays is not None:
+        if a.global_batch is not None:
+            p.error("--rays and --global-batch are exclusive")
+        a.global_batch = a.rays * a.gpus
+    a.global_batch_fixed = a.rays is None  # strong scaling unless the per-GPU size was given
+    return a
 
 
-def cpu_baseline(samples, target_s):
-    """Oracle = faithful scalar C++ restatement of MipNerfModel.GetGradient (MNcs:99-200), float,
-    OpenMP over rays on this host; bounded sample of the same workload."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
-    from nof import synth
-
-    cores = min(16, os.cpu_count() or 1)
-    spec = O.Spec()
-    P = O.glorot_init(spec, 0x5EED0002)
-    probe_n = cores
-    r = synth.blender_rays(probe_n, seed=99)
-    t0 = time.perf_counter()
-    O.step(spec, P, r, samples=tuple(samples), seed=1, nthreads=cores, dtype=np.float32, want=("grads",))
-    dt = time.perf_counter() - t0
-    n = max(cores, int(probe_n * max(1.0, (target_s - dt) / max(dt, 1e-3))) // cores * cores)
-    r = synth.blender_rays(n, seed=100)
-    t0 = time.perf_counter()
-    O.step(spec, P, r, samples=tuple(samples), seed=2, nthreads=cores, dtype=np.float32, want=("grads",))
-    dt = time.perf_counter() - t0
-    import platform
-    model = platform.processor()
+def host_cpus():
+    """(nproc, affinity, cgroup CPU quota or None, CPU model) of this host."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(math.ceil(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
@@ -98,9 +107,49 @@ def cpu_baseline(samples, target_s):
                     break
     except OSError:
         pass
-    return {"value": n / dt, "unit": "rays/s", "cores": cores, "kind": "port",
-            "sample": f"{n} rays x ({samples[0]}+{samples[1]}) samples, one full step (fwd+loss+bwd), float, "
-                      f"OpenMP over rays, {dt:.1f} s on {model}"}
+    return os.cpu_count() or 1, aff, quota, model
+
+
+def cpu_baseline(samples, target_s):
+    """Oracle = faithful scalar C++ restatement of MipNerfModel.GetGradient (MNcs:99-200) + the Adam
+    step (TrainState.cs:25-37 / AF:403-416), float, on a bounded sample of the same workload (BASELINE.md
+    §2): once single-threaded (the C# path is single-threaded) and once OpenMP over rays on every host
+    CPU this process may use (affinity, capped by a cgroup CPU quota when one is set)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from nof import synth
+
+    nproc, aff, quota, model = host_cpus()
+    spec = O.Spec()
+    P0 = O.glorot_init(spec, 0x5EED0002)
+
+    def timed(n, threads, seed):
+        r = synth.blender_rays(n, seed=seed)
+        P = P0.copy()
+        m = np.zeros_like(P)
+        v = np.zeros_like(P)
+        t0 = time.perf_counter()
+        out = O.step(spec, P, r, samples=tuple(samples), seed=seed, nthreads=threads, dtype=np.float32,
+                     want=("grads",))
+        O.adam_step(P, out["grads"], m, v, 5e-4, 1)
+        return time.perf_counter() - t0
+
+    def leg(threads, budget):
+        probe = max(1, threads // 2)
+        dt = timed(probe, threads, 99)
+        n = max(threads, int(probe * budget / max(dt, 1e-3)) // threads * threads)
+        dt = timed(n, threads, 100)
+        return n, dt
+
+    threads = min(aff, quota) if quota else aff
+    n1, dt1 = leg(1, target_s * 0.4)
+    nN, dtN = leg(threads, target_s * 0.6)
+    step = f"one full step (both levels fwd + loss + bwd + Adam), {samples[0]}+{samples[1]} samples, float"
+    return {"value": round(nN / dtN, 2), "unit": "rays/s", "cores": threads, "kind": "port",
+            "sample": f"{nN} rays, {step}, OpenMP over rays on {threads} threads: {dtN:.1f} s",
+            "single_thread": {"value": round(n1 / dt1, 3), "unit": "rays/s", "cores": 1,
+                              "sample": f"{n1} rays, {step}: {dt1:.1f} s"},
+            "host": {"nproc": nproc, "affinity": aff, "cgroup_cpu_quota": quota, "cpu_model": model}}
 
 
 def integrator_roofline(torch, nof, dev, n=1 << 20, S=128, reps=5):
@@ -143,12 +192,19 @@ def integrator_roofline(torch, nof, dev, n=1 << 20, S=128, reps=5):
             "workload": f"{n} rays x {S} samples, render fwd+bwd", "kernels": out}
 
 
-def workload_name(a):
+def workload_name(a, B):
     if a.scene == "llff":
-        return "BASELINE configs[4] per-GPU shape" if (a.rays, a.samples) == (512, [256, 256]) else "LLFF-shaped"
-    if (a.rays, a.samples) == (1024, [128, 128]):
+        return "BASELINE configs[4] per-GPU shape" if (B // a.gpus, a.samples) == (512, [256, 256]) else "LLFF-shaped"
+    if a.samples == [128, 128] and B == 65536:
+        return "BASELINE configs[3]"
+    if a.samples == [128, 128] and B == 1024 * a.gpus:
         return "BASELINE configs[1]"
     return "BASELINE configs[2]" if a.samples == [64, 128] else "Lego-shaped"
+
+
+def chunks(n, m):
+    """[lo, hi) micro-batches of at most m rays covering n."""
+    return [(lo, min(n, lo + m)) for lo in range(0, n, m)]
 
 
 def main():
@@ -158,12 +214,17 @@ def main():
 
     import nof
     from nof import synth
+    from nof.dp import BucketedAllReduce, NativeDP
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 via torch.distributed.run")
+    single = a.single_process
+    if single and world != 1:
+        raise SystemExit("--single-process drives every GPU from one process: do not launch it with torch.distributed")
+    if not single and world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 via torch.distributed.run "
+                         "(or --single-process)")
     # NOF_BENCH_DIST_BACKEND=gloo rehearses the N > 1 launch path (sharding, global sum of loss
     # multipliers, barriers, max-over-ranks timing) with several ranks on one GPU: the all-reduces go
     # through host memory, so its timings are not a scaling measurement.  Default: nccl (= RCCL).
@@ -188,103 +249,150 @@ def main():
             dist.all_reduce(h, op=op)
             t.copy_(h)
 
-    n = a.rays
+    G = a.gpus  # data-parallel width (ranks, or devices of the single process)
+    B = a.global_batch or (512 * G if a.scene == "llff" else 1024 if G == 1 else 65536)
+    if B % G:
+        raise SystemExit(f"--global-batch {B} does not split over {G} GPUs")
+    shard = B // G
+    micro = min(a.micro_batch, shard)
     samples = a.samples
-    stream = torch.cuda.current_stream(dev).cuda_stream
     seed = 0x5EED0002
-    # pre-staged synthetic batches (views of a 100-pose Lego-shaped scene; shard = disjoint views)
-    pool = []
-    for i in range(4):
-        r = (synth.llff_rays if a.scene == "llff" else synth.blender_rays)(n, seed=1000 * rank + i)
-        pool.append({k: torch.from_numpy(v).to(dev) for k, v in r.items()})
-    msum_global = float(n * world)  # lossmult = 1 everywhere: sum over all shards (D14, DP-global)
+    msum_global = float(B)  # lossmult = 1 everywhere: sum over all shards (D14, DP-global)
+    devs = list(range(G)) if single else [dev_idx]
+    ranks = list(range(G)) if single else [rank]
+
+    # pre-staged synthetic batches per device (views of a 100-pose Lego-shaped scene), global ray ids
+    def stage(r, d, n=shard):
+        out = []
+        for i in range(2):
+            h = (synth.llff_rays if a.scene == "llff" else synth.blender_rays)(n, seed=1000 * r + i)
+            out.append({k: torch.from_numpy(v).to(torch.device("cuda", d)) for k, v in h.items()})
+        return out
+
+    pools = [stage(r, d) for r, d in zip(ranks, devs)]
 
     native = None
-    if world > 1 and a.dp == "native":  # C-ABI RCCL communicator; the id travels over torch.distributed
-        from nof.dp import NativeDP
-
+    if single and G > 1:
+        native = NativeDP.init_all(devs)
+    elif world > 1 and a.dp == "native":  # C-ABI RCCL communicator; the id travels over torch.distributed
         obj = [NativeDP.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        native = NativeDP.init_rank(obj[0], world, rank, dev_idx)
+        native = [NativeDP.init_rank(obj[0], world, rank, dev_idx)]
 
-    def measure(prec):
-        """W untimed + K timed training steps of one precision mode, then a short untimed pass with
-        every kernel class event-timed (the per-kernel breakdown); returns (s, timing, psnr, in_sync).
-        Inside the timed region only the dominant kernel (mlp_fwd, the roofline kernel) is bracketed
-        by hipEvents: each event pair costs the dependent launch sequence a few us (measured 1.5 % of
-        the f32 step and 4 % of the f16x2 step with every kernel timed)."""
-        model = nof.AcceleratedMipNeRF(device=dev_idx, max_rays=n, num_samples=samples, seed=seed,
-                                       stream=stream, precision=PRECISIONS[prec])
-        model.set_rng(seed, 0, rank * n)  # global ray ids: sharding never changes a sample
-        opt = nof.AcceleratedAdamOptimizer(model.GetLayerSizes(), model.config)
-        params = model.mlp.allParams
-        gptr, P = model.mlp.flat_grads()
-        grad_view = nof.device_tensor(gptr, (P,), device=dev)
+    def measure(prec, B_run=None, steps=None, warmup=None, timers_on=True):
+        """W untimed + K timed training steps of one precision mode over the global batch (each
+        rank's shard in micro-batches accumulated into one gradient, one all-reduce), then a short
+        untimed pass with every kernel class event-timed (the per-kernel breakdown); returns
+        (s, timing, psnr, in_sync).  Inside the timed region only the dominant kernel (mlp_fwd, the
+        roofline kernel) is bracketed by hipEvents: each event pair costs the dependent launch
+        sequence a few us (measured 1.5 % of the f32 step and 4 % of the f16x2 step with every
+        kernel timed)."""
+        B_run = B_run or B
+        sh = B_run // G
+        mb = min(a.micro_batch, sh)
+        steps = steps or a.steps
+        warmup = a.warmup if warmup is None else warmup
+        pl = pools if sh == shard else [stage(r, d, sh) for r, d in zip(ranks, devs)]
+        models, opts, bucketed = [], [], []
+        for r, d in zip(ranks, devs):
+            st = torch.cuda.current_stream(torch.device("cuda", d)).cuda_stream
+            m = nof.AcceleratedMipNeRF(device=d, max_rays=mb, num_samples=samples, seed=seed, stream=st,
+                                       precision=PRECISIONS[prec])
+            models.append(m)
+            opts.append(nof.AcceleratedAdamOptimizer(m.GetLayerSizes(), m.config))
+        if world > 1 and native is None:  # torch.distributed: bucketed, overlapped with the backward
+            bucketed = [BucketedAllReduce(models[0], dev, allreduce=allreduce)]
+        if native is not None and not single:
+            native[0].attach(models[0])  # RCCL buckets on the library's internal comm stream
+        cs = chunks(sh, mb)
 
         def step(k):
-            b = pool[k % len(pool)]
-            grads = model.get_gradient_device(n, b["o"], b["d"], b["radius"], b["near"], b["far"],
-                                              b["lossmult"], b["pix"], msum_global)
+            for i, (r, m) in enumerate(zip(ranks, models)):
+                b = pl[i][k % 2]
+                for j, (lo, hi) in enumerate(cs):
+                    m.set_rng(seed, k, r * sh + lo)  # global ray ids: sharding never changes a sample
+                    m.get_gradient_device(hi - lo, b["o"][lo:hi], b["d"][lo:hi], b["radius"][lo:hi],
+                                          b["near"][lo:hi], b["far"][lo:hi], b["lossmult"][lo:hi], b["pix"][lo:hi],
+                                          msum_global, accumulate=j > 0, publish=j == len(cs) - 1)
+            if single and G > 1:
+                NativeDP.allreduce_grads_all(native, models)
+            for m, o in zip(models, opts):
+                o.step(m.mlp.allParams, m.mlp.allGradients, nof.learning_rate_decay(k + 1))
             if native is not None:
-                native.allreduce_grads(model, stream)
-            elif world > 1:
-                allreduce(grad_view)  # sum of per-shard gradient sums (no averaging: L is a sum)
-            opt.step(params, grads, nof.learning_rate_decay(k + 1))
+                for nd in native:
+                    nd.wait()  # failure detection: an RCCL error or a stall raises instead of hanging
 
-        for k in range(a.warmup):
+        def sync_all():
+            for d in devs:
+                torch.cuda.synchronize(d)
+
+        for k in range(warmup):
             step(k)
-        torch.cuda.synchronize()
+        sync_all()
         if world > 1:
             dist.barrier()
         timers = os.environ.get("NOF_BENCH_TIMERS", "mlp_fwd")
-        model.enable_timing(True, timers=timers.split(",") if timers != "all" else None)
-        torch.cuda.synchronize()
+        models[0].enable_timing(timers_on, timers=timers.split(",") if timers != "all" else None)
+        sync_all()
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
-        for k in range(a.warmup, a.warmup + a.steps):
+        for k in range(warmup, warmup + steps):
             step(k)
-        torch.cuda.synchronize()
+        sync_all()
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
-        live = model.read_timing()
-        # per-kernel breakdown: a few more steps with every kernel class timed (outside the clock)
-        kb = min(5, a.steps)
-        model.enable_timing(True)
-        for k in range(a.warmup + a.steps, a.warmup + a.steps + kb):
-            step(k)
-        timing = {name: (ms * a.steps / kb, cnt * a.steps // kb) for name, (ms, cnt) in model.read_timing().items()}
-        for name, v in live.items():  # the live (timed-region) figures where they were taken
-            if v[1]:
-                timing[name] = v
-        model.enable_timing(False)
+        live = models[0].read_timing()
+        timing = {}
+        kb = min(5, steps) if timers_on else 0
+        if kb:  # per-kernel breakdown: a few more steps with every kernel class timed (outside the clock)
+            models[0].enable_timing(True)
+            for k in range(warmup + steps, warmup + steps + kb):
+                step(k)
+            timing = {name: (ms * steps / kb, cnt * steps // kb) for name, (ms, cnt) in models[0].read_timing().items()}
+            for name, v in live.items():  # the live (timed-region) figures where they were taken
+                if v[1]:
+                    timing[name] = v
+            models[0].enable_timing(False)
         in_sync = None
-        if world > 1:
-            t = torch.tensor([dt], device=dev, dtype=torch.float64)
-            allreduce(t, op=dist.ReduceOp.MAX)
-            dt = float(t.item())
+        if world > 1 or (single and G > 1):
+            sync_all()
             # DP invariant (SURVEY §8e): identical all-reduced gradients + identical Adam -> every
             # rank holds bitwise-identical parameters; compare a checksum's max and min over ranks
-            pptr, P = model.mlp.flat_params()
-            pv = nof.device_tensor(pptr, (P,), device=dev).view(torch.int32).to(torch.int64)
-            cs = (pv * torch.arange(1, P + 1, device=dev, dtype=torch.int64)).sum().reshape(1)
-            hi, lo = cs.clone(), -cs
-            allreduce(hi, op=dist.ReduceOp.MAX)
-            allreduce(lo, op=dist.ReduceOp.MAX)
+            sums = []
+            for m, d in zip(models, devs):
+                pptr, P = m.mlp.flat_params()
+                dv = torch.device("cuda", d)
+                pv = nof.device_tensor(pptr, (P,), device=dv).view(torch.int32).to(torch.int64)
+                sums.append((pv * torch.arange(1, P + 1, device=dv, dtype=torch.int64)).sum().reshape(1).to(dev))
+            cs_ = torch.cat(sums)
+            hi, lo = cs_.max().reshape(1), (-cs_.min()).reshape(1)
+            if world > 1:
+                t = torch.tensor([dt], device=dev, dtype=torch.float64)
+                allreduce(t, op=dist.ReduceOp.MAX)
+                dt = float(t.item())
+                allreduce(hi, op=dist.ReduceOp.MAX)
+                allreduce(lo, op=dist.ReduceOp.MAX)
             in_sync = bool(hi.item() == -lo.item())
-        # fine-level PSNR of the last step's batch (MseToPsnr, MipHelpers.cs:672)
-        last = pool[(a.warmup + a.steps + kb - 1) % len(pool)]
-        comp = model.level_numpy(len(samples) - 1)["comp_rgb"]
-        mse = float(np.mean((comp - last["pix"].cpu().numpy()) ** 2))
+        # fine-level PSNR of the last micro-batch (MseToPsnr, MipHelpers.cs:672)
+        last = pl[0][(warmup + steps + kb - 1) % 2]
+        lo_, hi_ = cs[-1]
+        comp = models[0].level_numpy(len(samples) - 1)["comp_rgb"]
+        mse = float(np.mean((comp - last["pix"][lo_:hi_].cpu().numpy()) ** 2))
         psnr = -10.0 * math.log10(max(mse, 1e-12))
-        opt.close()
-        model.close()
+        for bk in bucketed:
+            bk.close()
+        if native is not None and not single:
+            native[0].attach(None)
+        for o, m in zip(opts, models):
+            o.close()
+            m.close()
         return dt, timing, psnr, in_sync
 
-    def summarize(prec, dt, timing):
+    def summarize(prec, dt, timing, sh=shard):
         ms_step = dt * 1e3 / a.steps
-        M = [n * s for s in samples]
+        M = [sh * s for s in samples]
         flop = {"mlp_fwd": 2 * MACS_FWD * sum(M), "mlp_bwd": 2 * MACS_DX * sum(M), "wgrad": 2 * MACS_DW * sum(M)}
         kernels = {}
         for name, (ms, cnt) in timing.items():
@@ -312,46 +420,66 @@ def main():
         }
 
     dt, timing, psnr, in_sync = measure(a.precision)
-    rays_per_s = n * world * a.steps / dt
+    rays_per_s = B * a.steps / dt
     alts = []
-    if world == 1 and not a.no_alt:
+    lead = rank == 0
+    if world == 1 and G == 1 and not a.no_alt:
         alts = [(p,) + measure(p) for p in PRECISIONS if p != a.precision]
+    cfg4 = None
+    if lead and world == 1 and G == 1 and not a.no_config4 and B != 65536 and a.scene == "blender" \
+            and samples == [128, 128]:
+        # SURVEY §8(e)'s scaling denominator: config 4's 65536-ray global batch on this one GPU,
+        # micro-batched into 8192-ray calls accumulated into one gradient, one Adam step per batch
+        c_dt, _, _, _ = measure(a.precision, B_run=65536, steps=3, warmup=1, timers_on=False)
+        cfg4 = {"workload": "BASELINE configs[3] on 1 GPU: 65536-ray global batch x 128+128 samples, 8 micro-batches "
+                            "of 8192 rays accumulated, one Adam step", "value": round(65536 * 3 / c_dt, 1),
+                "unit": "rays/s", "ms_per_step": round(c_dt * 1e3 / 3, 3), "steps": 3, "warmup": 1}
 
     result = None
-    if rank == 0:
+    if lead:
         ms_step, kernels, roof = summarize(a.precision, dt, timing)
+        strong = G > 1 and a.global_batch_fixed and a.scene == "blender"
         result = {
-            "metric": METRIC, "value": round(rays_per_s, 1), "unit": "rays/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
+            "metric": METRIC, "value": round(rays_per_s, 1), "unit": "rays/s", "n_gpus": G, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None, "dtype": DTYPES[a.precision],
             "data": "synthetic (Lego-shaped 800x800, 100 poses)" if a.scene == "blender"
                     else "synthetic (forward-facing LLFF-shaped 800x800, NDC)",
-            "config": {"workload": f"{workload_name(a)}: {n}-ray batches x {'+'.join(map(str, samples))} samples, "
-                                   "8x256 MLP fwd/bwd + Adam",
-                       "rays_per_gpu": n, "global_batch": n * world, "samples": samples,
-                       "parallelism": f"dp{world}", "precision": a.precision,
-                       "allreduce": a.dp if world > 1 else None},
+            "config": {"workload": f"{workload_name(a, B)}: {B}-ray global batch x {'+'.join(map(str, samples))} "
+                                   f"samples, 8x256 MLP fwd/bwd + Adam",
+                       "global_batch": B, "rays_per_gpu": shard, "micro_batch": micro,
+                       "micro_batches_per_step": len(chunks(shard, micro)), "samples": samples,
+                       "parallelism": f"dp{G}", "precision": a.precision,
+                       "allreduce": (("native (single process, grouped)" if single else
+                                      "native (bucketed, overlapped)" if a.dp == "native" else
+                                      "torch.distributed (bucketed, overlapped)") if G > 1 else None)},
             **roof,
             "kernels": kernels,
             "psnr_fine": round(psnr, 3),
         }
-        if world > 1:
+        if G > 1:
             result["params_in_sync"] = in_sync
-            if backend != "nccl":
+            if world > 1 and backend != "nccl":
                 result["rehearsal"] = f"{backend}: {world} ranks on {torch.cuda.device_count()} GPU(s), not a scaling run"
+        if cfg4:
+            result["config4_1gpu"] = cfg4
         if alts:  # the other precision modes, same workload (split: same 1e-5 parity; f16x2: 2e-3)
             result["alt_precision"] = []
             for aprec, adt, atiming, apsnr, _ in alts:
                 ams, akernels, aroof = summarize(aprec, adt, atiming)
                 result["alt_precision"].append({
-                    "precision": aprec, "dtype": DTYPES[aprec], "value": round(n * a.steps / adt, 1),
+                    "precision": aprec, "dtype": DTYPES[aprec], "value": round(B * a.steps / adt, 1),
                     "unit": "rays/s", "ms_per_step": round(ams, 4), **aroof,
                     "kernels": {k: v["avg_launch_ms"] for k, v in akernels.items()}, "psnr_fine": round(apsnr, 3)})
-        if not a.no_integrator and world == 1:
+        if not a.no_integrator and world == 1 and G == 1:
             result["roofline_integrator"] = integrator_roofline(torch, nof, dev)
-        if not a.no_cpu_baseline and world == 1:
+        if not a.no_cpu_baseline and world == 1 and G == 1:
             result["cpu_baseline"] = cpu_baseline(samples, a.cpu_seconds)
         print(json.dumps(result), flush=True)
+    if native is not None:
+        for nd in native:
+            nd.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

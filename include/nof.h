@@ -43,7 +43,7 @@ typedef struct nof_config {
   int32_t device;                         /* HIP device ordinal (reference: cudaSetDevice(0), MNcpp:10) */
   int32_t max_rays;                       /* capacity in rays per call (reference: 1024, helpers.h:18) */
   int32_t num_levels;                     /* 2 (helpers.h:16) */
-  int32_t num_samples[NOF_MAX_LEVELS];    /* per level; 128, 128 (helpers.h:17); GPU: multiple of 64, <= 512 */
+  int32_t num_samples[NOF_MAX_LEVELS];    /* per level; 128, 128 (helpers.h:17); GPU: 64, 128, 256 or 512 */
   int32_t net_depth, net_width;           /* 8, 256 */
   int32_t net_depth_condition, net_width_condition; /* 1, 128 */
   int32_t skip_layer;                     /* 4 */
@@ -103,6 +103,33 @@ nof_status nof_mipnerf_get_gradient_device(nof_mipnerf* h, int32_t n, const floa
                                            const float* dev_nears, const float* dev_fars,
                                            const float* dev_loss_mults, const float* dev_pixels,
                                            float loss_mult_sum, float* const** out_dev_grads);
+/* Gradient flags (build extension; the reference overwrites per call, MLPcpp:101-129):
+ *   NOF_GRAD_ACCUMULATE: add this call's gradient onto the arena (level 0 included) instead of
+ *                        overwriting it -- micro-batching a large batch into several calls;
+ *   NOF_GRAD_PUBLISH:    this call completes the step's gradient: with a bucket hook set
+ *                        (nof_mipnerf_set_grad_buckets), its last level's weight gradients run as
+ *                        NOF_GRAD_BUCKETS launches in reverse layer order and the hook fires after each
+ *                        bucket's final values are enqueued, so its all-reduce overlaps the rest.
+ * nof_mipnerf_get_gradient_device == _ex with flags = NOF_GRAD_PUBLISH. */
+enum { NOF_GRAD_ACCUMULATE = 1, NOF_GRAD_PUBLISH = 2 };
+#define NOF_GRAD_BUCKETS 2
+nof_status nof_mipnerf_get_gradient_device_ex(nof_mipnerf* h, int32_t n, const float* dev_origins,
+                                              const float* dev_directions, const float* dev_radii,
+                                              const float* dev_nears, const float* dev_fars,
+                                              const float* dev_loss_mults, const float* dev_pixels,
+                                              float loss_mult_sum, uint32_t flags, float* const** out_dev_grads);
+/* Bucket hook: invoked synchronously on the calling thread, in bucket order 0..NOF_GRAD_BUCKETS-1,
+ * once the work producing the bucket's final gradient values has been enqueued on the model's
+ * stream.  spans: (offset, count) in floats into the flat gradient arena; bucket 0 = W5..W10,
+ * bucket 1 = W0..W4 and all biases.  Typical use: make a communication stream wait on the model
+ * stream and enqueue the spans' all-reduce there.  fn = NULL removes the hook. */
+typedef void (*nof_grad_bucket_fn)(void* user, int32_t bucket, int32_t nspans, const int64_t* span_offsets,
+                                   const int64_t* span_counts);
+nof_status nof_mipnerf_set_grad_buckets(nof_mipnerf* h, nof_grad_bucket_fn fn, void* user);
+/* The spans the hook receives, from the 2L layer sizes of get_layer_sizes (host only; offsets and
+ * counts hold at least 2 entries each). */
+nof_status nof_grad_bucket_spans(int32_t bucket, const int32_t* layer_sizes, int32_t count, int64_t* offsets,
+                                 int64_t* counts, int32_t* nspans);
 /* GetLayerSizes MNcpp:146-149 -> get_layer_sizes MLPcpp:131-154 */
 nof_status nof_mipnerf_layer_sizes(nof_mipnerf* h, int32_t* out, int32_t cap, int32_t* count);
 /* public field `mlp` (AcceleratedMipNeRF.h:18), borrowed */
@@ -203,12 +230,27 @@ nof_status nof_checkpoint_load(const char* path, nof_mipnerf* h, nof_adam* adam)
  *                        n all-reduces. */
 typedef struct nof_dp nof_dp;
 nof_status nof_dp_unique_id(uint8_t id[128]);
+/* Communicators are non-blocking: initialisation waits at most timeout_ms for every rank to join
+ * (0 = NOF_DP_TIMEOUT_MS from the environment, else 300 s), then aborts and returns NOF_ERR_RCCL. */
 nof_status nof_dp_init_rank(const uint8_t id[128], int32_t world, int32_t rank, int32_t device, nof_dp** out);
+nof_status nof_dp_init_rank_timeout(const uint8_t id[128], int32_t world, int32_t rank, int32_t device,
+                                    int32_t timeout_ms, nof_dp** out);
 nof_status nof_dp_init_all(int32_t ndev, const int32_t* devices, nof_dp** out /* ndev handles */);
 nof_status nof_dp_allreduce(nof_dp* dp, float* dev_buf, int64_t count, void* stream);
 /* all-reduce of the model's gradient arena on its stream (or streams[i]) */
 nof_status nof_dp_allreduce_grads(nof_dp* dp, nof_mipnerf* h, void* stream);
 nof_status nof_dp_allreduce_grads_all(int32_t n, nof_dp* const* dps, nof_mipnerf* const* hs, void* const* streams);
+/* Overlapped mode: installs the model's bucket hook (nof_mipnerf_set_grad_buckets) so that every
+ * NOF_GRAD_PUBLISH call all-reduces each bucket on comm_stream (NULL = an internal stream) as soon
+ * as it is final, and the model's stream waits for the last one (work enqueued after the call, e.g.
+ * Adam, sees the reduced gradient).  h = NULL detaches. */
+nof_status nof_dp_attach(nof_dp* dp, nof_mipnerf* h, void* comm_stream);
+/* Failure detection: waits until the last all-reduce enqueued through dp has completed, polling
+ * ncclCommGetAsyncError; on an asynchronous RCCL error or after timeout_ms (0 = the init timeout)
+ * the communicator is aborted and NOF_ERR_RCCL returned.  Every later call on an aborted dp
+ * returns NOF_ERR_RCCL (never hangs). */
+nof_status nof_dp_wait(nof_dp* dp, int32_t timeout_ms);
+nof_status nof_dp_abort(nof_dp* dp);
 nof_status nof_dp_destroy(nof_dp* dp);
 
 /* Image metrics on device images [H][W][3] (float, any range; max_val as MathHelpers' maxVal):
@@ -228,6 +270,9 @@ nof_status nof_mlp_get_output(nof_mlp* m, const float* dev_enc_pos, const float*
  * level 0 overwrites the gradient arena, level > 0 accumulates (sum over levels, D10). */
 nof_status nof_mlp_get_gradient(nof_mlp* m, const float* dev_color_grad, const float* dev_density_grad,
                                 int32_t level, float* const** out_dev_grads);
+/* ... with NOF_GRAD_* flags (ACCUMULATE: level 0 accumulates too; PUBLISH: see above) */
+nof_status nof_mlp_get_gradient_ex(nof_mlp* m, const float* dev_color_grad, const float* dev_density_grad,
+                                   int32_t level, uint32_t flags, float* const** out_dev_grads);
 /* allParams / allGradients (AcceleratedMLP.h:24-25): 22 views into one flat arena */
 nof_status nof_mlp_params(nof_mlp* m, float* const** out);
 nof_status nof_mlp_grads(nof_mlp* m, float* const** out);

@@ -104,6 +104,28 @@ nof_status nof_mipnerf_get_gradient_device(nof_mipnerf* h, int32_t n, const floa
     *out_dev_grads = h->impl->GetGradientDevice(n, o, d, radii, nears, fars, lm, pix, msum);
   });
 }
+nof_status nof_mipnerf_get_gradient_device_ex(nof_mipnerf* h, int32_t n, const float* o, const float* d,
+                                              const float* radii, const float* nears, const float* fars,
+                                              const float* lm, const float* pix, float msum, uint32_t flags,
+                                              float* const** out_dev_grads) {
+  return guard([&] {
+    ARG(h && out_dev_grads);
+    *out_dev_grads = h->impl->GetGradientDevice(n, o, d, radii, nears, fars, lm, pix, msum, flags);
+  });
+}
+nof_status nof_grad_bucket_spans(int32_t bucket, const int32_t* layer_sizes, int32_t count, int64_t* offsets,
+                                 int64_t* counts, int32_t* nspans) {
+  return guard([&] {
+    ARG(layer_sizes && count > 0 && count % 2 == 0 && offsets && counts && nspans);
+    *nspans = grad_bucket_spans(layer_sizes, count / 2, bucket, offsets, counts);
+  });
+}
+nof_status nof_mipnerf_set_grad_buckets(nof_mipnerf* h, nof_grad_bucket_fn fn, void* user) {
+  return guard([&] {
+    ARG(h);
+    h->impl->mlp->set_bucket_hook(fn, user);
+  });
+}
 static void copy_sizes(const std::vector<int>& s, int32_t* out, int32_t cap, int32_t* count) {
   if (count) *count = (int32_t)s.size();
   if (out) {
@@ -200,7 +222,20 @@ nof_status nof_dp_unique_id(uint8_t id[128]) {
   return guard([&] { ARG(id); dp_unique_id(id); });
 }
 nof_status nof_dp_init_rank(const uint8_t id[128], int32_t world, int32_t rank, int32_t device, nof_dp** out) {
-  return guard([&] { ARG(id && out); *out = dp_init_rank(id, world, rank, device); });
+  return guard([&] { ARG(id && out); *out = dp_init_rank(id, world, rank, device, 0); });
+}
+nof_status nof_dp_init_rank_timeout(const uint8_t id[128], int32_t world, int32_t rank, int32_t device,
+                                    int32_t timeout_ms, nof_dp** out) {
+  return guard([&] { ARG(id && out && timeout_ms >= 0); *out = dp_init_rank(id, world, rank, device, timeout_ms); });
+}
+nof_status nof_dp_attach(nof_dp* dp, nof_mipnerf* h, void* comm_stream) {
+  return guard([&] { dp_attach(dp, h ? h->impl : nullptr, (hipStream_t)comm_stream); });
+}
+nof_status nof_dp_wait(nof_dp* dp, int32_t timeout_ms) {
+  return guard([&] { ARG(timeout_ms >= 0); dp_wait(dp, timeout_ms); });
+}
+nof_status nof_dp_abort(nof_dp* dp) {
+  return guard([&] { dp_abort(dp); });
 }
 nof_status nof_dp_init_all(int32_t ndev, const int32_t* devices, nof_dp** out) {
   return guard([&] { dp_init_all(ndev, devices, out); });
@@ -263,6 +298,10 @@ nof_status nof_mlp_get_output(nof_mlp* m, const float* enc_pos, const float* enc
 nof_status nof_mlp_get_gradient(nof_mlp* m, const float* color_grad, const float* density_grad, int32_t level,
                                 float* const** out) {
   return guard([&] { ARG(m && out); *out = M(m)->get_gradient(color_grad, density_grad, level); });
+}
+nof_status nof_mlp_get_gradient_ex(nof_mlp* m, const float* color_grad, const float* density_grad, int32_t level,
+                                   uint32_t flags, float* const** out) {
+  return guard([&] { ARG(m && out); *out = M(m)->get_gradient(color_grad, density_grad, level, flags); });
 }
 nof_status nof_mlp_params(nof_mlp* m, float* const** out) {
   return guard([&] { ARG(m && out); *out = M(m)->allParams(); });

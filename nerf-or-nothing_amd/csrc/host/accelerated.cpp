@@ -228,17 +228,42 @@ nof_mlp_debug AcceleratedMLP::debug_view(int level) const {
   return d;
 }
 
-AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M) {
+int grad_bucket_spans(const int* sizes, int num_layers, int b, int64_t* off, int64_t* cnt) {
+  // arena [W0..W(L-1), b0..b(L-1)] (MLPcpp:131-154); bucket 0 = W5..W(L-1), bucket 1 = the rest
+  NOF_REQUIRE(sizes && num_layers > 5 && b >= 0 && b < AcceleratedMLP::kBuckets, "bad bucket query");
+  int64_t w5 = 0, wend = 0, total = 0;
+  for (int l = 0; l < num_layers; ++l) {
+    if (l < 5) w5 += sizes[l];
+    wend += sizes[l];
+    total += sizes[l] + sizes[num_layers + l];
+  }
+  if (b == 0) {
+    off[0] = w5; cnt[0] = wend - w5;
+    return 1;
+  }
+  off[0] = 0; cnt[0] = w5;
+  off[1] = wend; cnt[1] = total - wend;
+  return 2;
+}
+
+int AcceleratedMLP::bucket_spans(int b, int64_t* off, int64_t* cnt) const {
+  const std::vector<int> s = get_layer_sizes();
+  return grad_bucket_spans(s.data(), kLayers, b, off, cnt);
+}
+
+AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M, int bucket) {
   Level& L = lv_[level];
-  auto it = L.sched.find(M);
+  auto it = L.sched.find({M, bucket});
   if (it != L.sched.end()) return it->second;
   const int nblk = M / kBlk;
   const size_t ls = (size_t)nblk * 256 * kBlk;
   std::vector<nof::WgProblem> P;
-  auto prob = [&](const float* A, int FA, int a0, int ntr, const float* B, int FB, int b0, int ntc) {
+  std::vector<int> pbucket;  // bucket of each problem's outputs: layers 5..10 -> 0, 0..4 -> 1
+  auto prob = [&](int layer, const float* A, int FA, int a0, int ntr, const float* B, int FB, int b0, int ntc) {
     nof::WgProblem p;
     p.A = A; p.FA = FA; p.a_row0 = a0; p.ntr = ntr; p.B = B; p.FB = FB; p.b_col0 = b0; p.ntc = ntc; p.shape = 0;
     P.push_back(p);
+    pbucket.push_back(layer >= 5 ? 0 : 1);
     return (int)P.size() - 1;
   };
   struct OutSpec { int prob, row_off, nrows, col_off, ncols; float* dst; int ld, dst_col; float* bias; };
@@ -252,23 +277,34 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M) {
   auto Wg = [&](int l) { return G + woff_[l]; };
   auto Bg = [&](int l) { return G + boff_[l]; };
   int p;
-  p = prob(delta_.p, 256, 0, 8, L.act_in.p, nof::kInF, 0, 3);
+  p = prob(0, delta_.p, 256, 0, 8, L.act_in.p, nof::kInF, 0, 3);
   os.push_back({p, 0, 256, 0, 96, Wg(0), 96, 0, Bg(0)});
   for (int l = 1; l < 8; ++l) {
-    p = prob(at(delta_.p, l * ls), 256, 0, 8, at(L.act_h.p, (l - 1) * ls), 256, 0, 8);
+    p = prob(l, at(delta_.p, l * ls), 256, 0, 8, at(L.act_h.p, (l - 1) * ls), 256, 0, 8);
     os.push_back({p, 0, 256, 0, 256, Wg(l), in_[l], 0, Bg(l)});
     if (l == 4) {
-      p = prob(at(delta_.p, l * ls), 256, 0, 8, L.act_in.p, nof::kInF, 0, 3);
+      p = prob(4, at(delta_.p, l * ls), 256, 0, 8, L.act_in.p, nof::kInF, 0, 3);
       os.push_back({p, 0, 256, 0, 96, Wg(4), in_[4], 256, nullptr});
     }
   }
-  p = prob(delta9x_.p, nof::kD9F, 0, 5, at(L.act_h.p, 7 * ls), 256, 0, 8);
+  p = prob(9, delta9x_.p, nof::kD9F, 0, 5, at(L.act_h.p, 7 * ls), 256, 0, 8);
   os.push_back({p, 0, 128, 0, 256, Wg(9), in_[9], 0, Bg(9)});
   os.push_back({p, 128, 1, 0, 256, Wg(8), in_[8], 0, Bg(8)});
-  p = prob(delta9x_.p, nof::kD9F, 0, 4, L.act_in.p, nof::kInF, 96, 1);
+  p = prob(9, delta9x_.p, nof::kD9F, 0, 4, L.act_in.p, nof::kInF, 96, 1);
   os.push_back({p, 0, 128, 0, 27, Wg(9), in_[9], 256, nullptr});
-  p = prob(delta9x_.p, nof::kD9F, 128, 1, L.act_h9.p, 128, 0, 4);
+  p = prob(10, delta9x_.p, nof::kD9F, 128, 1, L.act_h9.p, 128, 0, 4);
   os.push_back({p, 1, 3, 0, 128, Wg(10), in_[10], 0, Bg(10)});
+  if (bucket >= 0) {  // keep only this bucket's problems (and their outputs), renumbered
+    std::vector<int> remap(P.size(), -1);
+    std::vector<nof::WgProblem> Pb;
+    for (size_t i = 0; i < P.size(); ++i)
+      if (pbucket[i] == bucket) { remap[i] = (int)Pb.size(); Pb.push_back(P[i]); }
+    std::vector<OutSpec> ob;
+    for (OutSpec s : os)
+      if (remap[s.prob] >= 0) { s.prob = remap[s.prob]; ob.push_back(s); }
+    P.swap(Pb);
+    os.swap(ob);
+  }
 
   // cost per k-block, calibrated against per-item timings (NOF_DIAG_WG_TIME builds,
   // tools/diag_item_time.py).  fp32 (k_wgrad, MFMA-bound): wgrad_block_cost.  f16x2 (k_wgrad_h, an
@@ -351,7 +387,7 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M) {
     outs.push_back(o);
     max_elems = std::max(max_elems, s.nrows * s.ncols);
   }
-  Schedule& sc = L.sched[M];
+  Schedule& sc = L.sched[{M, bucket}];
   sc.probs.alloc(P.size());
   sc.items.alloc(items.size());
   sc.item_ptr.alloc(item_ptr.size());
@@ -368,12 +404,36 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M) {
   return sc;
 }
 
-float* const* AcceleratedMLP::get_gradient(const float* color_grad, const float* density_grad, int level) {
+void AcceleratedMLP::run_wgrad(Schedule& sc, int accumulate) {
+  tb(kTWgrad);
+  if (precision_ != NOF_PRECISION_F32)
+    NOF_HIP(nof::launch_wgrad_x3(sc.probs.p, sc.items.p, sc.item_ptr.p, sc.num_wg, sc.slab_off.p, slabs_.p,
+                                 bias_slabs_.p, precision_, st_));
+  else
+    NOF_HIP(nof::launch_wgrad(sc.probs.p, sc.items.p, sc.item_ptr.p, sc.num_wg, sc.slab_off.p, slabs_.p,
+                              bias_slabs_.p, st_));
+  te(kTWgrad);
+  tb(kTWgradReduce);
+  NOF_HIP(nof::launch_wgrad_reduce(sc.outs.p, sc.nouts, sc.max_elems, sc.items.p, sc.probs.p, sc.slab_off.p,
+                                   slabs_.p, bias_slabs_.p, accumulate,
+                                   precision_ == NOF_PRECISION_F16X2 ? amax_.p : nullptr, st_));
+  te(kTWgradReduce);
+}
+
+float* const* AcceleratedMLP::get_gradient(const float* color_grad, const float* density_grad, int level,
+                                           uint32_t flags) {
   NOF_REQUIRE(level >= 0 && level < (int)lv_.size(), "level out of range");
   Level& L = lv_[level];
   NOF_REQUIRE(L.M > 0, "get_gradient before get_output for this level");
   NOF_REQUIRE(color_grad && density_grad, "null output gradients");
-  Schedule& sc = schedule(level, L.M);
+  NOF_REQUIRE((flags & ~(uint32_t)(NOF_GRAD_ACCUMULATE | NOF_GRAD_PUBLISH)) == 0, "unknown gradient flags");
+  const bool buckets = (flags & NOF_GRAD_PUBLISH) && hook_;
+  // build every schedule this call needs before the first launch (a schedule may grow the slabs,
+  // which synchronises the stream)
+  Schedule* whole = buckets ? nullptr : &schedule(level, L.M);
+  Schedule* part[kBuckets] = {};
+  if (buckets)
+    for (int b = 0; b < kBuckets; ++b) part[b] = &schedule(level, L.M, b);
   nof::BwdArgs b{};
   b.M = L.M;
   b.split = precision_;
@@ -388,19 +448,18 @@ float* const* AcceleratedMLP::get_gradient(const float* color_grad, const float*
   tb(kTMlpBwd);
   NOF_HIP(nof::launch_mlp_bwd(b, st_));
   te(kTMlpBwd);
-  tb(kTWgrad);
-  if (precision_ != NOF_PRECISION_F32)
-    NOF_HIP(nof::launch_wgrad_x3(sc.probs.p, sc.items.p, sc.item_ptr.p, sc.num_wg, sc.slab_off.p, slabs_.p,
-                                 bias_slabs_.p, precision_, st_));
-  else
-    NOF_HIP(nof::launch_wgrad(sc.probs.p, sc.items.p, sc.item_ptr.p, sc.num_wg, sc.slab_off.p, slabs_.p,
-                              bias_slabs_.p, st_));
-  te(kTWgrad);
-  tb(kTWgradReduce);
-  NOF_HIP(nof::launch_wgrad_reduce(sc.outs.p, sc.nouts, sc.max_elems, sc.items.p, sc.probs.p, sc.slab_off.p,
-                                   slabs_.p, bias_slabs_.p, level > 0 ? 1 : 0,
-                                   precision_ == NOF_PRECISION_F16X2 ? amax_.p : nullptr, st_));
-  te(kTWgradReduce);
+  const int accumulate = (level > 0 || (flags & NOF_GRAD_ACCUMULATE)) ? 1 : 0;
+  if (!buckets) {
+    run_wgrad(*whole, accumulate);
+  } else {
+    // reverse layer order: the hook's all-reduce of layers 5..10 overlaps the layer-0..4 launch
+    for (int bk = 0; bk < kBuckets; ++bk) {
+      run_wgrad(*part[bk], accumulate);
+      int64_t off[2], cnt[2];
+      const int ns = bucket_spans(bk, off, cnt);
+      hook_(hook_user_, bk, ns, off, cnt);
+    }
+  }
   return grad_views_.data();
 }
 
@@ -442,21 +501,22 @@ float* const* AcceleratedMipNeRF::GetGradient(int n, const float* origins, const
   NOF_HIP(hipMemcpyAsync(nears_.p, nears, n * sizeof(float), hipMemcpyHostToDevice, st_));
   NOF_HIP(hipMemcpyAsync(fars_.p, fars, n * sizeof(float), hipMemcpyHostToDevice, st_));
   NOF_HIP(hipMemcpyAsync(lm_.p, loss_mults, n * sizeof(float), hipMemcpyHostToDevice, st_));
-  return run(n, o_.p, d_.p, radii_.p, nears_.p, fars_.p, lm_.p, nullptr, msum, cb, user);
+  return run(n, o_.p, d_.p, radii_.p, nears_.p, fars_.p, lm_.p, nullptr, msum, cb, user, NOF_GRAD_PUBLISH);
 }
 
 float* const* AcceleratedMipNeRF::GetGradientDevice(int n, const float* o, const float* d, const float* radii,
                                                     const float* nears, const float* fars, const float* loss_mults,
-                                                    const float* pixels, float msum) {
+                                                    const float* pixels, float msum, uint32_t flags) {
   NOF_REQUIRE(n > 0 && n <= cfg_.max_rays, "ray count out of range");
   NOF_REQUIRE(o && d && radii && nears && fars && loss_mults && pixels, "null argument");
   NOF_REQUIRE(msum > 0.0f, "loss_mult_sum must be > 0");
-  return run(n, o, d, radii, nears, fars, loss_mults, pixels, msum, nullptr, nullptr);
+  NOF_REQUIRE((flags & ~(uint32_t)(NOF_GRAD_ACCUMULATE | NOF_GRAD_PUBLISH)) == 0, "unknown gradient flags");
+  return run(n, o, d, radii, nears, fars, loss_mults, pixels, msum, nullptr, nullptr, flags);
 }
 
 float* const* AcceleratedMipNeRF::run(int n, const float* o, const float* d, const float* radii, const float* nears,
                                       const float* fars, const float* lm, const float* pix, float msum,
-                                      nof_output_grad_fn cb, void* user) {
+                                      nof_output_grad_fn cb, void* user, uint32_t flags) {
   const int L = cfg_.num_levels;
   mlp->pack_weights();
   for (int lv = 0; lv < L; ++lv) {  // MNcpp:85-123
@@ -492,7 +552,10 @@ float* const* AcceleratedMipNeRF::run(int n, const float* o, const float* d, con
     timer.end(kTRenderBwd);
   }
   float* const* grads = nullptr;
-  for (int lv = 0; lv < L; ++lv) grads = mlp->get_gradient(drgb_[lv].p, dsig_[lv].p, lv);  // MNcpp:135-142
+  for (int lv = 0; lv < L; ++lv) {  // MNcpp:135-142; level 0 overwrites unless accumulating
+    const uint32_t f = (lv == 0 ? (flags & NOF_GRAD_ACCUMULATE) : 0u) | (lv == L - 1 ? (flags & NOF_GRAD_PUBLISH) : 0u);
+    grads = mlp->get_gradient(drgb_[lv].p, dsig_[lv].p, lv, f);
+  }
   last_n_ = n;
   last_fused_ = cb == nullptr;
   ++step_;

@@ -100,8 +100,16 @@ class AcceleratedMLP {
   // get_output (MLPcpp:214-255), encoded inputs.  Returns {density, rgb}.
   std::pair<float*, float*> get_output(const float* enc_pos, const float* enc_dir, int level, int n_rays,
                                        int samples);
-  // get_gradient (MLPcpp:256-321); level 0 overwrites, level > 0 accumulates.
-  float* const* get_gradient(const float* color_grad, const float* density_grad, int level);
+  // get_gradient (MLPcpp:256-321); level 0 overwrites, level > 0 accumulates.  flags
+  // (NOF_GRAD_*): ACCUMULATE adds level 0 onto the arena too (micro-batching); PUBLISH marks the
+  // call that completes the step's gradient: with a bucket hook set, its weight gradients run as
+  // kBuckets launches in reverse layer order and the hook fires after each one is enqueued.
+  float* const* get_gradient(const float* color_grad, const float* density_grad, int level, uint32_t flags = 0);
+  static constexpr int kBuckets = 2;
+  void set_bucket_hook(nof_grad_bucket_fn fn, void* user) { hook_ = fn; hook_user_ = user; }
+  bool has_bucket_hook() const { return hook_ != nullptr; }
+  // arena spans (offset, count) of bucket b: 0 = W5..W10; 1 = W0..W4 and every bias
+  int bucket_spans(int b, int64_t* off, int64_t* cnt) const;
 
   float* const* allParams() const { return param_views_.data(); }
   float* const* allGradients() const { return grad_views_.data(); }
@@ -132,10 +140,15 @@ class AcceleratedMLP {
     int cap = 0, M = 0, n = 0, S = 0;
     DevBuf<float> act_in, act_h, act_h9, zhead, sigma, rgb;
     DevBuf<uint32_t> masks;
-    std::map<int, Schedule> sched;  // by M
+    std::map<std::pair<int, int>, Schedule> sched;  // by (M, bucket)
   };
   void run_forward(int level, const nof::FwdArgs& a);
-  Schedule& schedule(int level, int M);
+  // weight-gradient schedule of `level` at M samples: bucket -1 = every problem, b >= 0 = the
+  // problems whose outputs belong to bucket b (see bucket_spans)
+  Schedule& schedule(int level, int M, int bucket = -1);
+  void run_wgrad(Schedule& sc, int accumulate);
+  nof_grad_bucket_fn hook_ = nullptr;
+  void* hook_user_ = nullptr;
   void tb(int id) { if (timer) timer->begin(id); }
   void te(int id) { if (timer) timer->end(id); }
 
@@ -154,6 +167,10 @@ class AcceleratedMLP {
   size_t slab_cap_ = 0;
 };
 
+// Gradient-arena spans (offset, count) of bucket b for layer sizes [W sizes..., b sizes...] of
+// num_layers layers; returns the span count (host only, no device needed).
+int grad_bucket_spans(const int* sizes, int num_layers, int b, int64_t* off, int64_t* cnt);
+
 // ---------------------------------------------------------------------------------------------
 // AcceleratedMipNeRF (AcceleratedMipNeRF.h:10-41; MNcpp:7-176)
 // ---------------------------------------------------------------------------------------------
@@ -167,7 +184,8 @@ class AcceleratedMipNeRF {
                             const float* nears, const float* fars, const float* loss_mults, nof_output_grad_fn cb,
                             void* user);
   float* const* GetGradientDevice(int n, const float* o, const float* d, const float* radii, const float* nears,
-                                  const float* fars, const float* loss_mults, const float* pixels, float msum);
+                                  const float* fars, const float* loss_mults, const float* pixels, float msum,
+                                  uint32_t flags = NOF_GRAD_PUBLISH);
   std::vector<int> GetLayerSizes() const { return mlp->get_layer_sizes(); }
 
   void set_rng(uint64_t seed, uint32_t step, uint32_t ray_base) { seed_ = seed; step_ = step; ray_base_ = ray_base; }
@@ -184,7 +202,7 @@ class AcceleratedMipNeRF {
  private:
   float* const* run(int n, const float* o, const float* d, const float* radii, const float* nears,
                     const float* fars, const float* lm, const float* pix, float msum, nof_output_grad_fn cb,
-                    void* user);
+                    void* user, uint32_t flags);
   nof_config cfg_;
   hipStream_t st_;
   uint64_t seed_;

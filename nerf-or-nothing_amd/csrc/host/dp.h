@@ -4,9 +4,12 @@
 
 namespace AcceleratedNeRFUtils {
 void dp_unique_id(uint8_t out[128]);
-nof_dp* dp_init_rank(const uint8_t id[128], int world, int rank, int device);
+nof_dp* dp_init_rank(const uint8_t id[128], int world, int rank, int device, int timeout_ms);
 void dp_init_all(int ndev, const int* devices, nof_dp** out);
 void dp_allreduce(nof_dp* dp, float* buf, int64_t count, hipStream_t st);
 void dp_allreduce_grads(int n, nof_dp* const* dps, AcceleratedMipNeRF* const* models, hipStream_t const* streams);
+void dp_attach(nof_dp* dp, AcceleratedMipNeRF* model, hipStream_t comm_stream);
+void dp_wait(nof_dp* dp, int timeout_ms);
+void dp_abort(nof_dp* dp);
 void dp_destroy(nof_dp* dp);
 }  // namespace AcceleratedNeRFUtils

@@ -18,6 +18,7 @@ from .api import (  # noqa: F401
     device_count,
     device_tensor,
     generate_rays,
+    grad_bucket_spans,
     image_metrics,
     learning_rate_decay,
     to_numpy,

@@ -61,6 +61,8 @@ class nof_batch(C.Structure):
 
 
 OUTPUT_GRAD_FN = C.CFUNCTYPE(C.c_uint64, C.c_void_p, C.c_uint64, C.c_int32, C.c_float, C.c_uint64)
+GRAD_BUCKET_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64))
+NOF_GRAD_ACCUMULATE, NOF_GRAD_PUBLISH, NOF_GRAD_BUCKETS = 1, 2, 2
 
 P = C.c_void_p
 F = C.c_float
@@ -78,6 +80,10 @@ SIGNATURES = {
     "nof_mipnerf_destroy": [P],
     "nof_mipnerf_get_gradient": [P, I32, P, P, P, P, P, P, OUTPUT_GRAD_FN, P, C.POINTER(PP)],
     "nof_mipnerf_get_gradient_device": [P, I32, P, P, P, P, P, P, P, F, C.POINTER(PP)],
+    "nof_mipnerf_get_gradient_device_ex": [P, I32, P, P, P, P, P, P, P, F, U32, C.POINTER(PP)],
+    "nof_mipnerf_set_grad_buckets": [P, GRAD_BUCKET_FN, P],
+    "nof_grad_bucket_spans": [I32, C.POINTER(I32), I32, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                              C.POINTER(I32)],
     "nof_mipnerf_layer_sizes": [P, C.POINTER(I32), I32, C.POINTER(I32)],
     "nof_mipnerf_mlp": [P, C.POINTER(P)],
     "nof_mipnerf_set_rng": [P, U64, U32, U32],
@@ -96,6 +102,10 @@ SIGNATURES = {
     "nof_recenter_poses": [P, I32],
     "nof_dp_unique_id": [P],
     "nof_dp_init_rank": [P, I32, I32, I32, C.POINTER(P)],
+    "nof_dp_init_rank_timeout": [P, I32, I32, I32, I32, C.POINTER(P)],
+    "nof_dp_attach": [P, P, P],
+    "nof_dp_wait": [P, I32],
+    "nof_dp_abort": [P],
     "nof_dp_init_all": [I32, C.POINTER(I32), C.POINTER(P)],
     "nof_dp_allreduce": [P, P, C.c_int64, P],
     "nof_dp_allreduce_grads": [P, P, P],
@@ -108,6 +118,7 @@ SIGNATURES = {
     "nof_mipnerf_read_timing": [P, C.POINTER(F), C.POINTER(I32), I32],
     "nof_mlp_get_output": [P, P, P, I32, I32, I32, C.POINTER(U64), C.POINTER(U64)],
     "nof_mlp_get_gradient": [P, P, P, I32, C.POINTER(PP)],
+    "nof_mlp_get_gradient_ex": [P, P, P, I32, U32, C.POINTER(PP)],
     "nof_mlp_params": [P, C.POINTER(PP)],
     "nof_mlp_grads": [P, C.POINTER(PP)],
     "nof_mlp_flat_params": [P, C.POINTER(P), C.POINTER(C.c_int64)],

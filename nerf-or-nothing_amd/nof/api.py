@@ -76,10 +76,14 @@ class AcceleratedMLP:
              C.byref(r))
         return d.value, r.value
 
-    def get_gradient(self, color_gradient, density_gradient, level: int) -> list[int]:
-        """MLPcpp:256-321 -> 22 device gradient pointers."""
+    def get_gradient(self, color_gradient, density_gradient, level: int, flags: int | None = None) -> list[int]:
+        """MLPcpp:256-321 -> 22 device gradient pointers (flags: NOF_GRAD_* bits)."""
         pp = L.PP()
-        call("nof_mlp_get_gradient", self._h, _ptr(color_gradient), _ptr(density_gradient), level, C.byref(pp))
+        if flags is None:
+            call("nof_mlp_get_gradient", self._h, _ptr(color_gradient), _ptr(density_gradient), level, C.byref(pp))
+        else:
+            call("nof_mlp_get_gradient_ex", self._h, _ptr(color_gradient), _ptr(density_gradient), level, flags,
+                 C.byref(pp))
         return _ptr_list(pp, self.NUM_TENSORS)
 
     @property
@@ -148,6 +152,8 @@ class AcceleratedMipNeRF:
 
     def __init__(self, config: L.nof_config | None = None, **overrides):
         self.config = config if config is not None else L.default_config(**overrides)
+        self._hook_errors = []
+        self._bucket_cb = None
         h = C.c_void_p()
         call("nof_mipnerf_create", C.byref(self.config), C.byref(h))
         self._h = h
@@ -187,12 +193,41 @@ class AcceleratedMipNeRF:
         L.check(st, "nof_mipnerf_get_gradient")
         return _ptr_list(pp, AcceleratedMLP.NUM_TENSORS)
 
-    def get_gradient_device(self, n, origins, directions, radii, nears, fars, loss_mults, pixels, loss_mult_sum):
-        """All inputs device-resident (ints or torch tensors); loss gradient fused into the integrator."""
+    def get_gradient_device(self, n, origins, directions, radii, nears, fars, loss_mults, pixels, loss_mult_sum,
+                            accumulate: bool = False, publish: bool = True):
+        """All inputs device-resident (ints or torch tensors); loss gradient fused into the integrator.
+        accumulate: add onto the gradient arena (micro-batching); publish: this call completes the
+        step's gradient (fires the bucket hook, if one is set)."""
         pp = L.PP()
-        call("nof_mipnerf_get_gradient_device", self._h, n, _ptr(origins), _ptr(directions), _ptr(radii),
-             _ptr(nears), _ptr(fars), _ptr(loss_mults), _ptr(pixels), float(loss_mult_sum), C.byref(pp))
+        self._hook_errors = []
+        args = (self._h, n, _ptr(origins), _ptr(directions), _ptr(radii), _ptr(nears), _ptr(fars), _ptr(loss_mults),
+                _ptr(pixels), float(loss_mult_sum))
+        if not accumulate and publish:
+            st = lib().nof_mipnerf_get_gradient_device(*args, C.byref(pp))
+        else:
+            flags = (L.NOF_GRAD_ACCUMULATE if accumulate else 0) | (L.NOF_GRAD_PUBLISH if publish else 0)
+            st = lib().nof_mipnerf_get_gradient_device_ex(*args, flags, C.byref(pp))
+        if self._hook_errors:
+            raise self._hook_errors[0]
+        L.check(st, "nof_mipnerf_get_gradient_device")
         return _ptr_list(pp, AcceleratedMLP.NUM_TENSORS)
+
+    def set_grad_buckets(self, fn):
+        """fn(bucket, [(offset, count), ...]) is called during every publishing get_gradient call once
+        the bucket's gradient values are enqueued on the model's stream (include/nof.h); None removes it."""
+        if fn is None:
+            self._bucket_cb = None
+            call("nof_mipnerf_set_grad_buckets", self._h, L.GRAD_BUCKET_FN(), None)
+            return
+
+        def tramp(user, bucket, nspans, offs, cnts):
+            try:
+                fn(int(bucket), [(int(offs[i]), int(cnts[i])) for i in range(nspans)])
+            except Exception as e:  # never unwind through C; re-raised after the call
+                self._hook_errors.append(e)
+
+        self._bucket_cb = L.GRAD_BUCKET_FN(tramp)  # keep the thunk alive while installed
+        call("nof_mipnerf_set_grad_buckets", self._h, self._bucket_cb, None)
 
     def GetLayerSizes(self) -> list[int]:
         out = (C.c_int32 * 64)()
@@ -447,6 +482,14 @@ def learning_rate_decay(step, lr_init=5e-4, lr_final=5e-6, max_steps=1000000, lr
                         lr_delay_mult=0.01) -> float:
     """MathHelpers.LearningRateDecay (MipHelpers.cs:758-773); defaults = TrainState.cs:54-58."""
     return float(lib().nof_lr_decay(step, lr_init, lr_final, max_steps, lr_delay_steps, lr_delay_mult))
+
+
+def grad_bucket_spans(layer_sizes, bucket: int) -> list[tuple[int, int]]:
+    """(offset, count) spans of the flat gradient arena that gradient bucket `bucket` covers."""
+    sz = (C.c_int32 * len(layer_sizes))(*layer_sizes)
+    off, cnt, ns = (C.c_int64 * 4)(), (C.c_int64 * 4)(), C.c_int32()
+    call("nof_grad_bucket_spans", bucket, sz, len(layer_sizes), off, cnt, C.byref(ns))
+    return [(off[i], cnt[i]) for i in range(ns.value)]
 
 
 def device_count() -> int:

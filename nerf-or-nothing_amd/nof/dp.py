@@ -52,12 +52,15 @@ class NativeDP:
         return bytes(buf)
 
     @classmethod
-    def init_rank(cls, uid: bytes, world: int, rank: int, device: int) -> "NativeDP":
+    def init_rank(cls, uid: bytes, world: int, rank: int, device: int, timeout_ms: int = 0) -> "NativeDP":
+        """Non-blocking communicator: waits at most timeout_ms (0 = NOF_DP_TIMEOUT_MS or 300 s) for
+        every rank, then aborts (NofError NOF_ERR_RCCL)."""
         import ctypes as C
         from ._lib import call
 
         h = C.c_void_p()
-        call("nof_dp_init_rank", (C.c_uint8 * 128).from_buffer_copy(uid), world, rank, device, C.byref(h))
+        call("nof_dp_init_rank_timeout", (C.c_uint8 * 128).from_buffer_copy(uid), world, rank, device, timeout_ms,
+             C.byref(h))
         return cls(h)
 
     @classmethod
@@ -90,9 +93,71 @@ class NativeDP:
         call("nof_dp_allreduce_grads_all", n, (C.c_void_p * n)(*[d._h.value for d in dps]),
              (C.c_void_p * n)(*[m._h.value for m in models]), st)
 
+    def attach(self, model, comm_stream=None):
+        """Overlapped mode: each publishing get_gradient call all-reduces the gradient buckets on
+        comm_stream as they complete; the model's stream waits for the last (model=None detaches)."""
+        from ._lib import call
+
+        call("nof_dp_attach", self._h, model._h if model is not None else None, comm_stream)
+
+    def wait(self, timeout_ms: int = 0):
+        """Failure detection: block until the last all-reduce is done; an RCCL error or a timeout
+        aborts the communicator and raises NofError (NOF_ERR_RCCL)."""
+        from ._lib import call
+
+        call("nof_dp_wait", self._h, timeout_ms)
+
+    def abort(self):
+        from ._lib import call
+
+        call("nof_dp_abort", self._h)
+
     def close(self):
         if getattr(self, "_h", None):
             from ._lib import lib
 
             lib().nof_dp_destroy(self._h)
             self._h = None
+
+
+class BucketedAllReduce:
+    """torch.distributed (RCCL) all-reduce of the gradient arena, bucket by bucket, overlapped with
+    the rest of the backward: installed as the model's gradient-bucket hook (include/nof.h
+    nof_mipnerf_set_grad_buckets).  Each bucket's all-reduce is enqueued on a communication stream
+    behind the model's stream; after the last bucket the model's stream waits for the
+    communication stream, so Adam (or anything else enqueued on it) sees the reduced gradient.
+    `allreduce(tensor)` defaults to dist.all_reduce (sum)."""
+
+    def __init__(self, model, device, allreduce=None):
+        import torch
+        import torch.distributed as dist
+
+        from .api import device_tensor
+
+        self.model = model
+        self.device = torch.device(device)
+        st = model.config.stream
+        self.lib_stream = (torch.cuda.ExternalStream(st, device=self.device) if st
+                           else torch.cuda.default_stream(self.device))
+        self.comm = torch.cuda.Stream(self.device)
+        gptr, P = model.mlp.flat_grads()
+        self.grad = device_tensor(gptr, (P,), device=self.device)
+        self.allreduce = allreduce or dist.all_reduce
+        self.buckets_seen = []
+        model.set_grad_buckets(self._hook)
+
+    def _hook(self, bucket, spans):
+        import torch
+
+        from ._lib import NOF_GRAD_BUCKETS
+
+        self.buckets_seen.append(bucket)
+        self.comm.wait_stream(self.lib_stream)
+        with torch.cuda.stream(self.comm):
+            for off, cnt in spans:
+                self.allreduce(self.grad[off:off + cnt])
+        if bucket == NOF_GRAD_BUCKETS - 1:
+            self.lib_stream.wait_stream(self.comm)
+
+    def close(self):
+        self.model.set_grad_buckets(None)

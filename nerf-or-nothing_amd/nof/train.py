@@ -45,8 +45,15 @@ class Trainer:
         self.params = self.model.mlp.allParams
         self.step_idx = 0  # completed steps (Program.cs counts from 1)
         self.device = device
-        self._grad_view = None
         self.last_loss = None
+        # data parallel: the gradient arena is all-reduced bucket by bucket on a communication
+        # stream ordered after the library's stream (self.stream, which may be any stream), and the
+        # library's stream waits for the last bucket before Adam (nof.dp.BucketedAllReduce)
+        self._allreduce = None
+        if self.dist is not None:
+            from .dp import BucketedAllReduce
+
+            self._allreduce = BucketedAllReduce(self.model, f"cuda:{device}")
 
     # --- checkpoints -----------------------------------------------------------------------------
     def save(self, path):
@@ -71,11 +78,6 @@ class Trainer:
         p = {k: v[0] for k, v in b.items()}
         grads = self.model.get_gradient_device(self.n, p["o"], p["d"], p["radius"], p["near"], p["far"],
                                                p["lossmult"], p["pix"], msum)
-        if self.dist is not None:
-            if self._grad_view is None:
-                gptr, P = self.model.mlp.flat_grads()
-                self._grad_view = api.device_tensor(gptr, (P,), device=torch.device("cuda", self.device))
-            self.dist.all_reduce(self._grad_view)
         self.adam.step(self.params, grads, api.learning_rate_decay(step, **self.lr))
         self.step_idx = step
         if self.print_every and step % self.print_every == 0:
@@ -88,6 +90,7 @@ class Trainer:
 
     def fine_loss(self, batch) -> float:
         """Program.LossFn (Program.cs:64): sum m |C_fine - p|^2 / sum m over this rank's batch."""
+        api.call("nof_stream_sync", self.stream)  # the reads below are not ordered after self.stream
         L = self.cfg.num_levels
         C = self.model.level_numpy(L - 1)["comp_rgb"]
         pix = api.to_numpy(batch["pix"][0], (self.n, 3))

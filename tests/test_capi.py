@@ -80,3 +80,24 @@ def test_python_mirror_names():
                       ("AcceleratedAdamOptimizer", "step"), ("AcceleratedGradientCalculator", "get_output_gradient"),
                       ("OutputRetriever", "RetrieveOutput")]:
         assert hasattr(getattr(nof, cls), meth)
+
+
+def test_grad_bucket_spans_partition_the_arena():
+    """The gradient buckets of the overlapped all-reduce cover [W0..W10, b0..b10] exactly once:
+    bucket 0 = W5..W10 (the layers whose weight gradients finish first), bucket 1 = the rest."""
+    import nof
+
+    sizes = [24576, 65536, 65536, 65536, 90112, 65536, 65536, 65536, 256, 36224, 384,
+             256, 256, 256, 256, 256, 256, 256, 256, 1, 128, 3]  # MLPcpp:131-154
+    b0, b1 = nof.grad_bucket_spans(sizes, 0), nof.grad_bucket_spans(sizes, 1)
+    w5 = sum(sizes[:5])
+    assert b0 == [(w5, sum(sizes[5:11]))]
+    assert b1 == [(0, w5), (sum(sizes[:11]), sum(sizes[11:]))]
+    spans = sorted(b0 + b1)
+    pos = 0
+    for off, cnt in spans:
+        assert off == pos
+        pos += cnt
+    assert pos == sum(sizes) == 546948
+    with pytest.raises(nof.NofError):
+        nof.grad_bucket_spans(sizes, 2)

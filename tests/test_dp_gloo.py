@@ -1,5 +1,6 @@
 """World-size-2 data-parallel logic on CPU (gloo): sharded gradients with global ray ids and the
-global loss-multiplier sum, all-reduced, equal the single-process gradient of the whole batch.
+global loss-multiplier sum, all-reduced bucket by bucket in the overlapped path's order, equal the
+single-process gradient of the whole batch.
 The per-shard compute is the oracle (there is no GPU here); the sharding, normalisation and
 collective are the product's (nof.dp + torch.distributed), exactly as bench.py uses them."""
 import os
@@ -43,7 +44,14 @@ def _worker(rank, world, port, q):
     out = O.step(spec, P, shard, samples=SAMPLES, seed=11, step_idx=2, ray_base=base,
                  loss_mult_sum=dp.global_loss_mult_sum(rays), nthreads=1, want=("grads",))
     g = torch.from_numpy(out["grads"])
-    dist.all_reduce(g)
+    # the bucketed order of the overlapped all-reduce (nof.dp.BucketedAllReduce): bucket 0 (the
+    # layers whose weight gradients finish first) then bucket 1, each over its arena spans
+    sizes = [int(x) for x in O.layer_sizes(spec)]
+    import nof
+
+    for b in range(2):
+        for off, cnt in nof.grad_bucket_spans(sizes, b):
+            dist.all_reduce(g[off:off + cnt])
     loss = torch.tensor([out["loss"]], dtype=torch.float64)
     dist.all_reduce(loss)
     if rank == 0:

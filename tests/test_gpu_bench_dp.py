@@ -28,3 +28,15 @@ def test_bench_two_ranks_rehearsal(gpu):
     assert r["n_gpus"] == 2 and r["config"]["global_batch"] == 512 and r["config"]["parallelism"] == "dp2"
     assert r["params_in_sync"] is True
     assert r["value"] > 0 and "rehearsal" in r
+
+
+def test_bench_single_process_mode(gpu):
+    """--single-process: one process drives the devices through nof_dp_init_all (grouped all-reduce);
+    on the box's one GPU this is N = 1 with the 8192-ray micro-batching of a 16384-ray batch."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--single-process", "--steps", "2",
+           "--warmup", "1", "--global-batch", "16384", "--no-alt", "--no-integrator", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert r["config"]["global_batch"] == 16384 and r["config"]["micro_batches_per_step"] == 2
+    assert r["value"] > 0

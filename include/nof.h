@@ -153,6 +153,13 @@ typedef struct nof_level_view {
 nof_status nof_mipnerf_level_view(nof_mipnerf* h, int32_t level, nof_level_view* out);
 /* sum over rays and levels of lambda_l * m_r |C - p|^2 / sum m (fused path only; synchronises) */
 nof_status nof_mipnerf_loss(nof_mipnerf* h, float* out);
+/* Non-finite detection, every precision mode (the f16x2 perf mode's fp16 activation range is its
+ * stated limit: an overflow surfaces here instead of silently): NOF_NUMERIC_FORWARD = a training
+ * forward produced a non-finite composite colour; NOF_NUMERIC_DELTA = the f16x2 delta scaling saw a
+ * non-finite output gradient.  Bits accumulate until cleared (clear != 0).  Synchronises. */
+#define NOF_NUMERIC_FORWARD 1u
+#define NOF_NUMERIC_DELTA 2u
+nof_status nof_mipnerf_numeric_status(nof_mipnerf* h, uint32_t* flags, int32_t clear);
 
 /* ---- evaluation ------------------------------------------------------------
  * Forward-only two-level render: replaces MipNerfModel.Call(rays, randomized, whiteBackground)

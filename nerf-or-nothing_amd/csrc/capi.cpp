@@ -120,6 +120,12 @@ nof_status nof_grad_bucket_spans(int32_t bucket, const int32_t* layer_sizes, int
     *nspans = grad_bucket_spans(layer_sizes, count / 2, bucket, offsets, counts);
   });
 }
+nof_status nof_mipnerf_numeric_status(nof_mipnerf* h, uint32_t* flags, int32_t clear) {
+  return guard([&] {
+    ARG(h && flags);
+    *flags = h->impl->numeric_status(clear != 0);
+  });
+}
 nof_status nof_mipnerf_set_grad_buckets(nof_mipnerf* h, nof_grad_bucket_fn fn, void* user) {
   return guard([&] {
     ARG(h);

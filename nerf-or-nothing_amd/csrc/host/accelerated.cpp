@@ -20,6 +20,17 @@ void KernelTimer::enable(uint32_t mask, hipStream_t st) {
   st_ = st;
   used_ = 0;
   recs_.clear();
+  for (int i = 0; i < NOF_NUM_TIMERS; ++i) { tot_ms_[i] = 0.0f; tot_n_[i] = 0; }
+}
+void KernelTimer::fold() {
+  if (!recs_.empty()) NOF_HIP(hipEventSynchronize(recs_.back().b));
+  for (const Rec& r : recs_) {
+    float t = 0.0f;
+    NOF_HIP(hipEventElapsedTime(&t, r.a, r.b));
+    if (r.id < NOF_NUM_TIMERS) { tot_ms_[r.id] += t; tot_n_[r.id] += 1; }
+  }
+  recs_.clear();
+  used_ = 0;
 }
 hipEvent_t KernelTimer::get() {
   if (used_ == pool_.size()) {
@@ -31,6 +42,11 @@ hipEvent_t KernelTimer::get() {
 }
 void KernelTimer::begin(int id) {
   if (!((mask_ >> id) & 1u)) return;
+  if (recs_.size() >= kMaxRecs) {  // bounded pool: fold what is finished (no record is open here)
+    bool open = false;
+    for (hipEvent_t e : open_) open = open || e != nullptr;
+    if (!open) fold();
+  }
   open_[id] = get();
   NOF_HIP(hipEventRecord(open_[id], st_));
 }
@@ -42,15 +58,12 @@ void KernelTimer::end(int id) {
   open_[id] = nullptr;
 }
 void KernelTimer::read(float* ms, int* launches, int cap) {
-  for (int i = 0; i < cap; ++i) { ms[i] = 0.0f; launches[i] = 0; }
-  if (!recs_.empty()) NOF_HIP(hipEventSynchronize(recs_.back().b));
-  for (const Rec& r : recs_) {
-    float t = 0.0f;
-    NOF_HIP(hipEventElapsedTime(&t, r.a, r.b));
-    if (r.id < cap) { ms[r.id] += t; launches[r.id] += 1; }
+  fold();
+  for (int i = 0; i < cap; ++i) {
+    ms[i] = i < NOF_NUM_TIMERS ? tot_ms_[i] : 0.0f;
+    launches[i] = i < NOF_NUM_TIMERS ? tot_n_[i] : 0;
   }
-  recs_.clear();
-  used_ = 0;
+  for (int i = 0; i < NOF_NUM_TIMERS; ++i) { tot_ms_[i] = 0.0f; tot_n_[i] = 0; }
 }
 KernelTimer::~KernelTimer() {
   for (hipEvent_t e : pool_) (void)hipEventDestroy(e);
@@ -151,6 +164,8 @@ AcceleratedMLP::AcceleratedMLP(int deg_point, int deg_view, const nof_config& cf
   delta_.alloc(8 * nbm * 256 * kBlk);
   delta9x_.alloc(nbm * nof::kD9F * kBlk);
   NOF_HIP(hipMemset(delta9x_.p, 0, delta9x_.n * sizeof(float)));  // rows 132..159 stay zero
+  numeric_.alloc(2);
+  NOF_HIP(hipMemset(numeric_.p, 0, 2 * sizeof(uint32_t)));
   slab_cap_ = (size_t)(num_cu_ + 64) * 65536;
   slabs_.alloc(slab_cap_);
   bias_slabs_.alloc((size_t)(num_cu_ + 64) * 256);
@@ -438,7 +453,7 @@ float* const* AcceleratedMLP::get_gradient(const float* color_grad, const float*
   b.M = L.M;
   b.split = precision_;
   if (precision_ == NOF_PRECISION_F16X2) {
-    NOF_HIP(nof::launch_delta_amax(density_grad, color_grad, L.M, amax_.p, st_));
+    NOF_HIP(nof::launch_delta_amax(density_grad, color_grad, L.M, amax_.p, st_, numeric_.p));
     b.amax = amax_.p;
   }
   b.dsigma = density_grad; b.drgb = color_grad; b.zhead = L.zhead.p;
@@ -534,7 +549,7 @@ float* const* AcceleratedMipNeRF::run(int n, const float* o, const float* d, con
     mlp->forward_fused(lv, n, S, t_[lv].p, o, d, radii);
     timer.begin(kTRenderFwd);
     NOF_HIP(nof::launch_render_fwd(n, S, mlp->density(lv), mlp->rgb(lv), t_[lv].p, d, cfg_.white_bkgd, C_[lv].p,
-                                   w_[lv].p, st_));
+                                   w_[lv].p, st_, nullptr, nullptr, mlp->numeric_flags()));
     timer.end(kTRenderFwd);
   }
   for (int lv = 0; lv < L; ++lv) {  // MNcpp:125-134
@@ -610,6 +625,14 @@ float AcceleratedMipNeRF::loss() {
     for (float x : h) s += x;
   }
   return (float)s;
+}
+
+uint32_t AcceleratedMipNeRF::numeric_status(bool clear) {
+  uint32_t f[2];
+  NOF_HIP(hipMemcpyAsync(f, mlp->numeric_flags(), sizeof(f), hipMemcpyDeviceToHost, st_));
+  NOF_HIP(hipStreamSynchronize(st_));
+  if (clear) NOF_HIP(hipMemsetAsync(mlp->numeric_flags(), 0, sizeof(f), st_));
+  return (f[0] ? NOF_NUMERIC_FORWARD : 0u) | (f[1] ? NOF_NUMERIC_DELTA : 0u);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -62,7 +62,9 @@ struct DevBuf {
   }
 };
 
-// Per-kernel-class hipEvent timing on one stream.
+// Per-kernel-class hipEvent timing on one stream.  The event pool is bounded: past kMaxRecs open
+// records the finished ones are folded into running totals (one synchronisation), so a caller that
+// never reads does not grow it.
 class KernelTimer {
  public:
   void enable(uint32_t mask, hipStream_t st);  // bit i: timer id i
@@ -74,6 +76,10 @@ class KernelTimer {
 
  private:
   hipEvent_t get();
+  void fold();
+  static constexpr size_t kMaxRecs = 4096;
+  float tot_ms_[NOF_NUM_TIMERS] = {};
+  int tot_n_[NOF_NUM_TIMERS] = {};
   uint32_t mask_ = 0;
   hipStream_t st_ = nullptr;
   std::vector<hipEvent_t> pool_;
@@ -126,6 +132,8 @@ class AcceleratedMLP {
   KernelTimer* timer = nullptr;
   hipStream_t stream() const { return st_; }
   nof_mlp_debug debug_view(int level) const;
+  // non-finite flags: [0] forward (set by the owner's integrator), [1] output gradients (f16x2 scaling)
+  uint32_t* numeric_flags() const { return numeric_.p; }
 
  private:
   struct Schedule {
@@ -164,6 +172,7 @@ class AcceleratedMLP {
   int max_M_ = 0;
   DevBuf<float> delta_, delta9x_, slabs_, bias_slabs_;
   DevBuf<uint32_t> amax_;  // f16x2: bits of max |dsigma|, |drgb| of the level in flight (delta scale)
+  DevBuf<uint32_t> numeric_;
   size_t slab_cap_ = 0;
 };
 
@@ -192,6 +201,7 @@ class AcceleratedMipNeRF {
   void get_rng(uint64_t* seed, uint32_t* step, uint32_t* ray_base) const { *seed = seed_; *step = step_; *ray_base = ray_base_; }
   nof_level_view level_view(int level) const;
   float loss();
+  uint32_t numeric_status(bool clear);  // NOF_NUMERIC_* bits since the last clear (synchronises)
   // Forward-only two-level render (MipNerfModel.Call, MNcs:36-97, with its D22 defects fixed):
   // per level comp_rgb [n][3], distance [n], acc [n] (device, borrowed until the next call).
   // Uses the model's RNG (seed, step, ray_base) when randomized, never advances the step.

@@ -21,10 +21,11 @@ hipError_t launch_encode(int n, int S, const float* mean, const float* cov, cons
 
 // ---- render.hip (volumetric_rendering AF:318-344, get_output_gradient AF:347-361,
 //      volumetric_rendering_gradient AF:362-402) -------------------------------------------------
-// acc / dist (optional): accumulated opacity and the clamped weighted-midpoint distance (MH:472-492)
+// acc / dist (optional): accumulated opacity and the clamped weighted-midpoint distance (MH:472-492);
+// nonfinite (optional): word 0 set to 1 when a ray's composite colour is not finite
 hipError_t launch_render_fwd(int n, int S, const float* sigma, const float* rgb, const float* t, const float* d,
                              int white, float* C, float* w, hipStream_t st, float* acc = nullptr,
-                             float* dist = nullptr);
+                             float* dist = nullptr, uint32_t* nonfinite = nullptr);
 // g_ext != null: dL/dC supplied by the caller (callback path); else fused loss gradient from pix.
 hipError_t launch_render_bwd(int n, int S, const float* sigma, const float* rgb, const float* t, const float* d,
                              int white, const float* C, const float* g_ext, const float* pix,
@@ -62,8 +63,10 @@ struct BwdArgs {
   float* delta9x;  // [M/32][160][32]
 };
 hipError_t launch_mlp_bwd(const BwdArgs& a, hipStream_t st);
-// f16x2 mode: *amax = bits of max(|dsigma|, |drgb|) over M samples (clears *amax first)
-hipError_t launch_delta_amax(const float* dsigma, const float* drgb, int M, uint32_t* amax, hipStream_t st);
+// f16x2 mode: *amax = bits of max(|dsigma|, |drgb|) over M samples (clears *amax first); nonfinite
+// (optional): word 1 set to 1 when an input is not finite
+hipError_t launch_delta_amax(const float* dsigma, const float* drgb, int M, uint32_t* amax, hipStream_t st,
+                             uint32_t* nonfinite = nullptr);
 // fp32-precision kernels (v_mfma_f32_16x16x4_f32, two waves per SIMD): mlp_fwd16.hip / mlp_bwd16.hip
 hipError_t launch_mlp_fwd16(const FwdArgs& a, hipStream_t st);
 hipError_t launch_mlp_bwd16(const BwdArgs& a, hipStream_t st);

@@ -175,10 +175,15 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
 // amax of |dsigma|, |drgb| as float bits (non-negative floats order as unsigned ints); *amax must
 // be zero on entry (the launcher clears it on the stream first)
 __global__ void k_delta_amax(const float* __restrict__ dsigma, const float* __restrict__ drgb, int M,
-                             uint32_t* amax) {
+                             uint32_t* amax, uint32_t* nonfinite) {
   float v = 0.0f;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 4 * M; i += gridDim.x * blockDim.x)
-    v = fmaxf(v, fabsf(i < M ? dsigma[i] : drgb[i - M]));
+  bool bad = false;  // fmaxf drops NaN: non-finite inputs are flagged separately
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 4 * M; i += gridDim.x * blockDim.x) {
+    const float x = fabsf(i < M ? dsigma[i] : drgb[i - M]);
+    bad |= !__builtin_isfinite(x);
+    v = fmaxf(v, x);
+  }
+  if (bad && nonfinite) nonfinite[1] = 1u;  // plain store of a constant: racing writers agree
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   __shared__ float wmax[4];  // one atomic per block: 4096 same-address atomics serialise (~10 ns each)
@@ -188,11 +193,12 @@ __global__ void k_delta_amax(const float* __restrict__ dsigma, const float* __re
     atomicMax(amax, __float_as_uint(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]))));
 }
 
-hipError_t launch_delta_amax(const float* dsigma, const float* drgb, int M, uint32_t* amax, hipStream_t st) {
+hipError_t launch_delta_amax(const float* dsigma, const float* drgb, int M, uint32_t* amax, hipStream_t st,
+                             uint32_t* nonfinite) {
   hipError_t e = hipMemsetAsync(amax, 0, sizeof(uint32_t), st);
   if (e != hipSuccess || M <= 0) return e;
   const int blocks = std::min(256, (4 * M + 255) / 256);
-  hipLaunchKernelGGL(k_delta_amax, dim3(blocks), dim3(256), 0, st, dsigma, drgb, M, amax);
+  hipLaunchKernelGGL(k_delta_amax, dim3(blocks), dim3(256), 0, st, dsigma, drgb, M, amax, nonfinite);
   return hipGetLastError();
 }
 

@@ -54,6 +54,7 @@ struct RayState {
   float T[PER];      // T_k (exclusive transmittance)
   float tv[PER + 1]; // t_k .. t_{k+PER}
   float dl;          // |d|
+  float sg_sum;      // sum of this lane's sigma_k (non-finite iff one of them is: sigma >= 0)
 };
 
 // alpha_k = 1 - exp(-sigma_k * delta_k * |d|); T_k = prod_{j<k} (1 - alpha_j).
@@ -78,10 +79,12 @@ __device__ inline void ray_alpha_T(int S, int r, int lane, const float* __restri
   for (int p = 0; p < PER; ++p) rs.tv[p] = tl[p];
   rs.tv[PER] = lane == 63 ? tr[S] : tnext;
   float lp = 1.0f;
+  rs.sg_sum = 0.0f;
 #pragma unroll
   for (int p = 0; p < PER; ++p) {
     rs.a[p] = 1.0f - expf(-sg[p] * (rs.tv[p + 1] - rs.tv[p]) * rs.dl);
     lp *= (1.0f - rs.a[p]);
+    rs.sg_sum += sg[p];
   }
   float inc = lp;  // inclusive product scan over lanes
 #pragma unroll
@@ -103,7 +106,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(int n, int S, const float* _
                                                     const float* __restrict__ rgb, const float* __restrict__ t,
                                                     const float* __restrict__ d, int white, float* __restrict__ C,
                                                     float* __restrict__ w, float* __restrict__ acc_out,
-                                                    float* __restrict__ dist_out) {
+                                                    float* __restrict__ dist_out, uint32_t* __restrict__ nonfinite) {
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= n) return;  // wave-uniform; no block barriers below
@@ -123,11 +126,19 @@ __global__ __launch_bounds__(256) void k_render_fwd(int n, int S, const float* _
     if (dist_out) wd += wk[p] * (rs.tv[p] + rs.tv[p + 1]) / 2.0f;  // weighted midpoint (MH:488)
   }
   vstore<PER, PER>(w + (size_t)r * S + k0, wk);
+  if (nonfinite) {  // an inf sigma (fp16 overflow upstream) gives alpha = 1 and a finite colour: check inputs
+    float in = rs.sg_sum;
+#pragma unroll
+    for (int q = 0; q < 3 * PER; ++q) in += cr[q];
+    if (!__builtin_isfinite(in)) nonfinite[0] = 1u;  // plain store of a constant: racing writers agree
+  }
   c0 = wave_sum(c0); c1 = wave_sum(c1); c2 = wave_sum(c2); acc = wave_sum(acc);
   if (dist_out) wd = wave_sum(wd);
   if (lane == 0) {
     const float bg = white ? (1.0f - acc) : 0.0f;
     C[3 * r] = c0 + bg; C[3 * r + 1] = c1 + bg; C[3 * r + 2] = c2 + bg;
+    // non-finite detection (plain store of a constant: racing writers agree)
+    if (nonfinite && !__builtin_isfinite(c0 + c1 + c2 + acc)) nonfinite[0] = 1u;
     if (acc_out) acc_out[r] = acc;
     if (dist_out) {  // clamp(acc > 0 ? sum / acc : +inf, t_0, t_S)  (MH:490)
       const float t0 = t[(size_t)r * (S + 1)], tS = t[(size_t)r * (S + 1) + S];
@@ -212,11 +223,12 @@ __global__ void k_output_gradient(int n, const float* __restrict__ C, const floa
   }
 
 hipError_t launch_render_fwd(int n, int S, const float* sigma, const float* rgb, const float* t, const float* d,
-                             int white, float* C, float* w, hipStream_t st, float* acc, float* dist) {
+                             int white, float* C, float* w, hipStream_t st, float* acc, float* dist,
+                             uint32_t* nonfinite) {
   if (n <= 0) return hipSuccess;
   const dim3 grid((n + 3) / 4), block(256);
   NOF_RENDER_DISPATCH(S, hipLaunchKernelGGL(k_render_fwd<PER>, grid, block, 0, st, n, S, sigma, rgb, t, d, white, C, w,
-                                            acc, dist));
+                                            acc, dist, nonfinite));
   return hipGetLastError();
 }
 

@@ -63,6 +63,7 @@ class nof_batch(C.Structure):
 OUTPUT_GRAD_FN = C.CFUNCTYPE(C.c_uint64, C.c_void_p, C.c_uint64, C.c_int32, C.c_float, C.c_uint64)
 GRAD_BUCKET_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64))
 NOF_GRAD_ACCUMULATE, NOF_GRAD_PUBLISH, NOF_GRAD_BUCKETS = 1, 2, 2
+NOF_NUMERIC_FORWARD, NOF_NUMERIC_DELTA = 1, 2
 
 P = C.c_void_p
 F = C.c_float
@@ -90,6 +91,7 @@ SIGNATURES = {
     "nof_mipnerf_get_rng": [P, C.POINTER(U64), C.POINTER(U32), C.POINTER(U32)],
     "nof_mipnerf_level_view": [P, I32, C.POINTER(nof_level_view)],
     "nof_mipnerf_loss": [P, C.POINTER(F)],
+    "nof_mipnerf_numeric_status": [P, C.POINTER(U32), I32],
     "nof_mipnerf_render_device": [P, I32, P, P, P, P, P, I32, I32, C.POINTER(nof_render_out)],
     "nof_image_metrics": [P, P, I32, I32, F, C.POINTER(F), C.POINTER(F), P],
     "nof_dataset_open": [C.c_char_p, I32, C.POINTER(P)],

@@ -259,6 +259,12 @@ class AcceleratedMipNeRF:
         call("nof_mipnerf_loss", self._h, C.byref(out))
         return out.value
 
+    def numeric_status(self, clear: bool = True) -> int:
+        """NOF_NUMERIC_* bits (non-finite forward outputs / output gradients) since the last clear."""
+        out = C.c_uint32()
+        call("nof_mipnerf_numeric_status", self._h, C.byref(out), int(clear))
+        return out.value
+
     def render_device(self, n, origins, directions, radii, nears, fars, randomized=False, white_bkgd=None):
         """MipNerfModel.Call (MNcs:36-97): forward-only two-level render of device-resident rays.
         Returns [{"comp_rgb": (ptr, (n, 3)), "distance": (ptr, (n,)), "acc": (ptr, (n,))}] per level."""

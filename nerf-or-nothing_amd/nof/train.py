@@ -81,6 +81,10 @@ class Trainer:
         self.adam.step(self.params, grads, api.learning_rate_decay(step, **self.lr))
         self.step_idx = step
         if self.print_every and step % self.print_every == 0:
+            bad = self.model.numeric_status(clear=True)
+            if bad:  # e.g. fp16 activation overflow in the f16x2 perf mode: fail loudly, not silently
+                raise FloatingPointError(f"step {step}: non-finite values in the training step (flags {bad:#x}; "
+                                         "1 = forward outputs, 2 = output gradients)")
             self.last_loss = self.fine_loss(b)
             if self.rank == 0:
                 print(f"Step {step}/{self.lr['max_steps']}, Loss: {self.last_loss}", flush=True)

@@ -183,3 +183,40 @@ def test_glorot_init_matches_oracle(gpu, oracle):
     assert np.array_equal(P, oracle.glorot_init(oracle.Spec(), 1234))
     assert model.GetLayerSizes() == list(oracle.layer_sizes(oracle.Spec()))
     model.close()
+
+
+def test_sample_pdf_dotnet_semantics_cases(gpu, oracle):
+    """The crafted inputs of tests/test_dotnet_semantics.py (LINQ double Sum, BinarySearch exact hit)
+    through k_sample_pdf: bit-exact to the oracle, so the pinned .NET semantics hold on the GPU."""
+    import torch
+    import nof
+    from test_dotnet_semantics import _blur_pdf_cdf, _linspace_u
+
+    f32 = np.float32
+    cases = []
+    w = np.zeros(64, np.float32)
+    w[::7] = f32(0.3)
+    cases.append((np.linspace(2, 6, 65, dtype=np.float32), w, 64, 0.01))
+    # BinarySearch exact hit on 64 bins: w = [a, 1, ..., 1] with cdf_1 == u_1 bit for bit
+    u1 = _linspace_u(65)[1]
+    a = f32(1.0)
+    for _ in range(100000):
+        w = np.ones(64, np.float32)
+        w[0] = a
+        c1 = _blur_pdf_cdf(w, 0.0, True)[1]
+        if c1 == u1:
+            break
+        a = np.nextafter(a, f32(0)) if c1 > u1 else np.nextafter(a, f32(2))
+    assert c1 == u1
+    cases.append((np.linspace(2, 6, 65, dtype=np.float32), w, 64, 0.0))
+    for t_in, w, S_out, pad in cases:
+        n, S_in = 1, w.shape[0]
+        t = empty((n, S_out + 1), gpu)
+        idx = empty((n, S_out + 1), gpu, dtype=torch.int32)
+        nof._lib.call("nof_kernel_sample_pdf", n, S_in, T(t_in[None], gpu).data_ptr(), T(w[None], gpu).data_ptr(),
+                      S_out, pad, 0, 0, 0, 1, 0, t.data_ptr(), idx.data_ptr(), None)
+        sync()
+        rt, ridx = oracle.sample_pdf(t_in[None], w[None], S_out, pad, False)
+        assert np.array_equal(idx.cpu().numpy(), ridx)
+        assert np.array_equal(t.cpu().numpy(), rt)
+    assert ridx[0, 1] == 1 and rt[0, 1] == cases[-1][0][1]  # the exact hit: index 1, t = t_in[1]

@@ -152,6 +152,15 @@ def cpu_baseline(samples, target_s):
             "host": {"nproc": nproc, "affinity": aff, "cgroup_cpu_quota": quota, "cpu_model": model}}
 
 
+def profile_table(name):
+    """profiles/<name> written by tools/pmc_summary.py from the committed rocprofv3 passes ({} if absent)."""
+    f = os.path.join(ROOT, "profiles", name)
+    try:
+        return json.load(open(f)) if os.path.exists(f) else {}
+    except (OSError, ValueError):
+        return {}
+
+
 def integrator_roofline(torch, nof, dev, n=1 << 20, S=128, reps=5):
     """HBM roofline of the integrator fwd/bwd on an integrator-only 2^20 x 128 batch."""
     g = torch.Generator(device=dev).manual_seed(3)
@@ -187,8 +196,14 @@ def integrator_roofline(torch, nof, dev, n=1 << 20, S=128, reps=5):
     ach = tot_b / (tot_ms * 1e-3) / 1e9
     del sigma, rgb, t, d, C, w, gr, ds, dc
     torch.cuda.empty_cache()
+    # HBM bytes per fwd + bwd pair from the committed PMC passes (tools/profile_r02.sh integrator leg)
+    pmc = profile_table("pmc_traffic.json")
+    tf, tb = pmc.get("render_fwd_integrator"), pmc.get("render_bwd_integrator")
+    traffic = tf + tb if (tf is not None and tb is not None and S == 128 and n == 1 << 20) else None
+    for name, v in (("render_fwd", tf), ("render_bwd", tb)):
+        out[name]["traffic"] = v if traffic is not None else None
     return {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
+            "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic, "algorithmic_bytes": tot_b,
             "workload": f"{n} rays x {S} samples, render fwd+bwd", "kernels": out}
 
 
@@ -405,17 +420,18 @@ def main():
         mlp_ms = sum(kernels[k]["ms_per_step"] for k in flop if k in kernels)
         mlp_tf = sum(flop.values()) / (mlp_ms * 1e-3) / 1e12
         peak = PEAKS[prec]
-        traffic = None
-        tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(tfile):
-            try:
-                traffic = json.load(open(tfile)).get(dom + ("" if prec == "f32" else "_" + prec))
-            except (OSError, ValueError):
-                traffic = None
+        # committed rocprofv3 evidence (profiles/, tools/profile_r02.sh + tools/pmc_summary.py): HBM bytes
+        # and MFMA-busy fraction per launch of the same kernels in the same configuration
+        key = lambda k: k + ("" if prec == "f32" else "_" + prec)
+        traffic = profile_table("pmc_traffic.json").get(key(dom))
+        busy = profile_table("pmc_mfma.json")
+        for k in kernels:
+            if busy.get(key(k)) is not None:
+                kernels[k]["mfma_busy"] = busy[key(k)]
         return ms_step, kernels, {
             "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
-                         "flop_per_launch": fl_launch},
+                         "flop_per_launch": fl_launch, "mfma_busy": busy.get(key(dom))},
             "mlp_all_kernels": {"achieved": round(mlp_tf, 2), "unit": "TFLOP/s", "frac": round(mlp_tf / peak, 4)},
         }
 

@@ -1,13 +1,32 @@
-"""Summarise a tools/profile.sh run into profiles/<tag>_*.json/csv (committed evidence).
+"""Summarise a tools/profile_r02.sh (or profile.sh) run into profiles/<tag>_*.json/csv (committed
+evidence) and the lookups bench.py reads (profiles/pmc_traffic.json, profiles/pmc_mfma.json).
 
 traffic per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 B  — FETCH_SIZE (KB) reads half of a wide
 coalesced streaming read on gfx950 (MI355X_MICROARCH.md, HBM section), WRITE_SIZE is exact for
-16-B-per-lane stores; effective clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel duration.
+16-B-per-lane stores.
+MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel cycles), kernel cycles =
+GRBM_GUI_ACTIVE / 8 XCDs (rocprofv3 sums GRBM over the XCDs).
+effective clock = GRBM_GUI_ACTIVE / 8 / kernel duration — reported only for dispatches of at least
+0.3 ms: the quotient reads high on shorter ones (MI355X_MICROARCH.md, DVFS), and it is never above
+the 2.4 GHz peak clock by construction (a larger quotient is dropped as unreliable).
+
+usage: pmc_summary.py SRC_DIR TAG [SUFFIX]   (SRC_DIR holds trace/ and pmc_*/ subdirectories)
 """
-import csv, collections, json, os, shutil, sys
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+SIMDS = 1024          # 256 CUs x 4 SIMDs
+XCDS = 8
+PEAK_CLOCK_GHZ = 2.4
+MIN_CLOCK_MS = 0.3
 
 src, tag = sys.argv[1], sys.argv[2]
-suffix = sys.argv[3] if len(sys.argv) > 3 else ""  # "_split" / "_f16x2" for the other precision modes
+suffix = sys.argv[3] if len(sys.argv) > 3 else ""  # "_split" / "_f16x2" / "_integrator"
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 dst = os.path.join(root, "profiles")
 os.makedirs(dst, exist_ok=True)
@@ -15,10 +34,7 @@ shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst
 short = lambda n: n.split("(")[0].replace("void ", "").replace("nof::", "")
 stats = {short(r["Name"]): r for r in csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv")))}
 agg = collections.defaultdict(list)
-for sub in ("pmc_fetch", "pmc_write", "pmc_clk"):
-    p = os.path.join(src, sub, "run_counter_collection.csv")
-    if not os.path.exists(p):
-        continue
+for p in glob.glob(os.path.join(src, "pmc_*", "run_counter_collection.csv")):
     for r in csv.DictReader(open(p)):
         agg[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
 out = {}
@@ -27,26 +43,34 @@ for k, s in stats.items():
         continue
     avg_ns = float(s["AverageNs"])
     m = lambda c: (sum(agg[(k, c)]) / len(agg[(k, c)])) if agg.get((k, c)) else None
-    fetch, write, grbm = m("FETCH_SIZE"), m("WRITE_SIZE"), m("GRBM_GUI_ACTIVE")
+    fetch, write, grbm, mfma = m("FETCH_SIZE"), m("WRITE_SIZE"), m("GRBM_GUI_ACTIVE"), m("SQ_VALU_MFMA_BUSY_CYCLES")
     e = {"calls": int(s["Calls"]), "avg_ms": avg_ns / 1e6}
     if fetch is not None and write is not None:
         e["hbm_bytes_per_launch"] = (2 * fetch + write) * 1024
         e["hbm_GBps"] = e["hbm_bytes_per_launch"] / (avg_ns * 1e-9) / 1e9
     if grbm is not None:
-        e["eff_clock_GHz"] = grbm / 8 / (avg_ns * 1e-9) / 1e9
+        cycles = grbm / XCDS
+        clk = cycles / (avg_ns * 1e-9) / 1e9
+        if avg_ns * 1e-6 >= MIN_CLOCK_MS and clk <= PEAK_CLOCK_GHZ:
+            e["eff_clock_GHz"] = round(clk, 3)
+        else:
+            e["eff_clock_GHz"] = None
+            e["eff_clock_note"] = "dispatch < 0.3 ms: GRBM_GUI_ACTIVE quotient unreliable"
+        if mfma is not None:
+            e["mfma_busy_cycles"] = mfma
+            e["mfma_busy"] = round(mfma / (SIMDS * cycles), 4)  # fraction of SIMD-cycles with an MFMA busy
     out[k] = e
 json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
-# traffic lookup used by bench.py (bench kernel-timer names; split-mode kernels keyed with "_split")
-names = {"k_mlp_fwd16<true>": "mlp_fwd", "k_mlp_bwd16": "mlp_bwd", "k_wgrad": "wgrad",
-         "k_mlp_fwd16<0, true>": "mlp_fwd", "k_mlp_bwd16<0>": "mlp_bwd",
-         "k_mlp_fwd16<2, true>": "mlp_fwd_f16x2", "k_mlp_bwd16<2>": "mlp_bwd_f16x2",
-         "k_mlp_fwd<true, true>": "mlp_fwd_split", "k_mlp_bwd<true>": "mlp_bwd_split", "k_wgrad_x3": "wgrad_split",
+# lookups read by bench.py (bench kernel-timer names; other precision modes keyed with "_<mode>")
+names = {"k_mlp_fwd16<0, true>": "mlp_fwd", "k_mlp_bwd16<0>": "mlp_bwd", "k_wgrad": "wgrad",
+         "k_mlp_fwd16<2, true>": "mlp_fwd_f16x2", "k_mlp_bwd16<2>": "mlp_bwd_f16x2", "k_wgrad_h": "wgrad_f16x2",
          "k_mlp_fwd<1, true>": "mlp_fwd_split", "k_mlp_bwd<1>": "mlp_bwd_split", "k_wgrad_x3<1>": "wgrad_split",
-         "k_mlp_fwd<2, true>": "mlp_fwd_f16x2", "k_mlp_bwd<2>": "mlp_bwd_f16x2", "k_wgrad_h": "wgrad_f16x2",
          "k_render_fwd<2>": "render_fwd" + suffix, "k_render_bwd<2>": "render_bwd" + suffix}
-tfile = os.path.join(dst, "pmc_traffic.json")
-traffic = json.load(open(tfile)) if os.path.exists(tfile) else {}
-traffic.update({names[k]: v.get("hbm_bytes_per_launch") for k, v in out.items() if k in names})
-json.dump(traffic, open(tfile, "w"), indent=1, sort_keys=True)
+for fname, key in (("pmc_traffic.json", "hbm_bytes_per_launch"), ("pmc_mfma.json", "mfma_busy")):
+    f = os.path.join(dst, fname)
+    table = json.load(open(f)) if os.path.exists(f) else {}
+    table.update({names[k]: v[key] for k, v in out.items() if k in names and v.get(key) is not None})
+    table["_source"] = f"profiles/{tag}_pmc.json (tools/pmc_summary.py)"
+    json.dump(table, open(f, "w"), indent=1, sort_keys=True)
 for k, v in out.items():
     print(k, json.dumps(v))

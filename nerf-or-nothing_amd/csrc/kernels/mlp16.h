@@ -101,8 +101,19 @@ struct BlkStore16H {
     voff = 256u * g + ((((2 * half + (j >> 3)) ^ g) << 4) | ((j & 7) << 1));
   }
   __device__ __forceinline__ void store(__amdgpu_buffer_rsrc_t blk, int t, int r, float v) const {
-    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (_Float16)v), blk, (int)voff + 64 * r,
-                                          1024 * t, 0);
+    store_h(blk, t, r, (_Float16)v);
+  }
+  __device__ __forceinline__ void store_h(__amdgpu_buffer_rsrc_t blk, int t, int r, _Float16 h) const {
+    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, h), blk, (int)voff + 64 * r, 1024 * t, 0);
+  }
+  // both halves of a packed fp16 pair: features R (low half) and R + 1 (high half, store_short_d16_hi)
+  template <int R>
+  __device__ __forceinline__ void store_pair(__amdgpu_buffer_rsrc_t blk, int t, uint32_t pair) const {
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)pair, blk, (int)voff, 1024 * t + 64 * R, 0);
+    asm volatile("buffer_store_short_d16_hi %0, %1, %2, %3 offen offset:%4"
+                 :
+                 : "v"(pair), "v"(voff), "s"(blk), "s"(1024 * t), "n"(64 * (R + 1))
+                 : "memory");
   }
 };
 template <int P> struct Store16 { typedef BlkStore16 T; typedef float E; };
@@ -129,6 +140,63 @@ __device__ __forceinline__ float mask16_apply(const uint2& m, int t, int r, floa
   uint32_t all;
   asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(all) : "v"(w), "n"(31 - ((t & 7) * 4 + r)));
   return __uint_as_float(__float_as_uint(v) & all);
+}
+
+// ReLU with the mask bit, 3 VALU: h = max_i32(bits(z), 0) is z for z > 0 and +0 otherwise (every
+// non-NaN z: positive floats order as positive ints, negative ones and -0 as negative ints), then
+// mw = mw + mw + (h > 0) as a compare and an add-with-carry.  (The plain C forms compile to a
+// canonicalising max, a compare, two selects, a shift and an or3 per pair.)
+__device__ __forceinline__ float relu_bit(float z, uint32_t& mw) {
+  const int h = max(__float_as_int(z), 0);
+  asm volatile("v_cmp_lt_i32 vcc, 0, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(mw) : "v"(h) : "vcc");
+  return __int_as_float(h);
+}
+
+// f16x2 split of four fp32 values into packed fp16 pairs: hi = RNE(x) (v_cvt_pk_f16_f32), lo = RNE of
+// the exact residual x - hi, formed by one v_fma_mix_f32 each (x * 1 - hi with hi read as fp16
+// straight from the packed register) instead of a convert back and a subtract.
+__device__ __forceinline__ void split4h(const float (&x)[4], uint32_t& hi01, uint32_t& hi23, uint32_t& lo01,
+                                        uint32_t& lo23) {
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  hi01 = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2{x[0], x[1]}), h2));
+  hi23 = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2{x[2], x[3]}), h2));
+  float r[4];
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(r[0]) : "v"(x[0]), "v"(hi01));
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(r[1]) : "v"(x[1]), "v"(hi01));
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(r[2]) : "v"(x[2]), "v"(hi23));
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(r[3]) : "v"(x[3]), "v"(hi23));
+  lo01 = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2{r[0], r[1]}), h2));
+  lo23 = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2{r[2], r[3]}), h2));
+}
+
+// An epilogue's finished tile t (4 values) into the next layer's B operand, and its act / delta block
+// store: fp32 as is, or (f16x2, kSplit) pre-split into the MFMA fragments mlp_layer16h consumes —
+// for the tile pair (2u, 2u + 1) one slice reads, bin[2u] = hi {v0v1, v2v3 of tile 2u, v0v1, v2v3 of
+// tile 2u + 1} and bin[2u + 1] = the lo pieces — with the fp16 block storing those hi halves
+// (bit-identical to converting v).
+template <bool kSplit, bool kStore, class ST>
+__device__ __forceinline__ void put_tile(float (&bin)[16][4], int t, const float (&v)[4], const ST& bst,
+                                         __amdgpu_buffer_rsrc_t blk) {
+  if constexpr (kSplit) {
+    uint32_t hi01, hi23, lo01, lo23;
+    split4h(v, hi01, hi23, lo01, lo23);
+    const int row = t & ~1, c = 2 * (t & 1);
+    bin[row][c] = __uint_as_float(hi01);
+    bin[row][c + 1] = __uint_as_float(hi23);
+    bin[row + 1][c] = __uint_as_float(lo01);
+    bin[row + 1][c + 1] = __uint_as_float(lo23);
+    if constexpr (kStore) {
+      bst.template store_pair<0>(blk, t, hi01);
+      bst.template store_pair<2>(blk, t, hi23);
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      bin[t][r] = v[r];
+      if constexpr (kStore) bst.store(blk, t, r, v[r]);
+    }
+  }
 }
 
 // Epilogue hook of mlp_layer16: epi(tile) finishes one accumulator tile of the PREVIOUS layer
@@ -228,8 +296,9 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
 }
 // f16x2 mode on v_mfma_f32_16x16x32_f16 (same two-waves-per-SIMD structure).  One slice (32 input
 // features = input tiles 2t, 2t + 1) is ONE k-step: lane (g, j) supplies B[k = 8g + i][col j], and
-// k = 8g + i is taken to be feature 16 (2t + (i >> 2)) + 4g + (i & 3) — the registers bin[2t][0..3],
-// bin[2t + 1][0..3] as they stand, split once per slice into fp16 hi / lo.  The packed slice
+// k = 8g + i is taken to be feature 16 (2t + (i >> 2)) + 4g + (i & 3) — tiles 2t, 2t + 1, which the
+// caller's epilogue left PRE-SPLIT as the two fragments (bin[2t] = hi, bin[2t + 1] = lo, packed fp16
+// pairs in k order); the IPE slices (fp32) are split here.  The packed slice
 // (k_pack_weights_x3<2>) holds, per 16-row tile rt and piece p, the 16-B A fragment of lane (g, j):
 // W[16 rt + j][base + 16 (i >> 2) + 4g + (i & 3)], i = 0..7 (chunk (2 rt + p) 64 + lane: one
 // contiguous ds_read_b128 per fragment).  A group = one row-tile pair x 3 products (lo.hi, hi.lo,
@@ -250,11 +319,14 @@ __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const fl
     const bool dma = !(last_in_schedule && t + 2 >= NT_B + NT_I);  // slice t + 2 exists
     const int nxt2 = kSlots == 4 ? ((cur + 2) & 3) : (cur == 0 ? 2 : cur - 1);  // (cur + 2) % slots
     const f16x8* W = reinterpret_cast<const f16x8*>(lds + cur * kSliceFloats) + lane;
+    Frag<2> b;
     float v[8];
-    if (t < NT_B) {
+    if (t < NT_B) {  // pre-split by the epilogue: rows 2t (hi) and 2t + 1 (lo) are the fragments
       const int tb = t < NT_B ? 2 * t : 0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = bin[tb + (i >> 2)][i & 3];
+      const f32x4 hi = {bin[tb][0], bin[tb][1], bin[tb][2], bin[tb][3]};
+      const f32x4 lo = {bin[tb + 1][0], bin[tb + 1][1], bin[tb + 1][2], bin[tb + 1][3]};
+      b.p[0] = __builtin_bit_cast(f16x8, hi);
+      b.p[1] = __builtin_bit_cast(f16x8, lo);
     } else {
       const int ti = t >= NT_B ? 2 * (t - NT_B) : 0;
       if constexpr (kSlots == 4) {  // the wave's IPE registers
@@ -266,9 +338,8 @@ __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const fl
 #pragma unroll
         for (int i = 0; i < 4; ++i) { v[i] = u0[i]; v[4 + i] = u1[i]; }
       }
+      split8<2>(v, b);
     }
-    Frag<2> b;
-    split8<2>(v, b);
     Frag<2> a0, a1;
 #pragma unroll
     for (int p = 0; p < 2; ++p) { a0.p[p] = W[p * 64]; a1.p[p] = W[(2 + p) * 64]; }

@@ -17,8 +17,9 @@ namespace nof {
 
 
 // delta = mask ? acc (+ w8 * dz_s) : 0 -> B operand + delta block, one tile per call inside the
-// next layer's MFMA stream; w8 values loaded one tile ahead.
-template <bool kDensity, class ST>
+// next layer's MFMA stream; w8 values loaded one tile ahead.  kSplit (f16x2): the B operand is kept
+// pre-split (put_tile, mlp16.h).
+template <bool kDensity, class ST, bool kSplit = false>
 struct BwdEpi16 {
   static constexpr int kVmPerPart = 4;
   const f32x4 (&acc)[16];
@@ -49,14 +50,14 @@ struct BwdEpi16 {
       w4 = wnext;
       if (t + 1 < 16) wnext = *reinterpret_cast<const f32x4*>(w8 + 16 * (t + 1));
     }
+    float v[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float v = acc[t][r];
-      if constexpr (kDensity) v += w4[r] * dzs;
-      v = mask16_apply(mk, t, r, v);
-      bin[t][r] = v;
-      bst.store(dst_blk, t, r, v);
+      v[r] = acc[t][r];
+      if constexpr (kDensity) v[r] += w4[r] * dzs;
+      v[r] = mask16_apply(mk, t, r, v[r]);
     }
+    put_tile<kSplit, true>(bin, t, v, bst, dst_blk);
   }
   __device__ __forceinline__ void tile01() {
     (*this)(0);
@@ -115,13 +116,10 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
       const f32x4 wa = *reinterpret_cast<const f32x4*>(w10 + fb);
       const f32x4 wb = *reinterpret_cast<const f32x4*>(w10 + 128 + fb);
       const f32x4 wc = *reinterpret_cast<const f32x4*>(w10 + 256 + fb);
+      float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v = (wa[r] * dzc[0] + wb[r] * dzc[1]) + wc[r] * dzc[2];
-        v = mask16_apply(mk, t, r, v);
-        bin[t][r] = v;
-        bst.store(d9, t, r, v);
-      }
+      for (int r = 0; r < 4; ++r) v[r] = mask16_apply(mk, t, r, (wa[r] * dzc[0] + wb[r] * dzc[1]) + wc[r] * dzc[2]);
+      put_tile<P == 2, true>(bin, t, v, bst, d9);
     }
   }
   if (tid < 64) reinterpret_cast<f32x4*>(w8_lds)[tid] = reinterpret_cast<const f32x4*>(tail + kBwdTailW8)[tid];
@@ -132,12 +130,12 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
   f32x4 accA[16], accB[16];  // ping-pong, as in the forward
   AE* delta_blk = reinterpret_cast<AE*>(a.delta) + (size_t)blk * kWidth * kBlk;
   // ---- dh7 = W9[:, :256]^T delta9 + w8 dz_s ; delta7 ---------------------------------------
-  BwdEpi16<true, ST> e7(accA, bin, bst, lane);
+  BwdEpi16<true, ST, P == 2> e7(accA, bin, bst, lane);
   e7.begin(mask16_ptr(masks, blk, 7, half, lane), delta_blk + 7 * layer_stride, w8_lds, dzs);
   layer16<P, 4, 0, 16>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane);
   e7.tile01();
   // ---- dh_{l-1} = W_l[:, :256]^T delta_l ; delta_{l-1}, l = 7..1 (l odd: A -> B) ------------
-  BwdEpi16<false, ST> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
+  BwdEpi16<false, ST, P == 2> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
   eb.begin(mask16_ptr(masks, blk, 6, half, lane), delta_blk + 6 * layer_stride);
   layer16<P, 8, 0, 16>(bin, nullptr, accB, lds, cur, wsrc, false, tid, lane, e7);
   eb.tile01();

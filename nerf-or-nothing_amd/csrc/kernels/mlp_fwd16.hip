@@ -21,10 +21,13 @@ namespace nof {
 
 // ReLU epilogue of one accumulator tile (the bias is already in it: the layer's first MFMAs take it
 // as C) -> next layer's B operand, act block, mask bits; NT tiles per layer, run in tile order (the
-// mask words are shift-accumulated).  w8 comes from the workgroup's LDS copy, loaded one tile ahead.  kDensity folds the density head
-// (z_s = w8 . h7) into layer 7's epilogue.  A tail wave clamped onto the last block recomputes
-// bit-identical values, so its duplicate stores are benign.
-template <bool store, bool kDensity, int NT, class ST>
+// mask words are shift-accumulated: mw + mw + bit, a compare and an add-with-carry).  w8 comes from
+// the workgroup's LDS copy, loaded one tile ahead (relu_bit, mlp16.h: 3 VALU per value).  kDensity folds the density head (z_s = w8 . h7)
+// into layer 7's epilogue.  kSplit (f16x2 trunk layers): the B operand is kept pre-split as the MFMA
+// fragments (put_tile, mlp16.h), so the split happens once per value in the epilogue instead of per
+// slice in the layer.  A tail wave
+// clamped onto the last block recomputes bit-identical values, so its duplicate stores are benign.
+template <bool store, bool kDensity, int NT, class ST, bool kSplit = false>
 struct FwdEpi16 {
   static constexpr int kVmPerPart = store ? 4 : 0;
   const f32x4 (&acc)[16];
@@ -58,19 +61,15 @@ struct FwdEpi16 {
       w4 = wnext;
       if (more) wnext = *reinterpret_cast<const f32x4*>(w8 + 16 * (t + 1));
     }
+    float hv[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float z = acc[t][r];
-      const float hv = z > 0.0f ? z : 0.0f;
-      bin[t][r] = hv;
-      mw[t >> 3] = (mw[t >> 3] << 1) | (hv > 0.0f ? 1u : 0u);
-      if constexpr (kDensity) zs += w4[r] * hv;
+      hv[r] = relu_bit(acc[t][r], mw[t >> 3]);
+      if constexpr (kDensity) zs += w4[r] * hv[r];
     }
-    if constexpr (store && kVmPerPart > 0) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bst.store(act_blk, t, r, bin[t][r]);
+    put_tile<kSplit, store>(bin, t, hv, bst, act_blk);
+    if constexpr (store && kVmPerPart > 0)
       if (!more) *mask_dst = make_uint2(mw[0], mw[1]);
-    }
   }
   __device__ __forceinline__ void tile01() {
     (*this)(0);
@@ -187,7 +186,8 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
   AE* act_h_blk = reinterpret_cast<AE*>(a.act_h) + (size_t)blk * kWidth * kBlk;
 
   // ---- trunk: layer l writes acc(l odd ? B : A) ------------------------------------------
-  FwdEpi16<store, false, 16, ST> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
+  constexpr bool kPre = P == 2;  // f16x2: trunk epilogues keep the next B operand pre-split
+  FwdEpi16<store, false, 16, ST, kPre> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
   const float* bias_g = biases + 4 * g;  // the lane group's bias slot (the layers' initial accumulators)
   ea.begin(act_h_blk, mask16_ptr(a.masks, blk, 0, half, lane));
   layer16<P, 0, 3, 16>(bin, ipe_b, accA, lds, cur, wsrc, false, tid, lane, bias_g);
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
     ea.tile01();
   }
   static_assert(kDepth == 8 && kSkip % 2 == 0, "trunk pairing assumes 8 layers and an even skip layer");
-  FwdEpi16<store, true, 16, ST> e7(accB, bin, bst, lane);  // + density head (layer 8): z_s = w8 . h7 + b8
+  FwdEpi16<store, true, 16, ST, kPre> e7(accB, bin, bst, lane);  // + density head (layer 8): z_s = w8 . h7 + b8
   e7.begin(act_h_blk + 7 * layer_stride, mask16_ptr(a.masks, blk, 7, half, lane), bias_lds + 8 * 256);
   layer16<P, 8, 0, 16>(bin, ipe_b, accB, lds, cur, wsrc, false, tid, lane, ea, bias_g + 7 * 256);
   e7.tile01();

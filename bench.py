@@ -298,10 +298,10 @@ def main():
         """W untimed + K timed training steps of one precision mode over the global batch (each
         rank's shard in micro-batches accumulated into one gradient, one all-reduce), then a short
         untimed pass with every kernel class event-timed (the per-kernel breakdown); returns
-        (s, timing, psnr, in_sync).  Inside the timed region only the dominant kernel (mlp_fwd, the
-        roofline kernel) is bracketed by hipEvents: each event pair costs the dependent launch
-        sequence a few us (measured 1.5 % of the f32 step and 4 % of the f16x2 step with every
-        kernel timed)."""
+        (s, timing, psnr, in_sync).  Inside the timed region only the MLP kernel classes (mlp_fwd,
+        mlp_bwd, wgrad: the roofline kernel is among them) are bracketed by hipEvents: each event
+        pair costs the dependent launch sequence a few us (measured 1.5 % of the f32 step and 4 % of
+        the f16x2 step with every kernel class timed)."""
         B_run = B_run or B
         sh = B_run // G
         mb = min(a.micro_batch, sh)
@@ -346,7 +346,9 @@ def main():
         sync_all()
         if world > 1:
             dist.barrier()
-        timers = os.environ.get("NOF_BENCH_TIMERS", "mlp_fwd")
+        # the three MLP kernel classes are event-timed live (the roofline kernel is the one that takes
+        # the most time per step, which depends on the mode): 6 event pairs per step
+        timers = os.environ.get("NOF_BENCH_TIMERS", "mlp_fwd,mlp_bwd,wgrad")
         models[0].enable_timing(timers_on, timers=timers.split(",") if timers != "all" else None)
         sync_all()
         if world > 1:

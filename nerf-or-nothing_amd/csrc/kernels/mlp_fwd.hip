@@ -108,7 +108,7 @@ struct FwdEpi {
     const float hv = z > 0.0f ? z : 0.0f;
     bin[t][r] = hv;
     mw[t >> 1] = (mw[t >> 1] << 1) | (hv > 0.0f ? 1u : 0u);
-    if constexpr (kDensity) zs += wcur[jj] * hv;
+    if constexpr (kDensity) zs = __builtin_fmaf(wcur[jj], hv, zs);
     if constexpr (store) ao.put(act_blk + t * 32 * kBlk, r, hv);
     if (!more && jj == 3) {
       uint4 mv;
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
     float s = tail[kFwdTailBias + 9 * 256 + o];
     const float* w9 = tail + kFwdTailW9d + o * 32;
 #pragma unroll
-    for (int k = 0; k < kDirIn; ++k) s += w9[k] * pe[k];
+    for (int k = 0; k < kDirIn; ++k) s = __builtin_fmaf(w9[k], pe[k], s);
     dirb[o] = s;
   }
   __syncthreads();
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
       for (int q = 0; q < 4; ++q) {
         const f32x4 w4 = *reinterpret_cast<const f32x4*>(tail + kFwdTailW10 + c * 128 + ot * 32 + 8 * q + 4 * h);
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) zc[c] += w4[jj] * bin[ot][4 * q + jj];
+        for (int jj = 0; jj < 4; ++jj) zc[c] = __builtin_fmaf(w4[jj], bin[ot][4 * q + jj], zc[c]);
       }
     zc[c] += __shfl_xor(zc[c], 32, 64);
     zc[c] += tail[kFwdTailBias + 10 * 256 + c];

@@ -65,7 +65,7 @@ struct FwdEpi16 {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       hv[r] = relu_bit(acc[t][r], mw[t >> 3]);
-      if constexpr (kDensity) zs += w4[r] * hv[r];
+      if constexpr (kDensity) zs = __builtin_fmaf(w4[r], hv[r], zs);  // explicit fma: every variant rounds alike
     }
     put_tile<kSplit, store>(bin, t, hv, bst, act_blk);
     if constexpr (store && kVmPerPart > 0)
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
     float s = tail[kFwdTailBias + 9 * 256 + o];
     const float* w9 = tail + kFwdTailW9d + o * 32;
 #pragma unroll
-    for (int k = 0; k < kDirIn; ++k) s += w9[k] * pe[k];
+    for (int k = 0; k < kDirIn; ++k) s = __builtin_fmaf(w9[k], pe[k], s);
     dirb[o] = s;
   }
   __syncthreads();
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
     for (int t = 0; t < 8; ++t) {
       const f32x4 w4 = *reinterpret_cast<const f32x4*>(tail + kFwdTailW10 + c * 128 + 16 * t + 4 * g);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) zc[c] += w4[r] * bin[t][r];
+      for (int r = 0; r < 4; ++r) zc[c] = __builtin_fmaf(w4[r], bin[t][r], zc[c]);
     }
     zc[c] += __shfl_xor(zc[c], 16, 64);
     zc[c] += __shfl_xor(zc[c], 32, 64);

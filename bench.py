@@ -54,8 +54,8 @@ INTEGRATOR_BWD_B = lambda S: 12 + S * (12 + 4) + (S + 1) * 4 + 12 + S * (12 + 4)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--global-batch", type=int, default=None,
                    help="rays per step over all GPUs (default: 1024 at N=1 = configs[1]; 65536 at N>1 = configs[3], "
                         "strong scaling; LLFF: 512 per GPU = configs[4]'s per-GPU shape)")

@@ -7,6 +7,7 @@
 
 #include "../kernels/common.h"
 #include "../kernels/mlp_common.h"
+#include "trace.h"
 
 namespace AcceleratedNeRFUtils {
 
@@ -41,6 +42,7 @@ hipEvent_t KernelTimer::get() {
   return pool_[used_++];
 }
 void KernelTimer::begin(int id) {
+  roctxRangePushA(timer_range_name(id));  // every bracketed launch is also a roctx range
   if (!((mask_ >> id) & 1u)) return;
   if (recs_.size() >= kMaxRecs) {  // bounded pool: fold what is finished (no record is open here)
     bool open = false;
@@ -51,6 +53,7 @@ void KernelTimer::begin(int id) {
   NOF_HIP(hipEventRecord(open_[id], st_));
 }
 void KernelTimer::end(int id) {
+  roctxRangePop();
   if (!((mask_ >> id) & 1u) || !open_[id]) return;
   hipEvent_t b = get();
   NOF_HIP(hipEventRecord(b, st_));
@@ -472,6 +475,7 @@ float* const* AcceleratedMLP::get_gradient(const float* color_grad, const float*
       run_wgrad(*part[bk], accumulate);
       int64_t off[2], cnt[2];
       const int ns = bucket_spans(bk, off, cnt);
+      TraceRange hr("nof:gradient_bucket_hook");
       hook_(hook_user_, bk, ns, off, cnt);
     }
   }
@@ -532,9 +536,15 @@ float* const* AcceleratedMipNeRF::GetGradientDevice(int n, const float* o, const
 float* const* AcceleratedMipNeRF::run(int n, const float* o, const float* d, const float* radii, const float* nears,
                                       const float* fars, const float* lm, const float* pix, float msum,
                                       nof_output_grad_fn cb, void* user, uint32_t flags) {
+  static const char* const kFwd[] = {"nof:level0_forward", "nof:level1_forward", "nof:level2_forward",
+                                     "nof:level3_forward"};
+  static const char* const kBwd[] = {"nof:level0_backward", "nof:level1_backward", "nof:level2_backward",
+                                     "nof:level3_backward"};
   const int L = cfg_.num_levels;
+  TraceRange step_range("nof:get_gradient");
   mlp->pack_weights();
   for (int lv = 0; lv < L; ++lv) {  // MNcpp:85-123
+    TraceRange lr(kFwd[lv & 3]);
     const int S = cfg_.num_samples[lv];
     timer.begin(kTSample);
     if (lv == 0) {
@@ -569,6 +579,7 @@ float* const* AcceleratedMipNeRF::run(int n, const float* o, const float* d, con
   float* const* grads = nullptr;
   for (int lv = 0; lv < L; ++lv) {  // MNcpp:135-142; level 0 overwrites unless accumulating
     const uint32_t f = (lv == 0 ? (flags & NOF_GRAD_ACCUMULATE) : 0u) | (lv == L - 1 ? (flags & NOF_GRAD_PUBLISH) : 0u);
+    TraceRange lr(kBwd[lv & 3]);
     grads = mlp->get_gradient(drgb_[lv].p, dsig_[lv].p, lv, f);
   }
   last_n_ = n;
@@ -656,6 +667,7 @@ AcceleratedAdamOptimizer::AcceleratedAdamOptimizer(const std::vector<int>& layer
 
 void AcceleratedAdamOptimizer::step(float* const* params, float* const* grads, float lr) {
   NOF_REQUIRE(params && grads, "null params/grads");
+  TraceRange r("nof:adam");
   ++iteration_;
   // host-side bias corrections exactly as AcceleratedAdamOptimizer.cpp:26-28
   const float inv1 = 1.0f / (1.0f - std::pow(0.9f, (float)iteration_));

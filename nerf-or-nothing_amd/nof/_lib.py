@@ -166,6 +166,12 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"HIP extension missing: {LIB_PATH}. Build it with `python -c "
                                f"'import __graft_entry__ as g; g.build()'` or `make -C nerf-or-nothing_amd`.")
+        # torch first: its bundled libamdhip64 carries the soname libamdhip64.so.7 that libnof.so
+        # needs, so the library binds to the HIP runtime already in the process.  Loaded the other
+        # way round, torch's libraries (which name the file libamdhip64.so) bring in a second HIP +
+        # HSA runtime, and whichever initialises second finds no device.
+        import torch  # noqa: F401
+
         L = C.CDLL(LIB_PATH)
         for name, args in SIGNATURES.items():
             fn = getattr(L, name)

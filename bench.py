@@ -207,6 +207,43 @@ def integrator_roofline(torch, nof, dev, n=1 << 20, S=128, reps=5):
             "workload": f"{n} rays x {S} samples, render fwd+bwd", "kernels": out}
 
 
+def api_path(torch, nof, synth, dev, n, samples, prec, steps=20, warmup=3):
+    """The reference's own boundary, host buffers in (PCIe-inclusive): MipNerfModel hands host arrays
+    to AcceleratedMipNeRF::GetGradient (MNcpp:52-84 copies them to the device) and its output-gradient
+    callback uploads the host pixels through AcceleratedGradientCalculator (AGC:19-33), then Adam.
+    Same workload as the headline; the arrays are fresh host (pageable) numpy buffers each step, as
+    a C# caller's managed arrays would be.  Reported beside `value`, never as it."""
+    seed = 0x5EED0002
+    m = nof.AcceleratedMipNeRF(device=dev.index, max_rays=n, num_samples=samples, seed=seed,
+                               stream=torch.cuda.current_stream(dev).cuda_stream, precision=PRECISIONS[prec])
+    opt = nof.AcceleratedAdamOptimizer(m.GetLayerSizes(), m.config)
+    calc = nof.AcceleratedGradientCalculator(n, m.config)
+    batches = [synth.blender_rays(n, seed=7000 + i) for i in range(2)]
+
+    def step(k):
+        r = batches[k % 2]
+        m.set_rng(seed, k, 0)
+        cb = lambda comp, level, msum, lm: calc.get_output_gradient(comp, r["pix"], lm, msum, level)
+        grads = m.GetGradient(r["o"], r["d"], r["radius"], r["near"], r["far"], r["lossmult"], cb)
+        opt.step(m.mlp.allParams, grads, nof.learning_rate_decay(k + 1))
+
+    for k in range(warmup):
+        step(k)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(warmup, warmup + steps):
+        step(k)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    calc.close()
+    opt.close()
+    m.close()
+    h2d = n * (3 + 3 + 1 + 1 + 1 + 1) * 4 + len(samples) * n * 3 * 4
+    return {"value": round(n * steps / dt, 1), "unit": "rays/s", "ms_per_step": round(dt * 1e3 / steps, 4),
+            "steps": steps, "h2d_bytes_per_step": h2d,
+            "path": "GetGradient(host arrays) + output-gradient callback (host pixels) + Adam, precision " + prec}
+
+
 def workload_name(a, B):
     if a.scene == "llff":
         return "BASELINE configs[4] per-GPU shape" if (B // a.gpus, a.samples) == (512, [256, 256]) else "LLFF-shaped"
@@ -490,6 +527,8 @@ def main():
                     "precision": aprec, "dtype": DTYPES[aprec], "value": round(B * a.steps / adt, 1),
                     "unit": "rays/s", "ms_per_step": round(ams, 4), **aroof,
                     "kernels": {k: v["avg_launch_ms"] for k, v in akernels.items()}, "psnr_fine": round(apsnr, 3)})
+        if world == 1 and G == 1 and a.scene == "blender" and B <= 8192:
+            result["api_path_pcie"] = api_path(torch, nof, synth, dev, B, samples, a.precision)
         if not a.no_integrator and world == 1 and G == 1:
             result["roofline_integrator"] = integrator_roofline(torch, nof, dev)
         if not a.no_cpu_baseline and world == 1 and G == 1:

@@ -42,7 +42,7 @@ def rays(n, seed=0):
     return synth.blender_rays(n, seed=seed)
 
 
-@pytest.mark.parametrize("S", [64, 128, 256])
+@pytest.mark.parametrize("S", [64, 128, 256, 512])
 def test_sample_stratified_bitexact(gpu, oracle, S):
     import nof
 
@@ -55,7 +55,7 @@ def test_sample_stratified_bitexact(gpu, oracle, S):
     assert np.array_equal(t.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("S_in,S_out", [(128, 128), (64, 128), (128, 256)])
+@pytest.mark.parametrize("S_in,S_out", [(128, 128), (64, 128), (128, 256), (256, 512), (512, 64)])
 def test_sample_pdf_bitexact(gpu, oracle, S_in, S_out):
     import nof
 
@@ -125,7 +125,7 @@ def test_cast_bitexact_and_encode(gpu, oracle):
     assert rel_l2(ed.cpu().numpy(), oracle.dir_pe(spec, r["d"])) < TOL
 
 
-@pytest.mark.parametrize("S", [64, 128, 256])
+@pytest.mark.parametrize("S", [64, 128, 256, 512])
 def test_render_fwd_bwd(gpu, oracle, S):
     import nof
 

@@ -244,6 +244,58 @@ def api_path(torch, nof, synth, dev, n, samples, prec, steps=20, warmup=3):
             "path": "GetGradient(host arrays) + output-gradient callback (host pixels) + Adam, precision " + prec}
 
 
+def psnr_vs_ref(torch, nof, synth, dev, prec, n=64, steps=40, samples=(128, 128), n_eval=256):
+    """Part of the cpu_baseline leg.  The metric's "PSNR vs ref": the HIP path and the oracle's float restatement of the reference
+    (MipNerfModel.GetGradient MNcs:99-200 + the Adam step AF:403-416, the reference's CPU path in
+    float) train from the same Glorot init on the same batches and Philox samples for `steps` steps;
+    then both render a held-out batch deterministically (MipNerfModel.Call, MNcs:36-97) and the fine
+    level's PSNR (MseToPsnr, MipHelpers.cs:672) of each is reported.  LR: LearningRateDecay without
+    the 2500-step warm-up delay, so that a short run moves the weights."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    seed = 0x5EED0003
+    spec = O.Spec()
+    _, aff, quota, _ = host_cpus()
+    threads = min(aff, quota) if quota else aff
+    m = nof.AcceleratedMipNeRF(device=dev.index, max_rays=max(n, n_eval), num_samples=samples, seed=seed,
+                               stream=torch.cuda.current_stream(dev).cuda_stream, precision=PRECISIONS[prec])
+    opt = nof.AcceleratedAdamOptimizer(m.GetLayerSizes(), m.config)
+    P = O.glorot_init(spec, seed)
+    mo, vo = np.zeros_like(P), np.zeros_like(P)
+    lr = lambda k: nof.learning_rate_decay(k, lr_delay_steps=0)
+    t_ref = 0.0
+    for k in range(steps):
+        r = synth.blender_rays(n, seed=600 + k)
+        d = {kk: torch.from_numpy(v).to(dev) for kk, v in r.items()}
+        m.set_rng(seed, k, 0)
+        g = m.get_gradient_device(n, d["o"], d["d"], d["radius"], d["near"], d["far"], d["lossmult"], d["pix"],
+                                  float(np.sum(r["lossmult"], dtype=np.float32)))
+        opt.step(m.mlp.allParams, g, lr(k + 1))
+        t0 = time.perf_counter()
+        out = O.step(spec, P, r, samples=tuple(samples), seed=seed, step_idx=k, ray_base=0, nthreads=threads,
+                     dtype=np.float32, want=("grads",))
+        O.adam_step(P, out["grads"], mo, vo, lr(k + 1), k + 1)
+        t_ref += time.perf_counter() - t0
+    torch.cuda.synchronize(dev)
+    held = synth.blender_rays(n_eval, seed=999)
+    c_gpu = m.render_rays(held, randomized=False)[-1]["comp_rgb"]
+    ref = O.step(spec, P, held, samples=tuple(samples), seed=seed, randomized=False, nthreads=threads,
+                 dtype=np.float32, want=("C",))
+    pptr, cnt = m.mlp.flat_params()
+    p_gpu = nof.to_numpy(pptr, (cnt,))
+    psnr = lambda c: float(-10.0 * np.log10(np.mean((np.asarray(c, np.float64) - held["pix"]) ** 2)))
+    res = {"psnr_hip": round(psnr(c_gpu), 4), "psnr_ref": round(psnr(ref["C"][-1]), 4),
+           "params_rel_l2": float(np.linalg.norm(p_gpu - P) / np.linalg.norm(P)),
+           "ref": "oracle float restatement of MipNerfModel.GetGradient + Adam (the reference's CPU path)",
+           "training": f"{steps} steps x {n} rays x {'+'.join(map(str, samples))} samples, precision {prec}",
+           "eval": f"{n_eval} held-out rays, deterministic render, fine level", "ref_cpu_s": round(t_ref, 1)}
+    res["delta_db"] = round(res["psnr_hip"] - res["psnr_ref"], 4)
+    opt.close()
+    m.close()
+    return res
+
+
 def workload_name(a, B):
     if a.scene == "llff":
         return "BASELINE configs[4] per-GPU shape" if (B // a.gpus, a.samples) == (512, [256, 256]) else "LLFF-shaped"
@@ -533,6 +585,9 @@ def main():
             result["roofline_integrator"] = integrator_roofline(torch, nof, dev)
         if not a.no_cpu_baseline and world == 1 and G == 1:
             result["cpu_baseline"] = cpu_baseline(samples, a.cpu_seconds)
+            # same leg (the oracle runs only here): the reference's float CPU path trained beside the
+            # HIP path on identical batches -> the metric's "PSNR vs ref"
+            result["psnr_vs_ref"] = psnr_vs_ref(torch, nof, synth, dev, a.precision, samples=samples)
         print(json.dumps(result), flush=True)
     if native is not None:
         for nd in native:

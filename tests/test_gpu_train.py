@@ -142,3 +142,18 @@ def test_perf_mode_psnr_matches_f32(gpu):
     print("psnr", psnr)
     assert psnr[0] > psnr[("first", 0)] + 0.5  # it learns
     assert abs(psnr[2] - psnr[0]) < 0.1
+
+
+@pytest.mark.parametrize("precision,db", [("f32", 0.01), ("f16x2", 0.1)])
+def test_psnr_vs_reference_training(gpu, precision, db):
+    """bench.py's "PSNR vs ref" leg at a small size: the HIP path and the oracle's float restatement of
+    the reference train on identical batches, then render a held-out batch; the PSNRs agree."""
+    import bench
+    import torch
+    import nof
+    from nof import synth
+
+    res = bench.psnr_vs_ref(torch, nof, synth, gpu, precision, n=32, steps=8, samples=(64, 64), n_eval=64)
+    print(res)
+    assert abs(res["delta_db"]) < db
+    assert res["params_rel_l2"] < (1e-4 if precision == "f32" else 2e-3)

@@ -23,6 +23,9 @@ for p in $PRECS; do
   run ${p}_write --pmc WRITE_SIZE -d $OUT/$p/pmc_write -o run --output-format csv
   run ${p}_mfma --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/$p/pmc_clk -o run --output-format csv
 done
+# roctx phase ranges beside the kernel trace (marker domain; no counters in this pass)
+CMD=(bench.py $ARGS --precision f32)
+run roctx_f32 --marker-trace --kernel-trace -d $OUT/roctx -o run --output-format csv
 CMD=(tools/integrator_only.py)
 run integ_trace --kernel-trace --stats -d $OUT/integrator/trace -o run --output-format csv
 run integ_fetch --pmc FETCH_SIZE -d $OUT/integrator/pmc_fetch -o run --output-format csv

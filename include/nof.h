@@ -65,8 +65,14 @@ typedef struct nof_config {
  *               v_mfma_f32_32x32x16_bf16 per product, fp32 accumulation.  Same 1e-5 parity.
  *   F16X2     : perf mode (BASELINE config 5 "fp16 on MFMA"): fp16 hi + lo pieces,
  *               three v_mfma_f32_32x32x16_f16 per product, backward deltas power-of-2 scaled.
- *               Parity: per-tensor relative L2 <= 2e-3. */
-enum { NOF_PRECISION_F32 = 0, NOF_PRECISION_F32_SPLIT = 1, NOF_PRECISION_F16X2 = 2 };
+ *               Parity: per-tensor relative L2 <= 2e-3 (the weight gradients take ONE fp16 product of the
+ *               stored fp16 activation and delta: that product is the mode's error).
+ *   F32_F16SPLIT : fp16 hi + lo pieces in EVERY contraction: the F16X2 forward and dX chain (three
+ *               v_mfma_f32_16x16x32_f16 per product), activations and scaled deltas stored as fp32,
+ *               the weight gradients split into hi + lo again (three v_mfma_f32_32x32x16_f16 per
+ *               product).  22 significand bits per operand: the same 1e-5 parity as F32, within fp16's
+ *               exponent range (activations below 65504; deltas power-of-2 scaled per level). */
+enum { NOF_PRECISION_F32 = 0, NOF_PRECISION_F32_SPLIT = 1, NOF_PRECISION_F16X2 = 2, NOF_PRECISION_F32_F16SPLIT = 3 };
 
 void nof_config_default(nof_config* cfg);
 const char* nof_last_error(void);

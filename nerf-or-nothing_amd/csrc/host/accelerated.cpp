@@ -99,7 +99,7 @@ static void check_cfg(const nof_config& c) {
       c.skip_layer != 4 || c.min_deg_point != 0 || c.max_deg_point != 16 || c.deg_view != 4)
     throw Error(NOF_ERR_UNSUPPORTED, "GPU path implements the reference network (8x256, 1x128, skip 4, PE 16/4)");
   NOF_REQUIRE(c.precision == NOF_PRECISION_F32 || c.precision == NOF_PRECISION_F32_SPLIT ||
-                  c.precision == NOF_PRECISION_F16X2,
+                  c.precision == NOF_PRECISION_F16X2 || c.precision == NOF_PRECISION_F32_F16SPLIT,
               "unknown precision mode");
 }
 
@@ -140,7 +140,7 @@ AcceleratedMLP::AcceleratedMLP(int deg_point, int deg_view, const nof_config& cf
   if (precision_ == NOF_PRECISION_F32_SPLIT) {  // bf16 (hi, mid, lo) slices + the fp32 tails (mlp_common.h)
     wimg_f_.alloc(nof::fwd_image_split_floats<1>() + nof::kFwdTail);
     wimg_b_.alloc(nof::bwd_image_split_floats<1>() + nof::kBwdTail);
-  } else if (precision_ == NOF_PRECISION_F16X2) {  // f16 (hi, lo) slices + the fp32 tails
+  } else if (f16_pieces()) {  // f16 (hi, lo) slices + the fp32 tails
     wimg_f_.alloc(nof::fwd_image_split_floats<2>() + nof::kFwdTail);
     wimg_b_.alloc(nof::bwd_image_split_floats<2>() + nof::kBwdTail);
     amax_.alloc(1);
@@ -185,7 +185,7 @@ void AcceleratedMLP::pack_weights() {
   for (int l = 0; l < kLayers; ++l) { pa.woff[l] = woff_[l]; pa.boff[l] = boff_[l]; }
   tb(kTPack);
   if (precision_ != NOF_PRECISION_F32)
-    NOF_HIP(nof::launch_pack_weights_x3(params_.p, pa, wimg_f_.p, wimg_b_.p, precision_, st_));
+    NOF_HIP(nof::launch_pack_weights_x3(params_.p, pa, wimg_f_.p, wimg_b_.p, f16_pieces() ? 2 : 1, st_));
   else NOF_HIP(nof::launch_pack_weights(params_.p, pa, wimg_f_.p, wimg_b_.p, st_));
   te(kTPack);
 }
@@ -338,7 +338,8 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M, int bucket)
     } else if (precision_ != NOF_PRECISION_F32) {
       const int WC = nof::wgrad_x3_grid_cols();  // C/2 waves per SIMD
       const int RB = (P[i].ntr + 1) / 2, CB = (P[i].ntc + WC - 1) / WC;
-      cost[i] = 10 * RB * CB + 5 * (P[i].ntr + P[i].ntc);
+      // fp16 (hi, lo) pieces: 3 MFMAs per product instead of 6 (same loads and splits)
+      cost[i] = (precision_ == NOF_PRECISION_F32_F16SPLIT ? 5 : 10) * RB * CB + 5 * (P[i].ntr + P[i].ntc);
     } else {
       cost[i] = nof::wgrad_block_cost(P[i].ntr, P[i].ntc, &P[i].shape);
     }
@@ -434,7 +435,7 @@ void AcceleratedMLP::run_wgrad(Schedule& sc, int accumulate) {
   tb(kTWgradReduce);
   NOF_HIP(nof::launch_wgrad_reduce(sc.outs.p, sc.nouts, sc.max_elems, sc.items.p, sc.probs.p, sc.slab_off.p,
                                    slabs_.p, bias_slabs_.p, accumulate,
-                                   precision_ == NOF_PRECISION_F16X2 ? amax_.p : nullptr, st_));
+                                   f16_pieces() ? amax_.p : nullptr, st_));
   te(kTWgradReduce);
 }
 
@@ -455,7 +456,7 @@ float* const* AcceleratedMLP::get_gradient(const float* color_grad, const float*
   nof::BwdArgs b{};
   b.M = L.M;
   b.split = precision_;
-  if (precision_ == NOF_PRECISION_F16X2) {
+  if (f16_pieces()) {
     NOF_HIP(nof::launch_delta_amax(density_grad, color_grad, L.M, amax_.p, st_, numeric_.p));
     b.amax = amax_.p;
   }

@@ -21,6 +21,8 @@
 // Summation order: the MFMA is a k-ordered fmaf chain, so results differ from the 32x32 kernels
 // in the last bits only (both are fp32-accurate; parity vs the fp64 oracle is unchanged).
 #pragma once
+#include <type_traits>
+
 #include "mlp_common.h"
 
 namespace nof {
@@ -116,6 +118,8 @@ struct BlkStore16H {
                  : "memory");
   }
 };
+// block stores per precision: fp32 blocks (P = 0, and P = 3: the F32_F16SPLIT mode keeps its weight-
+// gradient operands in fp32), fp16 blocks (P = 2)
 template <int P> struct Store16 { typedef BlkStore16 T; typedef float E; };
 template <> struct Store16<2> { typedef BlkStore16H T; typedef _Float16 E; };
 template <class E>
@@ -171,10 +175,10 @@ __device__ __forceinline__ void split4h(const float (&x)[4], uint32_t& hi01, uin
 }
 
 // An epilogue's finished tile t (4 values) into the next layer's B operand, and its act / delta block
-// store: fp32 as is, or (f16x2, kSplit) pre-split into the MFMA fragments mlp_layer16h consumes —
-// for the tile pair (2u, 2u + 1) one slice reads, bin[2u] = hi {v0v1, v2v3 of tile 2u, v0v1, v2v3 of
-// tile 2u + 1} and bin[2u + 1] = the lo pieces — with the fp16 block storing those hi halves
-// (bit-identical to converting v).
+// store: fp32 as is, or (f16 pieces, kSplit) pre-split into the MFMA fragments mlp_layer16h consumes
+// — for the tile pair (2u, 2u + 1) one slice reads, bin[2u] = hi {v0v1, v2v3 of tile 2u, v0v1, v2v3
+// of tile 2u + 1} and bin[2u + 1] = the lo pieces — with an fp16 block (f16x2) storing those hi halves
+// (bit-identical to converting v) and an fp32 block (F32_F16SPLIT) the values themselves.
 template <bool kSplit, bool kStore, class ST>
 __device__ __forceinline__ void put_tile(float (&bin)[16][4], int t, const float (&v)[4], const ST& bst,
                                          __amdgpu_buffer_rsrc_t blk) {
@@ -187,8 +191,13 @@ __device__ __forceinline__ void put_tile(float (&bin)[16][4], int t, const float
     bin[row + 1][c] = __uint_as_float(lo01);
     bin[row + 1][c + 1] = __uint_as_float(lo23);
     if constexpr (kStore) {
-      bst.template store_pair<0>(blk, t, hi01);
-      bst.template store_pair<2>(blk, t, hi23);
+      if constexpr (std::is_same_v<ST, BlkStore16H>) {
+        bst.template store_pair<0>(blk, t, hi01);
+        bst.template store_pair<2>(blk, t, hi23);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bst.store(blk, t, r, v[r]);
+      }
     }
   } else {
 #pragma unroll
@@ -386,12 +395,12 @@ __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const fl
   }
 }
 
-// precision dispatch: P = 0 fp32 16x16x4, P = 2 f16x2 16x16x32
+// precision dispatch: P = 0 fp32 16x16x4, P = 2 / 3 fp16 (hi, lo) pieces on 16x16x32
 template <int P, int NT_B, int NT_I, int OT, class Epi>
 __device__ __forceinline__ void layer16(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16], float* lds,
                                         int& cur, const float*& wsrc, bool last_in_schedule, int tid, int lane,
                                         Epi& epi, const float* cinit = nullptr) {
-  if constexpr (P == 2)
+  if constexpr (P == 2 || P == 3)
     mlp_layer16h<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi, cinit);
   else
     mlp_layer16<NT_B, NT_I, OT, ring16_slots<P>()>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane,

@@ -65,7 +65,8 @@ struct BwdEpi16 {
   }
 };
 
-// P: 0 = fp32, 2 = f16x2 (16x16x32 f16, power-of-2 scaled deltas stored as fp16 blocks)
+// P: 0 = fp32, 2 = f16x2 (16x16x32 f16, power-of-2 scaled deltas stored as fp16 blocks),
+// 3 = F32_F16SPLIT (16x16x32 f16, the scaled deltas stored as fp32 blocks)
 template <int P>
 __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
   typedef typename Store16<P>::T ST;
@@ -95,7 +96,7 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
     const float s = sigmoid_f(zh[1 + c]);
     dzc[c] = a.drgb[(size_t)m * 3 + c] * (s * (1.0f - s)) * kRgbScale;
   }
-  if constexpr (P == 2) {  // f16x2: deltas enter the fp16 pieces scaled by a power of two
+  if constexpr (P >= 2) {  // f16 pieces: deltas enter them scaled by a power of two
     const float sc = delta_scale(a.amax, false);
     dzs *= sc;
 #pragma unroll
@@ -119,7 +120,7 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = mask16_apply(mk, t, r, (wa[r] * dzc[0] + wb[r] * dzc[1]) + wc[r] * dzc[2]);
-      put_tile<P == 2, true>(bin, t, v, bst, d9);
+      put_tile<P >= 2, true>(bin, t, v, bst, d9);
     }
   }
   if (tid < 64) reinterpret_cast<f32x4*>(w8_lds)[tid] = reinterpret_cast<const f32x4*>(tail + kBwdTailW8)[tid];
@@ -130,12 +131,12 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
   f32x4 accA[16], accB[16];  // ping-pong, as in the forward
   AE* delta_blk = reinterpret_cast<AE*>(a.delta) + (size_t)blk * kWidth * kBlk;
   // ---- dh7 = W9[:, :256]^T delta9 + w8 dz_s ; delta7 ---------------------------------------
-  BwdEpi16<true, ST, P == 2> e7(accA, bin, bst, lane);
+  BwdEpi16<true, ST, P >= 2> e7(accA, bin, bst, lane);
   e7.begin(mask16_ptr(masks, blk, 7, half, lane), delta_blk + 7 * layer_stride, w8_lds, dzs);
   layer16<P, 4, 0, 16>(bin, nullptr, accA, lds, cur, wsrc, false, tid, lane);
   e7.tile01();
   // ---- dh_{l-1} = W_l[:, :256]^T delta_l ; delta_{l-1}, l = 7..1 (l odd: A -> B) ------------
-  BwdEpi16<false, ST, P == 2> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
+  BwdEpi16<false, ST, P >= 2> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
   eb.begin(mask16_ptr(masks, blk, 6, half, lane), delta_blk + 6 * layer_stride);
   layer16<P, 8, 0, 16>(bin, nullptr, accB, lds, cur, wsrc, false, tid, lane, e7);
   eb.tile01();
@@ -156,6 +157,7 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
 hipError_t launch_mlp_bwd16(const BwdArgs& a, hipStream_t st) {
   const int nblk = a.M / kBlk;
   if (a.split == 2) hipLaunchKernelGGL(k_mlp_bwd16<2>, dim3((nblk + 3) / 4), dim3(kMlp16Threads), 0, st, a);
+  else if (a.split == 3) hipLaunchKernelGGL(k_mlp_bwd16<3>, dim3((nblk + 3) / 4), dim3(kMlp16Threads), 0, st, a);
   else hipLaunchKernelGGL(k_mlp_bwd16<0>, dim3((nblk + 3) / 4), dim3(kMlp16Threads), 0, st, a);
   return hipGetLastError();
 }

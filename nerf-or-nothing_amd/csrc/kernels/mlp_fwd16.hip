@@ -77,7 +77,8 @@ struct FwdEpi16 {
   }
 };
 
-// P: 0 = fp32 (16x16x4 fp32 MFMA, fp32 activation blocks), 2 = f16x2 (16x16x32 f16, fp16 blocks)
+// P: 0 = fp32 (16x16x4 fp32 MFMA, fp32 activation blocks), 2 = f16x2 (16x16x32 f16, fp16 blocks),
+// 3 = F32_F16SPLIT (16x16x32 f16, fp32 blocks)
 template <int P, bool store>  // store: side outputs for the backward pass (off for inference)
 __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
   typedef typename Store16<P>::T ST;
@@ -186,7 +187,7 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
   AE* act_h_blk = reinterpret_cast<AE*>(a.act_h) + (size_t)blk * kWidth * kBlk;
 
   // ---- trunk: layer l writes acc(l odd ? B : A) ------------------------------------------
-  constexpr bool kPre = P == 2;  // f16x2: trunk epilogues keep the next B operand pre-split
+  constexpr bool kPre = P >= 2;  // f16 pieces: trunk epilogues keep the next B operand pre-split
   FwdEpi16<store, false, 16, ST, kPre> ea(accA, bin, bst, lane), eb(accB, bin, bst, lane);
   const float* bias_g = biases + 4 * g;  // the lane group's bias slot (the layers' initial accumulators)
   ea.begin(act_h_blk, mask16_ptr(a.masks, blk, 0, half, lane));
@@ -250,6 +251,9 @@ hipError_t launch_mlp_fwd16(const FwdArgs& a, hipStream_t st) {
   if (a.split == 2) {
     if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd16<2, false>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((k_mlp_fwd16<2, true>), grid, block, 0, st, a);
+  } else if (a.split == 3) {  // the inference variant is <2, false>'s arithmetic with nothing stored
+    if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd16<2, false>), grid, block, 0, st, a);
+    else hipLaunchKernelGGL((k_mlp_fwd16<3, true>), grid, block, 0, st, a);
   } else {
     if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd16<0, false>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((k_mlp_fwd16<0, true>), grid, block, 0, st, a);

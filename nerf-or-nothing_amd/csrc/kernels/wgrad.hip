@@ -694,6 +694,8 @@ hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const in
                        slabs, bias_slabs);
     return hipGetLastError();
   }
+  if (precision == 3)  // F32_F16SPLIT: fp32 operand blocks split into fp16 (hi, lo), 3 products
+    return launch_wgrad_split<2>(probs, items, item_ptr, num_wg, slab_off, slabs, bias_slabs, st);
   return launch_wgrad_split<1>(probs, items, item_ptr, num_wg, slab_off, slabs, bias_slabs, st);
 }
 

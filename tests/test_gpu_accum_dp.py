@@ -55,7 +55,7 @@ def _accumulated(gpu, r, d, n, micro, seed, step, base, msum, precision=0):
     return g
 
 
-@pytest.mark.parametrize("precision", [0, 2])
+@pytest.mark.parametrize("precision", [0, 2, 3])
 def test_accumulated_microbatches_equal_one_call(gpu, precision):
     import torch
     import nof

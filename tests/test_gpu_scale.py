@@ -33,7 +33,7 @@ def _grads(m, r, gpu, seed, step, base, lo, hi, msum):
     return nof.to_numpy(m.mlp.flat_grads()[0], (P,)).astype(np.float64), m.loss()
 
 
-@pytest.mark.parametrize("precision", [0, 1, 2])
+@pytest.mark.parametrize("precision", [0, 1, 2, 3])
 def test_config4_shard_additivity(gpu, precision):
     import nof
     from nof import synth
@@ -53,7 +53,7 @@ def test_config4_shard_additivity(gpu, precision):
     assert abs((l_a + l_b) - l_all) <= 1e-5 * abs(l_all)
 
 
-@pytest.mark.parametrize("precision", [0, 2])  # config 5 names fp16 on MFMA: the f16x2 perf mode
+@pytest.mark.parametrize("precision", [0, 2, 3])  # config 5 names fp16 on MFMA: the f16 modes
 def test_config5_shape_deterministic(gpu, precision):
     import nof
     from nof import synth

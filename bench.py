@@ -368,10 +368,10 @@ def main():
     ranks = list(range(G)) if single else [rank]
 
     # pre-staged synthetic batches per device (views of a 100-pose Lego-shaped scene), global ray ids
-    def stage(r, d, n=shard):
+    def stage(r, d, n=shard, scene=None):
         out = []
         for i in range(2):
-            h = (synth.llff_rays if a.scene == "llff" else synth.blender_rays)(n, seed=1000 * r + i)
+            h = (synth.llff_rays if (scene or a.scene) == "llff" else synth.blender_rays)(n, seed=1000 * r + i)
             out.append({k: torch.from_numpy(v).to(torch.device("cuda", d)) for k, v in h.items()})
         return out
 
@@ -385,7 +385,7 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         native = [NativeDP.init_rank(obj[0], world, rank, dev_idx)]
 
-    def measure(prec, B_run=None, steps=None, warmup=None, timers_on=True):
+    def measure(prec, B_run=None, steps=None, warmup=None, timers_on=True, scene=None):
         """W untimed + K timed training steps of one precision mode over the global batch (each
         rank's shard in micro-batches accumulated into one gradient, one all-reduce), then a short
         untimed pass with every kernel class event-timed (the per-kernel breakdown); returns
@@ -398,7 +398,8 @@ def main():
         mb = min(a.micro_batch, sh)
         steps = steps or a.steps
         warmup = a.warmup if warmup is None else warmup
-        pl = pools if sh == shard else [stage(r, d, sh) for r, d in zip(ranks, devs)]
+        pl = pools if (sh == shard and scene in (None, a.scene)) else \
+            [stage(r, d, sh, scene) for r, d in zip(ranks, devs)]
         models, opts, bucketed = [], [], []
         for r, d in zip(ranks, devs):
             st = torch.cuda.current_stream(torch.device("cuda", d)).cuda_stream
@@ -535,6 +536,14 @@ def main():
     if world == 1 and G == 1 and not a.no_alt:
         alts = [(p,) + measure(p) for p in PRECISIONS if p != a.precision]
     cfg4 = None
+    llff = None
+    if lead and world == 1 and G == 1 and a.scene == "blender" and not a.no_alt:
+        # north_star's "rays/sec on synthetic LLFF-shape batches": the same step on forward-facing NDC
+        # rays (the MLP work per sample does not depend on the ray distribution)
+        l_dt, _, l_psnr, _ = measure(a.precision, steps=20, warmup=3, timers_on=False, scene="llff")
+        llff = {"workload": f"LLFF-shaped (forward-facing, NDC) {B}-ray batches x {'+'.join(map(str, samples))} "
+                            "samples", "value": round(B * 20 / l_dt, 1), "unit": "rays/s",
+                "ms_per_step": round(l_dt * 1e3 / 20, 4), "steps": 20, "precision": a.precision}
     if lead and world == 1 and G == 1 and not a.no_config4 and B != 65536 and a.scene == "blender" \
             and samples == [128, 128]:
         # SURVEY §8(e)'s scaling denominator: config 4's 65536-ray global batch on this one GPU,
@@ -571,6 +580,8 @@ def main():
             result["params_in_sync"] = in_sync
             if world > 1 and backend != "nccl":
                 result["rehearsal"] = f"{backend}: {world} ranks on {torch.cuda.device_count()} GPU(s), not a scaling run"
+        if llff:
+            result["llff_1gpu"] = llff
         if cfg4:
             result["config4_1gpu"] = cfg4
         if alts:  # the other precision modes, same workload (split: same 1e-5 parity; f16x2: 2e-3)

@@ -21,8 +21,6 @@
 // Summation order: the MFMA is a k-ordered fmaf chain, so results differ from the 32x32 kernels
 // in the last bits only (both are fp32-accurate; parity vs the fp64 oracle is unchanged).
 #pragma once
-#include <type_traits>
-
 #include "mlp_common.h"
 
 namespace nof {
@@ -74,7 +72,15 @@ __device__ __forceinline__ constexpr int feat16(int t, int g, int r) { return 16
 // blk_off) for sample 16 half + j: byte(f, s) = 128 f + ((((s >> 2) ^ (f & 7)) << 4) | ((s & 3) << 2))
 // with f = 16t + 4g + r, so f & 7 = 4 (g & 1) + r and the lane part is one of four offsets (by r);
 // the tile (t) part 2048 t + 128 r is the instruction's immediate.
+// Cache policy of the activation / delta block stores (gfx950 CPol): nt (streaming) for every fp32
+// block and for the backward's fp16 blocks.  A/B against default stores on one box (round 2, per
+// level fwd + bwd + wgrad): the weight-gradient launch that reads the blocks next runs 1.5 % (fp32),
+// 7 % (F32_F16SPLIT) and 10 % (f16x2) faster, the F32_F16SPLIT forward 2 % faster, the f16x2
+// backward 4 % slower: per level -0.5 % (fp32), -3.5 % (F32_F16SPLIT), -0.7 % (f16x2).  The f16x2
+// forward's 32-B half-line stores measured 3 % slower as nt and stay default.
+constexpr int kStoreNT = 2;  // aux bit of the buffer-store builtins: nt
 struct BlkStore16 {
+  static constexpr bool kHalf = false;
   uint32_t voff[4];
   __device__ __forceinline__ BlkStore16(int lane, int half) {
     const int g = lane >> 4, s = 16 * half + (lane & 15);
@@ -86,7 +92,7 @@ struct BlkStore16 {
   // lane part a 32-bit voffset (a flat 64-bit address per lane would cost a VALU add per store and
   // 8 VGPRs of hoisted offsets)
   __device__ __forceinline__ void store(__amdgpu_buffer_rsrc_t blk, int t, int r, float v) const {
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), blk, (int)voff[r], 2048 * t + 128 * r, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), blk, (int)voff[r], 2048 * t + 128 * r, kStoreNT);
   }
 };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t blk_rsrc(float* blk) {
@@ -95,8 +101,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t blk_rsrc(float* blk) {
 
 // fp16 counterpart (f16x2 mode, common.h blkh_off): byte(f, s) = 64 f + ((((s >> 3) ^ ((f >> 2) & 3)) << 4) |
 // ((s & 7) << 1)) with f = 16t + 4g + r, s = 16 half + j, so (f >> 2) & 3 = g and the lane part does not
-// depend on (t, r): one voffset, 1024 t in soffset, 64 r immediate.
+// depend on (t, r): one voffset, 1024 t in soffset, 64 r immediate.  kNT: nt stores (see BlkStore16).
+template <bool kNT>
 struct BlkStore16H {
+  static constexpr bool kHalf = true;
   uint32_t voff;
   __device__ __forceinline__ BlkStore16H(int lane, int half) {
     const int g = lane >> 4, j = lane & 15;
@@ -106,22 +114,29 @@ struct BlkStore16H {
     store_h(blk, t, r, (_Float16)v);
   }
   __device__ __forceinline__ void store_h(__amdgpu_buffer_rsrc_t blk, int t, int r, _Float16 h) const {
-    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, h), blk, (int)voff + 64 * r, 1024 * t, 0);
+    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, h), blk, (int)voff + 64 * r, 1024 * t,
+                                          kNT ? kStoreNT : 0);
   }
   // both halves of a packed fp16 pair: features R (low half) and R + 1 (high half, store_short_d16_hi)
   template <int R>
   __device__ __forceinline__ void store_pair(__amdgpu_buffer_rsrc_t blk, int t, uint32_t pair) const {
-    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)pair, blk, (int)voff, 1024 * t + 64 * R, 0);
-    asm volatile("buffer_store_short_d16_hi %0, %1, %2, %3 offen offset:%4"
-                 :
-                 : "v"(pair), "v"(voff), "s"(blk), "s"(1024 * t), "n"(64 * (R + 1))
-                 : "memory");
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)pair, blk, (int)voff, 1024 * t + 64 * R, kNT ? kStoreNT : 0);
+    if constexpr (kNT)
+      asm volatile("buffer_store_short_d16_hi %0, %1, %2, %3 offen offset:%4 nt"
+                   :
+                   : "v"(pair), "v"(voff), "s"(blk), "s"(1024 * t), "n"(64 * (R + 1))
+                   : "memory");
+    else
+      asm volatile("buffer_store_short_d16_hi %0, %1, %2, %3 offen offset:%4"
+                   :
+                   : "v"(pair), "v"(voff), "s"(blk), "s"(1024 * t), "n"(64 * (R + 1))
+                   : "memory");
   }
 };
 // block stores per precision: fp32 blocks (P = 0, and P = 3: the F32_F16SPLIT mode keeps its weight-
-// gradient operands in fp32), fp16 blocks (P = 2)
-template <int P> struct Store16 { typedef BlkStore16 T; typedef float E; };
-template <> struct Store16<2> { typedef BlkStore16H T; typedef _Float16 E; };
+// gradient operands in fp32), fp16 blocks (P = 2; kBwd: the backward's delta stores, nt)
+template <int P, bool kBwd> struct Store16 { typedef BlkStore16 T; typedef float E; };
+template <bool kBwd> struct Store16<2, kBwd> { typedef BlkStore16H<kBwd> T; typedef _Float16 E; };
 template <class E>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t blk_rsrc_t(E* blk) {
   return __builtin_amdgcn_make_buffer_rsrc(blk, (short)0, 0x7fffffff, 0x00020000);
@@ -191,7 +206,7 @@ __device__ __forceinline__ void put_tile(float (&bin)[16][4], int t, const float
     bin[row + 1][c] = __uint_as_float(lo01);
     bin[row + 1][c + 1] = __uint_as_float(lo23);
     if constexpr (kStore) {
-      if constexpr (std::is_same_v<ST, BlkStore16H>) {
+      if constexpr (ST::kHalf) {
         bst.template store_pair<0>(blk, t, hi01);
         bst.template store_pair<2>(blk, t, hi23);
       } else {

@@ -69,8 +69,8 @@ struct BwdEpi16 {
 // 3 = F32_F16SPLIT (16x16x32 f16, the scaled deltas stored as fp32 blocks)
 template <int P>
 __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
-  typedef typename Store16<P>::T ST;
-  typedef typename Store16<P>::E AE;
+  typedef typename Store16<P, true>::T ST;
+  typedef typename Store16<P, true>::E AE;
   __shared__ __attribute__((aligned(16))) float lds[ring16_floats<P>() + 256];
   float* w8_lds = lds + ring16_floats<P>();
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, j = lane & 15;

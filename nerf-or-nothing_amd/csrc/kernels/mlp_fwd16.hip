@@ -81,8 +81,8 @@ struct FwdEpi16 {
 // 3 = F32_F16SPLIT (16x16x32 f16, fp32 blocks)
 template <int P, bool store>  // store: side outputs for the backward pass (off for inference)
 __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
-  typedef typename Store16<P>::T ST;
-  typedef typename Store16<P>::E AE;
+  typedef typename Store16<P, false>::T ST;
+  typedef typename Store16<P, false>::E AE;
   constexpr int kRing = ring16_slots<P>() * kSliceFloats;
   constexpr bool kIpeReg = ring16_slots<P>() == 4;  // 4-slot ring: IPE B values stay in registers
   constexpr int kIpeLds = kIpeReg ? 0 : 8 * kIpe16Floats;

@@ -68,6 +68,8 @@ def parse():
                    help="one process drives --gpus devices (nof_dp_init_all, grouped all-reduce) instead of one "
                         "process per GPU")
     p.add_argument("--no-config4", action="store_true", help="skip the N=1 configs[3] (65536-ray) measurement")
+    p.add_argument("--no-config5", action="store_true",
+                   help="skip the configs[4] leg (4096 LLFF rays x 256+256, f16x2, at every N)")
     p.add_argument("--samples", type=int, nargs="+", default=[128, 128])
     p.add_argument("--scene", choices=["blender", "llff"], default="blender",
                    help="synthetic ray distribution: Lego-shaped 800x800 views (configs 2-4) or forward-facing "
@@ -385,7 +387,7 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         native = [NativeDP.init_rank(obj[0], world, rank, dev_idx)]
 
-    def measure(prec, B_run=None, steps=None, warmup=None, timers_on=True, scene=None):
+    def measure(prec, B_run=None, steps=None, warmup=None, timers_on=True, scene=None, smp=None):
         """W untimed + K timed training steps of one precision mode over the global batch (each
         rank's shard in micro-batches accumulated into one gradient, one all-reduce), then a short
         untimed pass with every kernel class event-timed (the per-kernel breakdown); returns
@@ -394,6 +396,7 @@ def main():
         pair costs the dependent launch sequence a few us (measured 1.5 % of the f32 step and 4 % of
         the f16x2 step with every kernel class timed)."""
         B_run = B_run or B
+        smp = list(smp or samples)
         sh = B_run // G
         mb = min(a.micro_batch, sh)
         steps = steps or a.steps
@@ -403,7 +406,7 @@ def main():
         models, opts, bucketed = [], [], []
         for r, d in zip(ranks, devs):
             st = torch.cuda.current_stream(torch.device("cuda", d)).cuda_stream
-            m = nof.AcceleratedMipNeRF(device=d, max_rays=mb, num_samples=samples, seed=seed, stream=st,
+            m = nof.AcceleratedMipNeRF(device=d, max_rays=mb, num_samples=smp, seed=seed, stream=st,
                                        precision=PRECISIONS[prec])
             models.append(m)
             opts.append(nof.AcceleratedAdamOptimizer(m.GetLayerSizes(), m.config))
@@ -487,7 +490,7 @@ def main():
         # fine-level PSNR of the last micro-batch (MseToPsnr, MipHelpers.cs:672)
         last = pl[0][(warmup + steps + kb - 1) % 2]
         lo_, hi_ = cs[-1]
-        comp = models[0].level_numpy(len(samples) - 1)["comp_rgb"]
+        comp = models[0].level_numpy(len(smp) - 1)["comp_rgb"]
         mse = float(np.mean((comp - last["pix"][lo_:hi_].cpu().numpy()) ** 2))
         psnr = -10.0 * math.log10(max(mse, 1e-12))
         for bk in bucketed:
@@ -553,6 +556,23 @@ def main():
                             "of 8192 rays accumulated, one Adam step", "value": round(65536 * 3 / c_dt, 1),
                 "unit": "rays/s", "ms_per_step": round(c_dt * 1e3 / 3, 3), "steps": 3, "warmup": 1}
 
+    cfg5 = None
+    if a.scene == "blender" and not a.no_config5:
+        # BASELINE configs[4] (north_star's "rays/sec on synthetic LLFF-shape batches at 1, 2, 4 and 8
+        # GPUs"): 4096 forward-facing NDC rays x 256 + 256 samples per step over all N GPUs (512 per
+        # GPU at N = 8), fp16 pieces on MFMA (the f16x2 perf mode), one all-reduce per step — at every N
+        c_B = 4096
+        if c_B % G == 0:
+            c_dt, _, _, c_sync = measure("f16x2", B_run=c_B, steps=20, warmup=3, timers_on=False, scene="llff",
+                                         smp=(256, 256))
+            cfg5 = {"workload": f"BASELINE configs[4]: LLFF-shaped (forward-facing, NDC) {c_B}-ray global batch x "
+                                f"256+256 samples, {c_B // G} rays per GPU, f16x2 perf mode (fp16 pieces on MFMA)",
+                    "value": round(c_B * 20 / c_dt, 1), "unit": "rays/s", "n_gpus": G,
+                    "ms_per_step": round(c_dt * 1e3 / 20, 4), "steps": 20, "warmup": 3, "scaling": "strong",
+                    "dtype": DTYPES["f16x2"]}
+            if c_sync is not None:
+                cfg5["params_in_sync"] = c_sync
+
     result = None
     if lead:
         ms_step, kernels, roof = summarize(a.precision, dt, timing)
@@ -584,6 +604,8 @@ def main():
             result["llff_1gpu"] = llff
         if cfg4:
             result["config4_1gpu"] = cfg4
+        if cfg5:
+            result["config5"] = cfg5
         if alts:  # the other precision modes, same workload (split: same 1e-5 parity; f16x2: 2e-3)
             result["alt_precision"] = []
             for aprec, adt, atiming, apsnr, _ in alts:

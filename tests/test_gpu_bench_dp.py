@@ -28,6 +28,8 @@ def test_bench_two_ranks_rehearsal(gpu):
     assert r["n_gpus"] == 2 and r["config"]["global_batch"] == 512 and r["config"]["parallelism"] == "dp2"
     assert r["params_in_sync"] is True
     assert r["value"] > 0 and "rehearsal" in r
+    c5 = r["config5"]  # configs[4]: 4096 LLFF rays x 256+256 (f16x2) over both ranks, its own all-reduce
+    assert c5["n_gpus"] == 2 and c5["value"] > 0 and c5["params_in_sync"] is True
 
 
 def test_bench_single_process_mode(gpu):
@@ -39,4 +41,4 @@ def test_bench_single_process_mode(gpu):
     assert out.returncode == 0, out.stderr[-2000:]
     r = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert r["config"]["global_batch"] == 16384 and r["config"]["micro_batches_per_step"] == 2
-    assert r["value"] > 0
+    assert r["value"] > 0 and r["config5"]["value"] > 0

@@ -10,7 +10,7 @@ TAG=${1:-r02}; shift
 PRECS=${*:-f32 split f16x2}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-integrator --no-alt --no-config4"
+ARGS="--steps 5 --warmup 2 --no-cpu-baseline --no-integrator --no-alt --no-config4 --no-config5"
 run() {  # name, then the rocprofv3 options
   local name=$1; shift
   echo "$(date +%T) $name" >> $OUT/progress.log

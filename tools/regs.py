@@ -6,7 +6,7 @@ import re
 import subprocess
 import sys
 
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fhip-fp32-correctly-rounded-divide-sqrt", "-c",
+FLAGS = [*__import__("os").environ.get("REGS_DEFS", "").split(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fhip-fp32-correctly-rounded-divide-sqrt", "-c",
          "-o", "/tmp/regs.o", "-Rpass-analysis=kernel-resource-usage"]
 for src in sys.argv[1:]:
     out = subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, src], capture_output=True, text=True).stderr

@@ -77,6 +77,106 @@ __global__ __launch_bounds__(512, 1) void k_w16(const float* __restrict__ img, i
   if (tid == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+
+// The forward epilogue's per-tile work (mlp16.h relu_bit + split4h + the two fp16 pair stores), on a
+// register set that no MFMA of the current layer touches (the previous layer's accumulators).
+__device__ __forceinline__ float relu_bit(float z, uint32_t& mw) {
+  const int h = max(__float_as_int(z), 0);
+  asm volatile("v_cmp_lt_i32 vcc, 0, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(mw) : "v"(h) : "vcc");
+  return __int_as_float(h);
+}
+template <int t>
+__device__ __forceinline__ void epi_tile_t(f32x4& v, uint32_t& mw, f16x8& bin, __amdgpu_buffer_rsrc_t blk, uint32_t voff) {
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  float x[4];
+  for (int r = 0; r < 4; ++r) x[r] = relu_bit(v[r], mw);
+  const uint32_t hi01 = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2{x[0], x[1]}), h2));
+  const uint32_t hi23 = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2{x[2], x[3]}), h2));
+  float r4[4];
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(r4[0]) : "v"(x[0]), "v"(hi01));
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(r4[1]) : "v"(x[1]), "v"(hi01));
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(r4[2]) : "v"(x[2]), "v"(hi23));
+  asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(r4[3]) : "v"(x[3]), "v"(hi23));
+  const uint32_t lo01 = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2{r4[0], r4[1]}), h2));
+  const uint32_t lo23 = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2{r4[2], r4[3]}), h2));
+  f32x4 u = {__uint_as_float(hi01), __uint_as_float(hi23), __uint_as_float(lo01), __uint_as_float(lo23)};
+  bin = __builtin_bit_cast(f16x8, u);
+  __builtin_amdgcn_raw_buffer_store_b16((unsigned short)hi01, blk, (int)voff, 1024 * t, 0);
+  asm volatile("buffer_store_short_d16_hi %0, %1, %2, %3 offen offset:64" : : "v"(hi01), "v"(voff), "s"(blk), "s"(1024 * t) : "memory");
+  __builtin_amdgcn_raw_buffer_store_b16((unsigned short)hi23, blk, (int)voff, 1024 * t + 128, 0);
+  asm volatile("buffer_store_short_d16_hi %0, %1, %2, %3 offen offset:192" : : "v"(hi23), "v"(voff), "s"(blk), "s"(1024 * t) : "memory");
+}
+
+// w16 + the epilogue of two tiles per slice.  EPI: 1 = groups 4, 6 for every wave (the kernels);
+// 2 = waves 4..7 (the SIMD partners) at groups 5, 7; 3 = waves 4..7 at groups 0, 2 (half a slice early).
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void k_w16e(const float* __restrict__ img, int reps, float* out, long long* cyc,
+                                                 float* scratch) {
+  constexpr int kSlots = 3, T = 512;
+  __shared__ __attribute__((aligned(16))) float lds[kSlots * kSliceFloats];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const bool up = __builtin_amdgcn_readfirstlane(tid >> 8) != 0;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(img), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t blk = __builtin_amdgcn_make_buffer_rsrc(
+      scratch + (size_t)(blockIdx.x * 8 + wv) * 4096, (short)0, 0x7fffffff, 0x00020000);
+  const uint32_t voff = 256u * (lane >> 4) + ((lane & 15) << 1);
+  f32x4 acc[16] = {};
+  f32x4 prev[16];
+  for (int i = 0; i < 16; ++i) prev[i] = f32x4{0.1f * i - 0.7f, 0.3f - 0.01f * lane, 0.2f, -0.4f + 0.05f * i};
+  f16x8 bin[2];
+  uint32_t mw = 0;
+  f16x8 b0, b1;
+  for (int i = 0; i < 8; ++i) { b0[i] = (_Float16)(0.37f * (i + lane % 7) - 1.1f); b1[i] = (_Float16)(0.013f * (i - lane % 5)); }
+  const int e1 = EPI == 1 ? 4 : EPI == 2 ? (up ? 5 : 4) : (up ? 0 : 4);
+  const int e2 = EPI == 1 ? 6 : EPI == 2 ? (up ? 7 : 6) : (up ? 2 : 6);
+  const long long t0 = __builtin_readcyclecounter();
+  for (int rep = 0; rep < reps; ++rep) {
+    auto dma = [&](int s, int i) {
+      float* dst = lds + (s % kSlots) * kSliceFloats;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lptr_t)(dst + (T * i + 64 * wave) * 4), 16, tid * 16,
+                                               (s * kSliceFloats + i * T * 4) * 4, 0, 0);
+    };
+    for (int i = 0; i < 4; ++i) { dma(0, i); dma(1, i); }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    for (int s = 0; s < kSlices; ++s) {
+      const f16x8* W = reinterpret_cast<const f16x8*>(lds + (s % kSlots) * kSliceFloats) + lane;
+      f16x8 fr[2][4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) fr[0][k] = W[k * 64];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (q + 1 < 8)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) fr[(q + 1) & 1][k] = W[(4 * (q + 1) + k) * 64];
+        if (s + 2 < kSlices && q < 4) dma(s + 2, q);
+        __builtin_amdgcn_sched_barrier(0);
+        const f16x8* f = fr[q & 1];
+        acc[2 * q] = mfma(f[1], b0, acc[2 * q]);
+        acc[2 * q + 1] = mfma(f[3], b0, acc[2 * q + 1]);
+        acc[2 * q] = mfma(f[0], b1, acc[2 * q]);
+        acc[2 * q + 1] = mfma(f[2], b1, acc[2 * q + 1]);
+        acc[2 * q] = mfma(f[0], b0, acc[2 * q]);
+        acc[2 * q + 1] = mfma(f[2], b0, acc[2 * q + 1]);
+        if (q == e1) epi_tile_t<0>(prev[2 * q], mw, bin[0], blk, voff);
+        if (q == e2) epi_tile_t<1>(prev[2 * q + 1], mw, bin[1], blk, voff);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      b0 = b0 + bin[0] * (_Float16)0.0f;  // keep the epilogue live (the next slice's B operand)
+      b1 = b1 + bin[1] * (_Float16)0.0f;
+      asm volatile("s_waitcnt vmcnt(8)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  }
+  const long long t1 = __builtin_readcyclecounter();
+  float sum = (float)mw;
+  for (int i = 0; i < 16; ++i) sum += acc[i][0] + acc[i][3];
+  out[blockIdx.x * 512 + tid] = sum;
+  if (tid == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
 // w32: 4 waves, 32 samples each; 8 groups of {4 reads one group ahead, 12 MFMAs over 4 accumulators};
 // DMA: 8 steps of 16 B per thread per slice, two per group in groups 0..3.  SLOTS = 3 (barrier per slice) or 4
 // (barrier per two slices).
@@ -166,6 +266,26 @@ static void run_k(const char* name, K kern, int threads, const float* img, float
               ms, per, ns, 1536.0 / per, 1536.0 / ns);
 }
 
+template <class K>
+static void run_e(const char* name, K kern, const float* img, float* out, long long* cyc, float* scratch, int reps) {
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  hipLaunchKernelGGL(kern, dim3(256), dim3(512), 0, 0, img, 1, out, cyc, scratch);
+  (void)hipEventRecord(a);
+  hipLaunchKernelGGL(kern, dim3(256), dim3(512), 0, 0, img, reps, out, cyc, scratch);
+  (void)hipEventRecord(b);
+  (void)hipEventSynchronize(b);
+  float ms = 0.0f;
+  (void)hipEventElapsedTime(&ms, a, b);
+  std::vector<long long> c(256);
+  (void)hipMemcpy(c.data(), cyc, 256 * sizeof(long long), hipMemcpyDeviceToHost);
+  double mean = 0;
+  for (long long x : c) mean += (double)x / 256;
+  const double per = mean / (kSlices * reps), ns = ms * 1e6 / (kSlices * reps);
+  std::printf("%-26s %8.3f ms  %6.0f ticks/slice  %6.1f ns/slice  MFMA-busy(ticks) %.2f\n", name, ms, per, ns, 1536.0 / per);
+}
+
 int main() {
   float *img, *out;
   long long* cyc;
@@ -178,7 +298,12 @@ int main() {
   (void)hipMalloc(&out, 256 * 512 * 4);
   (void)hipMalloc(&cyc, 256 * sizeof(long long));
   const int reps = 20;
+  float* scratch;
+  (void)hipMalloc(&scratch, (size_t)256 * 8 * 4096 * 4);
   for (int it = 0; it < 2; ++it) {
+    run_e("w16 + epilogue 4/6", k_w16e<1>, img, out, cyc, scratch, reps);
+    run_e("w16 + epi, up 5/7", k_w16e<2>, img, out, cyc, scratch, reps);
+    run_e("w16 + epi, up 0/2", k_w16e<3>, img, out, cyc, scratch, reps);
     run_k("w16 (2 waves/SIMD, 3 slots)", k_w16<>, 512, img, out, cyc, reps);
     run_k("w16 no reads", k_w16<false>, 512, img, out, cyc, reps);
     run_k("w16 no dma", k_w16<true, false>, 512, img, out, cyc, reps);

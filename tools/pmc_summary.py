@@ -65,6 +65,8 @@ json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
 names = {"k_mlp_fwd16<0, true>": "mlp_fwd", "k_mlp_bwd16<0>": "mlp_bwd", "k_wgrad": "wgrad",
          "k_mlp_fwd16<2, true>": "mlp_fwd_f16x2", "k_mlp_bwd16<2>": "mlp_bwd_f16x2", "k_wgrad_h": "wgrad_f16x2",
          "k_mlp_fwd<1, true>": "mlp_fwd_split", "k_mlp_bwd<1>": "mlp_bwd_split", "k_wgrad_x3<1>": "wgrad_split",
+         "k_mlp_fwd16<3, true>": "mlp_fwd_f16split", "k_mlp_bwd16<3>": "mlp_bwd_f16split",
+         "k_wgrad_x3<2>": "wgrad_f16split",
          "k_render_fwd<2>": "render_fwd" + suffix, "k_render_bwd<2>": "render_bwd" + suffix}
 for fname, key in (("pmc_traffic.json", "hbm_bytes_per_launch"), ("pmc_mfma.json", "mfma_busy")):
     f = os.path.join(dst, fname)

@@ -20,7 +20,14 @@
 //
 //   nof_train --records train_data.bin [--steps K] [--batch N] [--precision f32|split|f16x2|f16split]
 //             [--print-every P] [--save-every S --ckpt-dir DIR] [--resume CKPT] [--host-api]
-//             [--seed X] [--device D] [--dump-params FILE]
+//             [--seed X] [--device D | --gpus N] [--dump-params FILE]
+//
+// --gpus N: data parallelism in ONE process over devices 0..N-1 (SURVEY 8e's process model): the
+// global batch of --batch rays is sharded into N contiguous shards with global ray ids (every shard
+// draws exactly what the whole batch would), each device normalises by the GLOBAL loss-multiplier
+// sum, the gradient arenas are summed by one grouped RCCL all-reduce (nof_dp_init_all /
+// nof_dp_allreduce_grads_all, with failure detection: nof_dp_wait), and every device applies the
+// same Adam step — parameters stay bitwise identical across devices.
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -37,6 +44,7 @@ namespace {
 struct Args {
   std::string records, ckpt_dir, resume, dump_params;
   int steps = 100, batch = 1024, print_every = 100, save_every = 0, device = 0, precision = NOF_PRECISION_F32;
+  int gpus = 0;  // > 0: data parallel over devices 0..gpus-1 in this process (nof_dp_init_all)
   bool host_api = false;
   uint64_t seed = 0x5EED0000ull;
   // Config (TrainState.cs:54-58)
@@ -48,7 +56,7 @@ struct Args {
   std::fprintf(code ? stderr : stdout,
                "usage: nof_train --records FILE [--steps K] [--batch N] [--precision f32|split|f16x2|f16split]\n"
                "                 [--print-every P] [--save-every S --ckpt-dir DIR] [--resume CKPT] [--host-api]\n"
-               "                 [--seed X] [--device D] [--dump-params FILE]\n");
+               "                 [--seed X] [--device D | --gpus N] [--dump-params FILE]\n");
   std::exit(code);
 }
 
@@ -70,6 +78,7 @@ Args parse(int argc, char** argv) {
     else if (k == "--resume") a.resume = val();
     else if (k == "--dump-params") a.dump_params = val();
     else if (k == "--device") a.device = std::atoi(val());
+    else if (k == "--gpus") a.gpus = std::atoi(val());
     else if (k == "--seed") a.seed = std::strtoull(val(), nullptr, 0);
     else if (k == "--host-api") a.host_api = true;
     else if (k == "--precision") {
@@ -86,6 +95,7 @@ Args parse(int argc, char** argv) {
   }
   if (a.records.empty() || a.steps < 0 || a.batch <= 0 || a.print_every < 0 || a.save_every < 0) usage(2);
   if (a.save_every && a.ckpt_dir.empty()) usage(2);
+  if (a.gpus < 0 || (a.gpus > 0 && a.batch % a.gpus)) usage(2);
   return a;
 }
 
@@ -118,14 +128,16 @@ struct StepCtx {
   const float* host_pixels;
   int n;
   uint64_t fine_output;  // `output = inputptr`: the last level's compRgb
+  float global_msum;     // > 0 (data parallel): normalise by the whole batch's sum, not the shard's
 };
 uint64_t output_gradient(void* user, uint64_t dev_comp_rgb, int32_t level, float loss_mult_sum,
                          uint64_t dev_loss_mults) {
   StepCtx* c = static_cast<StepCtx*>(user);
   c->fine_output = dev_comp_rgb;
   uint64_t g = 0;
-  if (nof_gradcalc_output_gradient(c->calc, dev_comp_rgb, c->host_pixels, c->n, dev_loss_mults, loss_mult_sum, level,
-                                   &g) != NOF_OK)
+  const float msum = c->global_msum > 0.0f ? c->global_msum : loss_mult_sum;
+  if (nof_gradcalc_output_gradient(c->calc, dev_comp_rgb, c->host_pixels, c->n, dev_loss_mults, msum, level, &g) !=
+      NOF_OK)
     return 0;  // GetGradient reports the null gradient as an error
   return g;
 }
@@ -137,89 +149,155 @@ void d2h(std::vector<float>& dst, const float* src, size_t count) {
 
 }  // namespace
 
+// one device's share of the job: its dataset copy, model, optimizer (and output-gradient calculator)
+struct Replica {
+  int device = 0;
+  nof_dataset* ds = nullptr;
+  nof_mipnerf* model = nullptr;
+  nof_adam* adam = nullptr;
+  nof_gradcalc* calc = nullptr;
+  nof_mlp* mlp = nullptr;
+  float* const* params = nullptr;
+  nof_config cfg;
+  nof_batch b;
+  float msum = 0.0f;
+  uint64_t fine = 0;
+  std::vector<float> ho, hd, hr, hn, hf, hm, hp;  // host rays (--host-api) / loss inputs
+};
+
 int main(int argc, char** argv) {
   const Args a = parse(argc, argv);
-  CHECK(nof_set_device(a.device));
-  nof_dataset* ds = nullptr;
-  CHECK(nof_dataset_open(a.records.c_str(), a.device, &ds));
-  nof_config cfg;
-  nof_config_default(&cfg);
-  cfg.device = a.device;
-  cfg.max_rays = a.batch;
-  cfg.seed = a.seed;
-  cfg.precision = a.precision;
-  nof_mipnerf* model = nullptr;
-  CHECK(nof_mipnerf_create(&cfg, &model));
-  int32_t sizes[64], nsizes = 0;
-  CHECK(nof_mipnerf_layer_sizes(model, sizes, 64, &nsizes));
-  nof_adam* adam = nullptr;
-  CHECK(nof_adam_create(sizes, nsizes, &cfg, &adam));
-  nof_gradcalc* calc = nullptr;
-  if (a.host_api) CHECK(nof_gradcalc_create(a.batch, &cfg, &calc));
-  nof_mlp* mlp = nullptr;
-  CHECK(nof_mipnerf_mlp(model, &mlp));
-  float* const* params = nullptr;
-  CHECK(nof_mlp_params(mlp, &params));  // model.mlp.allParams
+  const int G = a.gpus > 0 ? a.gpus : 1;
+  const int shard = a.batch / G;
+  std::vector<Replica> rs(G);
+  for (int r = 0; r < G; ++r) {
+    Replica& R = rs[r];
+    R.device = a.gpus > 0 ? r : a.device;
+    CHECK(nof_set_device(R.device));
+    CHECK(nof_dataset_open(a.records.c_str(), R.device, &R.ds));  // BinDataset, resident on every device
+    nof_config_default(&R.cfg);
+    R.cfg.device = R.device;
+    R.cfg.max_rays = shard;
+    R.cfg.seed = a.seed;
+    R.cfg.precision = a.precision;
+    CHECK(nof_mipnerf_create(&R.cfg, &R.model));
+    int32_t sizes[64], nsizes = 0;
+    CHECK(nof_mipnerf_layer_sizes(R.model, sizes, 64, &nsizes));
+    CHECK(nof_adam_create(sizes, nsizes, &R.cfg, &R.adam));
+    if (a.host_api) CHECK(nof_gradcalc_create(shard, &R.cfg, &R.calc));
+    CHECK(nof_mipnerf_mlp(R.model, &R.mlp));
+    CHECK(nof_mlp_params(R.mlp, &R.params));  // model.mlp.allParams
+  }
+  // the same Glorot draw on every device (seeded Philox init), then one all-reduce per step
+  std::vector<nof_dp*> dps(G, nullptr);
+  std::vector<nof_mipnerf*> hs(G);
+  std::vector<int32_t> devs(G);
+  for (int r = 0; r < G; ++r) { hs[r] = rs[r].model; devs[r] = rs[r].device; }
+  if (a.gpus > 0) CHECK(nof_dp_init_all(G, devs.data(), dps.data()));
 
   int step0 = 0;
   if (!a.resume.empty()) {
-    CHECK(nof_checkpoint_load(a.resume.c_str(), model, adam));
-    CHECK(nof_adam_iteration(adam, &step0));
+    for (Replica& R : rs) CHECK(nof_checkpoint_load(a.resume.c_str(), R.model, R.adam));
+    CHECK(nof_adam_iteration(rs[0].adam, &step0));
   }
-  const int L = cfg.num_levels;
-  std::vector<float> ho, hd, hr, hn, hf, hm, hp;  // host rays (--host-api) / loss inputs
+  const int L = rs[0].cfg.num_levels;
   const auto t0 = std::chrono::steady_clock::now();
   for (int step = step0 + 1; step <= step0 + a.steps; ++step) {
-    nof_batch b;
+    // binDataset.Next(): every shard gathers its global ray ids; the loss-multiplier sum is global
     float msum = 0.0f;
-    CHECK(nof_dataset_next(ds, a.batch, a.seed, (uint32_t)step, 0, cfg.stream, &b, &msum));  // binDataset.Next()
-    const float lr = nof_lr_decay(step, a.lr_init, a.lr_final, a.max_steps, a.lr_delay_steps, a.lr_delay_mult);
-    CHECK(nof_mipnerf_set_rng(model, a.seed, (uint32_t)step, 0));
-    float* const* grads = nullptr;
-    uint64_t fine = 0;
-    const int n = a.batch;
-    if (a.host_api) {  // TrainStep as the reference runs it: host arrays in, host pixels via the callback
-      d2h(ho, b.origins, 3 * (size_t)n); d2h(hd, b.directions, 3 * (size_t)n); d2h(hr, b.radii, n);
-      d2h(hn, b.nears, n); d2h(hf, b.fars, n); d2h(hm, b.loss_mults, n); d2h(hp, b.pixels, 3 * (size_t)n);
-      StepCtx ctx{calc, hp.data(), n, 0};
-      CHECK(nof_mipnerf_get_gradient(model, n, ho.data(), hd.data(), hr.data(), hn.data(), hf.data(), hm.data(),
-                                     output_gradient, &ctx, &grads));
-      fine = ctx.fine_output;
-    } else {
-      CHECK(nof_mipnerf_get_gradient_device(model, n, b.origins, b.directions, b.radii, b.nears, b.fars, b.loss_mults,
-                                            b.pixels, msum, &grads));
-      nof_level_view v;
-      CHECK(nof_mipnerf_level_view(model, L - 1, &v));
-      fine = (uint64_t)(uintptr_t)v.comp_rgb;
+    for (int r = 0; r < G; ++r) {
+      Replica& R = rs[r];
+      CHECK(nof_dataset_next(R.ds, shard, a.seed, (uint32_t)step, (uint32_t)(r * shard), R.cfg.stream, &R.b, &R.msum));
+      msum += R.msum;
     }
-    CHECK(nof_adam_step(adam, params, grads, lr));  // optimizer.step(model.mlp.allParams, grad, lr)
-    if (a.print_every && step % a.print_every == 0) {
-      uint32_t bad = 0;
-      CHECK(nof_mipnerf_numeric_status(model, &bad, 1));
-      if (bad) {
-        std::fprintf(stderr, "nof_train: step %d: non-finite values in the training step (flags %#x)\n", step, bad);
-        return 1;
+    const float lr = nof_lr_decay(step, a.lr_init, a.lr_final, a.max_steps, a.lr_delay_steps, a.lr_delay_mult);
+    for (int r = 0; r < G; ++r) {
+      Replica& R = rs[r];
+      CHECK(nof_set_device(R.device));
+      CHECK(nof_mipnerf_set_rng(R.model, a.seed, (uint32_t)step, (uint32_t)(r * shard)));
+      float* const* grads = nullptr;
+      const int n = shard;
+      if (a.host_api) {  // TrainStep as the reference runs it: host arrays in, host pixels via the callback
+        d2h(R.ho, R.b.origins, 3 * (size_t)n); d2h(R.hd, R.b.directions, 3 * (size_t)n); d2h(R.hr, R.b.radii, n);
+        d2h(R.hn, R.b.nears, n); d2h(R.hf, R.b.fars, n); d2h(R.hm, R.b.loss_mults, n);
+        d2h(R.hp, R.b.pixels, 3 * (size_t)n);
+        StepCtx ctx{R.calc, R.hp.data(), n, 0, a.gpus > 1 ? msum : 0.0f};
+        CHECK(nof_mipnerf_get_gradient(R.model, n, R.ho.data(), R.hd.data(), R.hr.data(), R.hn.data(), R.hf.data(),
+                                       R.hm.data(), output_gradient, &ctx, &grads));
+        R.fine = ctx.fine_output;
+      } else {
+        CHECK(nof_mipnerf_get_gradient_device(R.model, n, R.b.origins, R.b.directions, R.b.radii, R.b.nears, R.b.fars,
+                                              R.b.loss_mults, R.b.pixels, msum, &grads));
+        nof_level_view v;
+        CHECK(nof_mipnerf_level_view(R.model, L - 1, &v));
+        R.fine = (uint64_t)(uintptr_t)v.comp_rgb;
       }
-      std::vector<float> C(3 * (size_t)n);
-      CHECK(nof_retrieve_output(fine, n, C.data()));  // OutputRetriever.RetrieveOutput
-      if (!a.host_api) { d2h(hm, b.loss_mults, n); d2h(hp, b.pixels, 3 * (size_t)n); }
-      std::printf("Step %d/%d, Loss: %.9g\n", step, a.max_steps, loss_fn(C, hm, hp, n));
+    }
+    if (a.gpus > 0) CHECK(nof_dp_allreduce_grads_all(G, dps.data(), hs.data(), nullptr));
+    for (Replica& R : rs) {
+      float* const* grads = nullptr;
+      CHECK(nof_mlp_grads(R.mlp, &grads));
+      CHECK(nof_adam_step(R.adam, R.params, grads, lr));  // optimizer.step(model.mlp.allParams, grad, lr)
+    }
+    if (a.gpus > 0)
+      for (nof_dp* d : dps) CHECK(nof_dp_wait(d, 0));  // an RCCL error or a stalled peer fails the run
+    if (a.print_every && step % a.print_every == 0) {
+      double num = 0.0, den = 0.0;  // Program.LossFn over the global batch (every shard's fine level)
+      float loss1 = 0.0f;
+      for (Replica& R : rs) {
+        CHECK(nof_set_device(R.device));
+        uint32_t bad = 0;
+        CHECK(nof_mipnerf_numeric_status(R.model, &bad, 1));
+        if (bad) {
+          std::fprintf(stderr, "nof_train: step %d: non-finite values on device %d (flags %#x)\n", step, R.device, bad);
+          return 1;
+        }
+        std::vector<float> C(3 * (size_t)shard);
+        CHECK(nof_retrieve_output(R.fine, shard, C.data()));  // OutputRetriever.RetrieveOutput
+        if (!a.host_api) { d2h(R.hm, R.b.loss_mults, shard); d2h(R.hp, R.b.pixels, 3 * (size_t)shard); }
+        const float l = loss_fn(C, R.hm, R.hp, shard);
+        loss1 = l;
+        double m = 0.0;
+        for (int i = 0; i < shard; ++i) m += (double)R.hm[i];
+        num += (double)l * m;
+        den += m;
+      }
+      std::printf("Step %d/%d, Loss: %.9g\n", step, a.max_steps, G == 1 ? (double)loss1 : num / den);
       std::fflush(stdout);
     }
     if (a.save_every && step % a.save_every == 0) {
       char name[64];
       std::snprintf(name, sizeof(name), "/ckpt_%08d.nof", step);
-      CHECK(nof_checkpoint_save((a.ckpt_dir + name).c_str(), model, adam));
+      CHECK(nof_checkpoint_save((a.ckpt_dir + name).c_str(), rs[0].model, rs[0].adam));
     }
   }
-  CHECK(nof_stream_sync(cfg.stream));
+  for (Replica& R : rs) {
+    CHECK(nof_set_device(R.device));
+    CHECK(nof_stream_sync(R.cfg.stream));
+  }
   const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   std::printf("%d steps in %.3f s: %.1f rays/s\n", a.steps, dt, dt > 0 ? a.steps * (double)a.batch / dt : 0.0);
+  if (a.gpus > 1) {  // the data-parallel invariant: bitwise-identical parameters on every device
+    std::vector<float> P0, Pr;
+    for (int r = 0; r < G; ++r) {
+      float* flat = nullptr;
+      int64_t count = 0;
+      CHECK(nof_mlp_flat_params(rs[r].mlp, &flat, &count));
+      CHECK(nof_set_device(rs[r].device));
+      d2h(r ? Pr : P0, flat, (size_t)count);
+      if (r && std::memcmp(P0.data(), Pr.data(), P0.size() * sizeof(float)) != 0) {
+        std::fprintf(stderr, "nof_train: parameters on device %d differ from device 0\n", rs[r].device);
+        return 1;
+      }
+    }
+    std::printf("parameters identical on %d devices\n", G);
+  }
   if (!a.dump_params.empty()) {  // flat parameter arena [W0..W10, b0..b10], raw float32
     float* flat = nullptr;
     int64_t count = 0;
-    CHECK(nof_mlp_flat_params(mlp, &flat, &count));
+    CHECK(nof_mlp_flat_params(rs[0].mlp, &flat, &count));
     std::vector<float> P;
+    CHECK(nof_set_device(rs[0].device));
     d2h(P, flat, (size_t)count);
     FILE* f = std::fopen(a.dump_params.c_str(), "wb");
     if (!f || std::fwrite(P.data(), sizeof(float), P.size(), f) != P.size()) {
@@ -228,9 +306,13 @@ int main(int argc, char** argv) {
     }
     std::fclose(f);
   }
-  if (calc) nof_gradcalc_destroy(calc);
-  nof_adam_destroy(adam);
-  nof_mipnerf_destroy(model);
-  nof_dataset_destroy(ds);
+  for (nof_dp* d : dps)
+    if (d) nof_dp_destroy(d);
+  for (Replica& R : rs) {
+    if (R.calc) nof_gradcalc_destroy(R.calc);
+    nof_adam_destroy(R.adam);
+    nof_mipnerf_destroy(R.model);
+    nof_dataset_destroy(R.ds);
+  }
   return 0;
 }

@@ -41,6 +41,30 @@ static nof_status guard(F&& f) {
   }
 }
 
+// Every call on an object runs on the object's device and leaves the caller's current device as
+// it was: one host thread may drive models on several GPUs (the single-process N-device model of
+// SURVEY 8e), and a NULL stream is the default stream of the object's device.
+struct DeviceScope {
+  int prev = -1;
+  explicit DeviceScope(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) NOF_HIP(hipSetDevice(dev));
+  }
+  ~DeviceScope() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+  DeviceScope(const DeviceScope&) = delete;
+  DeviceScope& operator=(const DeviceScope&) = delete;
+};
+#define DEV(obj) DeviceScope dsc_((obj)->impl->device())
+// the RCCL calls select each communicator's device themselves; the caller's device is restored
+static int current_device() {
+  int d = 0;
+  return hipGetDevice(&d) == hipSuccess ? d : 0;
+}
+#define KEEP_DEVICE DeviceScope keep_(current_device())
+
 #define ARG(cond)                                                              \
   do {                                                                         \
     if (!(cond)) throw Error(NOF_ERR_INVALID_ARG, "invalid argument: " #cond); \
@@ -74,6 +98,7 @@ nof_status nof_mipnerf_create(const nof_config* cfg, nof_mipnerf** out) {
     ARG(out);
     nof_config c;
     if (cfg) c = *cfg; else nof_config_default(&c);
+    DeviceScope dsc_(c.device);
     auto* h = new nof_mipnerf{nullptr};
     try { h->impl = new AcceleratedMipNeRF(c); } catch (...) { delete h; throw; }
     *out = h;
@@ -82,6 +107,7 @@ nof_status nof_mipnerf_create(const nof_config* cfg, nof_mipnerf** out) {
 nof_status nof_mipnerf_destroy(nof_mipnerf* h) {
   return guard([&] {
     if (!h) return;
+    DEV(h);
     delete h->impl;
     delete h;
   });
@@ -92,6 +118,7 @@ nof_status nof_mipnerf_get_gradient(nof_mipnerf* h, int32_t n, const float* orig
                                     float* const** out_dev_grads) {
   return guard([&] {
     ARG(h && out_dev_grads);
+    DEV(h);
     *out_dev_grads = h->impl->GetGradient(n, origins, directions, radii, nears, fars, loss_mults, cb, cb_user);
   });
 }
@@ -101,6 +128,7 @@ nof_status nof_mipnerf_get_gradient_device(nof_mipnerf* h, int32_t n, const floa
                                            float* const** out_dev_grads) {
   return guard([&] {
     ARG(h && out_dev_grads);
+    DEV(h);
     *out_dev_grads = h->impl->GetGradientDevice(n, o, d, radii, nears, fars, lm, pix, msum);
   });
 }
@@ -110,6 +138,7 @@ nof_status nof_mipnerf_get_gradient_device_ex(nof_mipnerf* h, int32_t n, const f
                                               float* const** out_dev_grads) {
   return guard([&] {
     ARG(h && out_dev_grads);
+    DEV(h);
     *out_dev_grads = h->impl->GetGradientDevice(n, o, d, radii, nears, fars, lm, pix, msum, flags);
   });
 }
@@ -123,6 +152,7 @@ nof_status nof_grad_bucket_spans(int32_t bucket, const int32_t* layer_sizes, int
 nof_status nof_mipnerf_numeric_status(nof_mipnerf* h, uint32_t* flags, int32_t clear) {
   return guard([&] {
     ARG(h && flags);
+    DEV(h);
     *flags = h->impl->numeric_status(clear != 0);
   });
 }
@@ -158,7 +188,7 @@ nof_status nof_mipnerf_level_view(nof_mipnerf* h, int32_t level, nof_level_view*
   return guard([&] { ARG(h && out); *out = h->impl->level_view(level); });
 }
 nof_status nof_mipnerf_loss(nof_mipnerf* h, float* out) {
-  return guard([&] { ARG(h && out); *out = h->impl->loss(); });
+  return guard([&] { ARG(h && out); DEV(h); *out = h->impl->loss(); });
 }
 nof_status nof_mipnerf_render_device(nof_mipnerf* h, int32_t n, const float* o, const float* d, const float* radii,
                                      const float* nears, const float* fars, int32_t randomized, int32_t white_bkgd,
@@ -166,12 +196,14 @@ nof_status nof_mipnerf_render_device(nof_mipnerf* h, int32_t n, const float* o, 
   return guard([&] {
     ARG(h && out);
     *out = nof_render_out{};
+    DEV(h);
     h->impl->Render(n, o, d, radii, nears, fars, randomized, white_bkgd, out);
   });
 }
 nof_status nof_dataset_open(const char* path, int32_t device, nof_dataset** out) {
   return guard([&] {
     ARG(path && out);
+    DeviceScope dsc_(device);
     auto* d = new nof_dataset{nullptr};
     try { d->impl = new RayDataset(std::string(path), device); } catch (...) { delete d; throw; }
     *out = d;
@@ -180,6 +212,7 @@ nof_status nof_dataset_open(const char* path, int32_t device, nof_dataset** out)
 nof_status nof_dataset_from_host(const float* records, int64_t count, int32_t device, nof_dataset** out) {
   return guard([&] {
     ARG(records && out);
+    DeviceScope dsc_(device);
     auto* d = new nof_dataset{nullptr};
     try { d->impl = new RayDataset(records, count, device); } catch (...) { delete d; throw; }
     *out = d;
@@ -192,12 +225,14 @@ nof_status nof_dataset_next(nof_dataset* ds, int32_t n, uint64_t seed, uint32_t 
                             nof_batch* out, float* loss_mult_sum) {
   return guard([&] {
     ARG(ds && out);
+    DEV(ds);
     ds->impl->next(n, seed, step, ray_base, (hipStream_t)stream, out, loss_mult_sum);
   });
 }
 nof_status nof_dataset_destroy(nof_dataset* ds) {
   return guard([&] {
     if (!ds) return;
+    DEV(ds);
     delete ds->impl;
     delete ds;
   });
@@ -210,6 +245,7 @@ nof_status nof_dataset_generate(const float* poses, int32_t V, int32_t w, int32_
                                 float far_, int32_t ndc, const float* dev_images, int32_t device, nof_dataset** out) {
   return guard([&] {
     ARG(poses && out);
+    DeviceScope dsc_(device);
     auto* d = new nof_dataset{nullptr};
     try { d->impl = new RayDataset(poses, V, w, h, focal, near_, far_, ndc, dev_images, device); } catch (...) { delete d; throw; }
     *out = d;
@@ -219,38 +255,38 @@ nof_status nof_recenter_poses(float* poses, int32_t V) {
   return guard([&] { recenter_poses(poses, V); });
 }
 nof_status nof_checkpoint_save(const char* path, nof_mipnerf* h, nof_adam* adam) {
-  return guard([&] { ARG(path && h && adam); save_checkpoint(path, *h->impl, *adam->impl); });
+  return guard([&] { ARG(path && h && adam); DEV(h); save_checkpoint(path, *h->impl, *adam->impl); });
 }
 nof_status nof_checkpoint_load(const char* path, nof_mipnerf* h, nof_adam* adam) {
-  return guard([&] { ARG(path && h && adam); load_checkpoint(path, *h->impl, *adam->impl); });
+  return guard([&] { ARG(path && h && adam); DEV(h); load_checkpoint(path, *h->impl, *adam->impl); });
 }
 nof_status nof_dp_unique_id(uint8_t id[128]) {
   return guard([&] { ARG(id); dp_unique_id(id); });
 }
 nof_status nof_dp_init_rank(const uint8_t id[128], int32_t world, int32_t rank, int32_t device, nof_dp** out) {
-  return guard([&] { ARG(id && out); *out = dp_init_rank(id, world, rank, device, 0); });
+  return guard([&] { KEEP_DEVICE; ARG(id && out); *out = dp_init_rank(id, world, rank, device, 0); });
 }
 nof_status nof_dp_init_rank_timeout(const uint8_t id[128], int32_t world, int32_t rank, int32_t device,
                                     int32_t timeout_ms, nof_dp** out) {
-  return guard([&] { ARG(id && out && timeout_ms >= 0); *out = dp_init_rank(id, world, rank, device, timeout_ms); });
+  return guard([&] { KEEP_DEVICE; ARG(id && out && timeout_ms >= 0); *out = dp_init_rank(id, world, rank, device, timeout_ms); });
 }
 nof_status nof_dp_attach(nof_dp* dp, nof_mipnerf* h, void* comm_stream) {
-  return guard([&] { dp_attach(dp, h ? h->impl : nullptr, (hipStream_t)comm_stream); });
+  return guard([&] { KEEP_DEVICE; dp_attach(dp, h ? h->impl : nullptr, (hipStream_t)comm_stream); });
 }
 nof_status nof_dp_wait(nof_dp* dp, int32_t timeout_ms) {
-  return guard([&] { ARG(timeout_ms >= 0); dp_wait(dp, timeout_ms); });
+  return guard([&] { KEEP_DEVICE; ARG(timeout_ms >= 0); dp_wait(dp, timeout_ms); });
 }
 nof_status nof_dp_abort(nof_dp* dp) {
-  return guard([&] { dp_abort(dp); });
+  return guard([&] { KEEP_DEVICE; dp_abort(dp); });
 }
 nof_status nof_dp_init_all(int32_t ndev, const int32_t* devices, nof_dp** out) {
-  return guard([&] { dp_init_all(ndev, devices, out); });
+  return guard([&] { KEEP_DEVICE; dp_init_all(ndev, devices, out); });
 }
 nof_status nof_dp_allreduce(nof_dp* dp, float* buf, int64_t count, void* stream) {
-  return guard([&] { dp_allreduce(dp, buf, count, (hipStream_t)stream); });
+  return guard([&] { KEEP_DEVICE; dp_allreduce(dp, buf, count, (hipStream_t)stream); });
 }
 nof_status nof_dp_allreduce_grads(nof_dp* dp, nof_mipnerf* h, void* stream) {
-  return guard([&] {
+  return guard([&] { KEEP_DEVICE;
     ARG(dp && h);
     AcceleratedMipNeRF* m = h->impl;
     hipStream_t st = stream ? (hipStream_t)stream : m->mlp->stream();
@@ -258,7 +294,7 @@ nof_status nof_dp_allreduce_grads(nof_dp* dp, nof_mipnerf* h, void* stream) {
   });
 }
 nof_status nof_dp_allreduce_grads_all(int32_t n, nof_dp* const* dps, nof_mipnerf* const* hs, void* const* streams) {
-  return guard([&] {
+  return guard([&] { KEEP_DEVICE;
     ARG(n >= 1 && dps && hs);
     std::vector<AcceleratedMipNeRF*> ms(n);
     std::vector<hipStream_t> st(n);
@@ -271,7 +307,7 @@ nof_status nof_dp_allreduce_grads_all(int32_t n, nof_dp* const* dps, nof_mipnerf
   });
 }
 nof_status nof_dp_destroy(nof_dp* dp) {
-  return guard([&] { dp_destroy(dp); });
+  return guard([&] { KEEP_DEVICE; dp_destroy(dp); });
 }
 nof_status nof_image_metrics(const float* img0, const float* img1, int32_t width, int32_t height, float max_val,
                              float* psnr, float* ssim, void* stream) {
@@ -281,13 +317,13 @@ nof_status nof_image_metrics(const float* img0, const float* img1, int32_t width
   });
 }
 nof_status nof_mipnerf_enable_timing(nof_mipnerf* h, int32_t enable) {
-  return guard([&] { ARG(h); h->impl->timer.enable(enable != 0 ? 0xFFu : 0u, h->impl->mlp->stream()); });
+  return guard([&] { ARG(h); DEV(h); h->impl->timer.enable(enable != 0 ? 0xFFu : 0u, h->impl->mlp->stream()); });
 }
 nof_status nof_mipnerf_enable_timing_mask(nof_mipnerf* h, uint32_t mask) {
-  return guard([&] { ARG(h); h->impl->timer.enable(mask, h->impl->mlp->stream()); });
+  return guard([&] { ARG(h); DEV(h); h->impl->timer.enable(mask, h->impl->mlp->stream()); });
 }
 nof_status nof_mipnerf_read_timing(nof_mipnerf* h, float* ms, int32_t* launches, int32_t cap) {
-  return guard([&] { ARG(h && ms && launches); h->impl->timer.read(ms, launches, cap); });
+  return guard([&] { ARG(h && ms && launches); DEV(h); h->impl->timer.read(ms, launches, cap); });
 }
 
 // ---- AcceleratedMLP (the handle IS the AcceleratedMLP owned by its AcceleratedMipNeRF) ------
@@ -296,6 +332,7 @@ nof_status nof_mlp_get_output(nof_mlp* m, const float* enc_pos, const float* enc
                               int32_t samples, uint64_t* dev_density, uint64_t* dev_rgb) {
   return guard([&] {
     ARG(m && dev_density && dev_rgb);
+    DeviceScope dsc_(M(m)->device());
     auto r = M(m)->get_output(enc_pos, enc_dir, level, n_rays, samples);
     *dev_density = (uint64_t)(uintptr_t)r.first;
     *dev_rgb = (uint64_t)(uintptr_t)r.second;
@@ -303,11 +340,15 @@ nof_status nof_mlp_get_output(nof_mlp* m, const float* enc_pos, const float* enc
 }
 nof_status nof_mlp_get_gradient(nof_mlp* m, const float* color_grad, const float* density_grad, int32_t level,
                                 float* const** out) {
-  return guard([&] { ARG(m && out); *out = M(m)->get_gradient(color_grad, density_grad, level); });
+  return guard([&] { ARG(m && out); DeviceScope dsc_(M(m)->device()); *out = M(m)->get_gradient(color_grad, density_grad, level); });
 }
 nof_status nof_mlp_get_gradient_ex(nof_mlp* m, const float* color_grad, const float* density_grad, int32_t level,
                                    uint32_t flags, float* const** out) {
-  return guard([&] { ARG(m && out); *out = M(m)->get_gradient(color_grad, density_grad, level, flags); });
+  return guard([&] {
+    ARG(m && out);
+    DeviceScope dsc_(M(m)->device());
+    *out = M(m)->get_gradient(color_grad, density_grad, level, flags);
+  });
 }
 nof_status nof_mlp_params(nof_mlp* m, float* const** out) {
   return guard([&] { ARG(m && out); *out = M(m)->allParams(); });
@@ -335,13 +376,14 @@ nof_status nof_adam_create(const int32_t* layer_sizes, int32_t num_layers, const
     nof_config c;
     if (cfg) c = *cfg; else nof_config_default(&c);
     std::vector<int> s(layer_sizes, layer_sizes + num_layers);
+    DeviceScope dsc_(c.device);
     auto* a = new nof_adam{nullptr};
     try { a->impl = new AcceleratedAdamOptimizer(s, c); } catch (...) { delete a; throw; }
     *out = a;
   });
 }
 nof_status nof_adam_step(nof_adam* a, float* const* params, float* const* grads, float lr) {
-  return guard([&] { ARG(a); a->impl->step(params, grads, lr); });
+  return guard([&] { ARG(a); DEV(a); a->impl->step(params, grads, lr); });
 }
 nof_status nof_adam_iteration(nof_adam* a, int32_t* it) {
   return guard([&] { ARG(a && it); *it = a->impl->iteration(); });
@@ -349,6 +391,7 @@ nof_status nof_adam_iteration(nof_adam* a, int32_t* it) {
 nof_status nof_adam_destroy(nof_adam* a) {
   return guard([&] {
     if (!a) return;
+    DEV(a);
     delete a->impl;
     delete a;
   });
@@ -360,6 +403,7 @@ nof_status nof_gradcalc_create(int32_t batch_size, const nof_config* cfg, nof_gr
     ARG(out);
     nof_config c;
     if (cfg) c = *cfg; else nof_config_default(&c);
+    DeviceScope dsc_(c.device);
     auto* g = new nof_gradcalc{nullptr};
     try { g->impl = new AcceleratedGradientCalculator(batch_size, c); } catch (...) { delete g; throw; }
     *out = g;
@@ -370,12 +414,14 @@ nof_status nof_gradcalc_output_gradient(nof_gradcalc* g, uint64_t dev_comp_rgb, 
                                         uint64_t* out_dev_grad) {
   return guard([&] {
     ARG(g && out_dev_grad);
+    DEV(g);
     *out_dev_grad = g->impl->get_output_gradient(dev_comp_rgb, host_pixels, n, dev_loss_mults, loss_mult_sum, level);
   });
 }
 nof_status nof_gradcalc_destroy(nof_gradcalc* g) {
   return guard([&] {
     if (!g) return;
+    DEV(g);
     delete g->impl;
     delete g;
   });

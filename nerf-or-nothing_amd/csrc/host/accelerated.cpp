@@ -651,7 +651,7 @@ uint32_t AcceleratedMipNeRF::numeric_status(bool clear) {
 // AcceleratedAdamOptimizer
 // ------------------------------------------------------------------------------------------------
 AcceleratedAdamOptimizer::AcceleratedAdamOptimizer(const std::vector<int>& layer_sizes, const nof_config& cfg)
-    : sizes_(layer_sizes) {
+    : device_(cfg.device), sizes_(layer_sizes) {
   NOF_REQUIRE(!layer_sizes.empty(), "empty layer sizes");
   NOF_HIP(hipSetDevice(cfg.device));
   st_ = (hipStream_t)cfg.stream;

@@ -131,6 +131,7 @@ class AcceleratedMLP {
   const float* rgb(int level) const { return lv_[level].rgb.p; }
   KernelTimer* timer = nullptr;
   hipStream_t stream() const { return st_; }
+  int device() const { return cfg_.device; }
   nof_mlp_debug debug_view(int level) const;
   // non-finite flags: [0] forward (set by the owner's integrator), [1] output gradients (f16x2 scaling)
   uint32_t* numeric_flags() const { return numeric_.p; }
@@ -222,6 +223,7 @@ class AcceleratedMipNeRF {
 
  public:
   const nof_config& config() const { return cfg_; }
+  int device() const { return cfg_.device; }
 
  private:
   uint32_t step_ = 0, ray_base_ = 0;
@@ -245,8 +247,10 @@ class AcceleratedAdamOptimizer {
   int64_t size() const { return total_; }
   void set_iteration(int it) { iteration_ = it; }
   hipStream_t stream() const { return st_; }
+  int device() const { return device_; }
 
  private:
+  int device_ = 0;
   std::vector<int> sizes_;
   std::vector<int64_t> off_;
   int64_t total_ = 0;
@@ -263,6 +267,7 @@ class AcceleratedGradientCalculator {
   AcceleratedGradientCalculator(int batch_size, const nof_config& cfg);
   uint64_t get_output_gradient(uint64_t input, const float* host_pixels, int n, uint64_t loss_mults,
                                float loss_mult_sum, int level);
+  int device() const { return cfg_.device; }
 
  private:
   int batch_;

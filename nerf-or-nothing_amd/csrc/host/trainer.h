@@ -17,6 +17,7 @@ class RayDataset {
   RayDataset(const float* host_poses, int V, int w, int h, float focal, float near, float far, int ndc,
              const float* dev_images, int device);
   int64_t count() const { return count_; }
+  int device() const { return device_; }
   // Gather n records for (seed, step, first global ray id); device SoA views owned by the dataset
   // (valid until the next call).  host_msum != null: also the loss-multiplier sum (synchronises st).
   void next(int n, uint64_t seed, uint32_t step, uint32_t ray_base, hipStream_t st, nof_batch* out, float* host_msum);

@@ -23,7 +23,8 @@ def test_usage(exe):
 
 
 @pytest.mark.parametrize("args", [[], ["--records"], ["--records", "x.bin", "--precision", "fp64"],
-                                  ["--records", "x.bin", "--save-every", "5"], ["--records", "x.bin", "--bogus"]])
+                                  ["--records", "x.bin", "--save-every", "5"], ["--records", "x.bin", "--bogus"],
+                                  ["--records", "x.bin", "--gpus", "3", "--batch", "256"]])
 def test_bad_arguments_exit_2(exe, args):
     out = subprocess.run([exe, *args], capture_output=True, text=True, timeout=60)
     assert out.returncode == 2 and "usage:" in out.stderr

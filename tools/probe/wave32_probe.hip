@@ -23,7 +23,7 @@ __device__ __forceinline__ f32x4 mfma(f16x8 a, f16x8 b, f32x4 c) {
 
 // w16 (as tools/probe/stage_probe.hip k_layer<1>): 8 groups of {4 reads one group ahead, 6 MFMAs}
 // kReads / kDma / kBar: decomposition (A fragments from LDS or held fixed, the slice DMA, the barrier)
-template <bool kReads = true, bool kDma = true, bool kBar = true>
+template <bool kReads = true, bool kDma = true, bool kBar = true, int AH = 1>
 __global__ __launch_bounds__(512, 1) void k_w16(const float* __restrict__ img, int reps, float* out, long long* cyc) {
   constexpr int kSlots = 3, T = 512;
   __shared__ __attribute__((aligned(16))) float lds[kSlots * kSliceFloats];
@@ -45,20 +45,24 @@ __global__ __launch_bounds__(512, 1) void k_w16(const float* __restrict__ img, i
     __syncthreads();
     for (int s = 0; s < kSlices; ++s) {
       const f16x8* W = reinterpret_cast<const f16x8*>(lds + (s % kSlots) * kSliceFloats) + lane;
-      f16x8 fr[2][4];
+      f16x8 fr[AH + 1][4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) fr[0][k] = W[k * 64];
+      for (int a = 0; a < AH; ++a)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) fr[a][k] = W[(4 * a + k) * 64];
       if (!kReads) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) fr[1][k] = fr[0][k] * (_Float16)0.5f;
+        for (int a = AH; a < AH + 1; ++a)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) fr[a][k] = fr[0][k] * (_Float16)0.5f;
       }
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        if (kReads && q + 1 < 8)
+        if (kReads && q + AH < 8)
 #pragma unroll
-          for (int k = 0; k < 4; ++k) fr[(q + 1) & 1][k] = W[(4 * (q + 1) + k) * 64];
+          for (int k = 0; k < 4; ++k) fr[(q + AH) % (AH + 1)][k] = W[(4 * (q + AH) + k) * 64];
         if (kDma && s + 2 < kSlices && q < 4) dma(s + 2, q);
-        const f16x8* f = fr[q & 1];
+        const f16x8* f = fr[q % (AH + 1)];
         acc[2 * q] = mfma(f[1], b0, acc[2 * q]);
         acc[2 * q + 1] = mfma(f[3], b0, acc[2 * q + 1]);
         acc[2 * q] = mfma(f[0], b1, acc[2 * q]);
@@ -305,6 +309,8 @@ int main() {
     run_e("w16 + epi, up 5/7", k_w16e<2>, img, out, cyc, scratch, reps);
     run_e("w16 + epi, up 0/2", k_w16e<3>, img, out, cyc, scratch, reps);
     run_k("w16 (2 waves/SIMD, 3 slots)", k_w16<>, 512, img, out, cyc, reps);
+    run_k("w16 reads 2 ahead", k_w16<true, true, true, 2>, 512, img, out, cyc, reps);
+    run_k("w16 reads 3 ahead", k_w16<true, true, true, 3>, 512, img, out, cyc, reps);
     run_k("w16 no reads", k_w16<false>, 512, img, out, cyc, reps);
     run_k("w16 no dma", k_w16<true, false>, 512, img, out, cyc, reps);
     run_k("w16 no barrier", k_w16<true, true, false>, 512, img, out, cyc, reps);

@@ -581,11 +581,17 @@ def main():
         if c_B % G == 0:
             c_dt, _, _, c_sync = measure("f16x2", B_run=c_B, steps=20, warmup=3, timers_on=False, scene="llff",
                                          smp=(256, 256))
+            # the whole step's algorithmic MLP work per GPU against the f16x2 3-MFMA ceiling
+            step_tf = 2 * (MACS_FWD + MACS_DX + MACS_DW) * (c_B // G) * 512 / (c_dt / 20) / 1e12
             cfg5 = {"workload": f"BASELINE configs[4]: LLFF-shaped (forward-facing, NDC) {c_B}-ray global batch x "
                                 f"256+256 samples, {c_B // G} rays per GPU, f16x2 perf mode (fp16 pieces on MFMA)",
                     "value": round(c_B * 20 / c_dt, 1), "unit": "rays/s", "n_gpus": G,
                     "ms_per_step": round(c_dt * 1e3 / 20, 4), "steps": 20, "warmup": 3, "scaling": "strong",
-                    "dtype": DTYPES["f16x2"]}
+                    "dtype": DTYPES["f16x2"],
+                    "roofline_step": {"bound": "mfma", "achieved": round(step_tf, 2), "peak": PEAK_F16X2_TFLOPS,
+                                      "unit": "TFLOP/s per GPU", "frac": round(step_tf / PEAK_F16X2_TFLOPS, 4),
+                                      "note": "whole step (sampling, integrator, all-reduce and Adam included) "
+                                              "over the MLP's algorithmic FLOP"}}
             if c_sync is not None:
                 cfg5["params_in_sync"] = c_sync
 
@@ -609,9 +615,17 @@ def main():
                                       "native (bucketed, overlapped)" if a.dp == "native" else
                                       "torch.distributed (bucketed, overlapped)") if G > 1 else None)},
             **roof,
+            # the whole step per GPU (sampling, integrator, all-reduce, Adam included) over the MLP's
+            # algorithmic FLOP: the scaling runs' roofline figure
+            "roofline_step": {"bound": "mfma",
+                              "achieved": round(2 * (MACS_FWD + MACS_DX + MACS_DW) * shard * sum(samples)
+                                                / (ms_step * 1e-3) / 1e12, 2),
+                              "peak": PEAKS[a.precision], "unit": "TFLOP/s per GPU"},
             "kernels": kernels,
             "psnr_fine": round(psnr, 3),
         }
+        rs_ = result["roofline_step"]
+        rs_["frac"] = round(rs_["achieved"] / rs_["peak"], 4)
         if G > 1:
             result["params_in_sync"] = in_sync
             if world > 1 and backend != "nccl":

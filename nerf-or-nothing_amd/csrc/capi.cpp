@@ -58,12 +58,21 @@ struct DeviceScope {
   DeviceScope& operator=(const DeviceScope&) = delete;
 };
 #define DEV(obj) DeviceScope dsc_((obj)->impl->device())
-// the RCCL calls select each communicator's device themselves; the caller's device is restored
-static int current_device() {
-  int d = 0;
-  return hipGetDevice(&d) == hipSuccess ? d : 0;
-}
-#define KEEP_DEVICE DeviceScope keep_(current_device())
+// Calls that select devices themselves (constructors after validating their config, the RCCL calls
+// per communicator) only restore the caller's device on exit.
+struct KeepDevice {
+  int prev = -1;
+  KeepDevice() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  ~KeepDevice() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+  KeepDevice(const KeepDevice&) = delete;
+  KeepDevice& operator=(const KeepDevice&) = delete;
+};
+#define KEEP_DEVICE KeepDevice keep_
 
 #define ARG(cond)                                                              \
   do {                                                                         \
@@ -98,7 +107,7 @@ nof_status nof_mipnerf_create(const nof_config* cfg, nof_mipnerf** out) {
     ARG(out);
     nof_config c;
     if (cfg) c = *cfg; else nof_config_default(&c);
-    DeviceScope dsc_(c.device);
+    KEEP_DEVICE;
     auto* h = new nof_mipnerf{nullptr};
     try { h->impl = new AcceleratedMipNeRF(c); } catch (...) { delete h; throw; }
     *out = h;
@@ -203,7 +212,7 @@ nof_status nof_mipnerf_render_device(nof_mipnerf* h, int32_t n, const float* o, 
 nof_status nof_dataset_open(const char* path, int32_t device, nof_dataset** out) {
   return guard([&] {
     ARG(path && out);
-    DeviceScope dsc_(device);
+    KEEP_DEVICE;
     auto* d = new nof_dataset{nullptr};
     try { d->impl = new RayDataset(std::string(path), device); } catch (...) { delete d; throw; }
     *out = d;
@@ -212,7 +221,7 @@ nof_status nof_dataset_open(const char* path, int32_t device, nof_dataset** out)
 nof_status nof_dataset_from_host(const float* records, int64_t count, int32_t device, nof_dataset** out) {
   return guard([&] {
     ARG(records && out);
-    DeviceScope dsc_(device);
+    KEEP_DEVICE;
     auto* d = new nof_dataset{nullptr};
     try { d->impl = new RayDataset(records, count, device); } catch (...) { delete d; throw; }
     *out = d;
@@ -245,7 +254,7 @@ nof_status nof_dataset_generate(const float* poses, int32_t V, int32_t w, int32_
                                 float far_, int32_t ndc, const float* dev_images, int32_t device, nof_dataset** out) {
   return guard([&] {
     ARG(poses && out);
-    DeviceScope dsc_(device);
+    KEEP_DEVICE;
     auto* d = new nof_dataset{nullptr};
     try { d->impl = new RayDataset(poses, V, w, h, focal, near_, far_, ndc, dev_images, device); } catch (...) { delete d; throw; }
     *out = d;
@@ -376,7 +385,7 @@ nof_status nof_adam_create(const int32_t* layer_sizes, int32_t num_layers, const
     nof_config c;
     if (cfg) c = *cfg; else nof_config_default(&c);
     std::vector<int> s(layer_sizes, layer_sizes + num_layers);
-    DeviceScope dsc_(c.device);
+    KEEP_DEVICE;
     auto* a = new nof_adam{nullptr};
     try { a->impl = new AcceleratedAdamOptimizer(s, c); } catch (...) { delete a; throw; }
     *out = a;
@@ -403,7 +412,7 @@ nof_status nof_gradcalc_create(int32_t batch_size, const nof_config* cfg, nof_gr
     ARG(out);
     nof_config c;
     if (cfg) c = *cfg; else nof_config_default(&c);
-    DeviceScope dsc_(c.device);
+    KEEP_DEVICE;
     auto* g = new nof_gradcalc{nullptr};
     try { g->impl = new AcceleratedGradientCalculator(batch_size, c); } catch (...) { delete g; throw; }
     *out = g;

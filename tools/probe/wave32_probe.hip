@@ -270,6 +270,91 @@ static void run_k(const char* name, K kern, int threads, const float* img, float
               ms, per, ns, 1536.0 / per, 1536.0 / ns);
 }
 
+
+// fp32 layer skeleton (mlp16.h mlp_layer16: v_mfma_f32_16x16x4_f32, 16 groups of {2 A reads one group
+// ahead, 8 MFMAs on two accumulators} per 32-KB slice, DMA steps in groups 0..3, 4-slot ring with a
+// barrier after odd slices) with the fp32 epilogue of two tiles per slice (ReLU + mask bit + 4
+// stores each).  STAG: 0 = every wave's epilogue at groups 4 / 12 (the kernels); 1 = waves 4..7
+// (the SIMD partners) at groups 8 / 15, dispatched once at kernel entry (two code copies, no
+// branch in the loop).
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+template <bool kUp>
+__device__ __forceinline__ void f32_body(const float* __restrict__ img, int reps, float* out, long long* cyc,
+                                         float* scratch, float* lds) {
+  constexpr int T = 512, kSlots = 4;
+  constexpr int E1 = kUp ? 8 : 4, E2 = kUp ? 15 : 12;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(img), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t blk = __builtin_amdgcn_make_buffer_rsrc(
+      scratch + (size_t)(blockIdx.x * 8 + wv) * 4096, (short)0, 0x7fffffff, 0x00020000);
+  const uint32_t voff = 512u * (lane >> 4) + ((lane & 15) << 2);
+  f32x4 acc[16] = {};
+  f32x4 prev[16];
+  for (int i = 0; i < 16; ++i) prev[i] = f32x4{0.1f * i - 0.7f, 0.3f - 0.01f * lane, 0.2f, -0.4f + 0.05f * i};
+  float bin[16][4];
+  for (int i = 0; i < 16; ++i) for (int r = 0; r < 4; ++r) bin[i][r] = 0.01f * (i + r) - 0.05f * (lane & 7);
+  uint32_t mw = 0;
+  const long long t0 = __builtin_readcyclecounter();
+  for (int rep = 0; rep < reps; ++rep) {
+    auto dma = [&](int s, int i) {
+      float* dst = lds + (s % kSlots) * kSliceFloats;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lptr_t)(dst + (T * i + 64 * wv) * 4), 16, tid * 16,
+                                               (s * kSliceFloats + i * T * 4) * 4, 0, 0);
+    };
+    for (int i = 0; i < 4; ++i) { dma(0, i); dma(1, i); }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    for (int s = 0; s < kSlices; ++s) {
+      const f32x4* W = reinterpret_cast<const f32x4*>(lds + (s % kSlots) * kSliceFloats) + lane;
+      f32x4 a0 = W[0], a1 = W[64];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        asm volatile("" ::"v"(a0), "v"(a1));
+        f32x4 n0 = a0, n1 = a1;
+        if (q + 1 < 16) { n0 = W[(2 * (q + 1)) * 64]; n1 = W[(2 * (q + 1) + 1) * 64]; }
+        if (s + 2 < kSlices && q < 4) dma(s + 2, q);
+        __builtin_amdgcn_sched_barrier(0);
+        const int tb = (q >> 3) & 1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          acc[q & 7] = mfma4(a0[r], bin[tb][r], acc[q & 7]);
+          acc[8 + (q & 7)] = mfma4(a1[r], bin[tb][r], acc[8 + (q & 7)]);
+        }
+        if (q == E1 || q == E2) {
+          const int t = q == E1 ? 0 : 1;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int h = max(__float_as_int(prev[t][r]), 0);
+            asm volatile("v_cmp_lt_i32 vcc, 0, %1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc" : "+v"(mw) : "v"(h) : "vcc");
+            v[r] = __int_as_float(h);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[r]), blk, (int)voff, 2048 * t + 128 * r, 2);
+          }
+          prev[t] = f32x4{v[1], v[2], v[3], v[0]};
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        a0 = n0;
+        a1 = n1;
+      }
+      if (s & 1) asm volatile("s_waitcnt vmcnt(8)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  }
+  const long long t1 = __builtin_readcyclecounter();
+  float sum = (float)mw;
+  for (int i = 0; i < 16; ++i) sum += acc[i][0] + acc[i][3] + prev[i & 1][0];
+  out[blockIdx.x * 512 + tid] = sum;
+  if (tid == 0) cyc[blockIdx.x] = t1 - t0;
+}
+template <int STAG>
+__global__ __launch_bounds__(512, 1) void k_f32(const float* __restrict__ img, int reps, float* out, long long* cyc,
+                                                float* scratch) {
+  __shared__ __attribute__((aligned(16))) float lds[4 * kSliceFloats];
+  if (STAG && __builtin_amdgcn_readfirstlane(threadIdx.x >> 8)) f32_body<true>(img, reps, out, cyc, scratch, lds);
+  else f32_body<false>(img, reps, out, cyc, scratch, lds);
+}
+
 template <class K>
 static void run_e(const char* name, K kern, const float* img, float* out, long long* cyc, float* scratch, int reps) {
   hipEvent_t a, b;
@@ -290,6 +375,28 @@ static void run_e(const char* name, K kern, const float* img, float* out, long l
   std::printf("%-26s %8.3f ms  %6.0f ticks/slice  %6.1f ns/slice  MFMA-busy(ticks) %.2f\n", name, ms, per, ns, 1536.0 / per);
 }
 
+template <class K>
+static void run_f(const char* name, K kern, const float* img, float* out, long long* cyc, float* scratch, int reps) {
+  hipLaunchKernelGGL(kern, dim3(256), dim3(512), 0, 0, img, 1, out, cyc, scratch);
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  (void)hipEventRecord(a);
+  hipLaunchKernelGGL(kern, dim3(256), dim3(512), 0, 0, img, reps, out, cyc, scratch);
+  (void)hipEventRecord(b);
+  (void)hipEventSynchronize(b);
+  const hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) { std::printf("%s: %s\n", name, hipGetErrorString(e)); std::exit(1); }
+  float ms = 0.0f;
+  (void)hipEventElapsedTime(&ms, a, b);
+  std::vector<long long> c(256);
+  (void)hipMemcpy(c.data(), cyc, 256 * sizeof(long long), hipMemcpyDeviceToHost);
+  double mean = 0;
+  for (long long x : c) mean += (double)x / 256;
+  const double per = mean / (kSlices * reps);
+  std::printf("%-26s %8.3f ms  %6.0f ticks/slice  MFMA-busy(ticks) %.3f\n", name, ms, per, 8192.0 / per);
+}
+
 int main() {
   float *img, *out;
   long long* cyc;
@@ -304,6 +411,13 @@ int main() {
   const int reps = 20;
   float* scratch;
   (void)hipMalloc(&scratch, (size_t)256 * 8 * 4096 * 4);
+  if (getenv("PROBE_F32")) {
+    for (int it = 0; it < 3; ++it) {
+      run_f("f32 layer, epi 4/12", k_f32<0>, img, out, cyc, scratch, 10);
+      run_f("f32 layer, up at 8/15", k_f32<1>, img, out, cyc, scratch, 10);
+    }
+    return 0;
+  }
   for (int it = 0; it < 2; ++it) {
     run_e("w16 + epilogue 4/6", k_w16e<1>, img, out, cyc, scratch, reps);
     run_e("w16 + epi, up 5/7", k_w16e<2>, img, out, cyc, scratch, reps);

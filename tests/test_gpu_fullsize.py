@@ -96,6 +96,9 @@ def _compare_step(oracle, model, r, samples, seed, step, base, msum, precision):
     ("config2", "blender", 1024, (128, 128), 2),
     ("config2", "blender", 1024, (128, 128), 3),
     ("config3", "blender", 1024, (64, 128), 0),
+    ("config3", "blender", 1024, (64, 128), 1),
+    ("config3", "blender", 1024, (64, 128), 2),
+    ("config3", "blender", 1024, (64, 128), 3),
     ("config5", "llff", 512, (256, 256), 2),
     ("config5", "llff", 512, (256, 256), 0),
     ("config5", "llff", 512, (256, 256), 3),

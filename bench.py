@@ -253,6 +253,28 @@ def api_path(torch, nof, synth, dev, n, samples, prec, steps=20, warmup=3):
             "path": "GetGradient(host arrays) + output-gradient callback (host pixels) + Adam, precision " + prec}
 
 
+def render_throughput(torch, nof, synth, dev, prec, n=8192, samples=(128, 128), reps=10):
+    """Evaluation path (MipNerfModel.Call, MNcs:36-97): the deterministic two-level
+    render — forward-only MLP kernels, integrator with distance / accumulation, resampling — of
+    device-resident rays, rays/s."""
+    m = nof.AcceleratedMipNeRF(device=dev.index, max_rays=n, num_samples=samples, seed=0x5EED0002,
+                               stream=torch.cuda.current_stream(dev).cuda_stream, precision=PRECISIONS[prec])
+    r = synth.blender_rays(n, seed=77)
+    t = {k: torch.from_numpy(r[k]).to(dev) for k in ("o", "d", "radius", "near", "far")}
+    go = lambda: m.render_device(n, t["o"], t["d"], t["radius"], t["near"], t["far"], False)
+    go()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        go()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    m.close()
+    return {"workload": f"deterministic two-level render of {n} Lego-shaped rays x {'+'.join(map(str, samples))} "
+                        f"samples (forward only), precision {prec}", "value": round(n * reps / dt, 1),
+            "unit": "rays/s", "ms_per_call": round(dt * 1e3 / reps, 4)}
+
+
 def psnr_vs_ref(torch, nof, synth, dev, prec, n=64, steps=40, samples=(128, 128), n_eval=256):
     """Part of the cpu_baseline leg.  The metric's "PSNR vs ref": the HIP path and the oracle's float restatement of the reference
     (MipNerfModel.GetGradient MNcs:99-200 + the Adam step AF:403-416, the reference's CPU path in
@@ -649,6 +671,7 @@ def main():
                     "kernels": {k: v["avg_launch_ms"] for k, v in akernels.items()}, "psnr_fine": round(apsnr, 3)})
         if world == 1 and G == 1 and a.scene == "blender" and B <= 8192:
             result["api_path_pcie"] = api_path(torch, nof, synth, dev, B, samples, a.precision)
+            result["render_1gpu"] = render_throughput(torch, nof, synth, dev, a.precision, samples=tuple(samples))
         if not a.no_integrator and world == 1 and G == 1:
             result["roofline_integrator"] = integrator_roofline(torch, nof, dev)
         if not a.no_cpu_baseline and world == 1 and G == 1:

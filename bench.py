@@ -349,7 +349,7 @@ def main():
 
     import nof
     from nof import synth
-    from nof.dp import BucketedAllReduce, NativeDP
+    from nof.dp import BucketedAllReduce, NativeDP, params_checksum
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -502,9 +502,7 @@ def main():
             sums = []
             for m, d in zip(models, devs):
                 pptr, P = m.mlp.flat_params()
-                dv = torch.device("cuda", d)
-                pv = nof.device_tensor(pptr, (P,), device=dv).view(torch.int32).to(torch.int64)
-                sums.append((pv * torch.arange(1, P + 1, device=dv, dtype=torch.int64)).sum().reshape(1).to(dev))
+                sums.append(params_checksum(nof.device_tensor(pptr, (P,), device=torch.device("cuda", d))).to(dev))
             cs_ = torch.cat(sums)
             hi, lo = cs_.max().reshape(1), (-cs_.min()).reshape(1)
             if world > 1:

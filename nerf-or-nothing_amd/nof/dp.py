@@ -35,6 +35,34 @@ def global_loss_mult_sum(rays: dict) -> float:
     return float(np.sum(np.asarray(rays["lossmult"], np.float32), dtype=np.float32))
 
 
+def params_checksum(flat):
+    """Order-sensitive checksum of a flat fp32 parameter tensor (any device): sum over i of
+    (i + 1) * bits(p_i) in wrapping int64 — equal on two ranks iff (with overwhelming probability)
+    their parameters are bitwise equal.  Returns a 1-element int64 tensor on flat's device."""
+    import torch
+
+    bits = flat.contiguous().view(torch.int32).to(torch.int64)
+    idx = torch.arange(1, bits.numel() + 1, device=bits.device, dtype=torch.int64)
+    return (bits * idx).sum().reshape(1)
+
+
+def params_in_sync(flat, allreduce=None) -> bool:
+    """SURVEY §8e's data-parallel invariant, checked across ranks: every rank applies Adam to the
+    same all-reduced gradient bits, so the parameters must stay bitwise identical.  One all-reduce
+    (MAX) of (checksum, -checksum): equal on every rank iff max == min.  `allreduce(t, op)`
+    defaults to torch.distributed.all_reduce (the trainers pass their own for gloo rehearsals)."""
+    import torch
+    import torch.distributed as dist
+
+    cs = params_checksum(flat)
+    both = torch.cat([cs, -cs])
+    if allreduce is None:
+        dist.all_reduce(both, op=dist.ReduceOp.MAX)
+    else:
+        allreduce(both, dist.ReduceOp.MAX)
+    return bool(both[0].item() == -both[1].item())
+
+
 class NativeDP:
     """The C ABI's RCCL data parallelism (nof_dp_*, include/nof.h) for hosts without
     torch.distributed: one in-place all-reduce (sum) of the gradient arena per step."""

@@ -25,7 +25,7 @@ from ._lib import default_config
 class Trainer:
     def __init__(self, dataset: api.RayDataset, batch_size: int = 1024, seed: int = 0x5EED0000, device: int = 0,
                  stream=None, print_every: int = 100, save_every: int = 0, ckpt_dir: str | None = None,
-                 lr_init=5e-4, lr_final=5e-6, max_steps=1000000, lr_delay_steps=2500, lr_delay_mult=0.01,
+                 sync_check_every: int = 0, lr_init=5e-4, lr_final=5e-6, max_steps=1000000, lr_delay_steps=2500, lr_delay_mult=0.01,
                  **config):
         import torch.distributed as dist
 
@@ -37,6 +37,7 @@ class Trainer:
         self.seed = seed
         self.stream = stream
         self.print_every, self.save_every, self.ckpt_dir = print_every, save_every, ckpt_dir
+        self.sync_check_every = sync_check_every  # data parallel: parameter checksum across ranks
         self.lr = dict(lr_init=lr_init, lr_final=lr_final, max_steps=max_steps, lr_delay_steps=lr_delay_steps,
                        lr_delay_mult=lr_delay_mult)
         self.cfg = default_config(device=device, max_rays=batch_size, seed=seed, stream=stream, **config)
@@ -88,9 +89,24 @@ class Trainer:
             self.last_loss = self.fine_loss(b)
             if self.rank == 0:
                 print(f"Step {step}/{self.lr['max_steps']}, Loss: {self.last_loss}", flush=True)
+        if self.dist is not None and self.sync_check_every and step % self.sync_check_every == 0:
+            self.check_sync()
         if self.save_every and self.ckpt_dir and step % self.save_every == 0 and self.rank == 0:
             os.makedirs(self.ckpt_dir, exist_ok=True)
             self.save(os.path.join(self.ckpt_dir, f"ckpt_{step:08d}.nof"))
+
+    def check_sync(self):
+        """SURVEY §8e's periodic assertion: every rank's parameters are bitwise identical (a rank that
+        diverged — a missed all-reduce, a different Adam step — fails here instead of training on)."""
+        import torch
+
+        from .dp import params_in_sync
+
+        api.call("nof_stream_sync", self.stream)  # Adam ran on self.stream
+        pptr, P = self.model.mlp.flat_params()
+        flat = api.device_tensor(pptr, (P,), device=torch.device("cuda", self.device))
+        if not params_in_sync(flat):
+            raise RuntimeError(f"step {self.step_idx}: parameters differ across the {self.world} ranks")
 
     def fine_loss(self, batch) -> float:
         """Program.LossFn (Program.cs:64): sum m |C_fine - p|^2 / sum m over this rank's batch."""
@@ -122,11 +138,13 @@ def main(argv=None):
     ap.add_argument("--save-every", type=int, default=0)
     ap.add_argument("--ckpt-dir")
     ap.add_argument("--resume", help="checkpoint to resume from")
+    ap.add_argument("--sync-check-every", type=int, default=0,
+                    help="under torch.distributed: assert bitwise-identical parameters across ranks every K steps")
     a = ap.parse_args(argv)
     ds = (api.RayDataset(a.records, device=a.device) if a.records else
           api.RayDataset(records=synth.pack_records(synth.blender_rays(a.synthetic, seed=1)), device=a.device))
     tr = Trainer(ds, batch_size=a.batch, device=a.device, print_every=a.print_every, save_every=a.save_every,
-                 ckpt_dir=a.ckpt_dir, precision={"f32": 0, "split": 1, "f16x2": 2, "f16split": 3}[a.precision])
+                 ckpt_dir=a.ckpt_dir, sync_check_every=a.sync_check_every, precision={"f32": 0, "split": 1, "f16x2": 2, "f16split": 3}[a.precision])
     if a.resume:
         tr.resume(a.resume)
     t0 = time.perf_counter()

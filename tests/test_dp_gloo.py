@@ -93,3 +93,44 @@ def test_shard_ranges_partition(n, world):
     assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
     sizes = [e - b for b, e in rs]
     assert max(sizes) - min(sizes) <= 1
+
+
+def _sync_worker(rank, world, port, perturb, q):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "nerf-or-nothing_amd")]
+    import torch
+    import torch.distributed as dist
+
+    from nof import dp
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    p = torch.from_numpy(np.random.default_rng(3).standard_normal(546948).astype(np.float32))
+    if perturb and rank == 1:  # one ulp of one parameter on one rank
+        p[1234] = torch.from_numpy(np.nextafter(p[1234:1235].numpy(), np.float32(np.inf)))
+    q.put((rank, dp.params_in_sync(p)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("perturb", [False, True])
+def test_params_in_sync_across_ranks(perturb):
+    """SURVEY §8e's periodic parameter assertion (nof.dp.params_in_sync, the Trainer's
+    sync_check_every): every rank agrees the replicas are identical, and a one-ulp difference on one
+    rank is reported on every rank."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_sync_worker, args=(r, 2, port, perturb, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == {0: not perturb, 1: not perturb}

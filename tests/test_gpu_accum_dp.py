@@ -10,7 +10,8 @@ one GPU:
 * failure detection: an aborted communicator returns NOF_ERR_RCCL instead of hanging, and a rank
   whose peer never joins times out (in a child process, bounded by its own timeout);
 * the Trainer on a non-default stream, under torch.distributed (world 1), matches the same
-  training without torch.distributed bit for bit (stream ordering of the all-reduce).
+  training without torch.distributed bit for bit (stream ordering of the all-reduce),
+  with the per-step cross-rank parameter checksum on.
 """
 import os
 import subprocess
@@ -219,7 +220,8 @@ if use_dist:
 torch.cuda.set_device(0)
 side = torch.cuda.Stream()  # a non-default stream for the library
 ds = nof.RayDataset(records=synth.pack_records(synth.blender_rays(4096, seed=1)), device=0)
-tr = Trainer(ds, batch_size=256, stream=side.cuda_stream, print_every=0, num_samples=(64, 64))
+tr = Trainer(ds, batch_size=256, stream=side.cuda_stream, print_every=0, num_samples=(64, 64),
+             sync_check_every=1 if use_dist else 0)
 tr.train(3)
 nof._lib.call("nof_stream_sync", side.cuda_stream)
 p = nof.to_numpy(tr.model.mlp.flat_params()[0], (546948,))

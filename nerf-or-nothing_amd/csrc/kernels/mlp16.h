@@ -102,13 +102,30 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t blk_rsrc(float* blk) {
 // fp16 counterpart (f16x2 mode, common.h blkh_off): byte(f, s) = 64 f + ((((s >> 3) ^ ((f >> 2) & 3)) << 4) |
 // ((s & 7) << 1)) with f = 16t + 4g + r, s = 16 half + j, so (f >> 2) & 3 = g and the lane part does not
 // depend on (t, r): one voffset, 1024 t in soffset, 64 r immediate.  kNT: nt stores (see BlkStore16).
+// The epilogues' tiles go out as dwords (store_pairs): two samples of one feature, formed by a lane-pair
+// exchange of the packed (f, f + 1) pairs split4h leaves — 2 dword stores per tile instead of 4
+// store_short (A/B on one box: f16x2 backward 0.332 -> 0.323 ms, forward unchanged, step -1.0 %).
 template <bool kNT>
 struct BlkStore16H {
   static constexpr bool kHalf = true;
   uint32_t voff;
+  uint32_t voff2;  // dword (feature 4g + (j & 1), samples s & ~1, s | 1) of the lane pair (j, j ^ 1)
+  uint32_t sel;    // v_perm selector: even lanes (own low, partner low), odd lanes (partner high, own high)
   __device__ __forceinline__ BlkStore16H(int lane, int half) {
     const int g = lane >> 4, j = lane & 15;
     voff = 256u * g + ((((2 * half + (j >> 3)) ^ g) << 4) | ((j & 7) << 1));
+    voff2 = 256u * g + 64u * (j & 1) + ((((2 * half + (j >> 3)) ^ g) << 4) | ((j & 6) << 1));
+    sel = (j & 1) ? 0x03020706u : 0x05040100u;
+  }
+  // the packed pairs (features 0, 1) and (2, 3) of one sample, stored as dwords of two samples of
+  // one feature: the lane pair (j, j ^ 1) swaps them (DPP quad_perm) and keeps its halves (v_perm)
+  __device__ __forceinline__ void store_pairs(__amdgpu_buffer_rsrc_t blk, int t, uint32_t p01, uint32_t p23) const {
+    const uint32_t q01 = (uint32_t)__builtin_amdgcn_mov_dpp((int)p01, 0xB1, 0xF, 0xF, false);  // lane ^ 1
+    const uint32_t q23 = (uint32_t)__builtin_amdgcn_mov_dpp((int)p23, 0xB1, 0xF, 0xF, false);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(q01, p01, sel), blk, (int)voff2, 1024 * t,
+                                          kNT ? kStoreNT : 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(q23, p23, sel), blk, (int)voff2 + 128, 1024 * t,
+                                          kNT ? kStoreNT : 0);
   }
   __device__ __forceinline__ void store(__amdgpu_buffer_rsrc_t blk, int t, int r, float v) const {
     store_h(blk, t, r, (_Float16)v);
@@ -116,21 +133,6 @@ struct BlkStore16H {
   __device__ __forceinline__ void store_h(__amdgpu_buffer_rsrc_t blk, int t, int r, _Float16 h) const {
     __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, h), blk, (int)voff + 64 * r, 1024 * t,
                                           kNT ? kStoreNT : 0);
-  }
-  // both halves of a packed fp16 pair: features R (low half) and R + 1 (high half, store_short_d16_hi)
-  template <int R>
-  __device__ __forceinline__ void store_pair(__amdgpu_buffer_rsrc_t blk, int t, uint32_t pair) const {
-    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)pair, blk, (int)voff, 1024 * t + 64 * R, kNT ? kStoreNT : 0);
-    if constexpr (kNT)
-      asm volatile("buffer_store_short_d16_hi %0, %1, %2, %3 offen offset:%4 nt"
-                   :
-                   : "v"(pair), "v"(voff), "s"(blk), "s"(1024 * t), "n"(64 * (R + 1))
-                   : "memory");
-    else
-      asm volatile("buffer_store_short_d16_hi %0, %1, %2, %3 offen offset:%4"
-                   :
-                   : "v"(pair), "v"(voff), "s"(blk), "s"(1024 * t), "n"(64 * (R + 1))
-                   : "memory");
   }
 };
 // block stores per precision: fp32 blocks (P = 0, and P = 3: the F32_F16SPLIT mode keeps its weight-
@@ -207,8 +209,7 @@ __device__ __forceinline__ void put_tile(float (&bin)[16][4], int t, const float
     bin[row + 1][c + 1] = __uint_as_float(lo23);
     if constexpr (kStore) {
       if constexpr (ST::kHalf) {
-        bst.template store_pair<0>(blk, t, hi01);
-        bst.template store_pair<2>(blk, t, hi23);
+        bst.store_pairs(blk, t, hi01, hi23);
       } else {
 #pragma unroll
         for (int r = 0; r < 4; ++r) bst.store(blk, t, r, v[r]);

@@ -77,7 +77,9 @@ __device__ __forceinline__ constexpr int feat16(int t, int g, int r) { return 16
 // level fwd + bwd + wgrad): the weight-gradient launch that reads the blocks next runs 1.5 % (fp32),
 // 7 % (F32_F16SPLIT) and 10 % (f16x2) faster, the F32_F16SPLIT forward 2 % faster, the f16x2
 // backward 4 % slower: per level -0.5 % (fp32), -3.5 % (F32_F16SPLIT), -0.7 % (f16x2).  The f16x2
-// forward's 32-B half-line stores measured 3 % slower as nt and stay default.
+// forward's store_short pairs measured 3 % slower as nt; since its tiles go out as dwords
+// (BlkStore16H::store_pairs) nt is neutral for the forward and the weight-gradient launch runs 7 %
+// faster (f16x2 step -2.3 %), so every block store is nt.
 constexpr int kStoreNT = 2;  // aux bit of the buffer-store builtins: nt
 struct BlkStore16 {
   static constexpr bool kHalf = false;
@@ -136,9 +138,9 @@ struct BlkStore16H {
   }
 };
 // block stores per precision: fp32 blocks (P = 0, and P = 3: the F32_F16SPLIT mode keeps its weight-
-// gradient operands in fp32), fp16 blocks (P = 2; kBwd: the backward's delta stores, nt)
+// gradient operands in fp32), fp16 blocks (P = 2); all nt
 template <int P, bool kBwd> struct Store16 { typedef BlkStore16 T; typedef float E; };
-template <bool kBwd> struct Store16<2, kBwd> { typedef BlkStore16H<kBwd> T; typedef _Float16 E; };
+template <bool kBwd> struct Store16<2, kBwd> { typedef BlkStore16H<true> T; typedef _Float16 E; };
 template <class E>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t blk_rsrc_t(E* blk) {
   return __builtin_amdgcn_make_buffer_rsrc(blk, (short)0, 0x7fffffff, 0x00020000);

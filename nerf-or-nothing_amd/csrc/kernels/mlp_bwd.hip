@@ -55,7 +55,7 @@ struct BwdEpi {
       }
     }
     float v = acc[t][r];
-    if constexpr (kDensity) v += wcur[jj] * dzs;
+    if constexpr (kDensity) v = __builtin_fmaf(wcur[jj], dzs, v);
     v = mask_bit(mk, t, r) ? v : 0.0f;
     bin[t][r] = v;
     ao.put(dst_blk + t * 32 * kBlk, r, v);
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
           const int r = 4 * q + jj;
-          float v = (wa[jj] * dzc[0] + wb[jj] * dzc[1]) + wc[jj] * dzc[2];
+          float v = __builtin_fmaf(wc[jj], dzc[2], __builtin_fmaf(wb[jj], dzc[1], wa[jj] * dzc[0]));
           v = mask_bit(mk, ot, r) ? v : 0.0f;
           bin[ot][r] = v;
         }

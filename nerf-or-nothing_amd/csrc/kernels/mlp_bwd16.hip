@@ -54,7 +54,7 @@ struct BwdEpi16 {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       v[r] = acc[t][r];
-      if constexpr (kDensity) v[r] += w4[r] * dzs;
+      if constexpr (kDensity) v[r] = __builtin_fmaf(w4[r], dzs, v[r]);  // explicit: every variant rounds alike
       v[r] = mask16_apply(mk, t, r, v[r]);
     }
     put_tile<kSplit, true>(bin, t, v, bst, dst_blk);
@@ -119,7 +119,8 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
       const f32x4 wc = *reinterpret_cast<const f32x4*>(w10 + 256 + fb);
       float v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = mask16_apply(mk, t, r, (wa[r] * dzc[0] + wb[r] * dzc[1]) + wc[r] * dzc[2]);
+      for (int r = 0; r < 4; ++r)  // explicit FMAs: every precision variant rounds alike
+        v[r] = mask16_apply(mk, t, r, __builtin_fmaf(wc[r], dzc[2], __builtin_fmaf(wb[r], dzc[1], wa[r] * dzc[0])));
       put_tile<P >= 2, true>(bin, t, v, bst, d9);
     }
   }

@@ -247,6 +247,111 @@ __global__ __launch_bounds__(256, 1) void k_w32(const float* __restrict__ img, i
   if (tid == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
+// w32 + the forward epilogue: 4 waves of 32 samples (two 16-sample B operand sets sharing every A
+// fragment), 4 slots, barrier per two slices; per slice 2 tiles x 2 sample sets of the previous layer's
+// accumulators finished by epi_tile_t (relu_bit + split4h + fp16 pair stores) at groups 4 and 6 — the
+// same epilogue work per sample as k_w16e, on half the waves (no SIMD partner to hide it).
+__global__ __launch_bounds__(256, 1) void k_w32e(const float* __restrict__ img, int reps, float* out, long long* cyc,
+                                                 float* scratch) {
+  constexpr int T = 256, SLOTS = 4;
+  __shared__ __attribute__((aligned(16))) float lds[SLOTS * kSliceFloats];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(img), (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t blk = __builtin_amdgcn_make_buffer_rsrc(
+      scratch + (size_t)(blockIdx.x * 8 + wv) * 4096, (short)0, 0x7fffffff, 0x00020000);
+  const uint32_t voff = 256u * (lane >> 4) + ((lane & 15) << 1);
+  f32x4 acc[2][16] = {};
+  f32x4 prev[2][16];
+  for (int c = 0; c < 2; ++c)
+    for (int i = 0; i < 16; ++i)
+      prev[c][i] = f32x4{0.1f * i - 0.7f + 0.01f * c, 0.3f - 0.01f * lane, 0.2f, -0.4f + 0.05f * i};
+  f16x8 bin[2][2];
+  uint32_t mw = 0;
+  f16x8 b[2][2];
+  for (int i = 0; i < 8; ++i) {
+    b[0][0][i] = (_Float16)(0.37f * (i + lane % 7) - 1.1f); b[0][1][i] = (_Float16)(0.013f * (i - lane % 5));
+    b[1][0][i] = (_Float16)(0.29f * (i - lane % 3) + 0.4f); b[1][1][i] = (_Float16)(0.017f * (i + lane % 9));
+  }
+  const long long t0 = __builtin_readcyclecounter();
+  for (int rep = 0; rep < reps; ++rep) {
+    auto dma = [&](int s, int i) {
+      float* dst = lds + (s % SLOTS) * kSliceFloats;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lptr_t)(dst + (T * i + 64 * wave) * 4), 16, tid * 16,
+                                               (s * kSliceFloats + i * T * 4) * 4, 0, 0);
+    };
+    for (int i = 0; i < 8; ++i) { dma(0, i); dma(1, i); }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    for (int s = 0; s < kSlices; ++s) {
+      const f16x8* W = reinterpret_cast<const f16x8*>(lds + (s % SLOTS) * kSliceFloats) + lane;
+      f16x8 fr[2][4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) fr[0][k] = W[k * 64];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (q + 1 < 8)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) fr[(q + 1) & 1][k] = W[(4 * (q + 1) + k) * 64];
+        if (s + 2 < kSlices && q < 4) { dma(s + 2, 2 * q); dma(s + 2, 2 * q + 1); }
+        __builtin_amdgcn_sched_barrier(0);
+        const f16x8* f = fr[q & 1];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          acc[c][2 * q] = mfma(f[1], b[c][0], acc[c][2 * q]);
+          acc[c][2 * q + 1] = mfma(f[3], b[c][0], acc[c][2 * q + 1]);
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          acc[c][2 * q] = mfma(f[0], b[c][1], acc[c][2 * q]);
+          acc[c][2 * q + 1] = mfma(f[2], b[c][1], acc[c][2 * q + 1]);
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          acc[c][2 * q] = mfma(f[0], b[c][0], acc[c][2 * q]);
+          acc[c][2 * q + 1] = mfma(f[2], b[c][0], acc[c][2 * q + 1]);
+        }
+        if (q == 4) { epi_tile_t<0>(prev[0][2 * q], mw, bin[0][0], blk, voff); epi_tile_t<2>(prev[1][2 * q], mw, bin[1][0], blk, voff); }
+        if (q == 6) { epi_tile_t<1>(prev[0][2 * q + 1], mw, bin[0][1], blk, voff); epi_tile_t<3>(prev[1][2 * q + 1], mw, bin[1][1], blk, voff); }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {  // keep the epilogue live (the next slice's B operands)
+        b[c][0] = b[c][0] + bin[c][0] * (_Float16)0.0f;
+        b[c][1] = b[c][1] + bin[c][1] * (_Float16)0.0f;
+      }
+      if (s & 1) asm volatile("s_waitcnt vmcnt(16)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  }
+  const long long t1 = __builtin_readcyclecounter();
+  float sum = (float)mw;
+  for (int c = 0; c < 2; ++c)
+    for (int i = 0; i < 16; ++i) sum += acc[c][i][0] + acc[c][i][3];
+  out[blockIdx.x * 256 + tid] = sum;
+  if (tid == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+template <class K>
+static void run_e32(const char* name, K kern, const float* img, float* out, long long* cyc, float* scratch, int reps) {
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  hipLaunchKernelGGL(kern, dim3(256), dim3(256), 0, 0, img, 1, out, cyc, scratch);
+  (void)hipEventRecord(a);
+  hipLaunchKernelGGL(kern, dim3(256), dim3(256), 0, 0, img, reps, out, cyc, scratch);
+  (void)hipEventRecord(b);
+  (void)hipEventSynchronize(b);
+  float ms = 0.0f;
+  (void)hipEventElapsedTime(&ms, a, b);
+  std::vector<long long> c(256);
+  (void)hipMemcpy(c.data(), cyc, 256 * sizeof(long long), hipMemcpyDeviceToHost);
+  double mean = 0;
+  for (long long x : c) mean += (double)x / 256;
+  const double per = mean / (kSlices * reps), ns = ms * 1e6 / (kSlices * reps);
+  std::printf("%-26s %8.3f ms  %6.0f ticks/slice  %6.1f ns/slice  MFMA-busy(ticks) %.2f\n", name, ms, per, ns, 1536.0 / per);
+}
+
 template <class K>
 static void run_k(const char* name, K kern, int threads, const float* img, float* out, long long* cyc, int reps) {
   hipEvent_t a, b;
@@ -415,6 +520,13 @@ int main() {
     for (int it = 0; it < 3; ++it) {
       run_f("f32 layer, epi 4/12", k_f32<0>, img, out, cyc, scratch, 10);
       run_f("f32 layer, up at 8/15", k_f32<1>, img, out, cyc, scratch, 10);
+    }
+    return 0;
+  }
+  if (getenv("PROBE_W32E")) {  // the 32-sample forward question, alternating
+    for (int it = 0; it < 4; ++it) {
+      run_e("w16 + epilogue 4/6", k_w16e<1>, img, out, cyc, scratch, reps);
+      run_e32("w32 + epilogue (4 slots)", k_w32e, img, out, cyc, scratch, reps);
     }
     return 0;
   }

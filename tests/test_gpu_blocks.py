@@ -7,7 +7,8 @@ pairs of two samples of one feature, mlp16.h BlkStore16H::store_pairs) versus fp
 blk_off layout (common.h).  So every f16x2 block element must be exactly the RNE fp16 of the
 F32_F16SPLIT element at the same (sample, feature): a bit-exact check of both store layouts, every
 block kind (IPE / view-PE inputs, trunk activations, view-layer activations, trunk deltas, the view
-and head deltas) and both levels' activations.
+and head deltas) and both levels' activations; the per-sample outputs and output gradients agree
+bit for bit as well.
 """
 import numpy as np
 import pytest
@@ -95,5 +96,12 @@ def test_f16_blocks_are_rne_of_f16split_blocks(gpu, kind, n, samples):
         assert np.count_nonzero(hb["act_h3"]) > hb["act_h3"].size // 8
     assert np.count_nonzero(hb["delta5"]) > hb["delta5"].size // 16
     assert not mism, "; ".join(mism)
+    # and the per-sample outputs the blocks feed are the same bits: t (both levels), density, rgb, the
+    # weights and composite, and the integrator's output gradients
+    for level in range(len(samples)):
+        la, lb = a.level_numpy(level), b.level_numpy(level)
+        for k in ("t", "density", "rgb", "weights", "comp_rgb", "density_grad", "rgb_grad"):
+            assert np.array_equal(la[k], lb[k]), f"level {level} {k} differs between f16x2 and f16split"
+    assert a.loss() == b.loss()
     a.close()
     b.close()

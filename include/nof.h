@@ -166,6 +166,19 @@ nof_status nof_mipnerf_loss(nof_mipnerf* h, float* out);
 #define NOF_NUMERIC_FORWARD 1u
 #define NOF_NUMERIC_DELTA 2u
 nof_status nof_mipnerf_numeric_status(nof_mipnerf* h, uint32_t* flags, int32_t clear);
+/* Device-side bounds checks (no reference counterpart; its CUDA path has real out-of-bounds writes,
+ * SURVEY.md Appendix A): a library built with `make check` (lib/libnof_check.so, -DNOF_DEVICE_CHECKS)
+ * checks launch geometry, sample bins, weight-gradient problem geometry and record indices inside
+ * the kernels; a failed check sets its bit (NOF_CHECK_*) instead of trapping.  Synchronises the
+ * current device and returns the bits seen on it since the last clear.  The product build returns
+ * NOF_ERR_UNSUPPORTED.  nof_device_checks_selftest fails NOF_CHECK_SELFTEST on purpose. */
+#define NOF_CHECK_MLP_BLOCK (1u << 0)
+#define NOF_CHECK_SAMPLE_IDX (1u << 1)
+#define NOF_CHECK_WGRAD_GEOM (1u << 2)
+#define NOF_CHECK_GATHER (1u << 3)
+#define NOF_CHECK_SELFTEST (1u << 31)
+nof_status nof_device_checks(uint32_t* bits, int32_t clear);
+nof_status nof_device_checks_selftest(void);
 
 /* ---- evaluation ------------------------------------------------------------
  * Forward-only two-level render: replaces MipNerfModel.Call(rays, randomized, whiteBackground)

@@ -165,6 +165,31 @@ nof_status nof_mipnerf_numeric_status(nof_mipnerf* h, uint32_t* flags, int32_t c
     *flags = h->impl->numeric_status(clear != 0);
   });
 }
+nof_status nof_device_checks(uint32_t* bits, int32_t clear) {
+  return guard([&] {
+    ARG(bits);
+    *bits = 0;
+#ifdef NOF_DEVICE_CHECKS
+    NOF_HIP(hipDeviceSynchronize());
+    const bool c = clear != 0;
+    *bits = nof::check_unit_sampling(c) | nof::check_unit_mlp_fwd16(c) | nof::check_unit_mlp_bwd16(c) |
+            nof::check_unit_wgrad(c) | nof::check_unit_dataset(c);
+#else
+    (void)clear;
+    throw Error(NOF_ERR_UNSUPPORTED, "device checks are compiled only into lib/libnof_check.so (make check)");
+#endif
+  });
+}
+nof_status nof_device_checks_selftest(void) {
+  return guard([&] {
+#ifdef NOF_DEVICE_CHECKS
+    NOF_HIP(nof::launch_check_selftest(nullptr));
+    NOF_HIP(hipDeviceSynchronize());
+#else
+    throw Error(NOF_ERR_UNSUPPORTED, "device checks are compiled only into lib/libnof_check.so (make check)");
+#endif
+  });
+}
 nof_status nof_mipnerf_set_grad_buckets(nof_mipnerf* h, nof_grad_bucket_fn fn, void* user) {
   return guard([&] {
     ARG(h);

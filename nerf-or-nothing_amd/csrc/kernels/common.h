@@ -86,6 +86,40 @@ __device__ inline f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+// ---------------------------------------------------------------------------
+// Device-side bounds checks (bounds asserts in debug builds), compiled in by
+// -DNOF_DEVICE_CHECKS (`make check` -> lib/libnof_check.so) and to nothing otherwise.  A failed check
+// never traps (a fault takes the GPU down): the failing lanes set word `bit` of their translation
+// unit's check array to 1 (a plain store of a constant: racing writers agree) and the kernel carries
+// on; nof_device_checks() ORs every unit's words into one bit mask after synchronising.
+// ---------------------------------------------------------------------------
+enum : int { kChkMlpBlock = 0, kChkSampleIdx = 1, kChkWgradGeom = 2, kChkGather = 3, kChkSelfTest = 31 };
+#ifdef NOF_DEVICE_CHECKS
+static __device__ uint32_t g_nof_checks[32];  // one copy per translation unit (no relocatable device code)
+#define NOF_DCHECK(cond, bit)                            \
+  do {                                                   \
+    if (!(cond)) ::nof::g_nof_checks[(bit)] = 1u;        \
+  } while (0)
+// the unit's host accessor: its words as a bit mask, optionally cleared (blocking copies)
+#define NOF_CHECK_UNIT(name)                                                                        \
+  uint32_t name(bool clear) {                                                                       \
+    uint32_t w[32] = {};                                                                            \
+    if (hipMemcpyFromSymbol(w, HIP_SYMBOL(g_nof_checks), sizeof(w)) != hipSuccess) return ~0u;      \
+    uint32_t m = 0;                                                                                 \
+    for (int i = 0; i < 32; ++i) m |= w[i] ? (1u << i) : 0u;                                        \
+    if (clear) {                                                                                    \
+      const uint32_t z[32] = {};                                                                    \
+      if (hipMemcpyToSymbol(HIP_SYMBOL(g_nof_checks), z, sizeof(z)) != hipSuccess) return ~0u;      \
+    }                                                                                               \
+    return m;                                                                                       \
+  }
+#else
+#define NOF_DCHECK(cond, bit) \
+  do {                        \
+  } while (0)
+#define NOF_CHECK_UNIT(name)
+#endif
+
 __device__ inline float softplus_f(float x) { return x > 20.0f ? x : log1pf(expf(x)); }  // D28
 __device__ inline float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
 

@@ -31,6 +31,7 @@ __global__ __launch_bounds__(256) void k_gather_batch(const float4* __restrict__
   const int r = g >> 2, q = g & 3;
   if (r >= n) return;
   const uint32_t idx = batch_record(seed, step, ray_base + (uint32_t)r, count);
+  NOF_DCHECK((int64_t)idx < count, kChkGather);
   const float4 v = rec[(size_t)idx * 4 + q];  // floats 4q .. 4q+3 of the record (BinDataset.cs:40-49)
   switch (q) {
     case 0:  // origin xyz, direction x
@@ -73,5 +74,13 @@ hipError_t launch_gather_batch(const float* records, int64_t count, int n, uint6
   if (lm_sum) hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, st, lm, n, lm_sum);
   return hipGetLastError();
 }
+
+// fails kChkSelfTest on purpose: proves a checked build's plumbing (nof_device_checks_selftest)
+__global__ void k_check_selftest(int zero) { NOF_DCHECK(zero != 0, kChkSelfTest); }
+hipError_t launch_check_selftest(hipStream_t st) {
+  hipLaunchKernelGGL(k_check_selftest, dim3(1), dim3(64), 0, st, 0);
+  return hipGetLastError();
+}
+NOF_CHECK_UNIT(check_unit_dataset)
 
 }  // namespace nof

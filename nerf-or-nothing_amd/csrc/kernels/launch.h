@@ -7,6 +7,15 @@
 
 namespace nof {
 
+// ---- device checks (common.h NOF_DCHECK; compiled in only with -DNOF_DEVICE_CHECKS) -------------
+// per translation unit: its failed-check bits, optionally cleared; ~0u if the copy failed
+uint32_t check_unit_sampling(bool clear);
+uint32_t check_unit_mlp_fwd16(bool clear);
+uint32_t check_unit_mlp_bwd16(bool clear);
+uint32_t check_unit_wgrad(bool clear);
+uint32_t check_unit_dataset(bool clear);
+hipError_t launch_check_selftest(hipStream_t st);  // fails kChkSelfTest on purpose
+
 // ---- sampling.hip (get_sample_t_vals AF:222-242, get_resampled_t_vals AF:246-291) ----------
 hipError_t launch_sample_stratified(int n, int S, const float* nears, const float* fars, int randomized,
                                     uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base, float* t,

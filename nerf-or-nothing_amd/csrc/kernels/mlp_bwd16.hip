@@ -81,6 +81,7 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
   const int blk_raw = blockIdx.x * 4 + (wave >> 1);
   const int blk = blk_raw < nblk ? blk_raw : nblk - 1;  // tail waves duplicate the last block
   const int m = blk * kBlk + 16 * half + j;
+  NOF_DCHECK(a.M % kBlk == 0 && blk >= 0 && blk < nblk, kChkMlpBlock);
   const float* tail = a.wimg_b + (size_t)kBwdSlices * kSliceFloats;
   const size_t layer_stride = (size_t)nblk * kWidth * kBlk;
   uint32_t* masks = const_cast<uint32_t*>(a.masks);
@@ -162,5 +163,7 @@ hipError_t launch_mlp_bwd16(const BwdArgs& a, hipStream_t st) {
   else hipLaunchKernelGGL(k_mlp_bwd16<0>, dim3((nblk + 3) / 4), dim3(kMlp16Threads), 0, st, a);
   return hipGetLastError();
 }
+
+NOF_CHECK_UNIT(check_unit_mlp_bwd16)
 
 }  // namespace nof

@@ -99,6 +99,8 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
   const int s0 = m0 - ray * a.S + 16 * half;
   const int m = m0 + 16 * half + j;
   const float* tail = a.wimg + (size_t)kFwdSlices * kSliceFloats;
+  // whole 32-sample blocks of one ray each, the block inside the launch
+  NOF_DCHECK(a.M % kBlk == 0 && a.S % kBlk == 0 && blk >= 0 && blk < nblk, kChkMlpBlock);
 
   ring16_prologue(a.wimg, lds, tid);  // first two slices in flight while the encodings are computed
 
@@ -260,5 +262,7 @@ hipError_t launch_mlp_fwd16(const FwdArgs& a, hipStream_t st) {
   }
   return hipGetLastError();
 }
+
+NOF_CHECK_UNIT(check_unit_mlp_fwd16)
 
 }  // namespace nof

@@ -106,6 +106,7 @@ __global__ __launch_bounds__(64) void k_sample_pdf(int n, int B, const float* __
       const int mid = (lo + hi + 1) >> 1;
       if (cdf[mid] <= u) lo = mid; else hi = mid - 1;
     }
+    NOF_DCHECK(lo >= 0 && lo < B, kChkSampleIdx);  // a bin of the input t row
     const float b0 = tr[lo], b1 = tr[lo + 1], c0 = cdf[lo], c1 = cdf[lo + 1];
     const float denom = c1 - c0;
     float tt = denom > 0.0f ? (u - c0) / denom : 0.0f;
@@ -185,5 +186,7 @@ hipError_t launch_encode(int n, int S, const float* mean, const float* cov, cons
   hipLaunchKernelGGL(k_encode, dim3((total + 255) / 256), dim3(256), 0, st, n, S, mean, cov, d, enc_pos, enc_dir);
   return hipGetLastError();
 }
+
+NOF_CHECK_UNIT(check_unit_sampling)
 
 }  // namespace nof

@@ -225,6 +225,10 @@ __global__ __launch_bounds__(kWgThreads, 1) void k_wgrad(const WgProblem* __rest
     NOF_IT_T0(0)
     const WgItem item = items[it];
     const WgProblem P = probs[item.prob];
+    // the item's k-blocks and its operand rows inside their blocks; at most 8 x 8 tiles
+    NOF_DCHECK(item.kb0 < item.kb1 && P.ntr >= 1 && P.ntr <= 8 && P.ntc >= 1 && P.ntc <= 8 &&
+                   P.a_row0 + 32 * P.ntr <= P.FA && P.b_col0 + 32 * P.ntc <= P.FB,
+               kChkWgradGeom);
     switch (P.shape) {  // kWgShapes
 #define NOF_WG_CASE(i)                                                                                     \
   case i:                                                                                                  \
@@ -473,6 +477,10 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_x3(const WgProblem* _
     NOF_IT_T0(1)
     const WgItem item = items[it];
     const WgProblem P = probs[item.prob];
+    // the item's k-blocks and its operand rows inside their blocks; at most 8 x 8 tiles
+    NOF_DCHECK(item.kb0 < item.kb1 && P.ntr >= 1 && P.ntr <= 8 && P.ntc >= 1 && P.ntc <= 8 &&
+                   P.a_row0 + 32 * P.ntr <= P.FA && P.b_col0 + 32 * P.ntc <= P.FB,
+               kChkWgradGeom);
     const int RB = (P.ntr + 1) >> 1, CB = (P.ntc + kX3WC - 1) / kX3WC;  // 2 x kX3WC wave grid
     switch (RB * 10 + CB) {
       case 11: wg_item_x3<PM, 1, 1>(item, P, lds, tid, wave, slabs, bias_slabs, slab_off); break;
@@ -618,6 +626,10 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_h(const WgProblem* __
     NOF_IT_T0(1)
     const WgItem item = items[it];
     const WgProblem P = probs[item.prob];
+    // the item's k-blocks and its operand rows inside their blocks; at most 8 x 8 tiles
+    NOF_DCHECK(item.kb0 < item.kb1 && P.ntr >= 1 && P.ntr <= 8 && P.ntc >= 1 && P.ntc <= 8 &&
+                   P.a_row0 + 32 * P.ntr <= P.FA && P.b_col0 + 32 * P.ntc <= P.FB,
+               kChkWgradGeom);
     switch (((P.ntr + 1) >> 1) * 10 + (P.ntc + kX3WC - 1) / kX3WC) {
       case 11: wg_item_h<1, 1>(item, P, ldsh, tid, wave, slabs, bias_slabs, slab_off); break;
       case 21: wg_item_h<2, 1>(item, P, ldsh, tid, wave, slabs, bias_slabs, slab_off); break;
@@ -758,5 +770,7 @@ hipError_t launch_wgrad_reduce(const WgOut* outs, int nouts, int max_elems, cons
                      slab_off, slabs, bias_slabs, accumulate, amax);
   return hipGetLastError();
 }
+
+NOF_CHECK_UNIT(check_unit_wgrad)
 
 }  // namespace nof

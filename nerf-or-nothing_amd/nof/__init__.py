@@ -15,6 +15,8 @@ from .api import (  # noqa: F401
     load_checkpoint,
     recenter_poses,
     save_checkpoint,
+    device_checks,
+    device_checks_selftest,
     device_count,
     device_tensor,
     generate_rays,

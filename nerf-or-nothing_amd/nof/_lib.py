@@ -92,6 +92,8 @@ SIGNATURES = {
     "nof_mipnerf_level_view": [P, I32, C.POINTER(nof_level_view)],
     "nof_mipnerf_loss": [P, C.POINTER(F)],
     "nof_mipnerf_numeric_status": [P, C.POINTER(U32), I32],
+    "nof_device_checks": [C.POINTER(U32), I32],
+    "nof_device_checks_selftest": [],
     "nof_mipnerf_render_device": [P, I32, P, P, P, P, P, I32, I32, C.POINTER(nof_render_out)],
     "nof_image_metrics": [P, P, I32, I32, F, C.POINTER(F), C.POINTER(F), P],
     "nof_dataset_open": [C.c_char_p, I32, C.POINTER(P)],

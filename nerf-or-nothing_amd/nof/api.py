@@ -484,6 +484,20 @@ def image_metrics(img0, img1, max_val=1.0, stream=None) -> tuple[float, float]:
     return psnr.value, ssim.value
 
 
+def device_checks(clear: bool = True) -> int:
+    """NOF_CHECK_* bits failed inside the kernels on the current device since the last clear
+    (synchronises).  Only a checked build (lib/libnof_check.so, `make check`, selected with NOF_LIB)
+    has the checks; the product library raises NofError(NOF_ERR_UNSUPPORTED)."""
+    out = C.c_uint32()
+    call("nof_device_checks", C.byref(out), int(clear))
+    return out.value
+
+
+def device_checks_selftest() -> None:
+    """Fail NOF_CHECK_SELFTEST on purpose (checked build only)."""
+    call("nof_device_checks_selftest")
+
+
 def learning_rate_decay(step, lr_init=5e-4, lr_final=5e-6, max_steps=1000000, lr_delay_steps=2500,
                         lr_delay_mult=0.01) -> float:
     """MathHelpers.LearningRateDecay (MipHelpers.cs:758-773); defaults = TrainState.cs:54-58."""

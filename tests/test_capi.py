@@ -101,3 +101,18 @@ def test_grad_bucket_spans_partition_the_arena():
     assert pos == sum(sizes) == 546948
     with pytest.raises(nof.NofError):
         nof.grad_bucket_spans(sizes, 2)
+
+
+def test_device_checks_product_vs_checked_build():
+    """The product library has no device checks (NOF_ERR_UNSUPPORTED, no GPU touched); the checked
+    build (lib/libnof_check.so, `make check`) exports the same C ABI."""
+    import nof
+
+    with pytest.raises(nof.NofError) as e:
+        nof.device_checks()
+    assert e.value.status == 5  # NOF_ERR_UNSUPPORTED
+    checked = os.path.join(ROOT, "nerf-or-nothing_amd", "lib", "libnof_check.so")
+    assert os.path.exists(checked), "build it with: make -C nerf-or-nothing_amd check"
+    lib = C.CDLL(checked)
+    missing = [n for n in declared_symbols() if not hasattr(lib, n)]
+    assert not missing, missing

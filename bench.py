@@ -43,17 +43,20 @@ PEAK_BF16_TFLOPS = 2516.6  # MI355X bf16 dense MFMA (no sparsity)
 # the f16x2 perf mode issues 3 fp16 MFMAs (same dense rate as bf16) per product
 PEAK_SPLIT_TFLOPS = round(PEAK_BF16_TFLOPS / 6, 1)
 PEAK_F16X2_TFLOPS = round(PEAK_BF16_TFLOPS / 3, 1)
-PRECISIONS = {"f32": 0, "split": 1, "f16x2": 2, "f16split": 3}  # NOF_PRECISION_*
+PRECISIONS = {"f32": 0, "split": 1, "f16x2": 2, "f16split": 3, "f16": 4}  # NOF_PRECISION_*
 # f16split: the f16x2 pieces in every contraction (weight gradients too) — 3 fp16 MFMAs per product
-PEAKS = {"f32": PEAK_F32_TFLOPS, "split": PEAK_SPLIT_TFLOPS, "f16x2": PEAK_F16X2_TFLOPS, "f16split": PEAK_F16X2_TFLOPS}
+# f16: one fp16 MFMA per product (plain mixed precision): the dense fp16 peak
+PEAKS = {"f32": PEAK_F32_TFLOPS, "split": PEAK_SPLIT_TFLOPS, "f16x2": PEAK_F16X2_TFLOPS, "f16split": PEAK_F16X2_TFLOPS,
+         "f16": PEAK_BF16_TFLOPS}
 DTYPES = {"f32": "f32", "split": "f32 (bf16x3 split MFMA)", "f16x2": "f16x2 (fp16 hi+lo, 3 MFMAs; perf mode, 2e-3)",
-          "f16split": "f32 via fp16 hi+lo in every contraction (3 MFMAs per product; 1e-5 parity, fp16 range)"}
+          "f16split": "f32 via fp16 hi+lo in every contraction (3 MFMAs per product; 1e-5 parity, fp16 range)",
+          "f16": "f16 (fp16 operands, fp32 accumulation, 1 MFMA per product; perf mode, 2e-3)"}
 PEAK_HBM_GBS = 8000.0
 # weight-gradient operands per sample per level, each needed once per launch (fp16 in the f16x2 mode):
 # activations IPE 96 + view PE 27 + h0..h7 8x256 + h9 128 = 2299, deltas 8x256 + d9 128 + the heads'
 # dz_sigma 1 and dz_rgb 3 = 2180 (the stored blocks add 33 zero rows: not counted)
 WGRAD_VALUES = 2299 + 2180
-WGRAD_BYTES_PER_VALUE = {"f32": 4, "split": 4, "f16x2": 2, "f16split": 4}
+WGRAD_BYTES_PER_VALUE = {"f32": 4, "split": 4, "f16x2": 2, "f16split": 4, "f16": 2}
 INTEGRATOR_FWD_B = lambda S: S * (12 + 4 + 4) + (S + 1) * 4 + 12 + 12  # rgb, sigma, w | t | d | C  (3100 @128)
 INTEGRATOR_BWD_B = lambda S: 12 + S * (12 + 4) + (S + 1) * 4 + 12 + S * (12 + 4)  # 4636 @128
 

@@ -71,8 +71,18 @@ typedef struct nof_config {
  *               v_mfma_f32_16x16x32_f16 per product), activations and scaled deltas stored as fp32,
  *               the weight gradients split into hi + lo again (three v_mfma_f32_32x32x16_f16 per
  *               product).  22 significand bits per operand: the same 1e-5 parity as F32, within fp16's
- *               exponent range (activations below 65504; deltas power-of-2 scaled per level). */
-enum { NOF_PRECISION_F32 = 0, NOF_PRECISION_F32_SPLIT = 1, NOF_PRECISION_F16X2 = 2, NOF_PRECISION_F32_F16SPLIT = 3 };
+ *               exponent range (activations below 65504; deltas power-of-2 scaled per level).
+ *   F16       : plain fp16 mixed precision (BASELINE config 5's "fp16 activations on MFMA"): the
+ *               F16X2 kernels with ONE v_mfma_f32_16x16x32_f16 per product, fp16(weight) x
+ *               fp16(activation or scaled delta), fp32 accumulation; fp16 blocks and single-product
+ *               weight gradients as F16X2.  Parity: the perf-mode bound, relative L2 <= 2e-3. */
+enum {
+  NOF_PRECISION_F32 = 0,
+  NOF_PRECISION_F32_SPLIT = 1,
+  NOF_PRECISION_F16X2 = 2,
+  NOF_PRECISION_F32_F16SPLIT = 3,
+  NOF_PRECISION_F16 = 4
+};
 
 void nof_config_default(nof_config* cfg);
 const char* nof_last_error(void);

@@ -18,7 +18,7 @@
 // Additions the reference declares but never implements: SaveEvery checkpoints and resume
 // (Config.SaveEvery, TrainState.cs:59).  Philox replaces the reference's unseeded System.Random.
 //
-//   nof_train --records train_data.bin [--steps K] [--batch N] [--precision f32|split|f16x2|f16split]
+//   nof_train --records train_data.bin [--steps K] [--batch N] [--precision f32|split|f16x2|f16split|f16]
 //             [--print-every P] [--save-every S --ckpt-dir DIR] [--resume CKPT] [--host-api]
 //             [--seed X] [--device D | --gpus N] [--dump-params FILE]
 //
@@ -54,7 +54,7 @@ struct Args {
 
 [[noreturn]] void usage(int code) {
   std::fprintf(code ? stderr : stdout,
-               "usage: nof_train --records FILE [--steps K] [--batch N] [--precision f32|split|f16x2|f16split]\n"
+               "usage: nof_train --records FILE [--steps K] [--batch N] [--precision f32|split|f16x2|f16split|f16]\n"
                "                 [--print-every P] [--save-every S --ckpt-dir DIR] [--resume CKPT] [--host-api]\n"
                "                 [--seed X] [--device D | --gpus N] [--dump-params FILE]\n");
   std::exit(code);
@@ -87,6 +87,7 @@ Args parse(int argc, char** argv) {
       else if (p == "split") a.precision = NOF_PRECISION_F32_SPLIT;
       else if (p == "f16x2") a.precision = NOF_PRECISION_F16X2;
       else if (p == "f16split") a.precision = NOF_PRECISION_F32_F16SPLIT;
+      else if (p == "f16") a.precision = NOF_PRECISION_F16;
       else usage(2);
     } else {
       std::fprintf(stderr, "unknown argument %s\n", k.c_str());

@@ -99,7 +99,8 @@ static void check_cfg(const nof_config& c) {
       c.skip_layer != 4 || c.min_deg_point != 0 || c.max_deg_point != 16 || c.deg_view != 4)
     throw Error(NOF_ERR_UNSUPPORTED, "GPU path implements the reference network (8x256, 1x128, skip 4, PE 16/4)");
   NOF_REQUIRE(c.precision == NOF_PRECISION_F32 || c.precision == NOF_PRECISION_F32_SPLIT ||
-                  c.precision == NOF_PRECISION_F16X2 || c.precision == NOF_PRECISION_F32_F16SPLIT,
+                  c.precision == NOF_PRECISION_F16X2 || c.precision == NOF_PRECISION_F32_F16SPLIT ||
+                  c.precision == NOF_PRECISION_F16,
               "unknown precision mode");
 }
 
@@ -288,7 +289,7 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M, int bucket)
   std::vector<OutSpec> os;
   float* G = grads_.p;
   // operand blocks hold fp16 in the f16x2 mode (mlp_common.h ActOut): element offsets in halves there
-  const bool half = precision_ == NOF_PRECISION_F16X2;
+  const bool half = f16_blocks();
   auto at = [&](float* base, size_t off) -> const float* {
     return half ? reinterpret_cast<const float*>(reinterpret_cast<const uint16_t*>(base) + off) : base + off;
   };
@@ -333,7 +334,7 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M, int bucket)
   // measured for the (8,8) / (8,3) / (5,8) / (4,1) / (1,4) problems = 160 / 96 / 124 / 47 / 37.
   std::vector<int64_t> cost(P.size());
   for (size_t i = 0; i < P.size(); ++i) {
-    if (precision_ == NOF_PRECISION_F16X2) {
+    if (f16_blocks()) {
       cost[i] = 10 * (P[i].ntr + P[i].ntc) + (P[i].ntc == 1 ? 12 : 0);
     } else if (precision_ != NOF_PRECISION_F32) {
       const int WC = nof::wgrad_x3_grid_cols();  // C/2 waves per SIMD

@@ -167,7 +167,11 @@ class AcceleratedMLP {
   int precision_ = 0;  // NOF_PRECISION_*
   // fp16 (hi, lo) MFMA pieces in the forward / dX chain (F16X2, F32_F16SPLIT): f16 weight images,
   // power-of-2 scaled deltas
-  bool f16_pieces() const { return precision_ == NOF_PRECISION_F16X2 || precision_ == NOF_PRECISION_F32_F16SPLIT; }
+  bool f16_pieces() const {
+    return precision_ == NOF_PRECISION_F16X2 || precision_ == NOF_PRECISION_F32_F16SPLIT || precision_ == NOF_PRECISION_F16;
+  }
+  // fp16 activation / delta blocks and the k_wgrad_h weight gradients (F16X2, F16)
+  bool f16_blocks() const { return precision_ == NOF_PRECISION_F16X2 || precision_ == NOF_PRECISION_F16; }
   size_t P_ = 0;
   std::array<int, kLayers> out_{}, in_{}, woff_{}, boff_{};
   DevBuf<float> params_, grads_, wimg_f_, wimg_b_;

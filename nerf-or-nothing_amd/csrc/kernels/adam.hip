@@ -146,11 +146,13 @@ __global__ void k_pack_weights_x3(const float* __restrict__ P_, PackArgs pa, flo
     const bool fwd = gid < nfc;
     const int64_t c = fwd ? gid : gid - nfc;
     const int slice = (int)(c / kChunks), q = (int)(c % kChunks);
-    const int lane = q & 63, rest = q >> 6, piece = rest % NP, so = rest / NP;
-    // P = 1 (32x32x16 fragments, mlp_common.h): so = 8 s + ot, lane (h, x): row 32 ot + x,
-    //   element j = column 16 s + 8 (j >> 2) + 4h + (j & 3);
-    // P = 2 (16x16x32 fragments, mlp16.h mlp_layer16h): so = row tile rt, lane (g, x): row 16 rt + x,
-    //   element j = column 16 (j >> 2) + 4g + (j & 3)
+    const int lane = q & 63, rest = q >> 6;
+    // P = 1 (32x32x16 fragments, mlp_common.h): chunk (so NP + piece) 64 + lane, so = 8 s + ot,
+    //   lane (h, x): row 32 ot + x, element j = column 16 s + 8 (j >> 2) + 4h + (j & 3);
+    // P = 2 (16x16x32 fragments, mlp16.h mlp_layer16h): PIECE-major, chunk (16 piece + so) 64 + lane,
+    //   so = row tile rt, lane (g, x): row 16 rt + x, element j = column 16 (j >> 2) + 4g + (j & 3) —
+    //   the hi pieces of a slice are its first 16 KB, all the one-product F16 mode streams
+    const int piece = P == 2 ? rest / 16 : rest % NP, so = P == 2 ? rest % 16 : rest / NP;
     const int row = P == 2 ? 16 * so + (lane & 15) : (so & 7) * 32 + (lane & 31);
     int l, base;
     if (fwd) fwd_slice(slice, l, base);

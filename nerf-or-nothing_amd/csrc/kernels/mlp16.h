@@ -141,6 +141,7 @@ struct BlkStore16H {
 // gradient operands in fp32), fp16 blocks (P = 2); all nt
 template <int P, bool kBwd> struct Store16 { typedef BlkStore16 T; typedef float E; };
 template <bool kBwd> struct Store16<2, kBwd> { typedef BlkStore16H<true> T; typedef _Float16 E; };
+template <bool kBwd> struct Store16<4, kBwd> { typedef BlkStore16H<true> T; typedef _Float16 E; };  // F16
 template <class E>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t blk_rsrc_t(E* blk) {
   return __builtin_amdgcn_make_buffer_rsrc(blk, (short)0, 0x7fffffff, 0x00020000);
@@ -327,16 +328,23 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
 // caller's epilogue left PRE-SPLIT as the two fragments (bin[2t] = hi, bin[2t + 1] = lo, packed fp16
 // pairs in k order); the IPE slices (fp32) are split here.  The packed slice
 // (k_pack_weights_x3<2>) holds, per 16-row tile rt and piece p, the 16-B A fragment of lane (g, j):
-// W[16 rt + j][base + 16 (i >> 2) + 4g + (i & 3)], i = 0..7 (chunk (2 rt + p) 64 + lane: one
-// contiguous ds_read_b128 per fragment).  A group = one row-tile pair x 3 products (lo.hi, hi.lo,
+// W[16 rt + j][base + 16 (i >> 2) + 4g + (i & 3)], i = 0..7 (chunk (16 p + rt) 64 + lane: one
+// contiguous ds_read_b128 per fragment; piece-major, so the hi pieces are the slice's first 16 KB).
+// kProd = 1 streams only that half: 2 DMA steps per slice instead of 4.  A group = one row-tile pair x 3 products (lo.hi, hi.lo,
 // hi.hi) interleaved over the pair's two accumulators; the next pair's fragments are read one group
 // ahead; the 4 DMA steps of slice t + 2 ride groups 0..3; epilogue tiles 2t + 2, 2t + 3 run after them.
-template <int NT_B, int NT_I, int OT, class Epi>
+// kProd = 1 (F16): the hi.hi product alone — only the hi A fragments are read, the lo pieces the
+// epilogues leave in `bin` go unused.
+template <int NT_B, int NT_I, int OT, class Epi, int kProd = 3>
 __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16],
                                              float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
                                              int lane, Epi& epi, const float* cinit) {
   typedef SplitMode<2> SM;
   static_assert(OT % 2 == 0 && OT <= 16, "row tiles come in pairs");
+  static_assert(kProd == 1 || kProd == SM::NPROD, "hi.hi alone or all three products");
+  constexpr int kPieces = kProd == 1 ? 1 : 2;     // A fragment pieces read per row tile
+  constexpr int kPP0 = SM::NPROD - kProd;         // first product (SM::pa / pb order; the last is hi.hi)
+  constexpr int kDmaSteps = kProd == 1 ? 2 : 4;   // 8-KB steps per slice: the hi half, or all of it
   constexpr int kSlots = ring16_slots<2>();
   constexpr int NG = OT / 2;  // groups per slice
   constexpr int kE1 = NG > 4 ? 4 : NG - 1;
@@ -369,30 +377,31 @@ __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const fl
     }
     Frag<2> a0, a1;
 #pragma unroll
-    for (int p = 0; p < 2; ++p) { a0.p[p] = W[p * 64]; a1.p[p] = W[(2 + p) * 64]; }
+    for (int p = 0; p < kPieces; ++p) { a0.p[p] = W[(16 * p) * 64]; a1.p[p] = W[(16 * p + 1) * 64]; }
     auto cread = [&](int rt) { return *reinterpret_cast<const f32x4*>(cinit + 16 * rt); };
     f32x4 c0 = {}, c1 = {};  // initial accumulators of the group's pair (slice 0): bias or 0
     if (t == 0 && cinit) { c0 = cread(0); c1 = cread(1); }
 #pragma unroll
     for (int q = 0; q < NG; ++q) {
-      asm volatile("" ::"v"(a0.p[0]), "v"(a0.p[1]), "v"(a1.p[0]), "v"(a1.p[1]), "v"(c0), "v"(c1));
+      if constexpr (kPieces == 2) asm volatile("" ::"v"(a0.p[0]), "v"(a0.p[1]), "v"(a1.p[0]), "v"(a1.p[1]), "v"(c0), "v"(c1));
+      else asm volatile("" ::"v"(a0.p[0]), "v"(a1.p[0]), "v"(c0), "v"(c1));
       Frag<2> n0 = a0, n1 = a1;
       f32x4 m0 = c0, m1 = c1;
       if (t == 0 && cinit && q + 1 < NG) { m0 = cread(2 * q + 2); m1 = cread(2 * q + 3); }
       if (q + 1 < NG) {
 #pragma unroll
-        for (int p = 0; p < 2; ++p) {
-          n0.p[p] = W[((2 * q + 2) * 2 + p) * 64];
-          n1.p[p] = W[((2 * q + 3) * 2 + p) * 64];
+        for (int p = 0; p < kPieces; ++p) {
+          n0.p[p] = W[(16 * p + 2 * q + 2) * 64];
+          n1.p[p] = W[(16 * p + 2 * q + 3) * 64];
         }
       }
-      if (dma && q < 4) slice16_dma_step(wsrc + 2 * kSliceFloats, lds + nxt2 * kSliceFloats, tid, q);
+      if (dma && q < kDmaSteps) slice16_dma_step(wsrc + 2 * kSliceFloats, lds + nxt2 * kSliceFloats, tid, q);
       __builtin_amdgcn_sched_barrier(0);
       const bool first = t == 0;
 #pragma unroll
-      for (int pp = 0; pp < SM::NPROD; ++pp) {
-        acc[2 * q] = SM::mfma16(a0.p[SM::pa(pp)], b.p[SM::pb(pp)], (first && pp == 0) ? c0 : acc[2 * q]);
-        acc[2 * q + 1] = SM::mfma16(a1.p[SM::pa(pp)], b.p[SM::pb(pp)], (first && pp == 0) ? c1 : acc[2 * q + 1]);
+      for (int pp = kPP0; pp < SM::NPROD; ++pp) {
+        acc[2 * q] = SM::mfma16(a0.p[SM::pa(pp)], b.p[SM::pb(pp)], (first && pp == kPP0) ? c0 : acc[2 * q]);
+        acc[2 * q + 1] = SM::mfma16(a1.p[SM::pa(pp)], b.p[SM::pb(pp)], (first && pp == kPP0) ? c1 : acc[2 * q + 1]);
       }
       if (t + 1 < NT_B && q == kE1) epi(2 * t + 2);
       if (t + 1 < NT_B && q == kE2) epi(2 * t + 3);
@@ -406,20 +415,22 @@ __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const fl
       if (cur & 1) slice_barrier(t + 1 < NT_B ? 2 * Epi::kVmPerPart : 0);
       cur = (cur + 1) & 3;
     } else {
-      slice_barrier((dma ? 4 : 0) + (t + 1 < NT_B ? 2 * Epi::kVmPerPart : 0));
+      slice_barrier((dma ? kDmaSteps : 0) + (t + 1 < NT_B ? 2 * Epi::kVmPerPart : 0));
       cur = cur == 2 ? 0 : cur + 1;
     }
     wsrc += kSliceFloats;
   }
 }
 
-// precision dispatch: P = 0 fp32 16x16x4, P = 2 / 3 fp16 (hi, lo) pieces on 16x16x32
+// precision dispatch: P = 0 fp32 16x16x4, P = 2 / 3 fp16 (hi, lo) pieces on 16x16x32, P = 4 fp16 hi.hi
 template <int P, int NT_B, int NT_I, int OT, class Epi>
 __device__ __forceinline__ void layer16(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16], float* lds,
                                         int& cur, const float*& wsrc, bool last_in_schedule, int tid, int lane,
                                         Epi& epi, const float* cinit = nullptr) {
   if constexpr (P == 2 || P == 3)
     mlp_layer16h<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi, cinit);
+  else if constexpr (P == 4)
+    mlp_layer16h<NT_B, NT_I, OT, Epi, 1>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi, cinit);
   else
     mlp_layer16<NT_B, NT_I, OT, ring16_slots<P>()>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane,
                                                    epi, cinit);

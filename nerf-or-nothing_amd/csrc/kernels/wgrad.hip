@@ -695,7 +695,7 @@ static hipError_t launch_wgrad_split(const WgProblem* probs, const WgItem* items
 hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,
                            const int64_t* slab_off, float* slabs, float* bias_slabs, int precision, hipStream_t st) {
   if (num_wg <= 0) return hipSuccess;
-  if (precision == 2) {  // fp16 operand blocks (k_wgrad_h)
+  if (precision == 2 || precision == 4) {  // fp16 operand blocks (k_wgrad_h): F16X2, F16
     static bool attr = false;
     if (!attr) {
       const hipError_t e = hipFuncSetAttribute((const void*)k_wgrad_h, hipFuncAttributeMaxDynamicSharedMemorySize, kWhLds);

@@ -109,7 +109,7 @@ class AcceleratedMLP:
         M = dv["M"]
         nb = M // 32
         out = np.zeros((M, 8 * 256 + 128), np.uint8)
-        if self._owner.config.precision in (0, 2, 3):  # 16x16 kernels (mlp16.h): [half][lane][uint2]
+        if self._owner.config.precision in (0, 2, 3, 4):  # 16x16 kernels (mlp16.h): [half][lane][uint2]
             raw = to_numpy(dv["masks"], (nb, 9, 2, 64, 2), np.uint32)
             lane = np.arange(64)
             j, g = lane & 15, lane >> 4

@@ -133,7 +133,7 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--device", type=int, default=0)
-    ap.add_argument("--precision", choices=["f32", "split", "f16x2", "f16split"], default="f32")
+    ap.add_argument("--precision", choices=["f32", "split", "f16x2", "f16split", "f16"], default="f32")
     ap.add_argument("--print-every", type=int, default=100)
     ap.add_argument("--save-every", type=int, default=0)
     ap.add_argument("--ckpt-dir")
@@ -144,7 +144,7 @@ def main(argv=None):
     ds = (api.RayDataset(a.records, device=a.device) if a.records else
           api.RayDataset(records=synth.pack_records(synth.blender_rays(a.synthetic, seed=1)), device=a.device))
     tr = Trainer(ds, batch_size=a.batch, device=a.device, print_every=a.print_every, save_every=a.save_every,
-                 ckpt_dir=a.ckpt_dir, sync_check_every=a.sync_check_every, precision={"f32": 0, "split": 1, "f16x2": 2, "f16split": 3}[a.precision])
+                 ckpt_dir=a.ckpt_dir, sync_check_every=a.sync_check_every, precision={"f32": 0, "split": 1, "f16x2": 2, "f16split": 3, "f16": 4}[a.precision])
     if a.resume:
         tr.resume(a.resume)
     t0 = time.perf_counter()

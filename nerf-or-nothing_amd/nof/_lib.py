@@ -24,7 +24,7 @@ class NofError(RuntimeError):
         self.status = status
 
 
-NOF_PRECISION_F32, NOF_PRECISION_F32_SPLIT, NOF_PRECISION_F16X2, NOF_PRECISION_F32_F16SPLIT = 0, 1, 2, 3
+NOF_PRECISION_F32, NOF_PRECISION_F32_SPLIT, NOF_PRECISION_F16X2, NOF_PRECISION_F32_F16SPLIT, NOF_PRECISION_F16 = 0, 1, 2, 3, 4
 
 
 class nof_config(C.Structure):

@@ -620,6 +620,18 @@ def main():
                                               "over the MLP's algorithmic FLOP"}}
             if c_sync is not None:
                 cfg5["params_in_sync"] = c_sync
+            # the same batch in the plain fp16 mode (one fp16 MFMA per product: configs[4]'s "fp16
+            # activations on MFMA" taken literally), against the dense fp16 peak
+            if not a.no_alt:
+                f_dt, _, _, f_sync = measure("f16", B_run=c_B, steps=20, warmup=3, timers_on=False, scene="llff",
+                                             smp=(256, 256))
+                f_tf = 2 * (MACS_FWD + MACS_DX + MACS_DW) * (c_B // G) * 512 / (f_dt / 20) / 1e12
+                cfg5["f16"] = {"value": round(c_B * 20 / f_dt, 1), "unit": "rays/s", "ms_per_step": round(f_dt * 1e3 / 20, 4),
+                               "dtype": DTYPES["f16"],
+                               "roofline_step": {"bound": "mfma", "achieved": round(f_tf, 2), "peak": PEAKS["f16"],
+                                                 "unit": "TFLOP/s per GPU", "frac": round(f_tf / PEAKS["f16"], 4)}}
+                if f_sync is not None:
+                    cfg5["f16"]["params_in_sync"] = f_sync
 
     result = None
     if lead:

@@ -44,7 +44,15 @@ for k, s in stats.items():
     avg_ns = float(s["AverageNs"])
     m = lambda c: (sum(agg[(k, c)]) / len(agg[(k, c)])) if agg.get((k, c)) else None
     fetch, write, grbm, mfma = m("FETCH_SIZE"), m("WRITE_SIZE"), m("GRBM_GUI_ACTIVE"), m("SQ_VALU_MFMA_BUSY_CYCLES")
+    lds, ldsc = m("SQ_LDS_IDX_ACTIVE"), m("SQ_LDS_BANK_CONFLICT")
     e = {"calls": int(s["Calls"]), "avg_ms": avg_ns / 1e6}
+    if lds is not None:
+        # LDS-array cycles summed over the CUs, against 256 CUs x the kernel's GPU cycles (GRBM_GUI_ACTIVE
+        # / 8): the fraction of CU-cycles the LDS array is busy (1.0 = 256 B/clk/CU for ds_read_b128)
+        e["lds_idx_active"] = lds
+        e["lds_bank_conflict"] = ldsc
+        if grbm:
+            e["lds_busy"] = round(lds / (256 * grbm / XCDS), 4)
     if fetch is not None and write is not None:
         e["hbm_bytes_per_launch"] = (2 * fetch + write) * 1024
         e["hbm_GBps"] = e["hbm_bytes_per_launch"] / (avg_ns * 1e-9) / 1e9
@@ -63,7 +71,10 @@ for k, s in stats.items():
 json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
 # lookups read by bench.py (bench kernel-timer names; other precision modes keyed with "_<mode>")
 names = {"k_mlp_fwd16<0, true>": "mlp_fwd", "k_mlp_bwd16<0>": "mlp_bwd", "k_wgrad": "wgrad",
-         "k_mlp_fwd16<2, true>": "mlp_fwd_f16x2", "k_mlp_bwd16<2>": "mlp_bwd_f16x2", "k_wgrad_h": "wgrad_f16x2",
+         "k_mlp_fwd16<2, true>": "mlp_fwd_f16x2", "k_mlp_bwd16<2>": "mlp_bwd_f16x2",
+         "k_mlp_fwd16<4, true>": "mlp_fwd_f16", "k_mlp_bwd16<4>": "mlp_bwd_f16",
+         # f16x2 and F16 share the fp16-block weight-gradient kernel: key it by the run's mode
+         "k_wgrad_h": "wgrad" + (suffix if suffix in ("_f16x2", "_f16") else "_f16x2"),
          "k_mlp_fwd<1, true>": "mlp_fwd_split", "k_mlp_bwd<1>": "mlp_bwd_split", "k_wgrad_x3<1>": "wgrad_split",
          "k_mlp_fwd16<3, true>": "mlp_fwd_f16split", "k_mlp_bwd16<3>": "mlp_bwd_f16split",
          "k_wgrad_x3<2>": "wgrad_f16split",

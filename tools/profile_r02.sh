@@ -2,6 +2,7 @@
 # Round-2 rocprofv3 evidence, one tag per run:
 #   per precision mode: kernel trace + stats, then separate --pmc passes
 #     FETCH_SIZE | WRITE_SIZE | SQ_VALU_MFMA_BUSY_CYCLES + SQ_BUSY_CYCLES + GRBM_GUI_ACTIVE
+#     [| SQ_LDS_IDX_ACTIVE + SQ_LDS_BANK_CONFLICT + GRBM_GUI_ACTIVE with LDS=1]
 #   integrator-only 2^20 x 128 batch: trace, FETCH_SIZE, WRITE_SIZE
 # counters never combined with runtime/sys traces; every pass under its own time limit.
 # usage: tools/profile_r02.sh TAG [precisions...]
@@ -30,5 +31,13 @@ CMD=(tools/integrator_only.py)
 run integ_trace --kernel-trace --stats -d $OUT/integrator/trace -o run --output-format csv
 run integ_fetch --pmc FETCH_SIZE -d $OUT/integrator/pmc_fetch -o run --output-format csv
 run integ_write --pmc WRITE_SIZE -d $OUT/integrator/pmc_write -o run --output-format csv
+# LDS-array occupancy (LDS=1): the forwards' A-fragment reads against the 256 B/clk/CU array; last,
+# so an unsupported counter cannot cost the passes above
+if [ -n "$LDS" ]; then
+  for p in $PRECS; do
+    CMD=(bench.py $ARGS --precision $p)
+    run ${p}_lds --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d $OUT/$p/pmc_lds -o run --output-format csv
+  done
+fi
 echo done >> $OUT/progress.log
 echo done

@@ -20,6 +20,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void* lptr_t;
 constexpr int kSliceFloats = 4096, kSlices = 70, kSlots = 3;  // 16-KB hi-half slices
 constexpr double kMfmaCyclesPerSlice = 512.0;
+constexpr int kScratchFloats = 128 * 1024;  // per wave: 128 slices x 2 KB x NC (NC <= 2)
 
 __device__ __forceinline__ f32x4 mfma(f16x8 a, f16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
@@ -48,7 +49,9 @@ __device__ __forceinline__ void epi_tile(const f32x4& v, uint32_t& mw, __amdgpu_
 // Per slice: 8 groups of {the next group's 2 hi fragments read one group ahead, 2 NC MFMAs}, the slice
 // DMA (16 KB) spread over the first groups, the epilogue of 2 NC previous-layer tiles (kEpi), one
 // counted barrier.
-template <int NC, bool kEpi>
+// AH: groups of A-fragment read-ahead (the kernels: 1).  Epilogue stores go to fresh lines (a 128-slice
+// ring of 2 NC KB per wave), as the kernels' block stores do.
+template <int NC, bool kEpi, int AH = 1>
 __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void k_p(const float* __restrict__ img, int reps, float* out,
                                                               long long* cyc, float* scratch) {
   constexpr int T = NC == 1 ? 512 : 256;
@@ -60,7 +63,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void k_p(const float* __res
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(img), (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t blk = __builtin_amdgcn_make_buffer_rsrc(
-      scratch + (size_t)(blockIdx.x * 8 + wv) * 8192, (short)0, 0x7fffffff, 0x00020000);
+      scratch + (size_t)(blockIdx.x * 8 + wv) * kScratchFloats, (short)0, 0x7fffffff, 0x00020000);
   const uint32_t voff = 256u * (lane >> 4) + 64u * (j & 1) + ((j & 6) << 1);
   const uint32_t sel = (j & 1) ? 0x03020706u : 0x05040100u;
   f32x4 acc[NC][16] = {};
@@ -83,27 +86,32 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void k_p(const float* __res
     __syncthreads();
     for (int s = 0; s < kSlices; ++s) {
       const f16x8* W = reinterpret_cast<const f16x8*>(lds + (s % kSlots) * kSliceFloats) + lane;
-      f16x8 a0 = W[0], a1 = W[64];
+      f16x8 fr[AH + 1][2];
+#pragma unroll
+      for (int a = 0; a < AH; ++a) { fr[a][0] = W[(2 * a) * 64]; fr[a][1] = W[(2 * a + 1) * 64]; }
+      const int ring = ((rep * kSlices + s) & 127) * 2048 * NC;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        asm volatile("" ::"v"(a0), "v"(a1));
-        f16x8 n0 = a0, n1 = a1;
-        if (q + 1 < 8) { n0 = W[(2 * q + 2) * 64]; n1 = W[(2 * q + 3) * 64]; }
+        asm volatile("" ::"v"(fr[q % (AH + 1)][0]), "v"(fr[q % (AH + 1)][1]));
+        if (q + AH < 8) {
+          fr[(q + AH) % (AH + 1)][0] = W[(2 * (q + AH)) * 64];
+          fr[(q + AH) % (AH + 1)][1] = W[(2 * (q + AH) + 1) * 64];
+        }
         if (s + 2 < kSlices && q < kSteps) dma(s + 2, q);
         __builtin_amdgcn_sched_barrier(0);
+        const f16x8 a0 = fr[q % (AH + 1)][0], a1 = fr[q % (AH + 1)][1];
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
           acc[c][2 * q] = mfma(a0, b[c], acc[c][2 * q]);
           acc[c][2 * q + 1] = mfma(a1, b[c], acc[c][2 * q + 1]);
         }
         if (kEpi && (q == 4 || q == 6)) {
-          const int t = (2 * s + (q == 6)) & 15;
+          // compile-time tile index: a runtime one sends prev[] to scratch (the first run of this
+          // probe indexed by slice and measured 4x slower epilogues for that reason alone)
 #pragma unroll
-          for (int c = 0; c < NC; ++c) epi_tile(prev[c][t], mw, blk, voff + 2048u * c, sel, 1024 * t);
+          for (int c = 0; c < NC; ++c) epi_tile(prev[c][q + (q == 6)], mw, blk, voff + 1024u * c + 512u * (q == 6), sel, ring);
         }
         __builtin_amdgcn_sched_barrier(0);
-        a0 = n0;
-        a1 = n1;
       }
       asm volatile("s_waitcnt vmcnt(8)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
@@ -151,13 +159,21 @@ int main() {
   (void)hipMemcpy(img, h.data(), n * 4, hipMemcpyHostToDevice);
   (void)hipMalloc(&out, 256 * 512 * 4);
   (void)hipMalloc(&cyc, 256 * sizeof(long long));
-  (void)hipMalloc(&scratch, (size_t)256 * 8 * 8192 * 4);
+  (void)hipMalloc(&scratch, (size_t)256 * 8 * kScratchFloats * 4);
   const int reps = 40;
-  for (int it = 0; it < 3; ++it) {
-    run("p16 skeleton (2 waves/SIMD)", k_p<1, false>, 512, img, out, cyc, scratch, reps);
-    run("p16 + epilogue", k_p<1, true>, 512, img, out, cyc, scratch, reps);
-    run("p32 skeleton (1 wave/SIMD)", k_p<2, false>, 256, img, out, cyc, scratch, reps);
-    run("p32 + epilogue", k_p<2, true>, 256, img, out, cyc, scratch, reps);
+  for (int it = 0; it < 2; ++it) {
+    run("p16 skeleton, reads 1 ahead", k_p<1, false, 1>, 512, img, out, cyc, scratch, reps);
+    run("p16 skeleton, reads 2 ahead", k_p<1, false, 2>, 512, img, out, cyc, scratch, reps);
+    run("p16 skeleton, reads 3 ahead", k_p<1, false, 3>, 512, img, out, cyc, scratch, reps);
+    run("p16 skeleton, reads 4 ahead", k_p<1, false, 4>, 512, img, out, cyc, scratch, reps);
+    run("p16 + epilogue, 1 ahead", k_p<1, true, 1>, 512, img, out, cyc, scratch, reps);
+    run("p16 + epilogue, 2 ahead", k_p<1, true, 2>, 512, img, out, cyc, scratch, reps);
+    run("p16 + epilogue, 3 ahead", k_p<1, true, 3>, 512, img, out, cyc, scratch, reps);
+    run("p16 + epilogue, 4 ahead", k_p<1, true, 4>, 512, img, out, cyc, scratch, reps);
+    run("p32 skeleton, reads 1 ahead", k_p<2, false, 1>, 256, img, out, cyc, scratch, reps);
+    run("p32 skeleton, reads 3 ahead", k_p<2, false, 3>, 256, img, out, cyc, scratch, reps);
+    run("p32 + epilogue, 1 ahead", k_p<2, true, 1>, 256, img, out, cyc, scratch, reps);
+    run("p32 + epilogue, 3 ahead", k_p<2, true, 3>, 256, img, out, cyc, scratch, reps);
   }
   return 0;
 }

@@ -230,9 +230,11 @@ __device__ __forceinline__ void put_tile(float (&bin)[16][4], int t, const float
 // Epilogue hook of mlp_layer16: epi(tile) finishes one accumulator tile of the PREVIOUS layer
 // (4 registers) into `bin`; tiles 2t + 2 and 2t + 3 run during slice t (in MFMA groups 1 and
 // kEpiGroup2), so both are complete before slice t + 1 reads them.  Tiles 0 and 1 are the caller's.
-// kVmPerPart = vector-memory ops one tile issues, for the counted slice barrier: it must not exceed the
-// stores a tile really issues (fp32 tiles 4, fp16 tiles 2), or a 4-slot ring's barrier lets the slice
-// DMA it has to retire stay in flight (an F16 4-slot ring raced on an over-count of 4, round 2).
+// kVmPerPart = vector-memory ops one tile issues (4: fp32 tiles), for the counted slice barrier.  fp16
+// tiles issue 2 (store_pairs): with the 3-slot ring the count of 4 then lets exactly the previous slice's
+// stores stay in flight too (they follow the DMA the barrier must retire), but a 4-slot ring, whose
+// barrier also retires the slice's own DMA, needs the exact 2 (an F16 4-slot ring raced on 4, round 2;
+// the exact count in the 3-slot path forces the previous slice's stores out: F16 step +1 %, A/B).
 struct NoEpi16 {
   static constexpr int kVmPerPart = 0;
   __device__ __forceinline__ void operator()(int) {}

@@ -21,7 +21,7 @@ namespace nof {
 // pre-split (put_tile, mlp16.h).
 template <bool kDensity, class ST, bool kSplit = false>
 struct BwdEpi16 {
-  static constexpr int kVmPerPart = ST::kHalf ? 2 : 4;  // stores per tile (fp16 tiles: 2 dword pairs)
+  static constexpr int kVmPerPart = 4;
   const f32x4 (&acc)[16];
   float (&bin)[16][4];
   const ST& bst;

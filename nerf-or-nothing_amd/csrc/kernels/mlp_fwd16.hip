@@ -29,7 +29,7 @@ namespace nof {
 // clamped onto the last block recomputes bit-identical values, so its duplicate stores are benign.
 template <bool store, bool kDensity, int NT, class ST, bool kSplit = false>
 struct FwdEpi16 {
-  static constexpr int kVmPerPart = store ? (ST::kHalf ? 2 : 4) : 0;  // stores per tile (fp16 tiles: 2 dword pairs)
+  static constexpr int kVmPerPart = store ? 4 : 0;
   const f32x4 (&acc)[16];
   float (&bin)[16][4];
   const ST& bst;

@@ -51,7 +51,9 @@ __device__ __forceinline__ void epi_tile(const f32x4& v, uint32_t& mw, __amdgpu_
 // counted barrier.
 // AH: groups of A-fragment read-ahead (the kernels: 1).  Epilogue stores go to fresh lines (a 128-slice
 // ring of 2 NC KB per wave), as the kernels' block stores do.
-template <int NC, bool kEpi, int AH = 1>
+// kDma / kBar: decomposition (the slice DMA, the per-slice barrier left out); kReg: the slice staged
+// through registers instead (global_load_dwordx4 at groups 0..kSteps-1, ds_write_b128 at groups 4..)
+template <int NC, bool kEpi, int AH = 1, bool kDma = true, bool kBar = true, bool kReg = false>
 __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void k_p(const float* __restrict__ img, int reps, float* out,
                                                               long long* cyc, float* scratch) {
   constexpr int T = NC == 1 ? 512 : 256;
@@ -90,6 +92,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void k_p(const float* __res
 #pragma unroll
       for (int a = 0; a < AH; ++a) { fr[a][0] = W[(2 * a) * 64]; fr[a][1] = W[(2 * a + 1) * 64]; }
       const int ring = ((rep * kSlices + s) & 127) * 2048 * NC;
+      f32x4 stage[kSteps];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         asm volatile("" ::"v"(fr[q % (AH + 1)][0]), "v"(fr[q % (AH + 1)][1]));
@@ -97,7 +100,11 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void k_p(const float* __res
           fr[(q + AH) % (AH + 1)][0] = W[(2 * (q + AH)) * 64];
           fr[(q + AH) % (AH + 1)][1] = W[(2 * (q + AH) + 1) * 64];
         }
-        if (s + 2 < kSlices && q < kSteps) dma(s + 2, q);
+        if (kDma && !kReg && s + 2 < kSlices && q < kSteps) dma(s + 2, q);
+        if (kReg && s + 2 < kSlices && q < kSteps)  // 16-B chunk kSteps... of this thread, into registers
+          stage[q] = *reinterpret_cast<const f32x4*>(img + (size_t)(s + 2) * kSliceFloats + (q * T + tid) * 4);
+        if (kReg && s + 2 < kSlices && q >= 4 && q < 4 + kSteps)
+          *reinterpret_cast<f32x4*>(lds + ((s + 2) % kSlots) * kSliceFloats + ((q - 4) * T + tid) * 4) = stage[q - 4];
         __builtin_amdgcn_sched_barrier(0);
         const f16x8 a0 = fr[q % (AH + 1)][0], a1 = fr[q % (AH + 1)][1];
 #pragma unroll
@@ -113,7 +120,8 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void k_p(const float* __res
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-      asm volatile("s_waitcnt vmcnt(8)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (kBar) asm volatile("s_waitcnt vmcnt(8)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
   }
   const long long t1 = __builtin_readcyclecounter();
@@ -162,18 +170,18 @@ int main() {
   (void)hipMalloc(&scratch, (size_t)256 * 8 * kScratchFloats * 4);
   const int reps = 40;
   for (int it = 0; it < 2; ++it) {
-    run("p16 skeleton, reads 1 ahead", k_p<1, false, 1>, 512, img, out, cyc, scratch, reps);
-    run("p16 skeleton, reads 2 ahead", k_p<1, false, 2>, 512, img, out, cyc, scratch, reps);
-    run("p16 skeleton, reads 3 ahead", k_p<1, false, 3>, 512, img, out, cyc, scratch, reps);
-    run("p16 skeleton, reads 4 ahead", k_p<1, false, 4>, 512, img, out, cyc, scratch, reps);
-    run("p16 + epilogue, 1 ahead", k_p<1, true, 1>, 512, img, out, cyc, scratch, reps);
-    run("p16 + epilogue, 2 ahead", k_p<1, true, 2>, 512, img, out, cyc, scratch, reps);
-    run("p16 + epilogue, 3 ahead", k_p<1, true, 3>, 512, img, out, cyc, scratch, reps);
-    run("p16 + epilogue, 4 ahead", k_p<1, true, 4>, 512, img, out, cyc, scratch, reps);
-    run("p32 skeleton, reads 1 ahead", k_p<2, false, 1>, 256, img, out, cyc, scratch, reps);
-    run("p32 skeleton, reads 3 ahead", k_p<2, false, 3>, 256, img, out, cyc, scratch, reps);
-    run("p32 + epilogue, 1 ahead", k_p<2, true, 1>, 256, img, out, cyc, scratch, reps);
-    run("p32 + epilogue, 3 ahead", k_p<2, true, 3>, 256, img, out, cyc, scratch, reps);
+    run("p16 skeleton", k_p<1, false>, 512, img, out, cyc, scratch, reps);
+    run("p16 skeleton, no DMA", k_p<1, false, 1, false>, 512, img, out, cyc, scratch, reps);
+    run("p16 skeleton, no barrier", k_p<1, false, 1, true, false>, 512, img, out, cyc, scratch, reps);
+    run("p16 skeleton, no DMA/barrier", k_p<1, false, 1, false, false>, 512, img, out, cyc, scratch, reps);
+    run("p16 skeleton, register staging", k_p<1, false, 1, true, true, true>, 512, img, out, cyc, scratch, reps);
+    run("p32 skeleton, register staging", k_p<2, false, 1, true, true, true>, 256, img, out, cyc, scratch, reps);
+    run("p16 + epilogue", k_p<1, true>, 512, img, out, cyc, scratch, reps);
+    run("p16 + epilogue, reads 2 ahead", k_p<1, true, 2>, 512, img, out, cyc, scratch, reps);
+    run("p16 + epilogue, no DMA", k_p<1, true, 1, false>, 512, img, out, cyc, scratch, reps);
+    run("p32 skeleton", k_p<2, false>, 256, img, out, cyc, scratch, reps);
+    run("p32 skeleton, no DMA", k_p<2, false, 1, false>, 256, img, out, cyc, scratch, reps);
+    run("p32 + epilogue", k_p<2, true>, 256, img, out, cyc, scratch, reps);
   }
   return 0;
 }

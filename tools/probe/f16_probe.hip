@@ -52,8 +52,10 @@ __device__ __forceinline__ void epi_tile(const f32x4& v, uint32_t& mw, __amdgpu_
 // AH: groups of A-fragment read-ahead (the kernels: 1).  Epilogue stores go to fresh lines (a 128-slice
 // ring of 2 NC KB per wave), as the kernels' block stores do.
 // kDma / kBar: decomposition (the slice DMA, the per-slice barrier left out); kReg: the slice staged
-// through registers instead (global_load_dwordx4 at groups 0..kSteps-1, ds_write_b128 at groups 4..)
-template <int NC, bool kEpi, int AH = 1, bool kDma = true, bool kBar = true, bool kReg = false>
+// through registers instead: 1 = global_load_dwordx4 at groups 0.. and ds_write_b128 at groups 4.. of the
+// same slice; 2 = loads of slice s + 3 at the last groups of slice s, held across the barrier, written at
+// the first groups of slice s + 1 (a whole slice of load latency covered)
+template <int NC, bool kEpi, int AH = 1, bool kDma = true, bool kBar = true, int kReg = 0>
 __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void k_p(const float* __restrict__ img, int reps, float* out,
                                                               long long* cyc, float* scratch) {
   constexpr int T = NC == 1 ? 512 : 256;
@@ -76,6 +78,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void k_p(const float* __res
   for (int c = 0; c < NC; ++c)
     for (int i = 0; i < 8; ++i) b[c][i] = (_Float16)(0.37f * (i + lane % 7) - 1.1f + 0.1f * c);
   uint32_t mw = 0;
+  f32x4 stage[kSteps];
   const long long t0 = __builtin_readcyclecounter();
   for (int rep = 0; rep < reps; ++rep) {
     auto dma = [&](int s, int i) {
@@ -84,6 +87,8 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void k_p(const float* __res
                                                (s * kSliceFloats + i * T * 4) * 4, 0, 0);
     };
     for (int i = 0; i < kSteps; ++i) { dma(0, i); dma(1, i); }
+    if (kReg == 2)
+      for (int i = 0; i < kSteps; ++i) stage[i] = *reinterpret_cast<const f32x4*>(img + (size_t)2 * kSliceFloats + (i * T + tid) * 4);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     for (int s = 0; s < kSlices; ++s) {
@@ -92,7 +97,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void k_p(const float* __res
 #pragma unroll
       for (int a = 0; a < AH; ++a) { fr[a][0] = W[(2 * a) * 64]; fr[a][1] = W[(2 * a + 1) * 64]; }
       const int ring = ((rep * kSlices + s) & 127) * 2048 * NC;
-      f32x4 stage[kSteps];
+
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         asm volatile("" ::"v"(fr[q % (AH + 1)][0]), "v"(fr[q % (AH + 1)][1]));
@@ -101,10 +106,15 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void k_p(const float* __res
           fr[(q + AH) % (AH + 1)][1] = W[(2 * (q + AH) + 1) * 64];
         }
         if (kDma && !kReg && s + 2 < kSlices && q < kSteps) dma(s + 2, q);
-        if (kReg && s + 2 < kSlices && q < kSteps)  // 16-B chunk kSteps... of this thread, into registers
+        if (kReg == 1 && s + 2 < kSlices && q < kSteps)  // 16-B chunk kSteps... of this thread, into registers
           stage[q] = *reinterpret_cast<const f32x4*>(img + (size_t)(s + 2) * kSliceFloats + (q * T + tid) * 4);
-        if (kReg && s + 2 < kSlices && q >= 4 && q < 4 + kSteps)
+        if (kReg == 1 && s + 2 < kSlices && q >= 4 && q < 4 + kSteps)
           *reinterpret_cast<f32x4*>(lds + ((s + 2) % kSlots) * kSliceFloats + ((q - 4) * T + tid) * 4) = stage[q - 4];
+        if (kReg == 2 && s + 2 < kSlices && q < kSteps)
+          *reinterpret_cast<f32x4*>(lds + ((s + 2) % kSlots) * kSliceFloats + (q * T + tid) * 4) = stage[q];
+        if (kReg == 2 && s + 3 < kSlices && q >= 8 - kSteps)
+          stage[q - (8 - kSteps)] =
+              *reinterpret_cast<const f32x4*>(img + (size_t)(s + 3) * kSliceFloats + ((q - (8 - kSteps)) * T + tid) * 4);
         __builtin_amdgcn_sched_barrier(0);
         const f16x8 a0 = fr[q % (AH + 1)][0], a1 = fr[q % (AH + 1)][1];
 #pragma unroll
@@ -174,8 +184,10 @@ int main() {
     run("p16 skeleton, no DMA", k_p<1, false, 1, false>, 512, img, out, cyc, scratch, reps);
     run("p16 skeleton, no barrier", k_p<1, false, 1, true, false>, 512, img, out, cyc, scratch, reps);
     run("p16 skeleton, no DMA/barrier", k_p<1, false, 1, false, false>, 512, img, out, cyc, scratch, reps);
-    run("p16 skeleton, register staging", k_p<1, false, 1, true, true, true>, 512, img, out, cyc, scratch, reps);
-    run("p32 skeleton, register staging", k_p<2, false, 1, true, true, true>, 256, img, out, cyc, scratch, reps);
+    run("p16 skeleton, register staging", k_p<1, false, 1, true, true, 1>, 512, img, out, cyc, scratch, reps);
+    run("p32 skeleton, register staging", k_p<2, false, 1, true, true, 1>, 256, img, out, cyc, scratch, reps);
+    run("p16 skeleton, staging a slice ahead", k_p<1, false, 1, true, true, 2>, 512, img, out, cyc, scratch, reps);
+    run("p32 skeleton, staging a slice ahead", k_p<2, false, 1, true, true, 2>, 256, img, out, cyc, scratch, reps);
     run("p16 + epilogue", k_p<1, true>, 512, img, out, cyc, scratch, reps);
     run("p16 + epilogue, reads 2 ahead", k_p<1, true, 2>, 512, img, out, cyc, scratch, reps);
     run("p16 + epilogue, no DMA", k_p<1, true, 1, false>, 512, img, out, cyc, scratch, reps);

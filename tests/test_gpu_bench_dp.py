@@ -19,7 +19,7 @@ def test_bench_two_ranks_rehearsal(gpu):
     env = dict(os.environ, NOF_BENCH_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", "29517", os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--rays", "256", "--no-alt"]
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--rays", "256"]
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
@@ -30,6 +30,8 @@ def test_bench_two_ranks_rehearsal(gpu):
     assert r["value"] > 0 and "rehearsal" in r
     c5 = r["config5"]  # configs[4]: 4096 LLFF rays x 256+256 (f16x2) over both ranks, its own all-reduce
     assert c5["n_gpus"] == 2 and c5["value"] > 0 and c5["params_in_sync"] is True
+    # the same batch in the plain fp16 mode, its own all-reduce at every N
+    assert c5["f16"]["value"] > 0 and c5["f16"]["params_in_sync"] is True
 
 
 def test_bench_single_process_mode(gpu):

@@ -55,10 +55,12 @@ __device__ __forceinline__ void epi_tile(const f32x4& v, uint32_t& mw, __amdgpu_
 // through registers instead: 1 = global_load_dwordx4 at groups 0.. and ds_write_b128 at groups 4.. of the
 // same slice; 2 = loads of slice s + 3 at the last groups of slice s, held across the barrier, written at
 // the first groups of slice s + 1 (a whole slice of load latency covered)
-template <int NC, bool kEpi, int AH = 1, bool kDma = true, bool kBar = true, int kReg = 0>
-__global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void k_p(const float* __restrict__ img, int reps, float* out,
+// TT: threads (0 = the shape's default: 512 for NC = 1, 256 for NC = 2; NC = 2 with 512 = two 32-sample
+// waves per SIMD, 256 samples per workgroup: half the DMA instructions per MFMA)
+template <int NC, bool kEpi, int AH = 1, bool kDma = true, bool kBar = true, int kReg = 0, int TT = 0>
+__global__ __launch_bounds__(TT ? TT : (NC == 1 ? 512 : 256), 1) void k_p(const float* __restrict__ img, int reps, float* out,
                                                               long long* cyc, float* scratch) {
-  constexpr int T = NC == 1 ? 512 : 256;
+  constexpr int T = TT ? TT : (NC == 1 ? 512 : 256);
   constexpr int kSteps = kSliceFloats * 4 / (16 * T);  // 16-B chunks per thread per slice
   // padded to 96 KB: one workgroup per CU, as the real kernels (their ring + IPE copy)
   __shared__ __attribute__((aligned(16))) float lds[6 * kSliceFloats];
@@ -144,7 +146,7 @@ __global__ __launch_bounds__(NC == 1 ? 512 : 256, 1) void k_p(const float* __res
 
 template <class K>
 static void run(const char* name, K kern, int threads, const float* img, float* out, long long* cyc, float* scratch,
-                int reps) {
+                int reps, double mfma_cycles = kMfmaCyclesPerSlice) {
   hipEvent_t a, b;
   (void)hipEventCreate(&a);
   (void)hipEventCreate(&b);
@@ -163,7 +165,7 @@ static void run(const char* name, K kern, int threads, const float* img, float* 
   for (long long x : c) mean += (double)x / 256;
   const double per = mean / (kSlices * reps), ns = ms * 1e6 / (kSlices * reps);
   std::printf("%-34s %8.3f ms  %6.0f ticks/slice  %6.1f ns/slice  MFMA-busy(ticks) %.2f\n", name, ms, per, ns,
-              kMfmaCyclesPerSlice / per);
+              mfma_cycles / per);
 }
 
 int main() {
@@ -188,6 +190,8 @@ int main() {
     run("p32 skeleton, register staging", k_p<2, false, 1, true, true, 1>, 256, img, out, cyc, scratch, reps);
     run("p16 skeleton, staging a slice ahead", k_p<1, false, 1, true, true, 2>, 512, img, out, cyc, scratch, reps);
     run("p32 skeleton, staging a slice ahead", k_p<2, false, 1, true, true, 2>, 256, img, out, cyc, scratch, reps);
+    run("p32 x2 waves/SIMD skeleton", k_p<2, false, 1, true, true, 0, 512>, 512, img, out, cyc, scratch, reps, 1024.0);
+    run("p32 x2 waves/SIMD, no DMA", k_p<2, false, 1, false, true, 0, 512>, 512, img, out, cyc, scratch, reps, 1024.0);
     run("p16 + epilogue", k_p<1, true>, 512, img, out, cyc, scratch, reps);
     run("p16 + epilogue, reads 2 ahead", k_p<1, true, 2>, 512, img, out, cyc, scratch, reps);
     run("p16 + epilogue, no DMA", k_p<1, true, 1, false>, 512, img, out, cyc, scratch, reps);

@@ -28,7 +28,7 @@ MIN_CLOCK_MS = 0.3
 src, tag = sys.argv[1], sys.argv[2]
 suffix = sys.argv[3] if len(sys.argv) > 3 else ""  # "_split" / "_f16x2" / "_integrator"
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-dst = os.path.join(root, "profiles")
+dst = os.environ.get("NOF_PROFILES_DIR") or os.path.join(root, "profiles")  # override: tests
 os.makedirs(dst, exist_ok=True)
 shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
 short = lambda n: n.split("(")[0].replace("void ", "").replace("nof::", "")

@@ -17,13 +17,13 @@ pytestmark = pytest.mark.gpu
 # (n, samples): one ray (two 32-sample blocks of a 4-block workgroup), one ray at 512 + 512
 # samples (8 values per lane in the integrator, 16 blocks), 5 rays x 128 + 64 (the fine level
 # smaller than the coarse one: resampling 128 -> 64)
-@pytest.mark.parametrize("precision", [0, 1, 2, 3])
+@pytest.mark.parametrize("precision", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("n,samples", [(1, (64, 64)), (1, (512, 512)), (5, (128, 64))])
 def test_step_parity_edges(gpu, oracle, n, samples, precision):
     step_tests.test_step_parity(gpu, oracle, "blender", n, samples, precision)
 
 
-@pytest.mark.parametrize("precision", [0, 2, 3])
+@pytest.mark.parametrize("precision", [0, 2, 3, 4])
 def test_masked_rays(gpu, oracle, precision):
     """lossmult = 0 rays (BinDataset records may carry any lossmult, MNcs:136-140): they add nothing to
     the loss or the gradient, and the loss normalises by the sum over the rest (D14)."""

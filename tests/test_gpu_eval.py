@@ -18,7 +18,7 @@ def _dev(r, gpu):
     return {k: torch.from_numpy(np.ascontiguousarray(v)).to(gpu) for k, v in r.items()}
 
 
-@pytest.mark.parametrize("precision", [0, 1, 2, 3])
+@pytest.mark.parametrize("precision", [0, 1, 2, 3, 4])
 def test_render_equals_training_forward(gpu, oracle, precision):
     """render_device (inference kernels: no side outputs) == the forward half of the training step,
     bitwise, on the same Philox state; distance / acc match the fp64 restatement."""

@@ -22,7 +22,7 @@ def _step(m, r, gpu):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("precision", [0, 2, 3])
+@pytest.mark.parametrize("precision", [0, 2, 3, 4])
 def test_nonfinite_flags(gpu, precision):
     import nof
     from nof import synth
@@ -41,7 +41,7 @@ def test_nonfinite_flags(gpu, precision):
     assert st & nof._lib.NOF_NUMERIC_FORWARD
     assert m.numeric_status(clear=True) == st  # read again, then cleared
     assert m.numeric_status() == 0
-    if precision in (2, 3):  # the f16 modes' delta scaling
+    if precision in (2, 3, 4):  # the f16 modes' delta scaling
         bad = {k: v.copy() for k, v in r.items()}
         bad["pix"][7, 1] = np.inf  # finite forward, non-finite output gradient
         _step(m, bad, gpu)

@@ -78,7 +78,7 @@ def test_dataset_file_equals_host(gpu, tmp_path):
         nof.RayDataset(tmp_path / "bad.bin")
 
 
-@pytest.mark.parametrize("precision", [0, 1, 2, 3])
+@pytest.mark.parametrize("precision", [0, 1, 2, 3, 4])
 def test_checkpoint_resume_bit_exact(gpu, tmp_path, precision):
     import torch
     import nof
@@ -121,14 +121,14 @@ def test_trainer_prints_fine_loss(gpu, capsys):
 
 
 def test_perf_mode_psnr_matches_f32(gpu):
-    """the f16x2 perf mode trains to within 0.1 dB PSNR of the fp32 mode after a fixed
-    number of steps (same init, same batches; config-2 shaped rays at 64+64 samples)."""
+    """the perf modes (f16x2, plain fp16) train to within 0.1 dB PSNR of the fp32 mode
+    after a fixed number of steps (same init, same batches; config-2 shaped rays at 64+64 samples)."""
     import nof
     from nof.train import Trainer
 
     ds = nof.RayDataset(records=_records(20000, 21))
     psnr = {}
-    for prec in (0, 2):
+    for prec in (0, 2, 4):
         tr = Trainer(ds, batch_size=256, seed=31, print_every=0, num_samples=(64, 64), precision=prec,
                      lr_delay_steps=0)
         losses = []
@@ -142,9 +142,10 @@ def test_perf_mode_psnr_matches_f32(gpu):
     print("psnr", psnr)
     assert psnr[0] > psnr[("first", 0)] + 0.5  # it learns
     assert abs(psnr[2] - psnr[0]) < 0.1
+    assert abs(psnr[4] - psnr[0]) < 0.1
 
 
-@pytest.mark.parametrize("precision,db", [("f32", 0.01), ("f16x2", 0.1), ("f16split", 0.01)])
+@pytest.mark.parametrize("precision,db", [("f32", 0.01), ("f16x2", 0.1), ("f16split", 0.01), ("f16", 0.1)])
 def test_psnr_vs_reference_training(gpu, precision, db):
     """bench.py's "PSNR vs ref" leg at a small size: the HIP path and the oracle's float restatement of
     the reference train on identical batches, then render a held-out batch; the PSNRs agree."""
@@ -156,4 +157,4 @@ def test_psnr_vs_reference_training(gpu, precision, db):
     res = bench.psnr_vs_ref(torch, nof, synth, gpu, precision, n=32, steps=8, samples=(64, 64), n_eval=64)
     print(res)
     assert abs(res["delta_db"]) < db
-    assert res["params_rel_l2"] < (2e-3 if precision == "f16x2" else 1e-4)
+    assert res["params_rel_l2"] < (2e-3 if precision in ("f16x2", "f16") else 1e-4)

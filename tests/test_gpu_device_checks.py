@@ -25,7 +25,7 @@ bits = nof.device_checks(clear=True)
 assert bits == 1 << 31, hex(bits)
 assert nof.device_checks(clear=True) == 0
 ds = nof.RayDataset(records=synth.pack_records(synth.blender_rays(5000, seed=3)), device=0)
-for prec in (0, 1, 2, 3):
+for prec in (0, 1, 2, 3, 4):
     for n, samples in ((96, (64, 128)), (8, (256, 256))):
         m = nof.AcceleratedMipNeRF(seed=5, max_rays=n, num_samples=samples, precision=prec)
         opt = nof.AcceleratedAdamOptimizer(m.GetLayerSizes(), m.config)

@@ -80,3 +80,23 @@ def test_native_driver_matches_python_trainer(gpu, tmp_path):
     torch.cuda.synchronize()
     assert np.array_equal(np.fromfile(tmp_path / "p_res.bin", np.float32),
                           nof.to_numpy(tr.model.mlp.flat_params()[0], (P,)))
+
+
+@pytest.mark.parametrize("name,precision", [("f16x2", 2), ("f16", 4)])
+def test_native_driver_perf_modes_match_python_trainer(gpu, tmp_path, name, precision):
+    """--precision reaches the library the same way from both drivers: the fused steps of the perf
+    modes end bit-identical too."""
+    import torch
+    import nof
+    from nof.train import Trainer
+
+    path = tmp_path / "train_data.bin"
+    _records(2000, 17).tofile(path)
+    _run("--records", path, "--batch", 256, "--seed", 5, "--print-every", 0, "--steps", 3, "--precision", name,
+         "--dump-params", tmp_path / "p.bin")
+    tr = Trainer(nof.RayDataset(path), batch_size=256, seed=5, print_every=0, precision=precision)
+    tr.train(3)
+    torch.cuda.synchronize()
+    p_py = nof.to_numpy(tr.model.mlp.flat_params()[0], (P,))
+    assert np.all(np.isfinite(p_py))
+    assert np.array_equal(np.fromfile(tmp_path / "p.bin", np.float32), p_py)

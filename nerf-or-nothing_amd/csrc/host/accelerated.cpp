@@ -7,6 +7,7 @@
 
 #include "../kernels/common.h"
 #include "../kernels/mlp_common.h"
+#include "../kernels/mlp_h32.h"
 #include "trace.h"
 
 namespace AcceleratedNeRFUtils {
@@ -141,6 +142,10 @@ AcceleratedMLP::AcceleratedMLP(int deg_point, int deg_view, const nof_config& cf
   if (precision_ == NOF_PRECISION_F32_SPLIT) {  // bf16 (hi, mid, lo) slices + the fp32 tails (mlp_common.h)
     wimg_f_.alloc(nof::fwd_image_split_floats<1>() + nof::kFwdTail);
     wimg_b_.alloc(nof::bwd_image_split_floats<1>() + nof::kBwdTail);
+  } else if (precision_ == NOF_PRECISION_F16) {  // fp16 k-step fragment streams + the fp32 tails (mlp_h32.h)
+    wimg_f_.alloc(nof::kFwdH32Floats + nof::kFwdTail);
+    wimg_b_.alloc(nof::kBwdH32Floats + nof::kBwdTail);
+    amax_.alloc(1);
   } else if (f16_pieces()) {  // f16 (hi, lo) slices + the fp32 tails
     wimg_f_.alloc(nof::fwd_image_split_floats<2>() + nof::kFwdTail);
     wimg_b_.alloc(nof::bwd_image_split_floats<2>() + nof::kBwdTail);
@@ -185,7 +190,9 @@ void AcceleratedMLP::pack_weights() {
   nof::PackArgs pa;
   for (int l = 0; l < kLayers; ++l) { pa.woff[l] = woff_[l]; pa.boff[l] = boff_[l]; }
   tb(kTPack);
-  if (precision_ != NOF_PRECISION_F32)
+  if (precision_ == NOF_PRECISION_F16)
+    NOF_HIP(nof::launch_pack_weights_h32(params_.p, pa, wimg_f_.p, wimg_b_.p, st_));
+  else if (precision_ != NOF_PRECISION_F32)
     NOF_HIP(nof::launch_pack_weights_x3(params_.p, pa, wimg_f_.p, wimg_b_.p, f16_pieces() ? 2 : 1, st_));
   else NOF_HIP(nof::launch_pack_weights(params_.p, pa, wimg_f_.p, wimg_b_.p, st_));
   te(kTPack);

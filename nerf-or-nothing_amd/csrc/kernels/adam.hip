@@ -7,6 +7,7 @@
 #include "common.h"
 #include "launch.h"
 #include "mlp_common.h"
+#include "mlp_h32.h"
 
 #pragma clang fp contract(off)
 
@@ -184,6 +185,58 @@ hipError_t launch_pack_weights_x3(const float* params, const PackArgs& pa, float
   const dim3 grid((unsigned)((total + 255) / 256));
   if (precision == 2) hipLaunchKernelGGL(k_pack_weights_x3<2>, grid, dim3(256), 0, st, params, pa, wimg_f, wimg_b);
   else hipLaunchKernelGGL(k_pack_weights_x3<1>, grid, dim3(256), 0, st, params, pa, wimg_f, wimg_b);
+  return hipGetLastError();
+}
+
+// F16-mode (h32) images (mlp_h32.h): the forward / backward k-step fragment streams in fp16 (RNE) plus the
+// fp32 tails.  One thread per 16-B fragment chunk (lane l = (x, h) of fragment g: 8 halves) or tail float.
+// Forward segment (layer l, chunk c, k-step kk): A[row 32c + x][column kfeat(kk, h, j)] = W_l[row][col]
+// (layer 4's k-steps 16..21: its IPE columns 256 + kfeat(kk - 16, h, j)).  Backward segment: A[i][o] =
+// W_l[o][i], i = 32c + x (a feature of h_{l-1}), o = kfeat(kk, h, j) (a feature of delta_l).
+__global__ void k_pack_weights_h32(const float* __restrict__ P, PackArgs pa, float* __restrict__ wf,
+                                   float* __restrict__ wb) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nfc = (int64_t)(kFwdFrags + kStreamPad) * 64, nbc = (int64_t)(kBwdFrags + kStreamPad) * 64;
+  if (gid < nfc + nbc) {
+    const bool fwd = gid < nfc;
+    const int64_t q = fwd ? gid : gid - nfc;
+    const int g = (int)(q >> 6), lane = (int)(q & 63), x = lane & 31, h = lane >> 5;
+    f16x8 out;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = (_Float16)0.0f;
+    if (g < (fwd ? kFwdFrags : kBwdFrags)) {
+      int start = 0, si = 0;
+      H32Seg sg = fwd ? fwd_seg(0) : bwd_seg(0);
+      while (g >= start + sg.nk * sg.nc) {
+        start += sg.nk * sg.nc;
+        ++si;
+        sg = fwd ? fwd_seg(si) : bwd_seg(si);
+      }
+      const int c = (g - start) / sg.nk, kk = (g - start) % sg.nk, l = sg.layer, in = layer_in(l);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float w;
+        if (fwd) {
+          const int col = kk < 16 ? kfeat(kk, h, j) : 256 + kfeat(kk - 16, h, j);
+          w = P[pa.woff[l] + (int64_t)(32 * c + x) * in + col];
+        } else {
+          w = P[pa.woff[l] + (int64_t)kfeat(kk, h, j) * in + 32 * c + x];
+        }
+        out[j] = (_Float16)w;
+      }
+    }
+    *reinterpret_cast<f16x8*>((fwd ? wf : wb) + (size_t)q * 4) = out;
+  } else {
+    const int t = (int)(gid - nfc - nbc);
+    if (t < kFwdTail) wf[kFwdH32Floats + t] = fwd_tail_value(P, pa, t);
+    else if (t < kFwdTail + kBwdTail) wb[kBwdH32Floats + (t - kFwdTail)] = bwd_tail_value(P, pa, t - kFwdTail);
+  }
+}
+hipError_t launch_pack_weights_h32(const float* params, const PackArgs& pa, float* wimg_f, float* wimg_b,
+                                   hipStream_t st) {
+  const int64_t total = (int64_t)(kFwdFrags + kBwdFrags + 2 * kStreamPad) * 64 + kFwdTail + kBwdTail;
+  hipLaunchKernelGGL(k_pack_weights_h32, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, params, pa, wimg_f,
+                     wimg_b);
   return hipGetLastError();
 }
 

@@ -79,6 +79,10 @@ hipError_t launch_delta_amax(const float* dsigma, const float* drgb, int M, uint
 // fp32-precision kernels (v_mfma_f32_16x16x4_f32, two waves per SIMD): mlp_fwd16.hip / mlp_bwd16.hip
 hipError_t launch_mlp_fwd16(const FwdArgs& a, hipStream_t st);
 hipError_t launch_mlp_bwd16(const BwdArgs& a, hipStream_t st);
+// F16 mode (mlp_h32.h, mlp_f16.hip): 32 samples per wave on 32x32x16 f16, row-chunk-outer layers;
+// activations / deltas as row-major [M][F] fp16, wimg / wimg_b the h32 images
+hipError_t launch_mlp_fwd_h32(const FwdArgs& a, hipStream_t st);
+hipError_t launch_mlp_bwd_h32(const BwdArgs& a, hipStream_t st);
 
 // ---- wgrad.hip: weight/bias gradients as one scheduled split-K launch + ordered reduce ------
 struct WgProblem {
@@ -131,6 +135,8 @@ hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v, 
 struct PackArgs { int woff[11]; int boff[11]; };
 hipError_t launch_pack_weights(const float* params, const PackArgs& pa, float* wimg_f, float* wimg_b, hipStream_t st);
 // split images: precision 1 (bf16 hi/mid/lo) or 2 (f16 hi/lo)
+hipError_t launch_pack_weights_h32(const float* params, const PackArgs& pa, float* wimg_f, float* wimg_b,
+                                   hipStream_t st);
 hipError_t launch_pack_weights_x3(const float* params, const PackArgs& pa, float* wimg_f, float* wimg_b,
                                   int precision, hipStream_t st);
 

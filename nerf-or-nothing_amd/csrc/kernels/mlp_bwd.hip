@@ -206,6 +206,7 @@ hipError_t launch_mlp_bwd(const BwdArgs& a, hipStream_t st) {
   if (a.M <= 0) return hipSuccess;
   if (a.M % kBlk != 0) return hipErrorInvalidValue;
   const int nblk = a.M / kBlk;
+  if (a.split == 4) return launch_mlp_bwd_h32(a, st);  // F16 (mlp_f16.hip)
   if (a.split != 1) return launch_mlp_bwd16(a, st);  // fp32 and f16x2: the 16x16 kernels (mlp_bwd16.hip)
   hipLaunchKernelGGL(k_mlp_bwd<1>, dim3((nblk + 3) / 4), dim3(kMlpThreads), 0, st, a);
   return hipGetLastError();

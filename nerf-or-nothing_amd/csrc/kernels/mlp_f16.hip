@@ -1,0 +1,504 @@
+// F16 mode (NOF_PRECISION_F16, BASELINE configs[4]'s "fp16 activations on MFMA"): the fused forward
+// (conical frustum + IPE + 8x256 MLP + heads) and the fused dX-chain backward on
+// v_mfma_f32_32x32x16_f16, 32 samples per wave, row-chunk-outer layers (mlp_h32.h).
+//
+// Replaces, for this mode, cast_rays (AF:292-317), encode_input_data (AF:187-221), the 11 per-layer
+// launches of AcceleratedMLP::get_output (MLPcpp:214-255: get_neuron_output*, AF:36-90) and of
+// AcceleratedMLP::get_gradient's dX part (MLPcpp:256-321: backpropagate_neuron*, AF:91-182).
+// Semantics per MLP.CallCached (MLPcs:112-136), the C# heads (MNcs:307-309, D23) and their
+// derivatives (MNcs:410-415, D28); gradient routing per D11 (dh7 = W8^T dz_s + W9[:, :256]^T delta9,
+// dh3 = W4[:, :256]^T delta4).  Numerics: every product is one fp16 x fp16 MFMA term accumulated in
+// fp32 (weights and activations rounded to fp16, deltas power-of-two scaled then rounded), the IPE
+// from a double-float range reduction and the hardware sin / exp2 (the encodings are rounded to fp16
+// before any product, so their ~1e-7 error is below that rounding).
+#include "common.h"
+#include "geometry.h"
+#include "launch.h"
+#include "mlp_h32.h"
+
+namespace nof {
+
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t h32_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void store_b64(__amdgpu_buffer_rsrc_t r, uint32_t voff, int imm, uint32_t lo, uint32_t hi) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  __builtin_amdgcn_raw_buffer_store_b64((u32x2{lo, hi}), r, (int)voff, imm, 0);
+}
+__device__ __forceinline__ void store_b128(__amdgpu_buffer_rsrc_t r, uint32_t voff, int imm, const u32x4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, imm, 0);
+}
+__device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
+  return __builtin_amdgcn_fdot2(__builtin_bit_cast(h16x2, a), __builtin_bit_cast(h16x2, b), c, false);
+}
+
+// ---- IPE of the F16 mode -----------------------------------------------------------------------------
+// sin(arg) = v_sin_f32(frac(arg / 2pi)) with arg / 2pi in double-float (exact product residual by FMA),
+// so the reduction error stays ~2^-24 revolutions at the top frequency (|arg| ~ 2^15 |mu|).
+__device__ __forceinline__ float sin_rev(float arg) {
+#pragma clang fp contract(off)
+  const float c_hi = 0.159154937f;    // fl(1 / 2pi)
+  const float c_lo = 6.42063824e-09f;  // 1 / 2pi - c_hi
+  const float n = __builtin_rintf(arg * c_hi);
+  // exact(arg c_hi) - n rounded once (|.| <= 1/2), then + arg c_lo
+  const float fr = __builtin_fmaf(arg, c_lo, __builtin_fmaf(arg, c_hi, -n));
+  return __builtin_amdgcn_sinf(fr);
+}
+// IPE feature 48h + c (c compile-time): frequency f = 8h + c / 6, axis / sin-or-cos from c % 6 — the
+// ordering of ipe_feature (geometry.h, MH:429-449), with mu_h = mu 2^(8h), nv_h = -0.5 log2(e) var 4^(8h)
+__device__ __forceinline__ float ipe_h32(int c, const float (&mu_h)[3], const float (&nv_h)[3]) {
+#pragma clang fp contract(off)
+  const int f = c / 6, rem = c % 6, ax = rem >= 3 ? rem - 3 : rem;
+  const float scale = (float)(1 << f);
+  const float y = mu_h[ax] * scale;                       // exact (power of two)
+  const float arg = rem >= 3 ? y + kHalfPi : y;           // the reference's fl(y + pi/2)
+  const float damp = __builtin_amdgcn_exp2f(nv_h[ax] * (scale * scale));
+  return damp * sin_rev(arg);
+}
+
+// ---- forward epilogues ----------------------------------------------------------------------------------
+// trunk: tile T of acc -> packed fp16 ReLU into dst (the next layer's B fragments), mask bits, the act
+// block stores; the density head's dot product (layer 7: z_s = w8 . h7, fp16 operands, fp32 sum)
+template <bool kStore>
+struct FwdEpiH {
+  static constexpr int kNC = 8;
+  const f32x16 (&acc)[2];
+  uint32_t (&dst)[16][4];
+  uint32_t (&mw)[4];  // mask words (a kernel-local array: a member array is left in scratch memory)
+  __amdgpu_buffer_rsrc_t blk, mrs;
+  uint32_t voff, moff;
+  int mimm;
+  const uint32_t* w8;  // LDS, packed w8 pairs of this lane half: [T][2][8] + 8h
+  float zs;
+  bool dens;
+  __device__ __forceinline__ FwdEpiH(const f32x16 (&a)[2], uint32_t (&d)[16][4], uint32_t (&mw_)[4], uint32_t voff_,
+                                     uint32_t moff_)
+      : acc(a), dst(d), mw(mw_), voff(voff_), moff(moff_) {}
+  __device__ __forceinline__ void begin(const void* blk_, const void* masks_blk, int slot, const uint32_t* w8_,
+                                        bool dens_) {
+    blk = h32_rsrc(blk_);
+    mrs = h32_rsrc(masks_blk);
+    mimm = slot * 1024;
+    mw[0] = mw[1] = mw[2] = mw[3] = 0u;
+    w8 = w8_;
+    zs = 0.0f;
+    dens = dens_;
+  }
+  __device__ __forceinline__ int piece(int T, int kk, int NK) {
+    int n = 0;
+#pragma unroll
+    for (int d = 0; d < 8; ++d)
+      if (kk == epi_valu_pos(d, NK)) {
+        const uint32_t p = relu_pk(pk_h(acc[T & 1][2 * d], acc[T & 1][2 * d + 1]));
+        mw[T >> 1] = mask_shift(mw[T >> 1], p);
+        dst[2 * T + (d >> 2)][d & 3] = p;
+        if (dens) zs = dot2(p, w8[T * 16 + d], zs);
+      }
+    if constexpr (kStore) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (kk == epi_store_pos(q, NK)) {
+          store_b64(blk, voff, 64 * T + 16 * q, dst[2 * T + (q >> 1)][2 * (q & 1)], dst[2 * T + (q >> 1)][2 * (q & 1) + 1]);
+          ++n;
+        }
+      if (T == kNC - 1 && kk == epi_store_pos(3, NK)) {
+        store_b128(mrs, moff, mimm, u32x4{mw[0], mw[1], mw[2], mw[3]});
+        ++n;
+      }
+    }
+    return n;
+  }
+};
+
+// view layer 9: tile T -> ReLU fp16, mask bits, act_h9 stores, and the RGB head's three dot products
+template <bool kStore>
+struct ViewEpiH {
+  static constexpr int kNC = 4;
+  const f32x16 (&acc)[2];
+  uint32_t (&mw)[4];
+  uint32_t (&p8)[8];
+  __amdgpu_buffer_rsrc_t blk, mrs;
+  uint32_t voff, moff;
+  const uint32_t* w10;  // LDS, packed W10 pairs: [3][T][2][8] + 8h
+  float zc[3];
+  __device__ __forceinline__ ViewEpiH(const f32x16 (&a)[2], uint32_t (&mw_)[4], uint32_t (&p8_)[8], uint32_t voff_,
+                                      uint32_t moff_, const void* blk_, const void* masks_blk, const uint32_t* w10_)
+      : acc(a), mw(mw_), p8(p8_), voff(voff_), moff(moff_), w10(w10_) {
+    blk = h32_rsrc(blk_);
+    mrs = h32_rsrc(masks_blk);
+    mw[0] = mw[1] = mw[2] = mw[3] = 0u;
+    zc[0] = zc[1] = zc[2] = 0.0f;
+  }
+  __device__ __forceinline__ int piece(int T, int kk, int NK) {
+    int n = 0;
+#pragma unroll
+    for (int d = 0; d < 8; ++d)
+      if (kk == epi_valu_pos(d, NK)) {
+        const uint32_t p = relu_pk(pk_h(acc[T & 1][2 * d], acc[T & 1][2 * d + 1]));
+        mw[T >> 1] = mask_shift(mw[T >> 1], p);
+        p8[d] = p;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) zc[c] = dot2(p, w10[(c * 4 + T) * 16 + d], zc[c]);
+      }
+    if constexpr (kStore) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (kk == epi_store_pos(q, NK)) {
+          store_b64(blk, voff, 64 * T + 16 * q, p8[2 * q], p8[2 * q + 1]);
+          ++n;
+        }
+      if (T == kNC - 1 && kk == epi_store_pos(3, NK)) {
+        store_b128(mrs, moff, 8 * 1024, u32x4{mw[0], mw[1], mw[2], mw[3]});
+        ++n;
+      }
+    }
+    return n;
+  }
+};
+
+template <bool kStore>
+__global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
+  constexpr int kBias = kH32RingFloats;           // fp32 trunk biases [8][256]
+  constexpr int kDirb = kBias + 8 * 256;          // per-wave view-direction bias [8][128]
+  constexpr int kW8 = kDirb + kH32Waves * 128;    // packed w8 [8][2][8]
+  constexpr int kW10 = kW8 + 128;                 // packed W10 [3][4][2][8]
+  __shared__ __attribute__((aligned(16))) float lds[kW10 + 192];
+  const int tid = threadIdx.x, lane = tid & 63, x = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nblk = a.M / kBlk;
+  const int blk_raw = blockIdx.x * kH32Waves + wave;
+  const int blk = blk_raw < nblk ? blk_raw : nblk - 1;  // tail waves duplicate the last block
+  const int m0 = blk * kBlk, ray = m0 / a.S;
+  const int m = m0 + x;
+  NOF_DCHECK(a.M % kBlk == 0 && a.S % kBlk == 0 && blk >= 0 && blk < nblk, kChkMlpBlock);
+  const float* tail = a.wimg + kFwdH32Floats;
+
+  H32Ring ring;
+  ring.lds = lds;
+  ring.prologue(a.wimg, tid);  // periods 0 and 1 in flight while the encodings are computed
+
+  // ---- encodings: lane h computes canonical IPE features 48h .. 48h + 47 of its sample -----------
+  // packed pairs: ix[kk][e] = features c = kfeat(kk, 0, 2e) + {0, 1} (the B-fragment half h' = 0),
+  // iy[kk][e] the half h' = 1, for k-steps 3h + kk
+  uint32_t ix[3][4], iy[3][4];
+  float d3[3];
+  d3[0] = a.dirs[3 * ray]; d3[1] = a.dirs[3 * ray + 1]; d3[2] = a.dirs[3 * ray + 2];
+  if (!a.encoded) {
+    const float o3[3] = {a.origins[3 * ray], a.origins[3 * ray + 1], a.origins[3 * ray + 2]};
+    const float* tr = a.t + (size_t)ray * (a.S + 1) + (m0 - ray * a.S) + x;
+    float mean[3], cov[3];
+    frustum_gaussian(tr[0], tr[1], o3, d3, a.radii[ray], mean, cov);
+    float mu_h[3], nv_h[3];
+    const float sh = h ? 256.0f : 1.0f;  // 2^(8h)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      mu_h[k] = mean[k] * sh;
+      nv_h[k] = (-0.5f * 1.44269504f) * (cov[k] * sh * sh);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 3; ++kk)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c0 = kfeat(kk, 0, 2 * e), c1 = kfeat(kk, 1, 2 * e);
+        ix[kk][e] = pk_h(ipe_h32(c0, mu_h, nv_h), ipe_h32(c0 + 1, mu_h, nv_h));
+        iy[kk][e] = pk_h(ipe_h32(c1, mu_h, nv_h), ipe_h32(c1 + 1, mu_h, nv_h));
+      }
+  } else {
+    const float* ep = a.enc_pos + (size_t)m * kPosIn + 48 * h;
+#pragma unroll
+    for (int kk = 0; kk < 3; ++kk)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c0 = kfeat(kk, 0, 2 * e), c1 = kfeat(kk, 1, 2 * e);
+        ix[kk][e] = pk_h(ep[c0], ep[c0 + 1]);
+        iy[kk][e] = pk_h(ep[c1], ep[c1 + 1]);
+      }
+  }
+  // view PE of the wave's ray: lane k < 27 evaluates feature k, every lane reads them back as scalars
+  const int kl = lane < kDirIn ? lane : 0;
+  const float pe_l = a.encoded ? a.enc_dir[(size_t)ray * kDirIn + kl] : dir_feature(kl, d3);
+  float pe[kDirIn];
+#pragma unroll
+  for (int k = 0; k < kDirIn; ++k) pe[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pe_l), k));
+
+  const uint32_t voff256 = (uint32_t)x * 512u + 8u * h;  // [M][256] rows: sample x, lane half h
+  const uint32_t voff128 = (uint32_t)x * 256u + 8u * h;  // [M][128] rows
+  const uint32_t moff = (uint32_t)lane * 16u;
+  const void* masks_blk = a.masks + (size_t)blk * kMaskSlots * 256;
+  if constexpr (kStore) {  // act_in row: IPE 0..95 (this lane: 48h ..), view PE 96..122, zeros 123..127
+    const __amdgpu_buffer_rsrc_t r = h32_rsrc(reinterpret_cast<const _Float16*>(a.act_in) + (size_t)m0 * kInF);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int kk = k >> 1, q = k & 1;
+      store_b128(r, (uint32_t)x * 256u + 96u * h, 16 * k,
+                 u32x4{ix[kk][2 * q], ix[kk][2 * q + 1], iy[kk][2 * q], iy[kk][2 * q + 1]});
+    }
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float v[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int k0 = 2 * i + u, k1 = 16 + 2 * i + u;  // feature 96 + 16h + 2i + u
+        v[u] = h ? (k1 < kDirIn ? pe[k1 < kDirIn ? k1 : 0] : 0.0f) : pe[k0];
+      }
+      w[i] = pk_h(v[0], v[1]);
+    }
+    store_b128(r, (uint32_t)x * 256u + 32u * h, 192, u32x4{w[0], w[1], w[2], w[3]});
+    store_b128(r, (uint32_t)x * 256u + 32u * h, 208, u32x4{w[4], w[5], w[6], w[7]});
+  }
+  // the B fragments of layers 0 / 4: k-steps 0..2 from the lane half h = 0, 3..5 from h = 1 — one
+  // permlane32 swap per packed dword moves each half's other-h' pairs across (tools/probe/h32_probe.hip)
+  uint32_t ipe[6][4];
+#pragma unroll
+  for (int kk = 0; kk < 3; ++kk)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {  // v_permlane32_swap: vdst lanes 32..63 <-> src0 lanes 0..31 (measured)
+      const auto r = __builtin_amdgcn_permlane32_swap(ix[kk][e], iy[kk][e], false, false);
+      ipe[kk][e] = r[0];      // h = 0: its own ix; h = 1: the h = 0 lane's iy
+      ipe[kk + 3][e] = r[1];  // h = 0: the h = 1 lane's ix; h = 1: its own iy
+    }
+
+  // ---- LDS tables: trunk biases, the wave's view-direction bias, packed w8 / W10 -------------------
+  for (int i = tid; i < 2048 / 4; i += kH32Threads)
+    *reinterpret_cast<f32x4*>(lds + kBias + 4 * i) = *reinterpret_cast<const f32x4*>(tail + kFwdTailBias + 4 * i);
+  {
+    float* dirb = lds + kDirb + wave * 128;
+#pragma unroll
+    for (int rep = 0; rep < 2; ++rep) {  // b9 + W9[:, 256:283] . PE(d)
+      const int o = lane + 64 * rep;
+      float s = tail[kFwdTailBias + 9 * 256 + o];
+      const float* w9 = tail + kFwdTailW9d + o * 32;
+#pragma unroll
+      for (int k = 0; k < kDirIn; ++k) s = __builtin_fmaf(w9[k], pe[k], s);
+      dirb[o] = s;
+    }
+  }
+  if (tid < 128 + 192) {  // packed pairs of features 32T + 8(d >> 1) + 4hh + 2(d & 1) + {0, 1}
+    const bool is8 = tid < 128;  // w8 [T][hh][d] | W10 [c][T][hh][d]
+    const int i = is8 ? tid : tid - 128;
+    const int d = i & 7, hh = (i >> 3) & 1, T = (i >> 4) & (is8 ? 7 : 3), c = is8 ? 0 : i >> 6;
+    const int f = 32 * T + 8 * (d >> 1) + 4 * hh + 2 * (d & 1);
+    const float* src = is8 ? tail + kFwdTailW8 : tail + kFwdTailW10 + c * 128;
+    reinterpret_cast<uint32_t*>(lds + (is8 ? kW8 : kW10))[i] = pk_h(src[f], src[f + 1]);
+  }
+  __syncthreads();  // tables written, periods 0 and 1 landed
+
+  // ---- layers -------------------------------------------------------------------------------------
+  f32x16 acc[2];
+  uint32_t X[16][4], Y[16][4];
+  const size_t lstride = (size_t)nblk * kBlk * kWidth;  // halves per act_h layer
+  const _Float16* act_h = reinterpret_cast<const _Float16*>(a.act_h) + (size_t)m0 * kWidth;
+  const float* bias_h = lds + kBias + 4 * h;
+  const uint32_t* w8h = reinterpret_cast<const uint32_t*>(lds + kW8) + 8 * h;
+  uint32_t mwX[4], mwY[4], mwV[4], p8[8];
+  FwdEpiH<kStore> eX(acc, X, mwX, voff256, moff), eY(acc, Y, mwY, voff256, moff);
+  NoEpiH none;
+  auto srcI = [&](int kk, uint32_t (&b)[4]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) b[e] = ipe[kk][e];
+  };
+  auto srcX = [&](int kk, uint32_t (&b)[4]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) b[e] = X[kk][e];
+  };
+  auto srcY = [&](int kk, uint32_t (&b)[4]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) b[e] = Y[kk][e];
+  };
+  auto srcYI = [&](int kk, uint32_t (&b)[4]) {  // layer 4: [h3, IPE]
+#pragma unroll
+    for (int e = 0; e < 4; ++e) b[e] = kk < 16 ? Y[kk < 16 ? kk : 0][e] : ipe[kk >= 16 ? kk - 16 : 0][e];
+  };
+  eX.begin(act_h, masks_blk, 0, w8h, false);
+  h32_layer<6, 8, true>(srcI, acc, ring, eX, none, bias_h, tid, lane);
+  for (int it = 0; it < 2; ++it) {  // layers 1..3, (4), 5..7
+    const int la = 1 + 4 * it;
+    eY.begin(act_h + la * lstride, masks_blk, la, w8h, false);
+    h32_layer<16, 8, true>(srcX, acc, ring, eY, eX, bias_h + la * 256, tid, lane);
+    eX.begin(act_h + (la + 1) * lstride, masks_blk, la + 1, w8h, false);
+    h32_layer<16, 8, true>(srcY, acc, ring, eX, eY, bias_h + (la + 1) * 256, tid, lane);
+    eY.begin(act_h + (la + 2) * lstride, masks_blk, la + 2, w8h, la + 2 == kDepth - 1);  // + density (layer 8)
+    h32_layer<16, 8, true>(srcX, acc, ring, eY, eX, bias_h + (la + 2) * 256, tid, lane);
+    if (it == 0) {
+      eX.begin(act_h + kSkip * lstride, masks_blk, kSkip, w8h, false);
+      h32_layer<22, 8, true>(srcYI, acc, ring, eX, eY, bias_h + kSkip * 256, tid, lane);
+    }
+  }
+  static_assert(kDepth == 8 && kSkip == 4, "the trunk schedule assumes 8 layers, skip into layer 4");
+  // ---- view layer 9: relu(W9[:, :256] h7 + dirbias), the RGB head (layer 10) in its epilogue ----------
+  ViewEpiH<kStore> eV(acc, mwV, p8, voff128, moff, reinterpret_cast<const _Float16*>(a.act_h9) + (size_t)m0 * kWidthCond,
+                      masks_blk, reinterpret_cast<const uint32_t*>(lds + kW10) + 8 * h);
+  h32_layer<16, 4, true>(srcY, acc, ring, eV, eY, lds + kDirb + wave * 128 + 4 * h, tid, lane);
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) eV.piece(3, kk, 16);  // the last view tile: nothing left to hide it under
+
+  // ---- heads: sigma = softplus(z_s - 1), rgb = sigmoid(z_c) 1.002 - 0.001 (MNcs:307-309) -------------
+  float zs = eY.zs;
+  zs += __shfl_xor(zs, 32, 64);
+  zs += tail[kFwdTailBias + 8 * 256];
+  float zc[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) zc[c] = eV.zc[c] + __shfl_xor(eV.zc[c], 32, 64) + tail[kFwdTailBias + 10 * 256 + c];
+  if (h == 0) {
+    a.sigma[m] = softplus_f(zs + kDensityBias);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) a.rgb[(size_t)m * 3 + c] = sigmoid_f(zc[c]) * kRgbScale - kRgbPadding;
+    if constexpr (kStore) reinterpret_cast<f32x4*>(a.zhead)[m] = f32x4{zs, zc[0], zc[1], zc[2]};
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's trailing DMAs land before the LDS is released
+}
+
+// ---- backward ---------------------------------------------------------------------------------------
+// delta = mask ? acc (+ w8 dz_s at layer 7) : 0, as packed fp16 (the deltas carry the level's power-of-
+// two scale), into dst (the next layer's B fragments) and the delta block
+struct BwdEpiH {
+  static constexpr int kNC = 8;
+  const f32x16 (&acc)[2];
+  uint32_t (&dst)[16][4];
+  __amdgpu_buffer_rsrc_t blk;
+  uint32_t voff;
+  uint4 mk;
+  const float* w8;  // LDS fp32 [T][2][16] + 16h, or null
+  float dzs;
+  __device__ __forceinline__ BwdEpiH(const f32x16 (&a)[2], uint32_t (&d)[16][4], uint32_t voff_)
+      : acc(a), dst(d), voff(voff_) {}
+  __device__ __forceinline__ void begin(const void* blk_, const uint32_t* mask, const float* w8_, float dzs_) {
+    blk = h32_rsrc(blk_);
+    mk = *reinterpret_cast<const uint4*>(mask);
+    w8 = w8_;
+    dzs = dzs_;
+  }
+  __device__ __forceinline__ int piece(int T, int kk, int NK) {
+    int n = 0;
+#pragma unroll
+    for (int d = 0; d < 8; ++d)
+      if (kk == epi_valu_pos(d, NK)) {
+        float v0 = acc[T & 1][2 * d], v1 = acc[T & 1][2 * d + 1];
+        if (w8) {
+          const float2 w = *reinterpret_cast<const float2*>(w8 + T * 32 + 2 * d);
+          v0 = __builtin_fmaf(w.x, dzs, v0);
+          v1 = __builtin_fmaf(w.y, dzs, v1);
+        }
+        const uint32_t word = (T >> 1) == 0 ? mk.x : ((T >> 1) == 1 ? mk.y : ((T >> 1) == 2 ? mk.z : mk.w));
+        dst[2 * T + (d >> 2)][d & 3] = pk_h(v0, v1) & mask_expand(word, 8 * (T & 1) + d);
+      }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (kk == epi_store_pos(q, NK)) {
+        store_b64(blk, voff, 64 * T + 16 * q, dst[2 * T + (q >> 1)][2 * (q & 1)], dst[2 * T + (q >> 1)][2 * (q & 1) + 1]);
+        ++n;
+      }
+    return n;
+  }
+};
+
+__global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
+  constexpr int kW8 = kH32RingFloats;  // fp32 w8 in D-register order [8][2][16]
+  __shared__ __attribute__((aligned(16))) float lds[kW8 + 256];
+  const int tid = threadIdx.x, lane = tid & 63, x = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nblk = a.M / kBlk;
+  const int blk_raw = blockIdx.x * kH32Waves + wave;
+  const int blk = blk_raw < nblk ? blk_raw : nblk - 1;
+  const int m0 = blk * kBlk, m = m0 + x;
+  NOF_DCHECK(a.M % kBlk == 0 && blk >= 0 && blk < nblk, kChkMlpBlock);
+  const float* tail = a.wimg_b + kBwdH32Floats;
+  const uint32_t* masks_blk = a.masks + (size_t)blk * kMaskSlots * 256 + lane * 4;
+
+  H32Ring ring;
+  ring.lds = lds;
+  ring.prologue(a.wimg_b, tid);
+  if (tid < 256) {
+    const int T = tid >> 5, hh = (tid >> 4) & 1, r = tid & 15;
+    lds[kW8 + tid] = tail[kBwdTailW8 + 32 * T + 8 * (r >> 2) + 4 * hh + (r & 3)];
+  }
+
+  // ---- heads (MNcs:410-415), scaled by the level's power of two ---------------------------------------
+  const f32x4 zh = reinterpret_cast<const f32x4*>(a.zhead)[m];
+  const float sc = delta_scale(a.amax, false);
+  const float dzs = a.dsigma[m] * sigmoid_f(zh[0] + kDensityBias) * sc;
+  float dzc[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float s = sigmoid_f(zh[1 + c]);
+    dzc[c] = a.drgb[(size_t)m * 3 + c] * (s * (1.0f - s)) * kRgbScale * sc;
+  }
+  // ---- delta9 = (W10^T dz_rgb) * relu'(layer 9) -> the B fragments of dh7, and delta9x ------------------
+  uint32_t X[16][4], Y[16][4];
+  const uint32_t voff160 = (uint32_t)x * 320u + 8u * h, voff256 = (uint32_t)x * 512u + 8u * h;
+  const __amdgpu_buffer_rsrc_t d9 = h32_rsrc(reinterpret_cast<const _Float16*>(a.delta9x) + (size_t)m0 * kD9F);
+  {
+    const uint4 mk9 = *reinterpret_cast<const uint4*>(masks_blk + 8 * 256);
+    const float* w10 = tail + kBwdTailW10;
+#pragma unroll
+    for (int T = 0; T < 4; ++T) {
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int f = 32 * T + 8 * q + 4 * h;
+        const f32x4 wa = *reinterpret_cast<const f32x4*>(w10 + f);
+        const f32x4 wb = *reinterpret_cast<const f32x4*>(w10 + 128 + f);
+        const f32x4 wc = *reinterpret_cast<const f32x4*>(w10 + 256 + f);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)  // explicit FMAs: the same rounding as every other precision mode
+          v[4 * q + e] = __builtin_fmaf(wc[e], dzc[2], __builtin_fmaf(wb[e], dzc[1], wa[e] * dzc[0]));
+      }
+      const uint32_t word = (T >> 1) == 0 ? mk9.x : mk9.y;
+#pragma unroll
+      for (int d = 0; d < 8; ++d) X[2 * T + (d >> 2)][d & 3] = pk_h(v[2 * d], v[2 * d + 1]) & mask_expand(word, 8 * (T & 1) + d);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        store_b64(d9, voff160, 64 * T + 16 * q, X[2 * T + (q >> 1)][2 * (q & 1)], X[2 * T + (q >> 1)][2 * (q & 1) + 1]);
+    }
+    if (h == 0) store_b64(d9, (uint32_t)x * 320u, 256, pk_h(dzs, dzc[0]), pk_h(dzc[1], dzc[2]));  // features 128..131
+  }
+  __syncthreads();  // w8 table written, periods 0 and 1 landed
+
+  f32x16 acc[2];
+  const size_t lstride = (size_t)nblk * kBlk * kWidth;
+  const _Float16* delta = reinterpret_cast<const _Float16*>(a.delta) + (size_t)m0 * kWidth;
+  BwdEpiH eX(acc, X, voff256), eY(acc, Y, voff256);
+  NoEpiH none;
+  auto srcX = [&](int kk, uint32_t (&b)[4]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) b[e] = X[kk][e];
+  };
+  auto srcY = [&](int kk, uint32_t (&b)[4]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) b[e] = Y[kk][e];
+  };
+  // dh7 = W9[:, :256]^T delta9 + w8 dz_s ; delta7
+  eY.begin(delta + 7 * lstride, masks_blk + 7 * 256, lds + kW8 + 16 * h, dzs);
+  h32_layer<8, 8, false>(srcX, acc, ring, eY, none, nullptr, tid, lane);
+  // dh_{l-1} = W_l[:, :256]^T delta_l ; delta_{l-1}, l = 7..2 in pairs, then l = 1
+  for (int it = 0; it < 3; ++it) {
+    const int l = kDepth - 1 - 2 * it;
+    eX.begin(delta + (l - 1) * lstride, masks_blk + (l - 1) * 256, nullptr, 0.0f);
+    h32_layer<16, 8, false>(srcY, acc, ring, eX, eY, nullptr, tid, lane);
+    eY.begin(delta + (l - 2) * lstride, masks_blk + (l - 2) * 256, nullptr, 0.0f);
+    h32_layer<16, 8, false>(srcX, acc, ring, eY, eX, nullptr, tid, lane);
+  }
+  eX.begin(delta, masks_blk, nullptr, 0.0f);
+  h32_layer<16, 8, false>(srcY, acc, ring, eX, eY, nullptr, tid, lane);
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) eX.piece(7, kk, 16);  // delta0's last tile
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+hipError_t launch_mlp_fwd_h32(const FwdArgs& a, hipStream_t st) {
+  const int nblk = a.M / kBlk;
+  const dim3 grid((nblk + kH32Waves - 1) / kH32Waves), block(kH32Threads);
+  if (a.no_store) hipLaunchKernelGGL(k_mlp_fwd_h32<false>, grid, block, 0, st, a);
+  else hipLaunchKernelGGL(k_mlp_fwd_h32<true>, grid, block, 0, st, a);
+  return hipGetLastError();
+}
+hipError_t launch_mlp_bwd_h32(const BwdArgs& a, hipStream_t st) {
+  const int nblk = a.M / kBlk;
+  hipLaunchKernelGGL(k_mlp_bwd_h32, dim3((nblk + kH32Waves - 1) / kH32Waves), dim3(kH32Threads), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace nof

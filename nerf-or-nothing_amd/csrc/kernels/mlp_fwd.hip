@@ -284,6 +284,7 @@ hipError_t launch_mlp_fwd(const FwdArgs& a, hipStream_t st) {
   if (a.M % kBlk != 0 || a.S % kBlk != 0) return hipErrorInvalidValue;
   const int nblk = a.M / kBlk;
   const dim3 grid((nblk + 3) / 4), block(kMlpThreads);
+  if (a.split == 4) return launch_mlp_fwd_h32(a, st);  // F16: 32-sample waves, row-chunk layers (mlp_f16.hip)
   if (a.split != 1) return launch_mlp_fwd16(a, st);  // fp32 and f16x2: the 16x16 kernels (mlp_fwd16.hip)
   if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd<1, false>), grid, block, 0, st, a);
   else hipLaunchKernelGGL((k_mlp_fwd<1, true>), grid, block, 0, st, a);

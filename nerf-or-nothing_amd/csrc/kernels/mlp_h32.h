@@ -1,0 +1,215 @@
+// F16 mode (NOF_PRECISION_F16) fused MLP on v_mfma_f32_32x32x16_f16: 32 samples per wave, two
+// waves per SIMD, 256 samples per workgroup — shared machinery of k_mlp_fwd_h32 / k_mlp_bwd_h32.
+//
+// Why a separate structure from the 16x16 kernels (mlp16.h): with one fp16 product per term the
+// 16-sample waves of mlp16.h read a 16-KB weight slice from LDS for every 16 samples, so the LDS
+// array (256 B/clk/CU) is as busy as the MFMA pipes and the per-slice DMA / barrier costs are paid
+// per 16 samples (round 2: 0.23 of the fp16 peak, MFMA busy 0.28).  Here:
+//   * a wave owns one 32-sample block and each A fragment (1 KB per wave) feeds a 32x32x16 MFMA
+//     of 32 samples: half the LDS read bytes per FLOP;
+//   * a layer is computed ROW-CHUNK by row-chunk (32 output features = one 32x32 accumulator
+//     tile, 16 registers) over the whole K: the layer's input stays resident as fp16 B fragments
+//     (256 features x 32 samples = 64 VGPRs), the output chunk is double-buffered (2 x 16
+//     registers), and the epilogue of chunk c - 1 (fp16 convert, packed ReLU, mask bits, side
+//     stores) runs inside chunk c's MFMA stream; the next layer's input is built in a second
+//     64-VGPR set.  About 200 VGPRs: two waves per SIMD.
+//   * the last chunk's epilogue of layer l runs inside layer l + 1's first chunk, before k-steps
+//     14/15 that read it, so no epilogue is exposed between layers.
+//
+// Register maps (gfx950 32x32x16 f16, verified by tools/probe/mfma_probe.hip): lane l = (x = l & 31,
+// h = l >> 5) supplies A[row x][k = 8h + j] and B[k = 8h + j][col x], j = 0..7; D register r of lane l
+// is D[row 8 (r >> 2) + 4h + (r & 3)][col x].  Output chunk T of a layer therefore leaves feature
+// 32T + 8 (r >> 2) + 4h + (r & 3) of sample x in register r; registers 8s .. 8s + 7 (s = 0, 1) converted
+// pairwise to fp16 are exactly the B fragment of k-step 2T + s of the next layer when that k-step's
+// element j is taken to be feature kfeat(kk, h, j) = 16 kk + 8 (j >> 2) + 4h + (j & 3) — and the packed
+// weight fragments (k_pack_weights_h32) follow that order.
+//
+// Weights stream through a 4-slot LDS ring of 16-KB periods (16 one-KB k-step fragments) by
+// LDS-DMA; every layer is a whole number of periods, so the DMA / barrier schedule is the same in
+// every layer: period P + 2 is fetched at positions 0 and 1 of period P (into the slot period P - 2
+// left), and the barrier ending period P waits for period P + 1 with a counted vmcnt that lets the
+// period's own DMA and side-output stores stay in flight.
+//
+// Side outputs (sample-major, the transpose the weight-gradient launch reads with
+// ds_read_b64_tr_b16): activation / delta buffers are plain row-major [M][F] fp16 matrices, a lane
+// storing 4 consecutive features (8 B) per store.  ReLU masks: per 32-sample block and layer slot
+// 1 KB = [64 lanes][4 words]; word u holds tiles 2u, 2u + 1 as two 16-bit shift registers (low half:
+// even registers, high half: odd registers) — packed dword k = 8 (T & 1) + d of tile T (registers 2d,
+// 2d + 1) at bit 15 - k of each half.
+#pragma once
+#include "mlp16.h"
+
+namespace nof {
+
+constexpr int kH32Threads = 512;  // 8 waves
+constexpr int kH32Waves = 8;      // one 32-sample block per wave
+constexpr int kFragFloats = 256;  // one k-step fragment image: 64 lanes x 8 halves (1 KB)
+constexpr int kPeriod = 16;       // fragments per ring slot
+constexpr int kPeriodFloats = kPeriod * kFragFloats;
+constexpr int kH32Slots = 4;
+constexpr int kH32RingFloats = kH32Slots * kPeriodFloats;  // 64 KB
+
+// weight streams: segments (layer, k-steps per chunk, chunks) in consumption order
+struct H32Seg {
+  int layer, nk, nc;
+};
+constexpr int kFwdSegs = 9, kBwdSegs = 8;
+__host__ __device__ constexpr H32Seg fwd_seg(int i) {
+  return i == 0 ? H32Seg{0, 6, 8} : (i == 4 ? H32Seg{4, 22, 8} : (i == 8 ? H32Seg{9, 16, 4} : H32Seg{i, 16, 8}));
+}
+__host__ __device__ constexpr H32Seg bwd_seg(int i) {  // L9 (dh7 <- delta9), then L7 .. L1 (dh_{l-1} <- delta_l)
+  return i == 0 ? H32Seg{9, 8, 8} : H32Seg{8 - i, 16, 8};
+}
+constexpr int kFwdFrags = 8 * 6 + 6 * 8 * 16 + 8 * 22 + 4 * 16;  // 1056
+constexpr int kBwdFrags = 8 * 8 + 7 * 8 * 16;                     // 960
+static_assert(kFwdFrags % kPeriod == 0 && kBwdFrags % kPeriod == 0, "streams are whole periods");
+constexpr int kStreamPad = 2 * kPeriod;  // the DMA runs two periods past the end: zero padding
+// images (floats): fragments (+ pad), then the fp32 tail of mlp_common.h (kFwdTail / kBwdTail layout)
+constexpr size_t kFwdH32Floats = (size_t)(kFwdFrags + kStreamPad) * kFragFloats;
+constexpr size_t kBwdH32Floats = (size_t)(kBwdFrags + kStreamPad) * kFragFloats;
+
+// k-step element j of lane half h <-> feature offset within the k-step's 16 (B fragment order)
+__host__ __device__ constexpr int kfeat(int kk, int h, int j) { return 16 * kk + 8 * (j >> 2) + 4 * h + (j & 3); }
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x16 mfma_h32(const f16x8& a, const uint32_t (&b)[4], const f32x16& c) {
+  const u32x4 bv = {b[0], b[1], b[2], b[3]};
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, __builtin_bit_cast(f16x8, bv), c, 0, 0, 0);
+}
+
+// RNE fp32 pair -> packed fp16 (v_cvt_pk_f16_f32)
+__device__ __forceinline__ uint32_t pk_h(float a, float b) {
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2{a, b}), h2));
+}
+// ReLU of both fp16 halves: max as int16 (negative values and -0 are negative int16)
+__device__ __forceinline__ uint32_t relu_pk(uint32_t p) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, p), (s16x2{0, 0})));
+}
+// shift one mask bit per half into w: w = 2w + min(relu'd half, 1) (inline asm: the compiler turns the
+// packed min into two compares, two selects and a perm)
+__device__ __forceinline__ uint32_t mask_shift(uint32_t w, uint32_t relu) {
+  uint32_t b, r;
+  asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(b) : "v"(relu));
+  asm("v_pk_mad_u16 %0, %1, 2, %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(w), "v"(b));
+  return r;
+}
+// 0xFFFF per half whose mask bit k (shifted in k-th of 16) is set (k constant after unrolling)
+__device__ __forceinline__ uint32_t mask_expand(uint32_t w, int k) {
+  const u16x2 m = __builtin_bit_cast(u16x2, w) << (u16x2{(unsigned short)k, (unsigned short)k});
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, m) >> (s16x2{15, 15}));
+}
+
+// End of a ring period: this wave's DMA of the next period has landed once at most n VMEM ops are
+// outstanding (n = the ops issued in this period: its 2 DMA steps and its stores, all younger), every
+// wave's LDS reads of this period are done, then the workgroup barrier.
+__device__ __forceinline__ void h32_barrier(int n) {
+#define NOF_H32_BAR(N) \
+  case N: asm volatile("s_waitcnt vmcnt(" #N ")\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+  switch (n < 0 ? 0 : (n > 24 ? 24 : n)) {
+    NOF_H32_BAR(0) NOF_H32_BAR(1) NOF_H32_BAR(2) NOF_H32_BAR(3) NOF_H32_BAR(4) NOF_H32_BAR(5) NOF_H32_BAR(6)
+    NOF_H32_BAR(7) NOF_H32_BAR(8) NOF_H32_BAR(9) NOF_H32_BAR(10) NOF_H32_BAR(11) NOF_H32_BAR(12) NOF_H32_BAR(13)
+    NOF_H32_BAR(14) NOF_H32_BAR(15) NOF_H32_BAR(16) NOF_H32_BAR(17) NOF_H32_BAR(18) NOF_H32_BAR(19) NOF_H32_BAR(20)
+    NOF_H32_BAR(21) NOF_H32_BAR(22) NOF_H32_BAR(23)
+    default: asm volatile("s_waitcnt vmcnt(24)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+  }
+#undef NOF_H32_BAR
+}
+
+// The weight ring.  `next` = stream position of period P + 2 while period P is consumed from slot `cur`.
+struct H32Ring {
+  float* lds;
+  const float* next;
+  int cur;
+  __device__ __forceinline__ void prologue(const float* stream, int tid) {  // periods 0, 1 -> slots 0, 1
+    slice16_dma_step(stream, lds, tid, 0);
+    slice16_dma_step(stream, lds, tid, 1);
+    slice16_dma_step(stream + kPeriodFloats, lds + kPeriodFloats, tid, 0);
+    slice16_dma_step(stream + kPeriodFloats, lds + kPeriodFloats, tid, 1);
+    next = stream + 2 * kPeriodFloats;
+    cur = 0;
+  }
+  __device__ __forceinline__ void dma(int step, int tid) {
+    slice16_dma_step(next, lds + ((cur + 2) & 3) * kPeriodFloats, tid, step);
+  }
+  __device__ __forceinline__ void end_period(int nstores) {
+    h32_barrier(2 + nstores);
+    cur = (cur + 1) & 3;
+    next += kPeriodFloats;
+  }
+  __device__ __forceinline__ f16x8 frag(int i, int lane) const {  // fragment i (0..15) of the current period
+    return reinterpret_cast<const f16x8*>(lds + cur * kPeriodFloats + i * kFragFloats)[lane];
+  }
+};
+
+// Epilogue piece schedule inside a host chunk of NK k-steps: the 8 packed dwords' VALU, then the 4
+// side stores (and the layer's mask store with the last), then the C-operand load of the next chunk.
+__host__ __device__ constexpr int epi_valu_pos(int d, int nk) { return nk >= 16 ? d : d >> 1; }
+__host__ __device__ constexpr int epi_store_pos(int q, int nk) { return nk >= 16 ? 8 + q : 4 + (q >> 1); }
+__host__ __device__ constexpr int cinit_pos(int nk) { return nk >= 16 ? 12 : nk - 1; }
+
+struct NoEpiH {
+  static constexpr int kNC = 2;
+  __device__ __forceinline__ int piece(int, int, int) { return 0; }
+};
+
+// C operand of chunk c: 16 values of a 256-float (layer) vector in the D-register order of lane half h
+// (4 ds_read_b128 of 4 consecutive rows), or zero
+__device__ __forceinline__ f32x16 cinit_load(const float* v, int c) {
+  f32x16 r;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(v + 32 * c + 8 * q);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[4 * q + e] = x[e];
+  }
+  return r;
+}
+
+// One layer: NC chunks of 32 output rows x NK k-steps.  bsrc(kk) gives k-step kk's B fragment (4
+// packed dwords); chunk c accumulates into acc[c & 1]; epi.piece(T, kk, NK) runs the epilogue of
+// this layer's tile T = c - 1 at k-step kk of chunk c, prev.piece the previous layer's last tile in
+// chunk 0 (its tile index NCp - 1 is odd: acc[1]).  cv: the layer's C-operand vector (LDS, + 4h;
+// kBias false: C = 0).  Returns with the last tile's epilogue pending (the caller's next layer or a
+// drain).  Every loop is unrolled: all positions and store counts are constants.
+template <int NK, int NC, bool kBias, class BSrc, class Epi, class Prev>
+__device__ __forceinline__ void h32_layer(const BSrc& bsrc, f32x16 (&acc)[2], H32Ring& ring, Epi& epi, Prev& prev,
+                                          const float* cv, int tid, int lane) {
+  static_assert((NK * NC) % kPeriod == 0, "a layer is a whole number of ring periods");
+  static_assert(NC % 2 == 0 && Prev::kNC % 2 == 0, "the pending last tile of a layer sits in acc[1]");
+  if constexpr (kBias) acc[0] = cinit_load(cv, 0);
+  int nst = 0;  // stores issued in the current period
+  f16x8 a = ring.frag(0, lane);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      const int i = c * NK + kk, pos = i & (kPeriod - 1);
+      asm volatile("" ::"v"(a));  // fragment i has landed in registers before the next read issues
+      f16x8 an = a;
+      if (pos == 0) ring.dma(0, tid);
+      if (pos == 1) ring.dma(1, tid);
+      if (pos != kPeriod - 1) an = ring.frag(pos + 1, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      uint32_t b[4];
+      bsrc(kk, b);
+      acc[c & 1] = mfma_h32(a, b, (kk == 0 && !kBias) ? f32x16{} : acc[c & 1]);
+      if (c == 0) nst += prev.piece(Prev::kNC - 1, kk, NK);  // the previous layer's last tile (acc[1])
+      else nst += epi.piece(c - 1, kk, NK);
+      if constexpr (kBias)
+        if (c + 1 < NC && kk == cinit_pos(NK)) acc[(c + 1) & 1] = cinit_load(cv, c + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (pos == kPeriod - 1) {
+        ring.end_period(nst);
+        nst = 0;
+        if (i + 1 < NK * NC) an = ring.frag(0, lane);
+      }
+      a = an;
+    }
+  }
+}
+
+}  // namespace nof

@@ -642,6 +642,148 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_h(const WgProblem* __
   NOF_WG_T1(1)
 }
 
+// ---- F16 mode: sample-major fp16 operands (row-major [M][F] matrices, mlp_h32.h) --------------------
+// The F16 forward / backward store each lane's 4 consecutive features (the MFMA output layout), so a
+// block's operand tile is 32 samples x 32 features = 32 rows of 64 B.  Staged as that 2-KB image by
+// LDS-DMA (16 rows x 64 B per wave-instruction) and read back transposed by ds_read_b64_tr_b16: lane
+// (x, h) gets feature x of samples 16ks + 8h .. + 7 in two reads (4 samples each) — the 32x32x16
+// fragment with k = samples.  64-B rows: a 32-lane half reads 4 rows x 64 B = all 64 banks once.
+// Same items, wave grid and slabs as k_wgrad_h.
+typedef short s16x4v __attribute__((vector_size(8)));
+template <int RB, int CB>
+__device__ __forceinline__ void wg_item_s(const WgItem& item, const WgProblem& P, _Float16* lds, int tid, int wave,
+                                          float* slabs, float* bias_slabs, const int64_t* slab_off) {
+  constexpr int ND = ((2 * RB + kX3WC * CB) * 128 + kWgX3Threads - 1) / kWgX3Threads;  // DMA instrs / block
+  int tq = tid;
+  asm volatile("" : "+v"(tq));
+  const int lane = tq & 63;
+  const int h = lane >> 5, x = lane & 31;
+  const int wr = wave / kX3WC, wc = wave % kX3WC;
+  const int r0 = wr * RB, c0 = wc * CB;
+  const bool active = r0 < P.ntr && c0 < P.ntc;  // wave-uniform
+  int rowt[RB], colt[CB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) rowt[r] = min(r0 + r, P.ntr - 1);
+#pragma unroll
+  for (int c = 0; c < CB; ++c) colt[c] = min(c0 + c, P.ntc - 1);
+  const int T = P.ntr + P.ntc;  // tiles per block
+  const size_t strideA = (size_t)P.FA * kBlk * 2, strideB = (size_t)P.FB * kBlk * 2;  // bytes per block
+  const char* baseA = reinterpret_cast<const char*>(P.A) + (size_t)item.kb0 * strideA + (size_t)P.a_row0 * 2;
+  const char* baseB = reinterpret_cast<const char*>(P.B) + (size_t)item.kb0 * strideB + (size_t)P.b_col0 * 2;
+  const int K = item.kb1 - item.kb0;
+  // this lane's 16-B piece of a DMA instruction: sample (lane >> 2) (+ 16), 16-B column chunk lane & 3
+  const int rowA = (lane >> 2) * P.FA * 2 + (lane & 3) * 16, rowB = (lane >> 2) * P.FB * 2 + (lane & 3) * 16;
+  auto dma = [&](int k) {
+    k = min(k, K - 1);
+    _Float16* stage = lds + (k % kWhStages) * kWhStageHalves;
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+      const int cw = min(i * kWgX3Threads + wave * 64, T * 128 - 64);  // wave's first 16-B chunk (uniform)
+      const int tt = cw >> 7, half = (cw >> 6) & 1;                      // tile, samples 16 half .. + 15
+      const char* src = tt < P.ntr ? baseA + (size_t)k * strideA + tt * 64 + half * 16 * P.FA * 2 + rowA
+                                   : baseB + (size_t)k * strideB + (tt - P.ntr) * 64 + half * 16 * P.FB * 2 + rowB;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(stage + cw * 8), 16, 0, 0);
+    }
+  };
+  f32x16 acc[RB][CB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r)
+#pragma unroll
+    for (int c = 0; c < CB; ++c) acc[r][c] = f32x16{};
+  float bsum[RB];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) bsum[r] = 0.0f;
+  // transposed-read address of this lane inside a tile image (halves): row 8h + q, column 16 (G & 1) + 4p
+  const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int toff = (8 * (G >> 1) + q) * 32 + 16 * (G & 1) + 4 * p;
+  typedef __attribute__((address_space(3))) s16x4v* tr_ptr;
+  auto frag = [&](const _Float16* tile, int ks) {
+    const _Float16* a = tile + toff + ks * 16 * 32;
+    const s16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr)(a));
+    const s16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr)(a + 4 * 32));
+    return __builtin_bit_cast(f16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+#pragma unroll
+  for (int k = 0; k < kWhStages - 1; ++k) dma(k);
+  for (int k = 0; k < K; ++k) {
+    wait_vmcnt<(kWhStages - 2) * ND>();  // block k landed (this wave's part); k + 1 .. k + NS - 2 in flight
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave's part; stage k - 1 read out
+    dma(k + kWhStages - 1);  // into stage (k - 1) % NS
+    const _Float16* st = lds + (k % kWhStages) * kWhStageHalves;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f16x8 fa[RB], fb[CB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) fa[r] = frag(st + rowt[r] * 1024, ks);
+#pragma unroll
+      for (int c = 0; c < CB; ++c) fb[c] = frag(st + (P.ntr + colt[c]) * 1024, ks);
+#pragma unroll
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int c = 0; c < CB; ++c) acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[r], fb[c], acc[r][c], 0, 0, 0);
+      if (wc == 0) {  // bias partials: row sums of delta (uniform branch)
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          float sum = 0.0f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) sum += (float)fa[r][j];
+          bsum[r] += sum;
+        }
+      }
+    }
+  }
+  wait_vmcnt<0>();  // retire the clamped tail DMAs before the ring is reused
+  if (active) {
+    float* slab = slabs + slab_off[item.slab];
+    const int ld_ = P.ntc * 32;
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int c = 0; c < CB; ++c) {
+        if (r0 + r < P.ntr && c0 + c < P.ntc) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int row = rowt[r] * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+            slab[(size_t)row * ld_ + colt[c] * 32 + x] = acc[r][c][e];
+          }
+        }
+      }
+  }
+  if (wc == 0) {
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const float v = bsum[r] + __shfl_xor(bsum[r], 32, 64);
+      if (r0 + r < P.ntr && h == 0) bias_slabs[(size_t)item.slab * 256 + rowt[r] * 32 + x] = v;
+    }
+  }
+  __syncthreads();  // the ring is reused by the next item
+}
+
+__global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_s(const WgProblem* __restrict__ probs,
+                                                             const WgItem* __restrict__ items,
+                                                             const int* __restrict__ item_ptr,
+                                                             const int64_t* __restrict__ slab_off, float* slabs,
+                                                             float* bias_slabs) {
+  extern __shared__ __attribute__((aligned(16))) _Float16 ldss[];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int it0 = item_ptr[blockIdx.x], it1 = item_ptr[blockIdx.x + 1];
+  for (int it = it0; it < it1; ++it) {
+    const WgItem item = items[it];
+    const WgProblem P = probs[item.prob];
+    NOF_DCHECK(item.kb0 < item.kb1 && P.ntr >= 1 && P.ntr <= 8 && P.ntc >= 1 && P.ntc <= 8 &&
+                   P.a_row0 + 32 * P.ntr <= P.FA && P.b_col0 + 32 * P.ntc <= P.FB,
+               kChkWgradGeom);
+    switch (((P.ntr + 1) >> 1) * 10 + (P.ntc + kX3WC - 1) / kX3WC) {
+      case 11: wg_item_s<1, 1>(item, P, ldss, tid, wave, slabs, bias_slabs, slab_off); break;
+      case 21: wg_item_s<2, 1>(item, P, ldss, tid, wave, slabs, bias_slabs, slab_off); break;
+      case 32: wg_item_s<3, 2>(item, P, ldss, tid, wave, slabs, bias_slabs, slab_off); break;
+      case 41: wg_item_s<4, 1>(item, P, ldss, tid, wave, slabs, bias_slabs, slab_off); break;
+      default: wg_item_s<4, 2>(item, P, ldss, tid, wave, slabs, bias_slabs, slab_off); break;
+    }
+  }
+}
+
 int wgrad_x3_grid_cols() { return kX3WC; }
 
 int wgrad_shape(int ntr, int ntc, int* cost2) {
@@ -695,7 +837,18 @@ static hipError_t launch_wgrad_split(const WgProblem* probs, const WgItem* items
 hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const int* item_ptr, int num_wg,
                            const int64_t* slab_off, float* slabs, float* bias_slabs, int precision, hipStream_t st) {
   if (num_wg <= 0) return hipSuccess;
-  if (precision == 2 || precision == 4) {  // fp16 operand blocks (k_wgrad_h): F16X2, F16
+  if (precision == 4) {  // F16: sample-major fp16 operands (k_wgrad_s)
+    static bool attr_s = false;
+    if (!attr_s) {
+      const hipError_t e = hipFuncSetAttribute((const void*)k_wgrad_s, hipFuncAttributeMaxDynamicSharedMemorySize, kWhLds);
+      if (e != hipSuccess) return e;
+      attr_s = true;
+    }
+    hipLaunchKernelGGL(k_wgrad_s, dim3(num_wg), dim3(kWgX3Threads), kWhLds, st, probs, items, item_ptr, slab_off,
+                       slabs, bias_slabs);
+    return hipGetLastError();
+  }
+  if (precision == 2) {  // fp16 operand blocks (k_wgrad_h): F16X2
     static bool attr = false;
     if (!attr) {
       const hipError_t e = hipFuncSetAttribute((const void*)k_wgrad_h, hipFuncAttributeMaxDynamicSharedMemorySize, kWhLds);

@@ -109,7 +109,21 @@ class AcceleratedMLP:
         M = dv["M"]
         nb = M // 32
         out = np.zeros((M, 8 * 256 + 128), np.uint8)
-        if self._owner.config.precision in (0, 2, 3, 4):  # 16x16 kernels (mlp16.h): [half][lane][uint2]
+        if self._owner.config.precision == 4:  # F16 (mlp_h32.h): [lane][4 words], two 16-bit shift registers
+            raw = to_numpy(dv["masks"], (nb, 9, 64, 4), np.uint32)
+            lane = np.arange(64)
+            x, h = lane & 31, lane >> 5
+            rows = np.arange(nb)[:, None] * 32 + x[None, :]
+            for slot in range(9):
+                base = slot * 256
+                for t in range(8 if slot < 8 else 4):
+                    for r in range(16):
+                        f = 32 * t + 8 * (r >> 2) + 4 * h + (r & 3)  # [64]
+                        k = 8 * (t & 1) + (r >> 1)  # packed dword shifted in k-th: bit 15 - k of its half
+                        bit = (raw[:, slot, :, t >> 1] >> np.uint32(16 * (r & 1) + 15 - k)) & np.uint32(1)
+                        out[rows, base + f[None, :]] = bit.astype(np.uint8)
+            return out
+        if self._owner.config.precision in (0, 2, 3):  # 16x16 kernels (mlp16.h): [half][lane][uint2]
             raw = to_numpy(dv["masks"], (nb, 9, 2, 64, 2), np.uint32)
             lane = np.arange(64)
             j, g = lane & 15, lane >> 4

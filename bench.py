@@ -445,89 +445,91 @@ def main():
         if native is not None and not single:
             native[0].attach(models[0])  # RCCL buckets on the library's internal comm stream
         cs = chunks(sh, mb)
+        try:  # the communicator is detached and the models closed whatever happens
 
-        def step(k):
-            for i, (r, m) in enumerate(zip(ranks, models)):
-                b = pl[i][k % 2]
-                for j, (lo, hi) in enumerate(cs):
-                    m.set_rng(seed, k, r * sh + lo)  # global ray ids: sharding never changes a sample
-                    m.get_gradient_device(hi - lo, b["o"][lo:hi], b["d"][lo:hi], b["radius"][lo:hi],
-                                          b["near"][lo:hi], b["far"][lo:hi], b["lossmult"][lo:hi], b["pix"][lo:hi],
-                                          msum_global, accumulate=j > 0, publish=j == len(cs) - 1)
-            if single and G > 1:
-                NativeDP.allreduce_grads_all(native, models)
-            for m, o in zip(models, opts):
-                o.step(m.mlp.allParams, m.mlp.allGradients, nof.learning_rate_decay(k + 1))
-            if native is not None:
-                for nd in native:
-                    nd.wait()  # failure detection: an RCCL error or a stall raises instead of hanging
+            def step(k):
+                for i, (r, m) in enumerate(zip(ranks, models)):
+                    b = pl[i][k % 2]
+                    for j, (lo, hi) in enumerate(cs):
+                        m.set_rng(seed, k, r * sh + lo)  # global ray ids: sharding never changes a sample
+                        m.get_gradient_device(hi - lo, b["o"][lo:hi], b["d"][lo:hi], b["radius"][lo:hi],
+                                              b["near"][lo:hi], b["far"][lo:hi], b["lossmult"][lo:hi], b["pix"][lo:hi],
+                                              msum_global, accumulate=j > 0, publish=j == len(cs) - 1)
+                if single and G > 1:
+                    NativeDP.allreduce_grads_all(native, models)
+                for m, o in zip(models, opts):
+                    o.step(m.mlp.allParams, m.mlp.allGradients, nof.learning_rate_decay(k + 1))
+                if native is not None:
+                    for nd in native:
+                        nd.wait()  # failure detection: an RCCL error or a stall raises instead of hanging
 
-        def sync_all():
-            for d in devs:
-                torch.cuda.synchronize(d)
+            def sync_all():
+                for d in devs:
+                    torch.cuda.synchronize(d)
 
-        for k in range(warmup):
-            step(k)
-        sync_all()
-        if world > 1:
-            dist.barrier()
-        # the three MLP kernel classes are event-timed live (the roofline kernel is the one that takes
-        # the most time per step, which depends on the mode): 6 event pairs per step
-        timers = os.environ.get("NOF_BENCH_TIMERS", "mlp_fwd,mlp_bwd,wgrad")
-        models[0].enable_timing(timers_on, timers=timers.split(",") if timers != "all" else None)
-        sync_all()
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        for k in range(warmup, warmup + steps):
-            step(k)
-        sync_all()
-        if world > 1:
-            dist.barrier()
-        dt = time.perf_counter() - t0
-        live = models[0].read_timing()
-        timing = {}
-        kb = min(5, steps) if timers_on else 0
-        if kb:  # per-kernel breakdown: a few more steps with every kernel class timed (outside the clock)
-            models[0].enable_timing(True)
-            for k in range(warmup + steps, warmup + steps + kb):
+            for k in range(warmup):
                 step(k)
-            timing = {name: (ms * steps / kb, cnt * steps // kb) for name, (ms, cnt) in models[0].read_timing().items()}
-            for name, v in live.items():  # the live (timed-region) figures where they were taken
-                if v[1]:
-                    timing[name] = v
-            models[0].enable_timing(False)
-        in_sync = None
-        if world > 1 or (single and G > 1):
             sync_all()
-            # DP invariant: identical all-reduced gradients + identical Adam -> every
-            # rank holds bitwise-identical parameters; compare a checksum's max and min over ranks
-            sums = []
-            for m, d in zip(models, devs):
-                pptr, P = m.mlp.flat_params()
-                sums.append(params_checksum(nof.device_tensor(pptr, (P,), device=torch.device("cuda", d))).to(dev))
-            cs_ = torch.cat(sums)
-            hi, lo = cs_.max().reshape(1), (-cs_.min()).reshape(1)
             if world > 1:
-                t = torch.tensor([dt], device=dev, dtype=torch.float64)
-                allreduce(t, op=dist.ReduceOp.MAX)
-                dt = float(t.item())
-                allreduce(hi, op=dist.ReduceOp.MAX)
-                allreduce(lo, op=dist.ReduceOp.MAX)
-            in_sync = bool(hi.item() == -lo.item())
-        # fine-level PSNR of the last micro-batch (MseToPsnr, MipHelpers.cs:672)
-        last = pl[0][(warmup + steps + kb - 1) % 2]
-        lo_, hi_ = cs[-1]
-        comp = models[0].level_numpy(len(smp) - 1)["comp_rgb"]
-        mse = float(np.mean((comp - last["pix"][lo_:hi_].cpu().numpy()) ** 2))
-        psnr = -10.0 * math.log10(max(mse, 1e-12))
-        for bk in bucketed:
-            bk.close()
-        if native is not None and not single:
-            native[0].attach(None)
-        for o, m in zip(opts, models):
-            o.close()
-            m.close()
+                dist.barrier()
+            # the three MLP kernel classes are event-timed live (the roofline kernel is the one that takes
+            # the most time per step, which depends on the mode): 6 event pairs per step
+            timers = os.environ.get("NOF_BENCH_TIMERS", "mlp_fwd,mlp_bwd,wgrad")
+            models[0].enable_timing(timers_on, timers=timers.split(",") if timers != "all" else None)
+            sync_all()
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            for k in range(warmup, warmup + steps):
+                step(k)
+            sync_all()
+            if world > 1:
+                dist.barrier()
+            dt = time.perf_counter() - t0
+            live = models[0].read_timing()
+            timing = {}
+            kb = min(5, steps) if timers_on else 0
+            if kb:  # per-kernel breakdown: a few more steps with every kernel class timed (outside the clock)
+                models[0].enable_timing(True)
+                for k in range(warmup + steps, warmup + steps + kb):
+                    step(k)
+                timing = {name: (ms * steps / kb, cnt * steps // kb) for name, (ms, cnt) in models[0].read_timing().items()}
+                for name, v in live.items():  # the live (timed-region) figures where they were taken
+                    if v[1]:
+                        timing[name] = v
+                models[0].enable_timing(False)
+            in_sync = None
+            if world > 1 or (single and G > 1):
+                sync_all()
+                # DP invariant: identical all-reduced gradients + identical Adam -> every
+                # rank holds bitwise-identical parameters; compare a checksum's max and min over ranks
+                sums = []
+                for m, d in zip(models, devs):
+                    pptr, P = m.mlp.flat_params()
+                    sums.append(params_checksum(nof.device_tensor(pptr, (P,), device=torch.device("cuda", d))).to(dev))
+                cs_ = torch.cat(sums)
+                hi, lo = cs_.max().reshape(1), (-cs_.min()).reshape(1)
+                if world > 1:
+                    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+                    allreduce(t, op=dist.ReduceOp.MAX)
+                    dt = float(t.item())
+                    allreduce(hi, op=dist.ReduceOp.MAX)
+                    allreduce(lo, op=dist.ReduceOp.MAX)
+                in_sync = bool(hi.item() == -lo.item())
+            # fine-level PSNR of the last micro-batch (MseToPsnr, MipHelpers.cs:672)
+            last = pl[0][(warmup + steps + kb - 1) % 2]
+            lo_, hi_ = cs[-1]
+            comp = models[0].level_numpy(len(smp) - 1)["comp_rgb"]
+            mse = float(np.mean((comp - last["pix"][lo_:hi_].cpu().numpy()) ** 2))
+            psnr = -10.0 * math.log10(max(mse, 1e-12))
+        finally:
+            for bk in bucketed:
+                bk.close()
+            if native is not None and not single:
+                native[0].attach(None)
+            for o, m in zip(opts, models):
+                o.close()
+                m.close()
         return dt, timing, psnr, in_sync
 
     def summarize(prec, dt, timing, sh=shard):

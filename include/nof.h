@@ -288,6 +288,25 @@ nof_status nof_dp_attach(nof_dp* dp, nof_mipnerf* h, void* comm_stream);
 nof_status nof_dp_wait(nof_dp* dp, int32_t timeout_ms);
 nof_status nof_dp_abort(nof_dp* dp);
 nof_status nof_dp_destroy(nof_dp* dp);
+/* Loopback group (SURVEY.md §4 "T0 DP logic"): k <= 8 communicators of this process on ONE device
+ * whose all-reduce sums the k members' buffers on the device in member order.  Every nof_dp_* call
+ * above works on them unchanged (grouped, attached / bucketed, nof_dp_train_step), so the
+ * data-parallel choreography runs with k models on one GPU.  A loopback collective completes when
+ * its last member arrives; the members' streams then wait for it. */
+nof_status nof_dp_init_loopback(int32_t k, int32_t device, nof_dp** out /* k handles */);
+/* One data-parallel TrainStep (Program.cs:48-62) — what a C# driver calls once per step.
+ * n replicas: one per device (nof_dp_init_all), a loopback group (n = k), or this process's one rank
+ * (n = 1, nof_dp_init_rank: the shard is its rank's); dps = NULL: one replica, no exchange.
+ * Replica r (rank r) takes the contiguous shard [r s, (r + 1) s) of the global batch (s =
+ * global_batch / world; global ray ids: the same rays and Philox samples whatever the sharding),
+ * gathered from datasets[r] for (seed, step); every shard normalises by the GLOBAL loss-multiplier
+ * sum; a shard runs as shard / micro_batch micro-batches (0 = one), the later ones accumulating;
+ * the gradient arenas are all-reduced (bucket by bucket when the communicators are attached, else one
+ * grouped all-reduce); every replica applies Adam(lr); then a bounded nof_dp_wait.  Replica
+ * parameters stay bitwise identical.  *loss_mult_sum (optional) = the global sum. */
+nof_status nof_dp_train_step(int32_t n, nof_dp* const* dps, nof_mipnerf* const* models, nof_adam* const* adams,
+                             nof_dataset* const* datasets, int32_t global_batch, int32_t micro_batch, uint64_t seed,
+                             int32_t step, float lr, float* loss_mult_sum);
 
 /* Image metrics on device images [H][W][3] (float, any range; max_val as MathHelpers' maxVal):
  * psnr = MseToPsnr(mean squared error) (MipHelpers.cs:672); ssim = ComputeSsimAverage with the

@@ -20,14 +20,18 @@
 //
 //   nof_train --records train_data.bin [--steps K] [--batch N] [--precision f32|split|f16x2|f16split|f16]
 //             [--print-every P] [--save-every S --ckpt-dir DIR] [--resume CKPT] [--host-api]
-//             [--seed X] [--device D | --gpus N] [--dump-params FILE]
+//             [--seed X] [--device D | --gpus N [--dp rccl|loopback] [--attach]] [--micro-batch M]
+//             [--dump-params FILE]
 //
 // --gpus N: data parallelism in ONE process over devices 0..N-1 (SURVEY 8e's process model): the
 // global batch of --batch rays is sharded into N contiguous shards with global ray ids (every shard
 // draws exactly what the whole batch would), each device normalises by the GLOBAL loss-multiplier
-// sum, the gradient arenas are summed by one grouped RCCL all-reduce (nof_dp_init_all /
-// nof_dp_allreduce_grads_all, with failure detection: nof_dp_wait), and every device applies the
-// same Adam step — parameters stay bitwise identical across devices.
+// sum, the gradient arenas are summed by one grouped RCCL all-reduce (nof_dp_init_all), and every
+// device applies the same Adam step — parameters stay bitwise identical across devices.  The device
+// path is one nof_dp_train_step call per step (shards, global sum, --micro-batch accumulation,
+// all-reduce, Adam, bounded nof_dp_wait); --dp loopback runs the N replicas on --device alone through
+// a loopback group (nof_dp_init_loopback: the same choreography, the all-reduce a device sum), and
+// --attach all-reduces bucket by bucket through the gradient-bucket hook (nof_dp_attach).
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -45,6 +49,9 @@ struct Args {
   std::string records, ckpt_dir, resume, dump_params;
   int steps = 100, batch = 1024, print_every = 100, save_every = 0, device = 0, precision = NOF_PRECISION_F32;
   int gpus = 0;  // > 0: data parallel over devices 0..gpus-1 in this process (nof_dp_init_all)
+  bool loopback = false;  // --dp loopback: the gpus replicas on --device, a loopback group
+  bool attach = false;    // bucketed all-reduce through the gradient-bucket hook
+  int micro = 0;          // micro-batch rays (0: the whole shard)
   bool host_api = false;
   uint64_t seed = 0x5EED0000ull;
   // Config (TrainState.cs:54-58)
@@ -56,7 +63,8 @@ struct Args {
   std::fprintf(code ? stderr : stdout,
                "usage: nof_train --records FILE [--steps K] [--batch N] [--precision f32|split|f16x2|f16split|f16]\n"
                "                 [--print-every P] [--save-every S --ckpt-dir DIR] [--resume CKPT] [--host-api]\n"
-               "                 [--seed X] [--device D | --gpus N] [--dump-params FILE]\n");
+               "                 [--seed X] [--device D | --gpus N [--dp rccl|loopback] [--attach]] [--micro-batch M]\n"
+               "                 [--dump-params FILE]\n");
   std::exit(code);
 }
 
@@ -81,6 +89,13 @@ Args parse(int argc, char** argv) {
     else if (k == "--gpus") a.gpus = std::atoi(val());
     else if (k == "--seed") a.seed = std::strtoull(val(), nullptr, 0);
     else if (k == "--host-api") a.host_api = true;
+    else if (k == "--attach") a.attach = true;
+    else if (k == "--micro-batch") a.micro = std::atoi(val());
+    else if (k == "--dp") {
+      const std::string d = val();
+      if (d == "loopback") a.loopback = true;
+      else if (d != "rccl") usage(2);
+    }
     else if (k == "--precision") {
       const std::string p = val();
       if (p == "f32") a.precision = NOF_PRECISION_F32;
@@ -97,6 +112,10 @@ Args parse(int argc, char** argv) {
   if (a.records.empty() || a.steps < 0 || a.batch <= 0 || a.print_every < 0 || a.save_every < 0) usage(2);
   if (a.save_every && a.ckpt_dir.empty()) usage(2);
   if (a.gpus < 0 || (a.gpus > 0 && a.batch % a.gpus)) usage(2);
+  const int shard = a.batch / (a.gpus > 0 ? a.gpus : 1);
+  if (a.micro < 0 || (a.micro > 0 && shard % a.micro)) usage(2);
+  if ((a.loopback || a.attach) && a.gpus == 0) usage(2);
+  if (a.host_api && (a.micro || a.attach)) usage(2);  // the reference's flow: one call per shard
   return a;
 }
 
@@ -170,15 +189,16 @@ int main(int argc, char** argv) {
   const Args a = parse(argc, argv);
   const int G = a.gpus > 0 ? a.gpus : 1;
   const int shard = a.batch / G;
+  const int micro = a.micro > 0 ? a.micro : shard;
   std::vector<Replica> rs(G);
   for (int r = 0; r < G; ++r) {
     Replica& R = rs[r];
-    R.device = a.gpus > 0 ? r : a.device;
+    R.device = a.gpus > 0 && !a.loopback ? r : a.device;
     CHECK(nof_set_device(R.device));
     CHECK(nof_dataset_open(a.records.c_str(), R.device, &R.ds));  // BinDataset, resident on every device
     nof_config_default(&R.cfg);
     R.cfg.device = R.device;
-    R.cfg.max_rays = shard;
+    R.cfg.max_rays = micro;
     R.cfg.seed = a.seed;
     R.cfg.precision = a.precision;
     CHECK(nof_mipnerf_create(&R.cfg, &R.model));
@@ -192,9 +212,16 @@ int main(int argc, char** argv) {
   // the same Glorot draw on every device (seeded Philox init), then one all-reduce per step
   std::vector<nof_dp*> dps(G, nullptr);
   std::vector<nof_mipnerf*> hs(G);
+  std::vector<nof_adam*> adams(G);
+  std::vector<nof_dataset*> dss(G);
   std::vector<int32_t> devs(G);
-  for (int r = 0; r < G; ++r) { hs[r] = rs[r].model; devs[r] = rs[r].device; }
-  if (a.gpus > 0) CHECK(nof_dp_init_all(G, devs.data(), dps.data()));
+  for (int r = 0; r < G; ++r) { hs[r] = rs[r].model; adams[r] = rs[r].adam; dss[r] = rs[r].ds; devs[r] = rs[r].device; }
+  if (a.gpus > 0) {
+    if (a.loopback) CHECK(nof_dp_init_loopback(G, a.device, dps.data()));
+    else CHECK(nof_dp_init_all(G, devs.data(), dps.data()));
+    if (a.attach)
+      for (int r = 0; r < G; ++r) CHECK(nof_dp_attach(dps[r], hs[r], nullptr));
+  }
 
   int step0 = 0;
   if (!a.resume.empty()) {
@@ -204,21 +231,33 @@ int main(int argc, char** argv) {
   const int L = rs[0].cfg.num_levels;
   const auto t0 = std::chrono::steady_clock::now();
   for (int step = step0 + 1; step <= step0 + a.steps; ++step) {
-    // binDataset.Next(): every shard gathers its global ray ids; the loss-multiplier sum is global
-    float msum = 0.0f;
-    for (int r = 0; r < G; ++r) {
-      Replica& R = rs[r];
-      CHECK(nof_dataset_next(R.ds, shard, a.seed, (uint32_t)step, (uint32_t)(r * shard), R.cfg.stream, &R.b, &R.msum));
-      msum += R.msum;
-    }
     const float lr = nof_lr_decay(step, a.lr_init, a.lr_final, a.max_steps, a.lr_delay_steps, a.lr_delay_mult);
-    for (int r = 0; r < G; ++r) {
-      Replica& R = rs[r];
-      CHECK(nof_set_device(R.device));
-      CHECK(nof_mipnerf_set_rng(R.model, a.seed, (uint32_t)step, (uint32_t)(r * shard)));
-      float* const* grads = nullptr;
-      const int n = shard;
-      if (a.host_api) {  // TrainStep as the reference runs it: host arrays in, host pixels via the callback
+    if (!a.host_api) {
+      // TrainStep on the device path: one call (shards, global loss-mult sum, micro-batches,
+      // all-reduce, Adam, bounded wait)
+      float msum = 0.0f;
+      CHECK(nof_dp_train_step(G, a.gpus > 0 ? dps.data() : nullptr, hs.data(), adams.data(), dss.data(), a.batch,
+                              micro, a.seed, step, lr, &msum));
+      for (int r = 0; r < G; ++r) {  // the fine level's output of each replica's last micro-batch (loss print)
+        Replica& R = rs[r];
+        nof_level_view v;
+        CHECK(nof_mipnerf_level_view(R.model, L - 1, &v));
+        R.fine = (uint64_t)(uintptr_t)v.comp_rgb;
+      }
+    } else {
+      // the reference's flow: host arrays in, host pixels uploaded by the output-gradient callback
+      float msum = 0.0f;
+      for (int r = 0; r < G; ++r) {
+        Replica& R = rs[r];
+        CHECK(nof_dataset_next(R.ds, shard, a.seed, (uint32_t)step, (uint32_t)(r * shard), R.cfg.stream, &R.b, &R.msum));
+        msum += R.msum;
+      }
+      for (int r = 0; r < G; ++r) {
+        Replica& R = rs[r];
+        CHECK(nof_set_device(R.device));
+        CHECK(nof_mipnerf_set_rng(R.model, a.seed, (uint32_t)step, (uint32_t)(r * shard)));
+        float* const* grads = nullptr;
+        const int n = shard;
         d2h(R.ho, R.b.origins, 3 * (size_t)n); d2h(R.hd, R.b.directions, 3 * (size_t)n); d2h(R.hr, R.b.radii, n);
         d2h(R.hn, R.b.nears, n); d2h(R.hf, R.b.fars, n); d2h(R.hm, R.b.loss_mults, n);
         d2h(R.hp, R.b.pixels, 3 * (size_t)n);
@@ -226,26 +265,21 @@ int main(int argc, char** argv) {
         CHECK(nof_mipnerf_get_gradient(R.model, n, R.ho.data(), R.hd.data(), R.hr.data(), R.hn.data(), R.hf.data(),
                                        R.hm.data(), output_gradient, &ctx, &grads));
         R.fine = ctx.fine_output;
-      } else {
-        CHECK(nof_mipnerf_get_gradient_device(R.model, n, R.b.origins, R.b.directions, R.b.radii, R.b.nears, R.b.fars,
-                                              R.b.loss_mults, R.b.pixels, msum, &grads));
-        nof_level_view v;
-        CHECK(nof_mipnerf_level_view(R.model, L - 1, &v));
-        R.fine = (uint64_t)(uintptr_t)v.comp_rgb;
       }
+      if (a.gpus > 0) CHECK(nof_dp_allreduce_grads_all(G, dps.data(), hs.data(), nullptr));
+      for (Replica& R : rs) {
+        float* const* grads = nullptr;
+        CHECK(nof_mlp_grads(R.mlp, &grads));
+        CHECK(nof_adam_step(R.adam, R.params, grads, lr));  // optimizer.step(model.mlp.allParams, grad, lr)
+      }
+      if (a.gpus > 0)
+        for (nof_dp* d : dps) CHECK(nof_dp_wait(d, 0));  // an RCCL error or a stalled peer fails the run
     }
-    if (a.gpus > 0) CHECK(nof_dp_allreduce_grads_all(G, dps.data(), hs.data(), nullptr));
-    for (Replica& R : rs) {
-      float* const* grads = nullptr;
-      CHECK(nof_mlp_grads(R.mlp, &grads));
-      CHECK(nof_adam_step(R.adam, R.params, grads, lr));  // optimizer.step(model.mlp.allParams, grad, lr)
-    }
-    if (a.gpus > 0)
-      for (nof_dp* d : dps) CHECK(nof_dp_wait(d, 0));  // an RCCL error or a stalled peer fails the run
     if (a.print_every && step % a.print_every == 0) {
       double num = 0.0, den = 0.0;  // Program.LossFn over the global batch (every shard's fine level)
       float loss1 = 0.0f;
-      for (Replica& R : rs) {
+      for (int r = 0; r < G; ++r) {
+        Replica& R = rs[r];
         CHECK(nof_set_device(R.device));
         uint32_t bad = 0;
         CHECK(nof_mipnerf_numeric_status(R.model, &bad, 1));
@@ -253,13 +287,19 @@ int main(int argc, char** argv) {
           std::fprintf(stderr, "nof_train: step %d: non-finite values on device %d (flags %#x)\n", step, R.device, bad);
           return 1;
         }
-        std::vector<float> C(3 * (size_t)shard);
-        CHECK(nof_retrieve_output(R.fine, shard, C.data()));  // OutputRetriever.RetrieveOutput
-        if (!a.host_api) { d2h(R.hm, R.b.loss_mults, shard); d2h(R.hp, R.b.pixels, 3 * (size_t)shard); }
-        const float l = loss_fn(C, R.hm, R.hp, shard);
+        const int nl = a.host_api ? shard : micro;  // the rays of the replica's last forward
+        std::vector<float> C(3 * (size_t)nl);
+        CHECK(nof_retrieve_output(R.fine, nl, C.data()));  // OutputRetriever.RetrieveOutput
+        if (!a.host_api) {  // the same gather again (deterministic in seed, step and global ray id)
+          CHECK(nof_dataset_next(R.ds, nl, a.seed, (uint32_t)step, (uint32_t)(r * shard + shard - nl), R.cfg.stream,
+                                 &R.b, nullptr));
+          d2h(R.hm, R.b.loss_mults, nl);
+          d2h(R.hp, R.b.pixels, 3 * (size_t)nl);
+        }
+        const float l = loss_fn(C, R.hm, R.hp, nl);
         loss1 = l;
         double m = 0.0;
-        for (int i = 0; i < shard; ++i) m += (double)R.hm[i];
+        for (int i = 0; i < nl; ++i) m += (double)R.hm[i];
         num += (double)l * m;
         den += m;
       }
@@ -307,6 +347,8 @@ int main(int argc, char** argv) {
     }
     std::fclose(f);
   }
+  for (int r = 0; r < G; ++r)
+    if (dps[r] && a.attach) CHECK(nof_dp_attach(dps[r], nullptr, nullptr));
   for (nof_dp* d : dps)
     if (d) nof_dp_destroy(d);
   for (Replica& R : rs) {

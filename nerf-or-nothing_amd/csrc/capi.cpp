@@ -343,6 +343,28 @@ nof_status nof_dp_allreduce_grads_all(int32_t n, nof_dp* const* dps, nof_mipnerf
 nof_status nof_dp_destroy(nof_dp* dp) {
   return guard([&] { KEEP_DEVICE; dp_destroy(dp); });
 }
+nof_status nof_dp_init_loopback(int32_t k, int32_t device, nof_dp** out) {
+  return guard([&] { KEEP_DEVICE; ARG(out); dp_init_loopback(k, device, out); });
+}
+nof_status nof_dp_train_step(int32_t n, nof_dp* const* dps, nof_mipnerf* const* models, nof_adam* const* adams,
+                             nof_dataset* const* datasets, int32_t global_batch, int32_t micro_batch, uint64_t seed,
+                             int32_t step, float lr, float* loss_mult_sum) {
+  return guard([&] {
+    KEEP_DEVICE;
+    ARG(n >= 1 && models && adams && datasets && step >= 1);
+    std::vector<AcceleratedMipNeRF*> ms(n);
+    std::vector<AcceleratedAdamOptimizer*> as(n);
+    std::vector<RayDataset*> ds(n);
+    for (int i = 0; i < n; ++i) {
+      ARG(models[i] && adams[i] && datasets[i]);
+      ms[i] = models[i]->impl;
+      as[i] = adams[i]->impl;
+      ds[i] = datasets[i]->impl;
+    }
+    dp_train_step(n, dps, ms.data(), as.data(), ds.data(), global_batch, micro_batch, seed, (uint32_t)step, lr,
+                  loss_mult_sum);
+  });
+}
 nof_status nof_image_metrics(const float* img0, const float* img1, int32_t width, int32_t height, float max_val,
                              float* psnr, float* ssim, void* stream) {
   return guard([&] {

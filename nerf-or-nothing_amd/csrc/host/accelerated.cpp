@@ -513,7 +513,13 @@ AcceleratedMipNeRF::AcceleratedMipNeRF(const nof_config& cfg) : mlp(nullptr), cf
   }
 }
 
-AcceleratedMipNeRF::~AcceleratedMipNeRF() { delete mlp; }
+AcceleratedMipNeRF::~AcceleratedMipNeRF() {
+  if (attached_dp) {
+    mlp->set_bucket_hook(nullptr, nullptr);
+    dp_model_destroyed(attached_dp, this);
+  }
+  delete mlp;
+}
 
 float* const* AcceleratedMipNeRF::GetGradient(int n, const float* origins, const float* directions,
                                               const float* radii, const float* nears, const float* fars,

@@ -184,6 +184,9 @@ class AcceleratedMLP {
   size_t slab_cap_ = 0;
 };
 
+// dp.cpp: a model destroyed while attached clears the communicator's pointer to it
+void dp_model_destroyed(nof_dp* dp, class AcceleratedMipNeRF* model);
+
 // Gradient-arena spans (offset, count) of bucket b for layer sizes [W sizes..., b sizes...] of
 // num_layers layers; returns the span count (host only, no device needed).
 int grad_bucket_spans(const int* sizes, int num_layers, int b, int64_t* off, int64_t* cnt);
@@ -216,6 +219,7 @@ class AcceleratedMipNeRF {
   void Render(int n, const float* o, const float* d, const float* radii, const float* nears, const float* fars,
               int randomized, int white_bkgd, nof_render_out* out);
   KernelTimer timer;
+  nof_dp* attached_dp = nullptr;  // nof_dp_attach's communicator (detached by the destructor)
 
  private:
   float* const* run(int n, const float* o, const float* d, const float* radii, const float* nears,

@@ -11,11 +11,20 @@
 //
 // Overlap: nof_dp_attach installs the model's gradient-bucket hook, so the all-reduce of layers
 // 5..10 runs on a communication stream while the layer-0..4 weight gradients are computed.
+//
+// Loopback groups (SURVEY.md §4 "T0 DP logic"): nof_dp_init_loopback makes K communicators of one
+// process on ONE device whose all-reduce is a device sum of the K members' buffers (member order).
+// Everything above the collective — grouped calls, the bucket hook and its reverse-layer spans,
+// accumulation, the one-call training step — then runs with K > 1 models on a single GPU.  A loopback
+// collective completes when its last member arrives (every member's stream then waits for it); work
+// enqueued on an earlier member's stream in between is not ordered after it, so drivers run every
+// replica's gradient before any replica's Adam (nof_dp_train_step does).
 #include <rccl/rccl.h>
 
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <cstdlib>
@@ -23,6 +32,12 @@
 #include <thread>
 
 #include "dp.h"
+#include "trainer.h"
+#include "../kernels/launch.h"
+
+namespace AcceleratedNeRFUtils {
+struct LoopGroup;
+}
 
 struct nof_dp {
   ncclComm_t comm = nullptr;
@@ -37,6 +52,10 @@ struct nof_dp {
   hipStream_t comm_stream = nullptr;
   bool own_stream = false;
   hipEvent_t ready[AcceleratedNeRFUtils::AcceleratedMLP::kBuckets] = {};
+  float* scalar = nullptr;          // device word for the loss-multiplier sum exchange
+  // loopback member (comm == nullptr)
+  AcceleratedNeRFUtils::LoopGroup* loop = nullptr;
+  int member = 0;
 };
 
 namespace AcceleratedNeRFUtils {
@@ -93,6 +112,112 @@ static void mark_pending(nof_dp* dp, hipStream_t st) {
   if (!dp->done) NOF_HIP(hipEventCreateWithFlags(&dp->done, hipEventDisableTiming));
   NOF_HIP(hipEventRecord(dp->done, st));
   dp->pending = true;
+}
+
+// ---- loopback groups ----------------------------------------------------------------------------
+// Member j's n-th collective call joins collective n of the group (a member may run ahead: the bucket
+// hook of replica 0 publishes both buckets before replica 1 computes anything).  A collective
+// launches when its last member arrives.
+struct LoopGroup {
+  int k = 0, device = 0, alive = 0;
+  hipStream_t st = nullptr;  // the group's reduction stream
+  struct Pending {
+    int arrived = 0;
+    std::vector<std::vector<std::pair<float*, int64_t>>> spans;  // per member
+    std::vector<hipStream_t> streams;
+    std::vector<hipEvent_t> ready;  // member j's buffers are final
+  };
+  std::map<long, Pending> pending;  // by sequence number
+  std::vector<long> next_seq;       // per member
+  std::vector<nof_dp*> members;
+  std::vector<hipEvent_t> free_events;
+  hipEvent_t event() {
+    hipEvent_t e;
+    if (!free_events.empty()) {
+      e = free_events.back();
+      free_events.pop_back();
+    } else {
+      NOF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    return e;
+  }
+};
+
+static void loop_arrive(nof_dp* dp, std::vector<std::pair<float*, int64_t>> spans, hipStream_t st) {
+  LoopGroup& g = *dp->loop;
+  const int me = dp->member;
+  const long seq = g.next_seq[me]++;
+  LoopGroup::Pending& c = g.pending[seq];
+  if (c.arrived == 0) {
+    c.spans.resize(g.k);
+    c.streams.resize(g.k);
+    c.ready.assign(g.k, nullptr);
+  } else {
+    int first = 0;
+    while (c.spans[first].empty()) ++first;
+    NOF_REQUIRE(c.spans[first].size() == spans.size(), "loopback members disagree on the all-reduce spans");
+    for (size_t s = 0; s < spans.size(); ++s)
+      NOF_REQUIRE(c.spans[first][s].second == spans[s].second, "loopback members disagree on the all-reduce counts");
+  }
+  NOF_HIP(hipSetDevice(g.device));
+  c.ready[me] = g.event();
+  NOF_HIP(hipEventRecord(c.ready[me], st));
+  c.spans[me] = std::move(spans);
+  c.streams[me] = st;
+  if (++c.arrived < g.k) return;
+  for (int j = 0; j < g.k; ++j) NOF_HIP(hipStreamWaitEvent(g.st, c.ready[j], 0));
+  std::vector<float*> bufs(g.k);
+  for (size_t s = 0; s < c.spans[0].size(); ++s) {
+    for (int j = 0; j < g.k; ++j) bufs[j] = c.spans[j][s].first;
+    NOF_HIP(nof::launch_loopback_sum(g.k, bufs.data(), c.spans[0][s].second, g.st));
+  }
+  for (int j = 0; j < g.k; ++j) {
+    nof_dp* m = g.members[j];
+    NOF_REQUIRE(m, "loopback member destroyed");
+    mark_pending(m, g.st);
+    NOF_HIP(hipStreamWaitEvent(c.streams[j], m->done, 0));
+    g.free_events.push_back(c.ready[j]);
+  }
+  g.pending.erase(seq);
+}
+
+// a collective this member joined that still waits for a peer
+static bool loop_incomplete(const nof_dp* dp) {
+  for (const auto& kv : dp->loop->pending)
+    if (!kv.second.spans.empty() && !kv.second.spans[dp->member].empty()) return true;
+  return false;
+}
+
+void dp_init_loopback(int k, int device, nof_dp** out) {
+  NOF_REQUIRE(k >= 1 && k <= nof::kLoopMax && out, "loopback group size must be 1..8");
+  NOF_HIP(hipSetDevice(device));
+  auto* g = new LoopGroup;
+  g->k = k;
+  g->device = device;
+  g->alive = k;
+  g->next_seq.assign(k, 0);
+  NOF_HIP(hipStreamCreateWithFlags(&g->st, hipStreamNonBlocking));
+  for (int j = 0; j < k; ++j) {
+    out[j] = new nof_dp;
+    out[j]->loop = g;
+    out[j]->member = j;
+    out[j]->device = device;
+    out[j]->timeout_ms = default_timeout_ms();
+    g->members.push_back(out[j]);
+  }
+}
+
+int dp_world(const nof_dp* dp, int* rank) {
+  NOF_REQUIRE(dp, "null communicator");
+  if (dp->loop) {
+    if (rank) *rank = dp->member;
+    return dp->loop->k;
+  }
+  int n = 1, r = 0;
+  if (ncclCommCount(dp->comm, &n) != ncclSuccess || ncclCommUserRank(dp->comm, &r) != ncclSuccess)
+    throw Error(NOF_ERR_RCCL, "ncclCommCount / ncclCommUserRank failed");
+  if (rank) *rank = r;
+  return n;
 }
 
 void dp_unique_id(uint8_t out[128]) {
@@ -179,6 +304,7 @@ void dp_allreduce(nof_dp* dp, float* buf, int64_t count, hipStream_t st) {
   check_live(dp);
   NOF_REQUIRE(buf && count > 0, "bad all-reduce arguments");
   NOF_HIP(hipSetDevice(dp->device));
+  if (dp->loop) return loop_arrive(dp, {{buf, count}}, st);
   settle(dp, ncclAllReduce(buf, buf, (size_t)count, ncclFloat32, ncclSum, dp->comm, st), "ncclAllReduce",
          dp->timeout_ms);
   mark_pending(dp, st);
@@ -187,6 +313,14 @@ void dp_allreduce(nof_dp* dp, float* buf, int64_t count, hipStream_t st) {
 void dp_allreduce_grads(int n, nof_dp* const* dps, AcceleratedMipNeRF* const* models, hipStream_t const* streams) {
   NOF_REQUIRE(n >= 1 && dps && models, "bad all-reduce arguments");
   for (int i = 0; i < n; ++i) check_live(dps[i]);
+  if (dps[0]->loop) {
+    for (int i = 0; i < n; ++i) {
+      NOF_REQUIRE(dps[i]->loop, "a grouped all-reduce mixes loopback and RCCL communicators");
+      AcceleratedMLP& mlp = *models[i]->mlp;
+      loop_arrive(dps[i], {{mlp.flat_grads(), mlp.num_params()}}, streams ? streams[i] : mlp.stream());
+    }
+    return;
+  }
   NOF_HIP(hipSetDevice(dps[0]->device));
   ncclResult_t r = ncclGroupStart();  // one process driving several GPUs: one group, no deadlock
   for (int i = 0; i < n && (r == ncclSuccess || r == ncclInProgress); ++i) {
@@ -211,6 +345,11 @@ static void bucket_hook(void* user, int32_t bucket, int32_t nspans, const int64_
   check_live(dp);
   AcceleratedMLP& mlp = *dp->model->mlp;
   NOF_HIP(hipSetDevice(dp->device));
+  if (dp->loop) {  // the group sums this bucket once every member has published it
+    std::vector<std::pair<float*, int64_t>> sp;
+    for (int s = 0; s < nspans; ++s) sp.push_back({mlp.flat_grads() + off[s], cnt[s]});
+    return loop_arrive(dp, std::move(sp), mlp.stream());
+  }
   NOF_HIP(hipEventRecord(dp->ready[bucket], mlp.stream()));
   NOF_HIP(hipStreamWaitEvent(dp->comm_stream, dp->ready[bucket], 0));
   ncclResult_t r = ncclGroupStart();
@@ -226,11 +365,25 @@ static void bucket_hook(void* user, int32_t bucket, int32_t nspans, const int64_
   }
 }
 
+static void detach(nof_dp* dp) {
+  if (dp->model) {
+    dp->model->mlp->set_bucket_hook(nullptr, nullptr);
+    dp->model->attached_dp = nullptr;
+  }
+  dp->model = nullptr;
+}
+
+// ~AcceleratedMipNeRF: a model destroyed while attached detaches itself, so the communicator never
+// touches a freed model
+void dp_model_destroyed(nof_dp* dp, AcceleratedMipNeRF* model) {
+  if (dp && dp->model == model) dp->model = nullptr;
+}
+
 void dp_attach(nof_dp* dp, AcceleratedMipNeRF* model, hipStream_t comm_stream) {
   check_live(dp);
-  if (dp->model) dp->model->mlp->set_bucket_hook(nullptr, nullptr);
-  dp->model = nullptr;
+  detach(dp);
   if (!model) return;
+  NOF_REQUIRE(model->attached_dp == nullptr, "model already attached to another communicator");
   NOF_HIP(hipSetDevice(dp->device));
   for (hipEvent_t& e : dp->ready)
     if (!e) NOF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -245,11 +398,19 @@ void dp_attach(nof_dp* dp, AcceleratedMipNeRF* model, hipStream_t comm_stream) {
     dp->own_stream = true;
   }
   dp->model = model;
+  model->attached_dp = dp;
   model->mlp->set_bucket_hook(&bucket_hook, dp);
 }
 
 void dp_wait(nof_dp* dp, int timeout_ms) {
   check_live(dp);
+  if (dp->loop && loop_incomplete(dp)) {  // a peer that never arrives: the loopback "missing rank"
+    const std::string why = "loopback all-reduce incomplete: a member of the group of " +
+                            std::to_string(dp->loop->k) + " never arrived";
+    dp->aborted = true;
+    dp->why = why;
+    throw Error(NOF_ERR_RCCL, why);
+  }
   if (!dp->pending) return;
   const int limit = timeout_ms > 0 ? timeout_ms : dp->timeout_ms;
   const auto t0 = Clock::now();
@@ -258,7 +419,7 @@ void dp_wait(nof_dp* dp, int timeout_ms) {
     if (e == hipSuccess) break;
     if (e != hipErrorNotReady) NOF_HIP(e);
     ncclResult_t r = ncclSuccess;
-    if (ncclCommGetAsyncError(dp->comm, &r) != ncclSuccess) r = ncclSystemError;
+    if (dp->comm && ncclCommGetAsyncError(dp->comm, &r) != ncclSuccess) r = ncclSystemError;
     if (r != ncclSuccess && r != ncclInProgress)
       abort_comm(dp, std::string("asynchronous RCCL error: ") + ncclGetErrorString(r));
     if (std::chrono::duration_cast<std::chrono::milliseconds>(Clock::now() - t0).count() > limit)
@@ -271,8 +432,7 @@ void dp_wait(nof_dp* dp, int timeout_ms) {
 void dp_abort(nof_dp* dp) {
   NOF_REQUIRE(dp, "null communicator");
   if (dp->aborted) return;
-  if (dp->model) dp->model->mlp->set_bucket_hook(nullptr, nullptr);
-  dp->model = nullptr;
+  detach(dp);
   if (dp->comm) (void)ncclCommAbort(dp->comm);
   dp->aborted = true;
   dp->pending = false;
@@ -281,13 +441,111 @@ void dp_abort(nof_dp* dp) {
 
 void dp_destroy(nof_dp* dp) {
   if (!dp) return;
-  if (dp->model) dp->model->mlp->set_bucket_hook(nullptr, nullptr);
+  detach(dp);
+  if (dp->loop && --dp->loop->alive == 0) {
+    LoopGroup* g = dp->loop;
+    (void)hipStreamSynchronize(g->st);
+    for (hipEvent_t e : g->free_events) (void)hipEventDestroy(e);
+    for (auto& kv : g->pending)
+      for (hipEvent_t e : kv.second.ready)
+        if (e) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(g->st);
+    delete g;
+  } else if (dp->loop) {
+    for (nof_dp*& m : dp->loop->members)
+      if (m == dp) m = nullptr;
+  }
   if (dp->comm && !dp->aborted) (void)ncclCommDestroy(dp->comm);
   if (dp->done) (void)hipEventDestroy(dp->done);
   for (hipEvent_t e : dp->ready)
     if (e) (void)hipEventDestroy(e);
   if (dp->own_stream) (void)hipStreamDestroy(dp->comm_stream);
+  if (dp->scalar) (void)hipFree(dp->scalar);
   delete dp;
+}
+
+// ---- one data-parallel training step (SURVEY.md 8b "(new) DP": Program.cs:48-62 over n replicas) ----
+// sum of one float over the ranks of an RCCL communicator (the global loss-multiplier sum)
+static float allreduce_scalar(nof_dp* dp, float v, hipStream_t st) {
+  NOF_HIP(hipSetDevice(dp->device));
+  if (!dp->scalar) NOF_HIP(hipMalloc(&dp->scalar, sizeof(float)));
+  NOF_HIP(hipMemcpyAsync(dp->scalar, &v, sizeof(float), hipMemcpyHostToDevice, st));
+  settle(dp, ncclAllReduce(dp->scalar, dp->scalar, 1, ncclFloat32, ncclSum, dp->comm, st), "ncclAllReduce (loss-mult sum)",
+         dp->timeout_ms);
+  mark_pending(dp, st);
+  dp_wait(dp, 0);
+  NOF_HIP(hipMemcpyAsync(&v, dp->scalar, sizeof(float), hipMemcpyDeviceToHost, st));
+  NOF_HIP(hipStreamSynchronize(st));
+  return v;
+}
+
+void dp_train_step(int n, nof_dp* const* dps, AcceleratedMipNeRF* const* models, AcceleratedAdamOptimizer* const* adams,
+                   RayDataset* const* datasets, int global_batch, int micro_batch, uint64_t seed, uint32_t step, float lr,
+                   float* msum_out) {
+  NOF_REQUIRE(n >= 1 && n <= 64 && models && adams && datasets, "bad train-step arguments");
+  for (int r = 0; r < n; ++r) NOF_REQUIRE(models[r] && adams[r] && datasets[r], "null replica");
+  // the replicas' shard indices: n replicas in this process, or this process's rank of `world`
+  int world = n, rank0 = 0;
+  bool attached = false;
+  if (dps) {
+    for (int r = 0; r < n; ++r) check_live(dps[r]);
+    if (n == 1) {
+      world = dp_world(dps[0], &rank0);
+      NOF_REQUIRE(!(dps[0]->loop && world > 1), "a loopback group's members step together: pass all of them");
+    } else {
+      NOF_REQUIRE(dp_world(dps[0], nullptr) == n, "n replicas need a group of n communicators");
+      for (int r = 0; r < n; ++r) {
+        int rk = -1;
+        (void)dp_world(dps[r], &rk);
+        NOF_REQUIRE(rk == r, "communicator r must be rank r of the group");
+      }
+    }
+    attached = dps[0]->model != nullptr;
+    for (int r = 0; r < n; ++r)
+      NOF_REQUIRE((dps[r]->model != nullptr) == attached && (!attached || dps[r]->model == models[r]),
+                  "attach every replica's communicator to its model, or none");
+  }
+  NOF_REQUIRE(global_batch > 0 && global_batch % world == 0, "the global batch must divide into equal shards");
+  const int shard = global_batch / world;
+  const int micro = micro_batch > 0 ? std::min(micro_batch, shard) : shard;
+  NOF_REQUIRE(shard % micro == 0, "the shard must divide into equal micro-batches");
+  for (int r = 0; r < n; ++r) NOF_REQUIRE(micro <= models[r]->config().max_rays, "micro-batch exceeds max_rays");
+  const int J = shard / micro;
+  auto ray_base = [&](int r, int j) { return (uint32_t)((rank0 + r) * shard + j * micro); };
+  nof_batch b;
+  // pass 1: the global loss-multiplier sum (D14: float; every shard normalises by it) — the gather is
+  // deterministic in (seed, step, global ray id), so pass 2 re-gathers the same rays
+  float msum = 0.0f;
+  for (int r = 0; r < n; ++r) {
+    NOF_HIP(hipSetDevice(models[r]->device()));
+    for (int j = 0; j < J; ++j) {
+      float m = 0.0f;
+      datasets[r]->next(micro, seed, step, ray_base(r, j), models[r]->mlp->stream(), &b, &m);
+      msum += m;
+    }
+  }
+  if (dps && n == 1 && world > 1) msum = allreduce_scalar(dps[0], msum, models[0]->mlp->stream());
+  NOF_REQUIRE(msum > 0.0f, "the global batch has no loss weight");
+  // pass 2: every replica's gradient, micro-batch by micro-batch (ACCUMULATE after the first; PUBLISH
+  // on the last, so an attached communicator all-reduces the buckets as they complete)
+  for (int r = 0; r < n; ++r) {
+    NOF_HIP(hipSetDevice(models[r]->device()));
+    for (int j = 0; j < J; ++j) {
+      datasets[r]->next(micro, seed, step, ray_base(r, j), models[r]->mlp->stream(), &b, nullptr);
+      models[r]->set_rng(seed, step, ray_base(r, j));
+      const uint32_t flags = (j > 0 ? NOF_GRAD_ACCUMULATE : 0u) | (j == J - 1 ? NOF_GRAD_PUBLISH : 0u);
+      models[r]->GetGradientDevice(micro, b.origins, b.directions, b.radii, b.nears, b.fars, b.loss_mults, b.pixels,
+                                   msum, flags);
+    }
+  }
+  if (dps && !attached) dp_allreduce_grads(n, dps, models, nullptr);
+  for (int r = 0; r < n; ++r) {  // the same Adam on identical bits everywhere
+    NOF_HIP(hipSetDevice(models[r]->device()));
+    adams[r]->step(models[r]->mlp->allParams(), models[r]->mlp->allGradients(), lr);
+  }
+  if (dps)
+    for (int r = 0; r < n; ++r) dp_wait(dps[r], 0);  // bounded: an RCCL error or a stalled peer fails the step
+  if (msum_out) *msum_out = msum;
 }
 
 }  // namespace AcceleratedNeRFUtils

@@ -12,4 +12,11 @@ void dp_attach(nof_dp* dp, AcceleratedMipNeRF* model, hipStream_t comm_stream);
 void dp_wait(nof_dp* dp, int timeout_ms);
 void dp_abort(nof_dp* dp);
 void dp_destroy(nof_dp* dp);
+void dp_init_loopback(int k, int device, nof_dp** out);
+int dp_world(const nof_dp* dp, int* rank);
+class AcceleratedAdamOptimizer;
+class RayDataset;
+void dp_train_step(int n, nof_dp* const* dps, AcceleratedMipNeRF* const* models, AcceleratedAdamOptimizer* const* adams,
+                   RayDataset* const* datasets, int global_batch, int micro_batch, uint64_t seed, uint32_t step, float lr,
+                   float* msum_out);
 }  // namespace AcceleratedNeRFUtils

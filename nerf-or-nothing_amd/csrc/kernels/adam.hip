@@ -36,6 +36,28 @@ hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v, 
   return hipGetLastError();
 }
 
+// Loopback all-reduce (dp.cpp, SURVEY §4's "loopback DP backend"): the K member buffers of one device
+// summed in member order (fp32, the same bits as adding them one after another) and written back to
+// every member.
+struct LoopPtrs { float* p[kLoopMax]; };
+__global__ void k_loopback_sum(int k, LoopPtrs b, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float s = b.p[0][i];
+    for (int j = 1; j < k; ++j) s += b.p[j][i];
+    for (int j = 0; j < k; ++j) b.p[j][i] = s;
+  }
+}
+hipError_t launch_loopback_sum(int k, float* const* bufs, int64_t n, hipStream_t st) {
+  if (k < 1 || k > kLoopMax) return hipErrorInvalidValue;
+  if (n <= 0) return hipSuccess;
+  LoopPtrs b{};
+  for (int j = 0; j < k; ++j) b.p[j] = bufs[j];
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(k_loopback_sum, dim3((unsigned)blocks), dim3(256), 0, st, k, b, n);
+  return hipGetLastError();
+}
+
 // layer dims of the fixed 8x256 / 128 network (MLPcpp:131-154)
 __device__ inline int layer_out(int l) { return l < 8 ? 256 : (l == 8 ? 1 : (l == 9 ? 128 : 3)); }
 __device__ inline int layer_in(int l) {

@@ -130,6 +130,9 @@ hipError_t launch_generate_rays(const float* poses, int V, int w, int h, float f
 hipError_t image_metrics(const float* a, const float* b, int W, int H, float max_val, float* psnr, float* ssim,
                          hipStream_t st);
 
+// loopback all-reduce: bufs[0..k) (k <= kLoopMax, one device) <- their element-wise sum in member order
+constexpr int kLoopMax = 8;
+hipError_t launch_loopback_sum(int k, float* const* bufs, int64_t n, hipStream_t st);
 hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v, float lr, float inv1, float inv2,
                        hipStream_t st);
 struct PackArgs { int woff[11]; int boff[11]; };

@@ -25,6 +25,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t h32_rsrc(const void* p) {
 }
 __device__ __forceinline__ void store_b64(__amdgpu_buffer_rsrc_t r, uint32_t voff, int imm, uint32_t lo, uint32_t hi) {
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+#ifdef NOF_DIAG_H32_NOSTORE  // diagnostic: no side-output stores (keeps one dependency so nothing is dead)
+  if (lo == 0x7fff1234u && hi == 0x1234u) __builtin_amdgcn_raw_buffer_store_b64((u32x2{lo, hi}), r, (int)voff, imm, 0);
+  return;
+#endif
   __builtin_amdgcn_raw_buffer_store_b64((u32x2{lo, hi}), r, (int)voff, imm, 0);
 }
 __device__ __forceinline__ void store_b128(__amdgpu_buffer_rsrc_t r, uint32_t voff, int imm, const u32x4& v) {
@@ -284,7 +288,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
     const float* src = is8 ? tail + kFwdTailW8 : tail + kFwdTailW10 + c * 128;
     reinterpret_cast<uint32_t*>(lds + (is8 ? kW8 : kW10))[i] = pk_h(src[f], src[f + 1]);
   }
-  __syncthreads();  // tables written, periods 0 and 1 landed
+  h32_prologue_barrier();  // tables written (lgkmcnt), periods 0 and 1 landed
 
   // ---- layers -------------------------------------------------------------------------------------
   f32x16 acc[2];
@@ -455,7 +459,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
     }
     if (h == 0) store_b64(d9, (uint32_t)x * 320u, 256, pk_h(dzs, dzc[0]), pk_h(dzc[1], dzc[2]));  // features 128..131
   }
-  __syncthreads();  // w8 table written, periods 0 and 1 landed
+  h32_prologue_barrier();  // w8 table written, periods 0 and 1 landed
 
   f32x16 acc[2];
   const size_t lstride = (size_t)nblk * kBlk * kWidth;

@@ -37,6 +37,8 @@
 // even registers, high half: odd registers) — packed dword k = 8 (T & 1) + d of tile T (registers 2d,
 // 2d + 1) at bit 15 - k of each half.
 #pragma once
+#include <type_traits>
+
 #include "mlp16.h"
 
 namespace nof {
@@ -46,8 +48,13 @@ constexpr int kH32Waves = 8;      // one 32-sample block per wave
 constexpr int kFragFloats = 256;  // one k-step fragment image: 64 lanes x 8 halves (1 KB)
 constexpr int kPeriod = 16;       // fragments per ring slot
 constexpr int kPeriodFloats = kPeriod * kFragFloats;
-constexpr int kH32Slots = 4;
-constexpr int kH32RingFloats = kH32Slots * kPeriodFloats;  // 64 KB
+// LDS-DMA takes ~1 us from issue to landing (MI355X_MICROARCH.md ldsdma-fill; measured here: with the
+// fetch two periods ahead the waves spent ~40 % of their time in the period barrier's vmcnt wait), so
+// the stream runs kDmaAhead periods ahead through an 8-slot ring (128 KB).
+constexpr int kH32Slots = 8;
+constexpr int kDmaAhead = 6;  // period P + kDmaAhead is fetched during period P (into the slot P - 2 left)
+static_assert(kDmaAhead + 2 <= kH32Slots, "a slot is refilled only after every wave has read it");
+constexpr int kH32RingFloats = kH32Slots * kPeriodFloats;  // 128 KB
 
 // weight streams: segments (layer, k-steps per chunk, chunks) in consumption order
 struct H32Seg {
@@ -63,7 +70,7 @@ __host__ __device__ constexpr H32Seg bwd_seg(int i) {  // L9 (dh7 <- delta9), th
 constexpr int kFwdFrags = 8 * 6 + 6 * 8 * 16 + 8 * 22 + 4 * 16;  // 1056
 constexpr int kBwdFrags = 8 * 8 + 7 * 8 * 16;                     // 960
 static_assert(kFwdFrags % kPeriod == 0 && kBwdFrags % kPeriod == 0, "streams are whole periods");
-constexpr int kStreamPad = 2 * kPeriod;  // the DMA runs two periods past the end: zero padding
+constexpr int kStreamPad = kDmaAhead * kPeriod;  // the DMA runs kDmaAhead periods past the end: zero padding
 // images (floats): fragments (+ pad), then the fp32 tail of mlp_common.h (kFwdTail / kBwdTail layout)
 constexpr size_t kFwdH32Floats = (size_t)(kFwdFrags + kStreamPad) * kFragFloats;
 constexpr size_t kBwdH32Floats = (size_t)(kBwdFrags + kStreamPad) * kFragFloats;
@@ -103,47 +110,63 @@ __device__ __forceinline__ uint32_t mask_expand(uint32_t w, int k) {
   return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, m) >> (s16x2{15, 15}));
 }
 
-// End of a ring period: this wave's DMA of the next period has landed once at most n VMEM ops are
-// outstanding (n = the ops issued in this period: its 2 DMA steps and its stores, all younger), every
-// wave's LDS reads of this period are done, then the workgroup barrier.
+// End of a ring period P: this wave's DMA of period P + 1 has landed once at most n VMEM ops are
+// outstanding — n = the ops issued after it: the DMA steps of periods P + 2 .. P + kDmaAhead (two each)
+// and this period's stores (a lower bound: the earlier periods' stores are older than some of those
+// DMAs and only make the true count larger); every wave's LDS reads of the period are done; then the
+// workgroup barrier.
 __device__ __forceinline__ void h32_barrier(int n) {
 #define NOF_H32_BAR(N) \
   case N: asm volatile("s_waitcnt vmcnt(" #N ")\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
-  switch (n < 0 ? 0 : (n > 24 ? 24 : n)) {
+  switch (n < 0 ? 0 : (n > 31 ? 31 : n)) {
     NOF_H32_BAR(0) NOF_H32_BAR(1) NOF_H32_BAR(2) NOF_H32_BAR(3) NOF_H32_BAR(4) NOF_H32_BAR(5) NOF_H32_BAR(6)
     NOF_H32_BAR(7) NOF_H32_BAR(8) NOF_H32_BAR(9) NOF_H32_BAR(10) NOF_H32_BAR(11) NOF_H32_BAR(12) NOF_H32_BAR(13)
     NOF_H32_BAR(14) NOF_H32_BAR(15) NOF_H32_BAR(16) NOF_H32_BAR(17) NOF_H32_BAR(18) NOF_H32_BAR(19) NOF_H32_BAR(20)
-    NOF_H32_BAR(21) NOF_H32_BAR(22) NOF_H32_BAR(23)
-    default: asm volatile("s_waitcnt vmcnt(24)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    NOF_H32_BAR(21) NOF_H32_BAR(22) NOF_H32_BAR(23) NOF_H32_BAR(24) NOF_H32_BAR(25) NOF_H32_BAR(26) NOF_H32_BAR(27)
+    NOF_H32_BAR(28) NOF_H32_BAR(29) NOF_H32_BAR(30)
+    default: asm volatile("s_waitcnt vmcnt(31)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
   }
 #undef NOF_H32_BAR
 }
+#ifdef NOF_DIAG_H32_NOBAR  // diagnostic: the period barrier without s_barrier
+#define h32_barrier(n) asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#endif
 
-// The weight ring.  `next` = stream position of period P + 2 while period P is consumed from slot `cur`.
+// The weight ring.  `next` = stream position of period P + kDmaAhead while period P is consumed from
+// slot `cur`.
 struct H32Ring {
   float* lds;
   const float* next;
   int cur;
-  __device__ __forceinline__ void prologue(const float* stream, int tid) {  // periods 0, 1 -> slots 0, 1
-    slice16_dma_step(stream, lds, tid, 0);
-    slice16_dma_step(stream, lds, tid, 1);
-    slice16_dma_step(stream + kPeriodFloats, lds + kPeriodFloats, tid, 0);
-    slice16_dma_step(stream + kPeriodFloats, lds + kPeriodFloats, tid, 1);
-    next = stream + 2 * kPeriodFloats;
+  // periods 0 .. kDmaAhead - 1 into slots 0 .. kDmaAhead - 1; the caller's barrier then waits for the
+  // first two (prologue_wait)
+  __device__ __forceinline__ void prologue(const float* stream, int tid) {
+#pragma unroll
+    for (int p = 0; p < kDmaAhead; ++p) {
+      slice16_dma_step(stream + p * kPeriodFloats, lds + p * kPeriodFloats, tid, 0);
+      slice16_dma_step(stream + p * kPeriodFloats, lds + p * kPeriodFloats, tid, 1);
+    }
+    next = stream + kDmaAhead * kPeriodFloats;
     cur = 0;
   }
   __device__ __forceinline__ void dma(int step, int tid) {
-    slice16_dma_step(next, lds + ((cur + 2) & 3) * kPeriodFloats, tid, step);
+#ifdef NOF_DIAG_H32_NODMA  // diagnostic builds only (timings; results are garbage)
+    return;
+#endif
+    slice16_dma_step(next, lds + ((cur + kDmaAhead) & (kH32Slots - 1)) * kPeriodFloats, tid, step);
   }
   __device__ __forceinline__ void end_period(int nstores) {
-    h32_barrier(2 + nstores);
-    cur = (cur + 1) & 3;
+    h32_barrier(2 * (kDmaAhead - 1) + nstores);
+    cur = (cur + 1) & (kH32Slots - 1);
     next += kPeriodFloats;
   }
   __device__ __forceinline__ f16x8 frag(int i, int lane) const {  // fragment i (0..15) of the current period
     return reinterpret_cast<const f16x8*>(lds + cur * kPeriodFloats + i * kFragFloats)[lane];
   }
 };
+// the prologue's barrier: periods 0 and 1 landed (this wave's part), the later ones may stay in flight;
+// then the workgroup barrier (which also publishes the LDS tables written before it)
+__device__ __forceinline__ void h32_prologue_barrier() { h32_barrier(2 * (kDmaAhead - 2)); }
 
 // Epilogue piece schedule inside a host chunk of NK k-steps: the 8 packed dwords' VALU, then the 4
 // side stores (and the layer's mask store with the last), then the C-operand load of the next chunk.
@@ -169,47 +192,59 @@ __device__ __forceinline__ f32x16 cinit_load(const float* v, int c) {
   return r;
 }
 
+// A-fragment reads run kReadAhead k-steps ahead of their MFMA (one ahead exposed the LDS latency: each
+// wave's MFMAs come 64 cycles apart at two waves per SIMD).  Reads of the next period's fragments need
+// its DMA landed in every wave's part, so the period's barrier sits kReadAhead fragments before its end.
+constexpr int kReadAhead = 2;
+constexpr int kBarrierPos = kPeriod - 1 - kReadAhead;
+
 // One layer: NC chunks of 32 output rows x NK k-steps.  bsrc(kk) gives k-step kk's B fragment (4
 // packed dwords); chunk c accumulates into acc[c & 1]; epi.piece(T, kk, NK) runs the epilogue of
 // this layer's tile T = c - 1 at k-step kk of chunk c, prev.piece the previous layer's last tile in
 // chunk 0 (its tile index NCp - 1 is odd: acc[1]).  cv: the layer's C-operand vector (LDS, + 4h;
 // kBias false: C = 0).  Returns with the last tile's epilogue pending (the caller's next layer or a
-// drain).  Every loop is unrolled: all positions and store counts are constants.
+// drain).  Every loop is unrolled: all positions and store counts are constants.  The layer starts at
+// a period boundary, one barrier past the point where its first kReadAhead fragments may be read.
+// compile-time loop: f(std::integral_constant<int, I>) for I = B .. E - 1 (a #pragma unroll loop of this
+// size is not always unrolled, and a runtime k-step index turns every B-register access into a select chain)
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
 template <int NK, int NC, bool kBias, class BSrc, class Epi, class Prev>
 __device__ __forceinline__ void h32_layer(const BSrc& bsrc, f32x16 (&acc)[2], H32Ring& ring, Epi& epi, Prev& prev,
                                           const float* cv, int tid, int lane) {
   static_assert((NK * NC) % kPeriod == 0, "a layer is a whole number of ring periods");
   static_assert(NC % 2 == 0 && Prev::kNC % 2 == 0, "the pending last tile of a layer sits in acc[1]");
+  constexpr int N = NK * NC;
+  constexpr int R = kReadAhead + 1;
   if constexpr (kBias) acc[0] = cinit_load(cv, 0);
-  int nst = 0;  // stores issued in the current period
-  f16x8 a = ring.frag(0, lane);
+  int nst = 0;  // stores issued in the current period before its barrier
+  f16x8 fr[R];
 #pragma unroll
-  for (int c = 0; c < NC; ++c) {
-#pragma unroll
-    for (int kk = 0; kk < NK; ++kk) {
-      const int i = c * NK + kk, pos = i & (kPeriod - 1);
-      asm volatile("" ::"v"(a));  // fragment i has landed in registers before the next read issues
-      f16x8 an = a;
-      if (pos == 0) ring.dma(0, tid);
-      if (pos == 1) ring.dma(1, tid);
-      if (pos != kPeriod - 1) an = ring.frag(pos + 1, lane);
-      __builtin_amdgcn_sched_barrier(0);
-      uint32_t b[4];
-      bsrc(kk, b);
-      acc[c & 1] = mfma_h32(a, b, (kk == 0 && !kBias) ? f32x16{} : acc[c & 1]);
-      if (c == 0) nst += prev.piece(Prev::kNC - 1, kk, NK);  // the previous layer's last tile (acc[1])
-      else nst += epi.piece(c - 1, kk, NK);
-      if constexpr (kBias)
-        if (c + 1 < NC && kk == cinit_pos(NK)) acc[(c + 1) & 1] = cinit_load(cv, c + 1);
-      __builtin_amdgcn_sched_barrier(0);
-      if (pos == kPeriod - 1) {
-        ring.end_period(nst);
-        nst = 0;
-        if (i + 1 < NK * NC) an = ring.frag(0, lane);
-      }
-      a = an;
+  for (int i = 0; i < kReadAhead; ++i) fr[i] = ring.frag(i, lane);  // (cur: already this period's slot)
+  static_for<0, N>([&](auto ic) {
+    constexpr int i = decltype(ic)::value, c = i / NK, kk = i % NK, pos = i % kPeriod;
+    asm volatile("" ::"v"(fr[i % R]));  // fragment i has landed before more reads issue
+    if constexpr (pos < 2) ring.dma(pos, tid);
+    if constexpr (i + kReadAhead < N) fr[(i + kReadAhead) % R] = ring.frag((pos + kReadAhead) % kPeriod, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t b[4];
+    bsrc(kk, b);
+    acc[c & 1] = mfma_h32(fr[i % R], b, (kk == 0 && !kBias) ? f32x16{} : acc[c & 1]);
+    if constexpr (c == 0) nst += prev.piece(Prev::kNC - 1, kk, NK);  // the previous layer's last tile (acc[1])
+    else nst += epi.piece(c - 1, kk, NK);
+    if constexpr (kBias && c + 1 < NC && kk == cinit_pos(NK)) acc[(c + 1) & 1] = cinit_load(cv, c + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (pos == kBarrierPos) {  // the next period's reads start at the next position
+      ring.end_period(nst);
+      nst = 0;
     }
-  }
+  });
 }
 
 }  // namespace nof

@@ -696,12 +696,15 @@ __device__ __forceinline__ void wg_item_s(const WgItem& item, const WgProblem& P
   // transposed-read address of this lane inside a tile image (halves): row 8h + q, column 16 (G & 1) + 4p
   const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   const int toff = (8 * (G >> 1) + q) * 32 + 16 * (G & 1) + 4 * p;
-  typedef __attribute__((address_space(3))) s16x4v* tr_ptr;
-  auto frag = [&](const _Float16* tile, int ks) {
-    const _Float16* a = tile + toff + ks * 16 * 32;
-    const s16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr)(a));
-    const s16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((tr_ptr)(a + 4 * 32));
-    return __builtin_bit_cast(f16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+  // inline asm: through the builtin the compiler orders every transposed read behind the LDS-DMA in
+  // flight (s_waitcnt vmcnt(0) before each k-block's reads); the ring's own counted waits order them
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
+  // (the asm outputs are written asynchronously: nothing may copy them before the lgkmcnt wait, so each
+  // read has its own output and the fragments are assembled after the wait)
+  auto frag = [&](const _Float16* tile, int ks, s16x4v& lo, s16x4v& hi) {
+    const uint32_t a = lds_base + (uint32_t)((tile - lds) + toff + ks * 16 * 32) * 2u;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a));
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:256" : "=v"(hi) : "v"(a));
   };
 #pragma unroll
   for (int k = 0; k < kWhStages - 1; ++k) dma(k);
@@ -712,11 +715,23 @@ __device__ __forceinline__ void wg_item_s(const WgItem& item, const WgProblem& P
     const _Float16* st = lds + (k % kWhStages) * kWhStageHalves;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
+      s16x4v al[RB], ah[RB], bl[CB], bh[CB];
+#pragma unroll
+      for (int r = 0; r < RB; ++r) frag(st + rowt[r] * 1024, ks, al[r], ah[r]);
+#pragma unroll
+      for (int c = 0; c < CB; ++c) frag(st + (P.ntr + colt[c]) * 1024, ks, bl[c], bh[c]);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       f16x8 fa[RB], fb[CB];
 #pragma unroll
-      for (int r = 0; r < RB; ++r) fa[r] = frag(st + rowt[r] * 1024, ks);
+      for (int r = 0; r < RB; ++r) {
+        asm volatile("" : "+v"(al[r]), "+v"(ah[r]));  // defined here, after the wait
+        fa[r] = __builtin_bit_cast(f16x8, __builtin_shufflevector(al[r], ah[r], 0, 1, 2, 3, 4, 5, 6, 7));
+      }
 #pragma unroll
-      for (int c = 0; c < CB; ++c) fb[c] = frag(st + (P.ntr + colt[c]) * 1024, ks);
+      for (int c = 0; c < CB; ++c) {
+        asm volatile("" : "+v"(bl[c]), "+v"(bh[c]));
+        fb[c] = __builtin_bit_cast(f16x8, __builtin_shufflevector(bl[c], bh[c], 0, 1, 2, 3, 4, 5, 6, 7));
+      }
 #pragma unroll
       for (int r = 0; r < RB; ++r)
 #pragma unroll

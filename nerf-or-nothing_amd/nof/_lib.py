@@ -115,6 +115,9 @@ SIGNATURES = {
     "nof_dp_allreduce_grads": [P, P, P],
     "nof_dp_allreduce_grads_all": [I32, C.POINTER(P), C.POINTER(P), C.POINTER(P)],
     "nof_dp_destroy": [P],
+    "nof_dp_init_loopback": [I32, I32, C.POINTER(P)],
+    "nof_dp_train_step": [I32, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P), I32, I32, U64, I32, F,
+                          C.POINTER(F)],
     "nof_checkpoint_save": [C.c_char_p, P, P],
     "nof_checkpoint_load": [C.c_char_p, P, P],
     "nof_mipnerf_enable_timing": [P, I32],
@@ -168,11 +171,15 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"HIP extension missing: {LIB_PATH}. Build it with `python -c "
                                f"'import __graft_entry__ as g; g.build()'` or `make -C nerf-or-nothing_amd`.")
-        # torch first: its bundled libamdhip64 carries the soname libamdhip64.so.7 that libnof.so
-        # needs, so the library binds to the HIP runtime already in the process.  Loaded the other
-        # way round, torch's libraries (which name the file libamdhip64.so) bring in a second HIP +
-        # HSA runtime, and whichever initialises second finds no device.
-        import torch  # noqa: F401
+        # torch first when it is installed: its bundled libamdhip64 carries the soname
+        # libamdhip64.so.7 that libnof.so needs, so the library binds to the HIP runtime already in
+        # the process.  Loaded the other way round, torch's libraries (which name the file
+        # libamdhip64.so) bring in a second HIP + HSA runtime, and whichever initialises second finds
+        # no device.  Without torch (a C# / plain-ctypes host) libnof.so loads the system runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
 
         L = C.CDLL(LIB_PATH)
         for name, args in SIGNATURES.items():

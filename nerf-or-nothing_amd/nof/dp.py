@@ -69,6 +69,7 @@ class NativeDP:
 
     def __init__(self, handle):
         self._h = handle
+        self._model = None  # the attached model, kept alive while attached
 
     @staticmethod
     def unique_id() -> bytes:
@@ -90,6 +91,17 @@ class NativeDP:
         call("nof_dp_init_rank_timeout", (C.c_uint8 * 128).from_buffer_copy(uid), world, rank, device, timeout_ms,
              C.byref(h))
         return cls(h)
+
+    @classmethod
+    def init_loopback(cls, k: int, device: int = 0) -> list:
+        """k communicators on ONE device whose all-reduce is a device sum in member order (SURVEY §4's
+        loopback backend): the native DP choreography with k models on one GPU."""
+        import ctypes as C
+        from ._lib import call
+
+        hs = (C.c_void_p * k)()
+        call("nof_dp_init_loopback", k, device, hs)
+        return [cls(C.c_void_p(h)) for h in hs]
 
     @classmethod
     def init_all(cls, devices) -> list:
@@ -127,6 +139,7 @@ class NativeDP:
         from ._lib import call
 
         call("nof_dp_attach", self._h, model._h if model is not None else None, comm_stream)
+        self._model = model
 
     def wait(self, timeout_ms: int = 0):
         """Failure detection: block until the last all-reduce is done; an RCCL error or a timeout
@@ -146,6 +159,24 @@ class NativeDP:
 
             lib().nof_dp_destroy(self._h)
             self._h = None
+            self._model = None
+
+
+def train_step(dps, models, adams, datasets, global_batch: int, step: int, lr: float, seed: int,
+               micro_batch: int = 0) -> float:
+    """nof_dp_train_step (include/nof.h): one data-parallel TrainStep over len(models) replicas —
+    shards with global ray ids, the global loss-multiplier sum, micro-batch accumulation, the gradient
+    all-reduce, Adam and a bounded wait; dps = None: one replica, no exchange.  Returns the global sum."""
+    import ctypes as C
+    from ._lib import call
+
+    n = len(models)
+    msum = C.c_float()
+    dph = (C.c_void_p * n)(*[d._h.value for d in dps]) if dps else None
+    call("nof_dp_train_step", n, dph, (C.c_void_p * n)(*[m._h.value for m in models]),
+         (C.c_void_p * n)(*[a._h.value for a in adams]), (C.c_void_p * n)(*[d._h.value for d in datasets]),
+         global_batch, micro_batch, seed, step, lr, C.byref(msum))
+    return msum.value
 
 
 class BucketedAllReduce:

@@ -83,9 +83,13 @@ class Trainer:
         self.step_idx = step
         if self.print_every and step % self.print_every == 0:
             bad = self.model.numeric_status(clear=True)
+            if self.dist is not None:  # every rank raises together (a lone raise would hang its peers)
+                t = torch.tensor([bad], dtype=torch.int64, device=f"cuda:{self.device}")
+                self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+                bad = int(t.item())
             if bad:  # e.g. fp16 activation overflow in the f16x2 perf mode: fail loudly, not silently
-                raise FloatingPointError(f"step {step}: non-finite values in the training step (flags {bad:#x}; "
-                                         "1 = forward outputs, 2 = output gradients)")
+                raise FloatingPointError(f"step {step}: non-finite values in the training step on some rank "
+                                         f"(flags {bad:#x}; 1 = forward outputs, 2 = output gradients)")
             self.last_loss = self.fine_loss(b)
             if self.rank == 0:
                 print(f"Step {step}/{self.lr['max_steps']}, Loss: {self.last_loss}", flush=True)

@@ -31,8 +31,12 @@ __device__ __forceinline__ void store_b64(__amdgpu_buffer_rsrc_t r, uint32_t vof
 #endif
   __builtin_amdgcn_raw_buffer_store_b64((u32x2{lo, hi}), r, (int)voff, imm, 0);
 }
+// 16-B store: the data registers stay untouched for two wait states after the store issues — measured:
+// a VALU that overwrote a data register in the next instruction corrupted the stored dword
+// (nondeterministic act_h9 tiles; the compiler inserted no wait state for this >8-byte store-data hazard)
 __device__ __forceinline__ void store_b128(__amdgpu_buffer_rsrc_t r, uint32_t voff, int imm, const u32x4& v) {
   __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, imm, 0);
+  asm volatile("s_nop 1" ::"v"(v) : "memory");
 }
 __device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
   return __builtin_amdgcn_fdot2(__builtin_bit_cast(h16x2, a), __builtin_bit_cast(h16x2, b), c, false);
@@ -101,13 +105,17 @@ struct FwdEpiH {
         if (dens) zs = dot2(p, w8[T * 16 + d], zs);
       }
     if constexpr (kStore) {
+      if (kk == epi_rows_pos(NK)) {
+        uint32_t p[8];
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (kk == epi_store_pos(q, NK)) {
-          store_b64(blk, voff, 64 * T + 16 * q, dst[2 * T + (q >> 1)][2 * (q & 1)], dst[2 * T + (q >> 1)][2 * (q & 1) + 1]);
-          ++n;
-        }
-      if (T == kNC - 1 && kk == epi_store_pos(3, NK)) {
+        for (int d = 0; d < 8; ++d) p[d] = dst[2 * T + (d >> 2)][d & 3];
+        u32x4 ra, rb;
+        tile_row(p, ra, rb);
+        store_b128(blk, voff, 2048 * T, ra);
+        store_b128(blk, voff, 2048 * T + 16, rb);
+        n += 2;
+      }
+      if (T == kNC - 1 && kk == epi_mask_pos(NK)) {
         store_b128(mrs, moff, mimm, u32x4{mw[0], mw[1], mw[2], mw[3]});
         ++n;
       }
@@ -147,13 +155,14 @@ struct ViewEpiH {
         for (int c = 0; c < 3; ++c) zc[c] = dot2(p, w10[(c * 4 + T) * 16 + d], zc[c]);
       }
     if constexpr (kStore) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (kk == epi_store_pos(q, NK)) {
-          store_b64(blk, voff, 64 * T + 16 * q, p8[2 * q], p8[2 * q + 1]);
-          ++n;
-        }
-      if (T == kNC - 1 && kk == epi_store_pos(3, NK)) {
+      if (kk == epi_rows_pos(NK)) {
+        u32x4 ra, rb;
+        tile_row(p8, ra, rb);
+        store_b128(blk, voff, 2048 * T, ra);
+        store_b128(blk, voff, 2048 * T + 16, rb);
+        n += 2;
+      }
+      if (T == kNC - 1 && kk == epi_mask_pos(NK)) {
         store_b128(mrs, moff, 8 * 1024, u32x4{mw[0], mw[1], mw[2], mw[3]});
         ++n;
       }
@@ -227,16 +236,15 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
 #pragma unroll
   for (int k = 0; k < kDirIn; ++k) pe[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pe_l), k));
 
-  const uint32_t voff256 = (uint32_t)x * 512u + 8u * h;  // [M][256] rows: sample x, lane half h
-  const uint32_t voff128 = (uint32_t)x * 256u + 8u * h;  // [M][128] rows
+  const uint32_t vrow = tile_row_off(x, h);  // (sample x, lane half h) in a tiled block
   const uint32_t moff = (uint32_t)lane * 16u;
   const void* masks_blk = a.masks + (size_t)blk * kMaskSlots * 256;
   if constexpr (kStore) {  // act_in row: IPE 0..95 (this lane: 48h ..), view PE 96..122, zeros 123..127
     const __amdgpu_buffer_rsrc_t r = h32_rsrc(reinterpret_cast<const _Float16*>(a.act_in) + (size_t)m0 * kInF);
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      const int kk = k >> 1, q = k & 1;
-      store_b128(r, (uint32_t)x * 256u + 96u * h, 16 * k,
+    for (int k = 0; k < 6; ++k) {  // features 48h + 8k .. + 7: tile (48h + 8k) >> 5, column (48h + 8k) & 31
+      const int kk = k >> 1, q = k & 1, f = 48 * h + 8 * k;
+      store_b128(r, (uint32_t)(f >> 5) * 2048u + (uint32_t)x * 64u + (uint32_t)(f & 31) * 2u, 0,
                  u32x4{ix[kk][2 * q], ix[kk][2 * q + 1], iy[kk][2 * q], iy[kk][2 * q + 1]});
     }
     uint32_t w[8];
@@ -250,20 +258,21 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
       }
       w[i] = pk_h(v[0], v[1]);
     }
-    store_b128(r, (uint32_t)x * 256u + 32u * h, 192, u32x4{w[0], w[1], w[2], w[3]});
-    store_b128(r, (uint32_t)x * 256u + 32u * h, 208, u32x4{w[4], w[5], w[6], w[7]});
+    store_b128(r, vrow, 3 * 2048, u32x4{w[0], w[1], w[2], w[3]});  // tile 3: features 96 + 16h ..
+    store_b128(r, vrow, 3 * 2048 + 16, u32x4{w[4], w[5], w[6], w[7]});
   }
   // the B fragments of layers 0 / 4: k-steps 0..2 from the lane half h = 0, 3..5 from h = 1 — one
   // permlane32 swap per packed dword moves each half's other-h' pairs across (tools/probe/h32_probe.hip)
   uint32_t ipe[6][4];
 #pragma unroll
-  for (int kk = 0; kk < 3; ++kk)
+  for (int kk = 0; kk < 3; ++kk) {  // after the swap: ix = k-step kk's pairs, iy = k-step kk + 3's
+    swap32x4(ix[kk], iy[kk]);       // (h = 0 keeps its ix, gets the h = 1 lane's ix; h = 1 the reverse for iy)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {  // v_permlane32_swap: vdst lanes 32..63 <-> src0 lanes 0..31 (measured)
-      const auto r = __builtin_amdgcn_permlane32_swap(ix[kk][e], iy[kk][e], false, false);
-      ipe[kk][e] = r[0];      // h = 0: its own ix; h = 1: the h = 0 lane's iy
-      ipe[kk + 3][e] = r[1];  // h = 0: the h = 1 lane's ix; h = 1: its own iy
+    for (int e = 0; e < 4; ++e) {
+      ipe[kk][e] = ix[kk][e];
+      ipe[kk + 3][e] = iy[kk][e];
     }
+  }
 
   // ---- LDS tables: trunk biases, the wave's view-direction bias, packed w8 / W10 -------------------
   for (int i = tid; i < 2048 / 4; i += kH32Threads)
@@ -298,7 +307,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   const float* bias_h = lds + kBias + 4 * h;
   const uint32_t* w8h = reinterpret_cast<const uint32_t*>(lds + kW8) + 8 * h;
   uint32_t mwX[4], mwY[4], mwV[4], p8[8];
-  FwdEpiH<kStore> eX(acc, X, mwX, voff256, moff), eY(acc, Y, mwY, voff256, moff);
+  FwdEpiH<kStore> eX(acc, X, mwX, vrow, moff), eY(acc, Y, mwY, vrow, moff);
   NoEpiH none;
   auto srcI = [&](int kk, uint32_t (&b)[4]) {
 #pragma unroll
@@ -333,7 +342,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   }
   static_assert(kDepth == 8 && kSkip == 4, "the trunk schedule assumes 8 layers, skip into layer 4");
   // ---- view layer 9: relu(W9[:, :256] h7 + dirbias), the RGB head (layer 10) in its epilogue ----------
-  ViewEpiH<kStore> eV(acc, mwV, p8, voff128, moff, reinterpret_cast<const _Float16*>(a.act_h9) + (size_t)m0 * kWidthCond,
+  ViewEpiH<kStore> eV(acc, mwV, p8, vrow, moff, reinterpret_cast<const _Float16*>(a.act_h9) + (size_t)m0 * kWidthCond,
                       masks_blk, reinterpret_cast<const uint32_t*>(lds + kW10) + 8 * h);
   h32_layer<16, 4, true>(srcY, acc, ring, eV, eY, lds + kDirb + wave * 128 + 4 * h, tid, lane);
 #pragma unroll
@@ -389,12 +398,16 @@ struct BwdEpiH {
         const uint32_t word = (T >> 1) == 0 ? mk.x : ((T >> 1) == 1 ? mk.y : ((T >> 1) == 2 ? mk.z : mk.w));
         dst[2 * T + (d >> 2)][d & 3] = pk_h(v0, v1) & mask_expand(word, 8 * (T & 1) + d);
       }
+    if (kk == epi_rows_pos(NK)) {
+      uint32_t p[8];
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (kk == epi_store_pos(q, NK)) {
-        store_b64(blk, voff, 64 * T + 16 * q, dst[2 * T + (q >> 1)][2 * (q & 1)], dst[2 * T + (q >> 1)][2 * (q & 1) + 1]);
-        ++n;
-      }
+      for (int d = 0; d < 8; ++d) p[d] = dst[2 * T + (d >> 2)][d & 3];
+      u32x4 ra, rb;
+      tile_row(p, ra, rb);
+      store_b128(blk, voff, 2048 * T, ra);
+      store_b128(blk, voff, 2048 * T + 16, rb);
+      n += 2;
+    }
     return n;
   }
 };
@@ -432,7 +445,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   }
   // ---- delta9 = (W10^T dz_rgb) * relu'(layer 9) -> the B fragments of dh7, and delta9x ------------------
   uint32_t X[16][4], Y[16][4];
-  const uint32_t voff160 = (uint32_t)x * 320u + 8u * h, voff256 = (uint32_t)x * 512u + 8u * h;
+  const uint32_t vrow = tile_row_off(x, h);
   const __amdgpu_buffer_rsrc_t d9 = h32_rsrc(reinterpret_cast<const _Float16*>(a.delta9x) + (size_t)m0 * kD9F);
   {
     const uint4 mk9 = *reinterpret_cast<const uint4*>(masks_blk + 8 * 256);
@@ -451,20 +464,25 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
           v[4 * q + e] = __builtin_fmaf(wc[e], dzc[2], __builtin_fmaf(wb[e], dzc[1], wa[e] * dzc[0]));
       }
       const uint32_t word = (T >> 1) == 0 ? mk9.x : mk9.y;
+      uint32_t p[8];
 #pragma unroll
-      for (int d = 0; d < 8; ++d) X[2 * T + (d >> 2)][d & 3] = pk_h(v[2 * d], v[2 * d + 1]) & mask_expand(word, 8 * (T & 1) + d);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        store_b64(d9, voff160, 64 * T + 16 * q, X[2 * T + (q >> 1)][2 * (q & 1)], X[2 * T + (q >> 1)][2 * (q & 1) + 1]);
+      for (int d = 0; d < 8; ++d) {
+        p[d] = pk_h(v[2 * d], v[2 * d + 1]) & mask_expand(word, 8 * (T & 1) + d);
+        X[2 * T + (d >> 2)][d & 3] = p[d];
+      }
+      u32x4 ra, rb;
+      tile_row(p, ra, rb);
+      store_b128(d9, vrow, 2048 * T, ra);
+      store_b128(d9, vrow, 2048 * T + 16, rb);
     }
-    if (h == 0) store_b64(d9, (uint32_t)x * 320u, 256, pk_h(dzs, dzc[0]), pk_h(dzc[1], dzc[2]));  // features 128..131
+    if (h == 0) store_b64(d9, (uint32_t)x * 64u, 4 * 2048, pk_h(dzs, dzc[0]), pk_h(dzc[1], dzc[2]));  // features 128..131
   }
   h32_prologue_barrier();  // w8 table written, periods 0 and 1 landed
 
   f32x16 acc[2];
   const size_t lstride = (size_t)nblk * kBlk * kWidth;
   const _Float16* delta = reinterpret_cast<const _Float16*>(a.delta) + (size_t)m0 * kWidth;
-  BwdEpiH eX(acc, X, voff256), eY(acc, Y, voff256);
+  BwdEpiH eX(acc, X, vrow), eY(acc, Y, vrow);
   NoEpiH none;
   auto srcX = [&](int kk, uint32_t (&b)[4]) {
 #pragma unroll

@@ -31,11 +31,15 @@
 // period's own DMA and side-output stores stay in flight.
 //
 // Side outputs (sample-major, the transpose the weight-gradient launch reads with
-// ds_read_b64_tr_b16): activation / delta buffers are plain row-major [M][F] fp16 matrices, a lane
-// storing 4 consecutive features (8 B) per store.  ReLU masks: per 32-sample block and layer slot
-// 1 KB = [64 lanes][4 words]; word u holds tiles 2u, 2u + 1 as two 16-bit shift registers (low half:
-// even registers, high half: odd registers) — packed dword k = 8 (T & 1) + d of tile T (registers 2d,
-// 2d + 1) at bit 15 - k of each half.
+// ds_read_b64_tr_b16): activation / delta buffers are [M/32 blocks][F/32 tiles][32 samples][32
+// features] fp16 — every 32 x 32 tile a contiguous 2 KB of 64-B sample rows.  An epilogue tile leaves
+// each lane 4-feature runs of its sample (the MFMA output layout); one v_permlane32_swap per dword
+// pair gives lane half h the tile row's features 16h .. 16h + 15, stored as two 16-B stores (8-B
+// stores of the 4-feature runs ran at half the rate: MI355X_MICROARCH.md's store-issue tail), and the
+// weight-gradient launch stages each tile with two 1-KB LDS-DMA instructions.  ReLU masks: per
+// 32-sample block and layer slot 1 KB = [64 lanes][4 words]; word u holds tiles 2u, 2u + 1 as two
+// 16-bit shift registers (low half: even registers, high half: odd registers) — packed dword
+// k = 8 (T & 1) + d of tile T (registers 2d, 2d + 1) at bit 15 - k of each half.
 #pragma once
 #include <type_traits>
 
@@ -168,11 +172,35 @@ struct H32Ring {
 // then the workgroup barrier (which also publishes the LDS tables written before it)
 __device__ __forceinline__ void h32_prologue_barrier() { h32_barrier(2 * (kDmaAhead - 2)); }
 
-// Epilogue piece schedule inside a host chunk of NK k-steps: the 8 packed dwords' VALU, then the 4
-// side stores (and the layer's mask store with the last), then the C-operand load of the next chunk.
+// Epilogue piece schedule inside a host chunk of NK k-steps: the 8 packed dwords' VALU, then the
+// tile's row stores, the layer's mask store (last tile), the C-operand load of the next chunk.
 __host__ __device__ constexpr int epi_valu_pos(int d, int nk) { return nk >= 16 ? d : d >> 1; }
-__host__ __device__ constexpr int epi_store_pos(int q, int nk) { return nk >= 16 ? 8 + q : 4 + (q >> 1); }
+__host__ __device__ constexpr int epi_rows_pos(int nk) { return nk >= 16 ? 8 : 4; }
+__host__ __device__ constexpr int epi_mask_pos(int nk) { return nk >= 16 ? 9 : 5; }
 __host__ __device__ constexpr int cinit_pos(int nk) { return nk >= 16 ? 12 : nk - 1; }
+
+// byte offset of (sample x, lane half h) in a tiled [32][F] block: + 2048 t for tile t
+__device__ __forceinline__ uint32_t tile_row_off(int x, int h) { return (uint32_t)x * 64u + (uint32_t)h * 32u; }
+// v_permlane32_swap of four register pairs: vdst of lanes 32..63 <-> src0 of lanes 0..31 (measured,
+// tools/probe/h32_probe.hip), in inline asm with wait states on both sides — issued by the builtin
+// right after the VALU that wrote its operands (the epilogue drain after the last layer, nothing in
+// between) it returned stale values in some lanes (nondeterministic act_h9 tiles).
+__device__ __forceinline__ void swap32x4(uint32_t (&v)[4], uint32_t (&s)[4]) {
+  asm volatile(
+      "s_nop 4\n\t"
+      "v_permlane32_swap_b32 %0, %4\n\tv_permlane32_swap_b32 %1, %5\n\t"
+      "v_permlane32_swap_b32 %2, %6\n\tv_permlane32_swap_b32 %3, %7\n\t"
+      "s_nop 4"
+      : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(s[0]), "+v"(s[1]), "+v"(s[2]), "+v"(s[3]));
+}
+// A tile's 8 packed dwords (p[d] = registers 2d, 2d + 1: features 8 (d >> 1) + 4h + 2 (d & 1) + {0, 1})
+// -> the 32 contiguous bytes of the tile row that lane half h stores (features 16h .. 16h + 15).
+__device__ __forceinline__ void tile_row(const uint32_t (&p)[8], u32x4& a, u32x4& b) {
+  uint32_t r0[4] = {p[0], p[1], p[2], p[3]}, r1[4] = {p[4], p[5], p[6], p[7]};
+  swap32x4(r0, r1);
+  a = u32x4{r0[0], r0[1], r1[0], r1[1]};
+  b = u32x4{r0[2], r0[3], r1[2], r1[3]};
+}
 
 struct NoEpiH {
   static constexpr int kNC = 2;

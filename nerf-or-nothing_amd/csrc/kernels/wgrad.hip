@@ -642,13 +642,12 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_h(const WgProblem* __
   NOF_WG_T1(1)
 }
 
-// ---- F16 mode: sample-major fp16 operands (row-major [M][F] matrices, mlp_h32.h) --------------------
-// The F16 forward / backward store each lane's 4 consecutive features (the MFMA output layout), so a
-// block's operand tile is 32 samples x 32 features = 32 rows of 64 B.  Staged as that 2-KB image by
-// LDS-DMA (16 rows x 64 B per wave-instruction) and read back transposed by ds_read_b64_tr_b16: lane
-// (x, h) gets feature x of samples 16ks + 8h .. + 7 in two reads (4 samples each) — the 32x32x16
-// fragment with k = samples.  64-B rows: a 32-lane half reads 4 rows x 64 B = all 64 banks once.
-// Same items, wave grid and slabs as k_wgrad_h.
+// ---- F16 mode: tiled sample-major fp16 operands (mlp_h32.h) ---------------------------------------
+// The F16 forward / backward store every 32-sample x 32-feature tile as a contiguous 2 KB of 64-B
+// sample rows ([M/32][F/32][32][32] fp16), so a tile is staged by two 1-KB LDS-DMA instructions and
+// read back transposed by ds_read_b64_tr_b16: lane (x, h) gets feature x of samples 16ks + 8h .. + 7 in
+// two reads (4 samples each) — the 32x32x16 fragment with k = samples.  64-B rows: a 32-lane half
+// reads 4 rows x 64 B = all 64 banks once.  Same items, wave grid and slabs as k_wgrad_h.
 typedef short s16x4v __attribute__((vector_size(8)));
 template <int RB, int CB>
 __device__ __forceinline__ void wg_item_s(const WgItem& item, const WgProblem& P, _Float16* lds, int tid, int wave,
@@ -668,20 +667,18 @@ __device__ __forceinline__ void wg_item_s(const WgItem& item, const WgProblem& P
   for (int c = 0; c < CB; ++c) colt[c] = min(c0 + c, P.ntc - 1);
   const int T = P.ntr + P.ntc;  // tiles per block
   const size_t strideA = (size_t)P.FA * kBlk * 2, strideB = (size_t)P.FB * kBlk * 2;  // bytes per block
-  const char* baseA = reinterpret_cast<const char*>(P.A) + (size_t)item.kb0 * strideA + (size_t)P.a_row0 * 2;
-  const char* baseB = reinterpret_cast<const char*>(P.B) + (size_t)item.kb0 * strideB + (size_t)P.b_col0 * 2;
+  const char* baseA = reinterpret_cast<const char*>(P.A) + (size_t)item.kb0 * strideA + (size_t)(P.a_row0 >> 5) * 2048;
+  const char* baseB = reinterpret_cast<const char*>(P.B) + (size_t)item.kb0 * strideB + (size_t)(P.b_col0 >> 5) * 2048;
   const int K = item.kb1 - item.kb0;
-  // this lane's 16-B piece of a DMA instruction: sample (lane >> 2) (+ 16), 16-B column chunk lane & 3
-  const int rowA = (lane >> 2) * P.FA * 2 + (lane & 3) * 16, rowB = (lane >> 2) * P.FB * 2 + (lane & 3) * 16;
   auto dma = [&](int k) {
     k = min(k, K - 1);
     _Float16* stage = lds + (k % kWhStages) * kWhStageHalves;
 #pragma unroll
     for (int i = 0; i < ND; ++i) {
       const int cw = min(i * kWgX3Threads + wave * 64, T * 128 - 64);  // wave's first 16-B chunk (uniform)
-      const int tt = cw >> 7, half = (cw >> 6) & 1;                      // tile, samples 16 half .. + 15
-      const char* src = tt < P.ntr ? baseA + (size_t)k * strideA + tt * 64 + half * 16 * P.FA * 2 + rowA
-                                   : baseB + (size_t)k * strideB + (tt - P.ntr) * 64 + half * 16 * P.FB * 2 + rowB;
+      const int tt = cw >> 7;                                            // tile (uniform)
+      const char* src = (tt < P.ntr ? baseA + (size_t)k * strideA + tt * 2048
+                                    : baseB + (size_t)k * strideB + (tt - P.ntr) * 2048) + (cw & 127) * 16 + lane * 16;
       __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(stage + cw * 8), 16, 0, 0);
     }
   };

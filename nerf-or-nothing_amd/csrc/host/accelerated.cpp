@@ -286,8 +286,9 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M, int bucket)
   std::vector<nof::WgProblem> P;
   std::vector<int> pbucket;  // bucket of each problem's outputs: layers 5..10 -> 0, 0..4 -> 1
   auto prob = [&](int layer, const float* A, int FA, int a0, int ntr, const float* B, int FB, int b0, int ntc) {
-    nof::WgProblem p;
+    nof::WgProblem p{};
     p.A = A; p.FA = FA; p.a_row0 = a0; p.ntr = ntr; p.B = B; p.FB = FB; p.b_col0 = b0; p.ntc = ntc; p.shape = 0;
+    p.ntc1 = ntc;
     P.push_back(p);
     pbucket.push_back(layer >= 5 ? 0 : 1);
     return (int)P.size() - 1;
@@ -302,13 +303,25 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M, int bucket)
   };
   auto Wg = [&](int l) { return G + woff_[l]; };
   auto Bg = [&](int l) { return G + boff_[l]; };
+  // F16 (k_wgrad_s): the problems that share an A operand are one problem with more output columns —
+  // delta_4 x [h3 | IPE] and delta_9x x [h7 | view PE | h9] — so each delta block is read once
+  const bool merge = precision_ == NOF_PRECISION_F16;
+  auto extra_b = [&](int p, const float* B, int FB, int b0, int ntc) {
+    nof::WgProblem& q = P[p];
+    if (q.ntc2 == 0) { q.B2 = B; q.FB2 = FB; q.b2_col0 = b0; q.ntc2 = ntc; }
+    else { q.B3 = B; q.FB3 = FB; q.b3_col0 = b0; q.ntc3 = ntc; }
+    q.ntc += ntc;
+  };
   int p;
   p = prob(0, delta_.p, 256, 0, 8, L.act_in.p, nof::kInF, 0, 3);
   os.push_back({p, 0, 256, 0, 96, Wg(0), 96, 0, Bg(0)});
   for (int l = 1; l < 8; ++l) {
     p = prob(l, at(delta_.p, l * ls), 256, 0, 8, at(L.act_h.p, (l - 1) * ls), 256, 0, 8);
     os.push_back({p, 0, 256, 0, 256, Wg(l), in_[l], 0, Bg(l)});
-    if (l == 4) {
+    if (l == 4 && merge) {
+      extra_b(p, L.act_in.p, nof::kInF, 0, 3);
+      os.push_back({p, 0, 256, 256, 96, Wg(4), in_[4], 256, nullptr});
+    } else if (l == 4) {
       p = prob(4, at(delta_.p, l * ls), 256, 0, 8, L.act_in.p, nof::kInF, 0, 3);
       os.push_back({p, 0, 256, 0, 96, Wg(4), in_[4], 256, nullptr});
     }
@@ -316,10 +329,17 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M, int bucket)
   p = prob(9, delta9x_.p, nof::kD9F, 0, 5, at(L.act_h.p, 7 * ls), 256, 0, 8);
   os.push_back({p, 0, 128, 0, 256, Wg(9), in_[9], 0, Bg(9)});
   os.push_back({p, 128, 1, 0, 256, Wg(8), in_[8], 0, Bg(8)});
-  p = prob(9, delta9x_.p, nof::kD9F, 0, 4, L.act_in.p, nof::kInF, 96, 1);
-  os.push_back({p, 0, 128, 0, 27, Wg(9), in_[9], 256, nullptr});
-  p = prob(10, delta9x_.p, nof::kD9F, 128, 1, L.act_h9.p, 128, 0, 4);
-  os.push_back({p, 1, 3, 0, 128, Wg(10), in_[10], 0, Bg(10)});
+  if (merge) {  // columns 256..287: the view PE tile, 288..415: h9
+    extra_b(p, L.act_in.p, nof::kInF, 96, 1);
+    extra_b(p, L.act_h9.p, 128, 0, 4);
+    os.push_back({p, 0, 128, 256, 27, Wg(9), in_[9], 256, nullptr});
+    os.push_back({p, 129, 3, 288, 128, Wg(10), in_[10], 0, Bg(10)});
+  } else {
+    p = prob(9, delta9x_.p, nof::kD9F, 0, 4, L.act_in.p, nof::kInF, 96, 1);
+    os.push_back({p, 0, 128, 0, 27, Wg(9), in_[9], 256, nullptr});
+    p = prob(10, delta9x_.p, nof::kD9F, 128, 1, L.act_h9.p, 128, 0, 4);
+    os.push_back({p, 1, 3, 0, 128, Wg(10), in_[10], 0, Bg(10)});
+  }
   if (bucket >= 0) {  // keep only this bucket's problems (and their outputs), renumbered
     std::vector<int> remap(P.size(), -1);
     std::vector<nof::WgProblem> Pb;
@@ -341,7 +361,13 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M, int bucket)
   // measured for the (8,8) / (8,3) / (5,8) / (4,1) / (1,4) problems = 160 / 96 / 124 / 47 / 37.
   std::vector<int64_t> cost(P.size());
   for (size_t i = 0; i < P.size(); ++i) {
-    if (f16_blocks()) {
+    if (precision_ == NOF_PRECISION_F16) {
+      // k_wgrad_s streams T = ntr + ntc tiles per block: 1.65 / 1.17 us per block measured for the
+      // 16- / 11-tile problems (tools/diag_item_time.py f16); the merged 19- / 18-tile problems run
+      // the unpipelined 12-accumulator path, 2.13 / 2.08 us
+      const int RB = (P[i].ntr + 1) / 2, CB = (P[i].ntc + 3) / 4;
+      cost[i] = (RB * CB > 8 ? 11 : 10) * (P[i].ntr + P[i].ntc);
+    } else if (f16_blocks()) {
       cost[i] = 10 * (P[i].ntr + P[i].ntc) + (P[i].ntc == 1 ? 12 : 0);
     } else if (precision_ != NOF_PRECISION_F32) {
       const int WC = nof::wgrad_x3_grid_cols();  // C/2 waves per SIMD

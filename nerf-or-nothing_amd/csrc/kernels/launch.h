@@ -90,6 +90,11 @@ struct WgProblem {
   int FA, a_row0, ntr;   // A rows [a_row0, a_row0 + 32*ntr) of an [FA][32]-block buffer
   int FB, b_col0, ntc;   // B rows (= output columns) [b_col0, b_col0 + 32*ntc)
   int shape;             // fp32 k_wgrad wave-grid shape (wgrad_shape); unused by k_wgrad_x3
+  // F16 (k_wgrad_s) only: output columns past the first ntc1 tiles come from up to two more operands
+  // (B2 rows [b2_col0, +32 ntc2), then B3), so the problems that share an A operand read it once
+  int ntc1;              // tiles of B (ntc = ntc1 + ntc2 + ntc3)
+  const float* B2; int FB2, b2_col0, ntc2;
+  const float* B3; int FB3, b3_col0, ntc3;
 };
 struct WgItem { int prob, kb0, kb1; int slab; };  // slab = index into slab_off[]
 struct WgOut {

@@ -23,19 +23,26 @@ typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t h32_rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
 }
+#ifndef NOF_DIAG_H32_NTSTORE  // diagnostic: bit 0 = forward, bit 1 = backward side outputs non-temporal
+#define NOF_DIAG_H32_NTSTORE 0
+#endif
+constexpr int kFwdAux = (NOF_DIAG_H32_NTSTORE & 1) ? 2 : 0;  // side-output store cache policy
+constexpr int kBwdAux = (NOF_DIAG_H32_NTSTORE & 2) ? 2 : 0;
+template <int aux>
 __device__ __forceinline__ void store_b64(__amdgpu_buffer_rsrc_t r, uint32_t voff, int imm, uint32_t lo, uint32_t hi) {
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 #ifdef NOF_DIAG_H32_NOSTORE  // diagnostic: no side-output stores (keeps one dependency so nothing is dead)
-  if (lo == 0x7fff1234u && hi == 0x1234u) __builtin_amdgcn_raw_buffer_store_b64((u32x2{lo, hi}), r, (int)voff, imm, 0);
+  if (lo == 0x7fff1234u && hi == 0x1234u) __builtin_amdgcn_raw_buffer_store_b64((u32x2{lo, hi}), r, (int)voff, imm, aux);
   return;
 #endif
-  __builtin_amdgcn_raw_buffer_store_b64((u32x2{lo, hi}), r, (int)voff, imm, 0);
+  __builtin_amdgcn_raw_buffer_store_b64((u32x2{lo, hi}), r, (int)voff, imm, aux);
 }
 // 16-B store: the data registers stay untouched for two wait states after the store issues — measured:
 // a VALU that overwrote a data register in the next instruction corrupted the stored dword
 // (nondeterministic act_h9 tiles; the compiler inserted no wait state for this >8-byte store-data hazard)
+template <int aux>
 __device__ __forceinline__ void store_b128(__amdgpu_buffer_rsrc_t r, uint32_t voff, int imm, const u32x4& v) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, imm, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, imm, aux);
   asm volatile("s_nop 1" ::"v"(v) : "memory");
 }
 __device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
@@ -111,12 +118,12 @@ struct FwdEpiH {
         for (int d = 0; d < 8; ++d) p[d] = dst[2 * T + (d >> 2)][d & 3];
         u32x4 ra, rb;
         tile_row(p, ra, rb);
-        store_b128(blk, voff, 2048 * T, ra);
-        store_b128(blk, voff, 2048 * T + 16, rb);
+        store_b128<kFwdAux>(blk, voff, 2048 * T, ra);
+        store_b128<kFwdAux>(blk, voff, 2048 * T + 16, rb);
         n += 2;
       }
       if (T == kNC - 1 && kk == epi_mask_pos(NK)) {
-        store_b128(mrs, moff, mimm, u32x4{mw[0], mw[1], mw[2], mw[3]});
+        store_b128<kFwdAux>(mrs, moff, mimm, u32x4{mw[0], mw[1], mw[2], mw[3]});
         ++n;
       }
     }
@@ -158,12 +165,12 @@ struct ViewEpiH {
       if (kk == epi_rows_pos(NK)) {
         u32x4 ra, rb;
         tile_row(p8, ra, rb);
-        store_b128(blk, voff, 2048 * T, ra);
-        store_b128(blk, voff, 2048 * T + 16, rb);
+        store_b128<kFwdAux>(blk, voff, 2048 * T, ra);
+        store_b128<kFwdAux>(blk, voff, 2048 * T + 16, rb);
         n += 2;
       }
       if (T == kNC - 1 && kk == epi_mask_pos(NK)) {
-        store_b128(mrs, moff, 8 * 1024, u32x4{mw[0], mw[1], mw[2], mw[3]});
+        store_b128<kFwdAux>(mrs, moff, 8 * 1024, u32x4{mw[0], mw[1], mw[2], mw[3]});
         ++n;
       }
     }
@@ -244,7 +251,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
 #pragma unroll
     for (int k = 0; k < 6; ++k) {  // features 48h + 8k .. + 7: tile (48h + 8k) >> 5, column (48h + 8k) & 31
       const int kk = k >> 1, q = k & 1, f = 48 * h + 8 * k;
-      store_b128(r, (uint32_t)(f >> 5) * 2048u + (uint32_t)x * 64u + (uint32_t)(f & 31) * 2u, 0,
+      store_b128<kFwdAux>(r, (uint32_t)(f >> 5) * 2048u + (uint32_t)x * 64u + (uint32_t)(f & 31) * 2u, 0,
                  u32x4{ix[kk][2 * q], ix[kk][2 * q + 1], iy[kk][2 * q], iy[kk][2 * q + 1]});
     }
     uint32_t w[8];
@@ -258,8 +265,8 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
       }
       w[i] = pk_h(v[0], v[1]);
     }
-    store_b128(r, vrow, 3 * 2048, u32x4{w[0], w[1], w[2], w[3]});  // tile 3: features 96 + 16h ..
-    store_b128(r, vrow, 3 * 2048 + 16, u32x4{w[4], w[5], w[6], w[7]});
+    store_b128<kFwdAux>(r, vrow, 3 * 2048, u32x4{w[0], w[1], w[2], w[3]});  // tile 3: features 96 + 16h ..
+    store_b128<kFwdAux>(r, vrow, 3 * 2048 + 16, u32x4{w[4], w[5], w[6], w[7]});
   }
   // the B fragments of layers 0 / 4: k-steps 0..2 from the lane half h = 0, 3..5 from h = 1 — one
   // permlane32 swap per packed dword moves each half's other-h' pairs across (tools/probe/h32_probe.hip)
@@ -404,8 +411,8 @@ struct BwdEpiH {
       for (int d = 0; d < 8; ++d) p[d] = dst[2 * T + (d >> 2)][d & 3];
       u32x4 ra, rb;
       tile_row(p, ra, rb);
-      store_b128(blk, voff, 2048 * T, ra);
-      store_b128(blk, voff, 2048 * T + 16, rb);
+      store_b128<kBwdAux>(blk, voff, 2048 * T, ra);
+      store_b128<kBwdAux>(blk, voff, 2048 * T + 16, rb);
       n += 2;
     }
     return n;
@@ -472,10 +479,10 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
       }
       u32x4 ra, rb;
       tile_row(p, ra, rb);
-      store_b128(d9, vrow, 2048 * T, ra);
-      store_b128(d9, vrow, 2048 * T + 16, rb);
+      store_b128<kBwdAux>(d9, vrow, 2048 * T, ra);
+      store_b128<kBwdAux>(d9, vrow, 2048 * T + 16, rb);
     }
-    if (h == 0) store_b64(d9, (uint32_t)x * 64u, 4 * 2048, pk_h(dzs, dzc[0]), pk_h(dzc[1], dzc[2]));  // features 128..131
+    if (h == 0) store_b64<kBwdAux>(d9, (uint32_t)x * 64u, 4 * 2048, pk_h(dzs, dzc[0]), pk_h(dzc[1], dzc[2]));  // features 128..131
   }
   h32_prologue_barrier();  // w8 table written, periods 0 and 1 landed
 

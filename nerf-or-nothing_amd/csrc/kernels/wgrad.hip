@@ -644,15 +644,33 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_h(const WgProblem* __
 
 // ---- F16 mode: tiled sample-major fp16 operands (mlp_h32.h) ---------------------------------------
 // The F16 forward / backward store every 32-sample x 32-feature tile as a contiguous 2 KB of 64-B
-// sample rows ([M/32][F/32][32][32] fp16), so a tile is staged by two 1-KB LDS-DMA instructions and
-// read back transposed by ds_read_b64_tr_b16: lane (x, h) gets feature x of samples 16ks + 8h .. + 7 in
-// two reads (4 samples each) — the 32x32x16 fragment with k = samples.  64-B rows: a 32-lane half
-// reads 4 rows x 64 B = all 64 banks once.  Same items, wave grid and slabs as k_wgrad_h.
+// sample rows ([M/32][F/32][32][32] fp16).  A stage of the ring is one 32-sample block of every tile
+// of the problem (T x 2 KB, each tile's two 1-KB halves by two LDS-DMA instructions issued together),
+// as many stages as fit in 160 KB.  Measured with tools/probe/stream_probe.hip (no compute, same
+// item shapes): whole-tile stages stream at 5.8 TB/s, 6.3 TB/s with the non-temporal load policy;
+// k-step (half-tile) stages only 4.7 TB/s whatever the depth — the other half of every 2-KB DRAM
+// burst is fetched a stage later.  Fragments are read back transposed by ds_read_b64_tr_b16: lane
+// (x, h) gets feature x of samples 16 ks + 8h .. + 7 in two reads — the 32x32x16 fragment with
+// k = samples; 64-B rows, so a 32-lane half reads 4 rows x 64 B = all banks once.  Output columns may
+// come from up to three operands (WgProblem B / B2 / B3).  Same items, 2 x kX3WC wave grid and slabs
+// as k_wgrad_h.
 typedef short s16x4v __attribute__((vector_size(8)));
+constexpr int kWsLdsBytes = 160 * 1024;
+constexpr int kWsAux = 2;  // global_load_lds cache policy: non-temporal (streamed once)
+template <int RB, int CB>
+struct WsRing {
+  // tiles a problem of this grid can have (the 3 x 4 grid serves the 5 x 13 view-layer problem only)
+  static constexpr int TC = (RB == 3 && CB == 4) ? 18 : 2 * RB + kX3WC * CB;
+  static constexpr int ND = (2 * TC + 7) / 8;  // 1-KB DMA instructions per wave per stage
+  static constexpr int NS = kWsLdsBytes / (TC * 2048) < 8 ? kWsLdsBytes / (TC * 2048) : 8;  // stages
+  static_assert((NS - 1) * ND < 64 && NS >= 4, "vmcnt range / ring depth");
+};
+
 template <int RB, int CB>
 __device__ __forceinline__ void wg_item_s(const WgItem& item, const WgProblem& P, _Float16* lds, int tid, int wave,
                                           float* slabs, float* bias_slabs, const int64_t* slab_off) {
-  constexpr int ND = ((2 * RB + kX3WC * CB) * 128 + kWgX3Threads - 1) / kWgX3Threads;  // DMA instrs / block
+  typedef WsRing<RB, CB> R;
+  constexpr int ND = R::ND, NS = R::NS, kStage = R::TC * 1024;  // halves per stage
   int tq = tid;
   asm volatile("" : "+v"(tq));
   const int lane = tq & 63;
@@ -665,21 +683,48 @@ __device__ __forceinline__ void wg_item_s(const WgItem& item, const WgProblem& P
   for (int r = 0; r < RB; ++r) rowt[r] = min(r0 + r, P.ntr - 1);
 #pragma unroll
   for (int c = 0; c < CB; ++c) colt[c] = min(c0 + c, P.ntc - 1);
-  const int T = P.ntr + P.ntc;  // tiles per block
-  const size_t strideA = (size_t)P.FA * kBlk * 2, strideB = (size_t)P.FB * kBlk * 2;  // bytes per block
-  const char* baseA = reinterpret_cast<const char*>(P.A) + (size_t)item.kb0 * strideA + (size_t)(P.a_row0 >> 5) * 2048;
-  const char* baseB = reinterpret_cast<const char*>(P.B) + (size_t)item.kb0 * strideB + (size_t)(P.b_col0 >> 5) * 2048;
+  const int T = P.ntr + P.ntc;  // tiles per stage
+  // this wave's 1-KB DMA pieces c = 8i + wave: tile c >> 1, half c & 1 (clamped: the surplus
+  // instructions of narrower problems repeat the last piece, an L2 hit) — block-kb0 source and bytes
+  // per block, all wave-uniform
+  const char* tsrc[ND];
+  int64_t tstr[ND];
+  int tdst[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) {
+    const int c = min(i * 8 + wave, 2 * T - 1);
+    int t = c >> 1;
+    tdst[i] = c * 512;
+    const float* base;
+    int F, row0;
+    if (t < P.ntr) {
+      base = P.A; F = P.FA; row0 = P.a_row0;
+    } else if ((t -= P.ntr) < P.ntc1) {
+      base = P.B; F = P.FB; row0 = P.b_col0;
+    } else if ((t -= P.ntc1) < P.ntc2) {
+      base = P.B2; F = P.FB2; row0 = P.b2_col0;
+    } else {
+      t -= P.ntc2;
+      base = P.B3; F = P.FB3; row0 = P.b3_col0;
+    }
+    tstr[i] = (int64_t)F * kBlk * 2;
+    tsrc[i] = reinterpret_cast<const char*>(base) + (int64_t)item.kb0 * tstr[i] + (int64_t)((row0 >> 5) + t) * 2048 +
+              (c & 1) * 1024;
+  }
   const int K = item.kb1 - item.kb0;
-  auto dma = [&](int k) {
+  // block k into ring slot `slot` (k clamped to K - 1: a duplicate lands in a slot nobody reads
+  // before it is refilled)
+  auto dma = [&](int k, int slot) {
     k = min(k, K - 1);
-    _Float16* stage = lds + (k % kWhStages) * kWhStageHalves;
+    _Float16* stage = lds + slot * kStage;
 #pragma unroll
     for (int i = 0; i < ND; ++i) {
-      const int cw = min(i * kWgX3Threads + wave * 64, T * 128 - 64);  // wave's first 16-B chunk (uniform)
-      const int tt = cw >> 7;                                            // tile (uniform)
-      const char* src = (tt < P.ntr ? baseA + (size_t)k * strideA + tt * 2048
-                                    : baseB + (size_t)k * strideB + (tt - P.ntr) * 2048) + (cw & 127) * 16 + lane * 16;
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(stage + cw * 8), 16, 0, 0);
+      const char* src = tsrc[i] + (int64_t)k * tstr[i] + lane * 16;
+#ifndef NOF_DIAG_WS_NODMA
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(stage + tdst[i]), 16, 0, kWsAux);
+#else
+      asm volatile("" ::"s"(src), "s"(stage + tdst[i]));
+#endif
     }
   };
   f32x16 acc[RB][CB];
@@ -687,61 +732,114 @@ __device__ __forceinline__ void wg_item_s(const WgItem& item, const WgProblem& P
   for (int r = 0; r < RB; ++r)
 #pragma unroll
     for (int c = 0; c < CB; ++c) acc[r][c] = f32x16{};
-  float bsum[RB];
-#pragma unroll
-  for (int r = 0; r < RB; ++r) bsum[r] = 0.0f;
-  // transposed-read address of this lane inside a tile image (halves): row 8h + q, column 16 (G & 1) + 4p
+  float bsum = 0.0f;  // bias partial of row tile rowt[wc] (wave columns wc < RB)
+  // transposed-read address of this lane inside a tile (halves): sample row 16 ks + 8h + q (+4 for the
+  // second read), feature column 16 (G & 1) + 4p
   const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   const int toff = (8 * (G >> 1) + q) * 32 + 16 * (G & 1) + 4 * p;
   // inline asm: through the builtin the compiler orders every transposed read behind the LDS-DMA in
-  // flight (s_waitcnt vmcnt(0) before each k-block's reads); the ring's own counted waits order them
+  // flight (s_waitcnt vmcnt(0) before each k-step's reads); the ring's own counted waits order them
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
   // (the asm outputs are written asynchronously: nothing may copy them before the lgkmcnt wait, so each
   // read has its own output and the fragments are assembled after the wait)
-  auto frag = [&](const _Float16* tile, int ks, s16x4v& lo, s16x4v& hi) {
-    const uint32_t a = lds_base + (uint32_t)((tile - lds) + toff + ks * 16 * 32) * 2u;
+  auto frag = [&](uint32_t stage_b, int tile, s16x4v& lo, s16x4v& hi) {
+    const uint32_t a = stage_b + (uint32_t)(tile * 1024 + toff) * 2u;
+#if defined(NOF_DIAG_WS_NOREAD)
+    lo = s16x4v{(short)a, 0, 0, 0};
+    hi = lo;
+#else
     asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a));
     asm volatile("ds_read_b64_tr_b16 %0, %1 offset:256" : "=v"(hi) : "v"(a));
+#endif
   };
+  struct Frags { s16x4v al[RB], ah[RB], bl[CB], bh[CB]; };
+  auto issue = [&](int slot, int ks, Frags& f) {  // k-step ks (samples 16 ks ..) of the block in `slot`
+    const uint32_t sb = lds_base + (uint32_t)(slot * kStage + ks * 512) * 2u;
 #pragma unroll
-  for (int k = 0; k < kWhStages - 1; ++k) dma(k);
-  for (int k = 0; k < K; ++k) {
-    wait_vmcnt<(kWhStages - 2) * ND>();  // block k landed (this wave's part); k + 1 .. k + NS - 2 in flight
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave's part; stage k - 1 read out
-    dma(k + kWhStages - 1);  // into stage (k - 1) % NS
-    const _Float16* st = lds + (k % kWhStages) * kWhStageHalves;
+    for (int r = 0; r < RB; ++r) frag(sb, rowt[r], f.al[r], f.ah[r]);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      s16x4v al[RB], ah[RB], bl[CB], bh[CB];
+    for (int c = 0; c < CB; ++c) frag(sb, P.ntr + colt[c], f.bl[c], f.bh[c]);
+  };
+  auto settle = [&](Frags& f) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int r = 0; r < RB; ++r) frag(st + rowt[r] * 1024, ks, al[r], ah[r]);
+    for (int r = 0; r < RB; ++r) asm volatile("" : "+v"(f.al[r]), "+v"(f.ah[r]));  // defined here, after the wait
 #pragma unroll
-      for (int c = 0; c < CB; ++c) frag(st + (P.ntr + colt[c]) * 1024, ks, bl[c], bh[c]);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      f16x8 fa[RB], fb[CB];
+    for (int c = 0; c < CB; ++c) asm volatile("" : "+v"(f.bl[c]), "+v"(f.bh[c]));
+  };
+  auto compute = [&](const Frags& f) {
+    f16x8 fa[RB], fb[CB];
 #pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        asm volatile("" : "+v"(al[r]), "+v"(ah[r]));  // defined here, after the wait
-        fa[r] = __builtin_bit_cast(f16x8, __builtin_shufflevector(al[r], ah[r], 0, 1, 2, 3, 4, 5, 6, 7));
+    for (int r = 0; r < RB; ++r)
+      fa[r] = __builtin_bit_cast(f16x8, __builtin_shufflevector(f.al[r], f.ah[r], 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+    for (int c = 0; c < CB; ++c)
+      fb[c] = __builtin_bit_cast(f16x8, __builtin_shufflevector(f.bl[c], f.bh[c], 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int c = 0; c < CB; ++c)
+#ifdef NOF_DIAG_WS_NOMFMA
+        acc[r][c][0] += (float)fa[r][0] * (float)fb[c][1];
+#else
+        acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[r], fb[c], acc[r][c], 0, 0, 0);
+#endif
+    // bias partials: row sums of delta, row tile rowt[wc] on wave column wc (spread over the four SIMDs;
+    // a wave-uniform select, no branch): four packed dot products with ones per k-step
+    if (wc < RB) {
+      f16x8 a = fa[0];
+#pragma unroll
+      for (int r = 1; r < RB; ++r) a = wc == r ? fa[r] : a;
+      typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+      const h2 one = {(_Float16)1.0f, (_Float16)1.0f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bsum = __builtin_amdgcn_fdot2(h2{a[2 * j], a[2 * j + 1]}, one, bsum, false);
+    }
+  };
+  if constexpr (RB * CB <= 8) {
+    // software pipeline, one barrier per block: the reads of k-step 1 of block k run under the MFMAs of
+    // its k-step 0, and the reads of block k + 1's k-step 0 (after the barrier that publishes it and
+    // frees the slot of block k) under the MFMAs of k-step 1.  Fixed fragment sets, settled at the end
+    // of the half-step that issued them, so no copy of an in-flight read can be scheduled.
+    Frags f0, f1;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) dma(k, k);
+    wait_vmcnt<(NS - 1) * ND>();  // block 0
+    asm volatile("s_barrier" ::: "memory");
+    issue(0, 0, f0);
+    settle(f0);
+    int slot = 0;  // ring slot of block k
+    for (int k = 0; k < K; ++k) {
+      issue(slot, 1, f1);
+      compute(f0);
+      settle(f1);
+      wait_vmcnt<(NS - 2) * ND>();  // block k + 1 landed (this wave's part); k + 2 .. k + NS - 1 in flight
+      asm volatile("s_barrier" ::: "memory");  // everyone's part; every wave's reads of block k settled
+      dma(k + NS, slot);
+      slot = slot + 1 == NS ? 0 : slot + 1;
+      issue(slot, 0, f0);  // (past the last block: a clamped duplicate, never used)
+      compute(f1);
+      settle(f0);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < NS - 1; ++k) dma(k, k);
+    // 12 accumulator tiles (the merged problems) leave no room for a second fragment set at two waves
+    // per SIMD: read, settle and multiply each k-step of block k between the barriers
+    Frags f;
+    int slot = 0, fill = NS - 1;
+    for (int k = 0; k < K; ++k) {
+      wait_vmcnt<(NS - 2) * ND>();  // block k landed (this wave's part); k + 1 .. k + NS - 2 in flight
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // everyone's; slot `fill` read out
+      dma(k + NS - 1, fill);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        issue(slot, ks, f);
+        settle(f);
+        compute(f);
       }
-#pragma unroll
-      for (int c = 0; c < CB; ++c) {
-        asm volatile("" : "+v"(bl[c]), "+v"(bh[c]));
-        fb[c] = __builtin_bit_cast(f16x8, __builtin_shufflevector(bl[c], bh[c], 0, 1, 2, 3, 4, 5, 6, 7));
-      }
-#pragma unroll
-      for (int r = 0; r < RB; ++r)
-#pragma unroll
-        for (int c = 0; c < CB; ++c) acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[r], fb[c], acc[r][c], 0, 0, 0);
-      if (wc == 0) {  // bias partials: row sums of delta (uniform branch)
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          float sum = 0.0f;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) sum += (float)fa[r][j];
-          bsum[r] += sum;
-        }
-      }
+      slot = slot + 1 == NS ? 0 : slot + 1;
+      fill = fill + 1 == NS ? 0 : fill + 1;
     }
   }
   wait_vmcnt<0>();  // retire the clamped tail DMAs before the ring is reused
@@ -761,12 +859,9 @@ __device__ __forceinline__ void wg_item_s(const WgItem& item, const WgProblem& P
         }
       }
   }
-  if (wc == 0) {
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      const float v = bsum[r] + __shfl_xor(bsum[r], 32, 64);
-      if (r0 + r < P.ntr && h == 0) bias_slabs[(size_t)item.slab * 256 + rowt[r] * 32 + x] = v;
-    }
+  if (wc < RB) {
+    const float v = bsum + __shfl_xor(bsum, 32, 64);
+    if (r0 + wc < P.ntr && h == 0) bias_slabs[(size_t)item.slab * 256 + (r0 + wc) * 32 + x] = v;
   }
   __syncthreads();  // the ring is reused by the next item
 }
@@ -777,23 +872,33 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_s(const WgProblem* __
                                                              const int64_t* __restrict__ slab_off, float* slabs,
                                                              float* bias_slabs) {
   extern __shared__ __attribute__((aligned(16))) _Float16 ldss[];
+  NOF_WG_T0(1)
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int it0 = item_ptr[blockIdx.x], it1 = item_ptr[blockIdx.x + 1];
   for (int it = it0; it < it1; ++it) {
+    NOF_IT_T0(1)
     const WgItem item = items[it];
     const WgProblem P = probs[item.prob];
-    NOF_DCHECK(item.kb0 < item.kb1 && P.ntr >= 1 && P.ntr <= 8 && P.ntc >= 1 && P.ntc <= 8 &&
-                   P.a_row0 + 32 * P.ntr <= P.FA && P.b_col0 + 32 * P.ntc <= P.FB,
+    // the item's k-blocks, its operand tiles inside their buffers, at most 6 x 16 tiles
+    NOF_DCHECK(item.kb0 < item.kb1 && P.ntr >= 1 && P.ntr <= 8 && P.ntc >= 1 && P.ntc <= 16 &&
+                   P.ntc == P.ntc1 + P.ntc2 + P.ntc3 && P.a_row0 + 32 * P.ntr <= P.FA &&
+                   P.b_col0 + 32 * P.ntc1 <= P.FB && (P.ntc2 == 0 || P.b2_col0 + 32 * P.ntc2 <= P.FB2) &&
+                   (P.ntc3 == 0 || P.b3_col0 + 32 * P.ntc3 <= P.FB3),
                kChkWgradGeom);
     switch (((P.ntr + 1) >> 1) * 10 + (P.ntc + kX3WC - 1) / kX3WC) {
       case 11: wg_item_s<1, 1>(item, P, ldss, tid, wave, slabs, bias_slabs, slab_off); break;
       case 21: wg_item_s<2, 1>(item, P, ldss, tid, wave, slabs, bias_slabs, slab_off); break;
       case 32: wg_item_s<3, 2>(item, P, ldss, tid, wave, slabs, bias_slabs, slab_off); break;
+      case 34: wg_item_s<3, 4>(item, P, ldss, tid, wave, slabs, bias_slabs, slab_off); break;
       case 41: wg_item_s<4, 1>(item, P, ldss, tid, wave, slabs, bias_slabs, slab_off); break;
-      default: wg_item_s<4, 2>(item, P, ldss, tid, wave, slabs, bias_slabs, slab_off); break;
+      case 43: wg_item_s<4, 3>(item, P, ldss, tid, wave, slabs, bias_slabs, slab_off); break;
+      case 42: wg_item_s<4, 2>(item, P, ldss, tid, wave, slabs, bias_slabs, slab_off); break;
+      default: NOF_DCHECK(false, kChkWgradGeom); break;
     }
+    NOF_IT_T1(1)
   }
+  NOF_WG_T1(1)
 }
 
 int wgrad_x3_grid_cols() { return kX3WC; }
@@ -852,11 +957,12 @@ hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const in
   if (precision == 4) {  // F16: sample-major fp16 operands (k_wgrad_s)
     static bool attr_s = false;
     if (!attr_s) {
-      const hipError_t e = hipFuncSetAttribute((const void*)k_wgrad_s, hipFuncAttributeMaxDynamicSharedMemorySize, kWhLds);
+      const hipError_t e =
+          hipFuncSetAttribute((const void*)k_wgrad_s, hipFuncAttributeMaxDynamicSharedMemorySize, kWsLdsBytes);
       if (e != hipSuccess) return e;
       attr_s = true;
     }
-    hipLaunchKernelGGL(k_wgrad_s, dim3(num_wg), dim3(kWgX3Threads), kWhLds, st, probs, items, item_ptr, slab_off,
+    hipLaunchKernelGGL(k_wgrad_s, dim3(num_wg), dim3(kWgX3Threads), kWsLdsBytes, st, probs, items, item_ptr, slab_off,
                        slabs, bias_slabs);
     return hipGetLastError();
   }

@@ -25,7 +25,7 @@ pytestmark = pytest.mark.gpu
 TOLS = {0: 1e-5, 1: 1e-5, 2: 2e-3, 3: 1e-5, 4: 2e-3}
 # adopted ReLU decisions that differ from the fp64 oracle's own, as a fraction of all units (ties at
 # z ~ 0; measured 5e-8 .. 1.3e-7 in all three modes, the f16x2 mode included)
-FLIP_BOUND = {0: 1e-5, 1: 1e-5, 2: 1e-5, 3: 1e-5, 4: 2e-3}  # f16: fp16 pre-activations (2^-11)
+FLIP_BOUND = {0: 1e-5, 1: 1e-5, 2: 1e-5, 3: 1e-5, 4: 5e-4}  # f16: fp16 pre-activations (2^-11)
 NTHREADS = min(16, len(os.sched_getaffinity(0)))
 PER_RAY = ("density", "rgb", "weights", "comp_rgb", "density_grad", "rgb_grad")
 ORACLE_KEY = {"density": "sigma", "rgb": "rgb", "weights": "w", "comp_rgb": "C", "density_grad": "dsigma",

@@ -1,7 +1,7 @@
 """Diagnostic (NOF_DIAG_WG_TIME builds): per-item durations of the last weight-gradient launch,
 fitted per problem as overhead + cost per k-block (calibration data for the host's item schedule),
 and the slowest workgroups with their items and XCD (blockIdx % 8).
-usage: NOF_LIB=.../libnof_wgt.so python tools/diag_item_time.py f32|f16x2"""
+usage: NOF_LIB=.../libnof_wgt.so python tools/diag_item_time.py f32|f16x2|f16"""
 import ctypes as C, os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -10,7 +10,7 @@ import torch
 import nof
 from nof import synth
 
-prec = {"f32": 0, "split": 1, "f16x2": 2}[sys.argv[1] if len(sys.argv) > 1 else "f32"]
+prec = {"f32": 0, "split": 1, "f16x2": 2, "f16": 4}[sys.argv[1] if len(sys.argv) > 1 else "f32"]
 n = 1024
 m = nof.AcceleratedMipNeRF(max_rays=n, num_samples=(128, 128), precision=prec)
 r = synth.blender_rays(n, seed=1)

@@ -42,8 +42,19 @@ __device__ __forceinline__ void store_b64(__amdgpu_buffer_rsrc_t r, uint32_t vof
 // (nondeterministic act_h9 tiles; the compiler inserted no wait state for this >8-byte store-data hazard)
 template <int aux>
 __device__ __forceinline__ void store_b128(__amdgpu_buffer_rsrc_t r, uint32_t voff, int imm, const u32x4& v) {
+#ifdef NOF_DIAG_H32_NOSTORE
+  asm volatile("" ::"v"(v));
+  return;
+#endif
   __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, imm, aux);
   asm volatile("s_nop 1" ::"v"(v) : "memory");
+}
+// one 32 x 32 fp16 tile T of a side output in the slot layout (mlp_h32.h): lane (x, h) holds sample x's
+// packed pairs p[d] (features 8 (d >> 1) + 4h + 2 (d & 1) + {0, 1}); vslot = slot_off(x, h)
+template <int aux>
+__device__ __forceinline__ void store_tile(__amdgpu_buffer_rsrc_t r, uint32_t vslot, int T, const uint32_t (&p)[8]) {
+  store_b128<aux>(r, vslot, 2048 * T, u32x4{p[0], p[1], p[2], p[3]});
+  store_b128<aux>(r, vslot, 2048 * T + 1024, u32x4{p[4], p[5], p[6], p[7]});
 }
 __device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
   return __builtin_amdgcn_fdot2(__builtin_bit_cast(h16x2, a), __builtin_bit_cast(h16x2, b), c, false);
@@ -116,10 +127,7 @@ struct FwdEpiH {
         uint32_t p[8];
 #pragma unroll
         for (int d = 0; d < 8; ++d) p[d] = dst[2 * T + (d >> 2)][d & 3];
-        u32x4 ra, rb;
-        tile_row(p, ra, rb);
-        store_b128<kFwdAux>(blk, voff, 2048 * T, ra);
-        store_b128<kFwdAux>(blk, voff, 2048 * T + 16, rb);
+        store_tile<kFwdAux>(blk, voff, T, p);
         n += 2;
       }
       if (T == kNC - 1 && kk == epi_mask_pos(NK)) {
@@ -163,10 +171,7 @@ struct ViewEpiH {
       }
     if constexpr (kStore) {
       if (kk == epi_rows_pos(NK)) {
-        u32x4 ra, rb;
-        tile_row(p8, ra, rb);
-        store_b128<kFwdAux>(blk, voff, 2048 * T, ra);
-        store_b128<kFwdAux>(blk, voff, 2048 * T + 16, rb);
+        store_tile<kFwdAux>(blk, voff, T, p8);
         n += 2;
       }
       if (T == kNC - 1 && kk == epi_mask_pos(NK)) {
@@ -243,31 +248,9 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
 #pragma unroll
   for (int k = 0; k < kDirIn; ++k) pe[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pe_l), k));
 
-  const uint32_t vrow = tile_row_off(x, h);  // (sample x, lane half h) in a tiled block
+  const uint32_t vrow = slot_off(x, h);  // (sample x, lane half h): its 16-B slot in a tile half
   const uint32_t moff = (uint32_t)lane * 16u;
   const void* masks_blk = a.masks + (size_t)blk * kMaskSlots * 256;
-  if constexpr (kStore) {  // act_in row: IPE 0..95 (this lane: 48h ..), view PE 96..122, zeros 123..127
-    const __amdgpu_buffer_rsrc_t r = h32_rsrc(reinterpret_cast<const _Float16*>(a.act_in) + (size_t)m0 * kInF);
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {  // features 48h + 8k .. + 7: tile (48h + 8k) >> 5, column (48h + 8k) & 31
-      const int kk = k >> 1, q = k & 1, f = 48 * h + 8 * k;
-      store_b128<kFwdAux>(r, (uint32_t)(f >> 5) * 2048u + (uint32_t)x * 64u + (uint32_t)(f & 31) * 2u, 0,
-                 u32x4{ix[kk][2 * q], ix[kk][2 * q + 1], iy[kk][2 * q], iy[kk][2 * q + 1]});
-    }
-    uint32_t w[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float v[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int k0 = 2 * i + u, k1 = 16 + 2 * i + u;  // feature 96 + 16h + 2i + u
-        v[u] = h ? (k1 < kDirIn ? pe[k1 < kDirIn ? k1 : 0] : 0.0f) : pe[k0];
-      }
-      w[i] = pk_h(v[0], v[1]);
-    }
-    store_b128<kFwdAux>(r, vrow, 3 * 2048, u32x4{w[0], w[1], w[2], w[3]});  // tile 3: features 96 + 16h ..
-    store_b128<kFwdAux>(r, vrow, 3 * 2048 + 16, u32x4{w[4], w[5], w[6], w[7]});
-  }
   // the B fragments of layers 0 / 4: k-steps 0..2 from the lane half h = 0, 3..5 from h = 1 — one
   // permlane32 swap per packed dword moves each half's other-h' pairs across (tools/probe/h32_probe.hip)
   uint32_t ipe[6][4];
@@ -279,6 +262,24 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
       ipe[kk][e] = ix[kk][e];
       ipe[kk + 3][e] = iy[kk][e];
     }
+  }
+  if constexpr (kStore) {  // act_in: IPE 0..95 (k-steps 2t, 2t + 1 = the halves of tile t), view PE 96..122, zeros
+    const __amdgpu_buffer_rsrc_t r = h32_rsrc(reinterpret_cast<const _Float16*>(a.act_in) + (size_t)m0 * kInF);
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      store_b128<kFwdAux>(r, vrow, (k >> 1) * 2048 + (k & 1) * 1024, u32x4{ipe[k][0], ipe[k][1], ipe[k][2], ipe[k][3]});
+    uint32_t w[8];
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {  // tile 3 feature 8 (d >> 1) + 4h + 2 (d & 1) + u = view PE feature of that index
+      float v[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int f0 = 8 * (d >> 1) + 2 * (d & 1) + u, f1 = f0 + 4;  // lane half h = 0 / 1
+        v[u] = h ? (f1 < kDirIn ? pe[f1 < kDirIn ? f1 : 0] : 0.0f) : (f0 < kDirIn ? pe[f0 < kDirIn ? f0 : 0] : 0.0f);
+      }
+      w[d] = pk_h(v[0], v[1]);
+    }
+    store_tile<kFwdAux>(r, vrow, 3, w);
   }
 
   // ---- LDS tables: trunk biases, the wave's view-direction bias, packed w8 / W10 -------------------
@@ -409,10 +410,7 @@ struct BwdEpiH {
       uint32_t p[8];
 #pragma unroll
       for (int d = 0; d < 8; ++d) p[d] = dst[2 * T + (d >> 2)][d & 3];
-      u32x4 ra, rb;
-      tile_row(p, ra, rb);
-      store_b128<kBwdAux>(blk, voff, 2048 * T, ra);
-      store_b128<kBwdAux>(blk, voff, 2048 * T + 16, rb);
+      store_tile<kBwdAux>(blk, voff, T, p);
       n += 2;
     }
     return n;
@@ -452,7 +450,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   }
   // ---- delta9 = (W10^T dz_rgb) * relu'(layer 9) -> the B fragments of dh7, and delta9x ------------------
   uint32_t X[16][4], Y[16][4];
-  const uint32_t vrow = tile_row_off(x, h);
+  const uint32_t vrow = slot_off(x, h);
   const __amdgpu_buffer_rsrc_t d9 = h32_rsrc(reinterpret_cast<const _Float16*>(a.delta9x) + (size_t)m0 * kD9F);
   {
     const uint4 mk9 = *reinterpret_cast<const uint4*>(masks_blk + 8 * 256);
@@ -477,12 +475,9 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
         p[d] = pk_h(v[2 * d], v[2 * d + 1]) & mask_expand(word, 8 * (T & 1) + d);
         X[2 * T + (d >> 2)][d & 3] = p[d];
       }
-      u32x4 ra, rb;
-      tile_row(p, ra, rb);
-      store_b128<kBwdAux>(d9, vrow, 2048 * T, ra);
-      store_b128<kBwdAux>(d9, vrow, 2048 * T + 16, rb);
+      store_tile<kBwdAux>(d9, vrow, T, p);
     }
-    if (h == 0) store_b64<kBwdAux>(d9, (uint32_t)x * 64u, 4 * 2048, pk_h(dzs, dzc[0]), pk_h(dzc[1], dzc[2]));  // features 128..131
+    if (h == 0) store_b64<kBwdAux>(d9, vrow, 4 * 2048, pk_h(dzs, dzc[0]), pk_h(dzc[1], dzc[2]));  // features 128..131
   }
   h32_prologue_barrier();  // w8 table written, periods 0 and 1 landed
 

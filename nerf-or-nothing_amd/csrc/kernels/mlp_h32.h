@@ -30,16 +30,12 @@
 // left), and the barrier ending period P waits for period P + 1 with a counted vmcnt that lets the
 // period's own DMA and side-output stores stay in flight.
 //
-// Side outputs (sample-major, the transpose the weight-gradient launch reads with
-// ds_read_b64_tr_b16): activation / delta buffers are [M/32 blocks][F/32 tiles][32 samples][32
-// features] fp16 — every 32 x 32 tile a contiguous 2 KB of 64-B sample rows.  An epilogue tile leaves
-// each lane 4-feature runs of its sample (the MFMA output layout); one v_permlane32_swap per dword
-// pair gives lane half h the tile row's features 16h .. 16h + 15, stored as two 16-B stores (8-B
-// stores of the 4-feature runs ran at half the rate: MI355X_MICROARCH.md's store-issue tail), and the
-// weight-gradient launch stages each tile with two 1-KB LDS-DMA instructions.  ReLU masks: per
-// 32-sample block and layer slot 1 KB = [64 lanes][4 words]; word u holds tiles 2u, 2u + 1 as two
-// 16-bit shift registers (low half: even registers, high half: odd registers) — packed dword
-// k = 8 (T & 1) + d of tile T (registers 2d, 2d + 1) at bit 15 - k of each half.
+// Side outputs: activation / delta buffers are [M/32 blocks][F/32 tiles] of 2-KB fp16 tiles in the
+// slot layout below (slot_off) — exactly the epilogue's registers, two contiguous 1-KB stores per tile
+// — which the weight-gradient launch stages with LDS-DMA and reads back transposed with
+// ds_read_b64_tr_b16.  ReLU masks: per 32-sample block and layer slot 1 KB = [64 lanes][4 words]; word u
+// holds tiles 2u, 2u + 1 as two 16-bit shift registers (low half: even registers, high half: odd
+// registers) — packed dword k = 8 (T & 1) + d of tile T (registers 2d, 2d + 1) at bit 15 - k of each half.
 #pragma once
 #include <type_traits>
 
@@ -103,6 +99,9 @@ __device__ __forceinline__ uint32_t relu_pk(uint32_t p) {
 // shift one mask bit per half into w: w = 2w + min(relu'd half, 1) (inline asm: the compiler turns the
 // packed min into two compares, two selects and a perm)
 __device__ __forceinline__ uint32_t mask_shift(uint32_t w, uint32_t relu) {
+#ifdef NOF_DIAG_H32_NOMASK  // diagnostic: no mask bits (results garbage)
+  return w ^ relu;
+#endif
   uint32_t b, r;
   asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(b) : "v"(relu));
   asm("v_pk_mad_u16 %0, %1, 2, %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(w), "v"(b));
@@ -138,10 +137,16 @@ __device__ __forceinline__ void h32_barrier(int n) {
 
 // The weight ring.  `next` = stream position of period P + kDmaAhead while period P is consumed from
 // slot `cur`.
+#ifdef NOF_DIAG_H32_NOSTAGGER
+constexpr int kDmaLatePos = 0;
+#else
+constexpr int kDmaLatePos = 8;
+#endif
 struct H32Ring {
   float* lds;
   const float* next;
   int cur;
+  bool early;  // waves 0-3 (wave-uniform): DMA at positions 0 / 1, else at kDmaLatePos
   // periods 0 .. kDmaAhead - 1 into slots 0 .. kDmaAhead - 1; the caller's barrier then waits for the
   // first two (prologue_wait)
   __device__ __forceinline__ void prologue(const float* stream, int tid) {
@@ -152,6 +157,7 @@ struct H32Ring {
     }
     next = stream + kDmaAhead * kPeriodFloats;
     cur = 0;
+    early = kDmaLatePos == 0 || __builtin_amdgcn_readfirstlane(tid >> 6) < 4;
   }
   __device__ __forceinline__ void dma(int step, int tid) {
 #ifdef NOF_DIAG_H32_NODMA  // diagnostic builds only (timings; results are garbage)
@@ -160,6 +166,9 @@ struct H32Ring {
     slice16_dma_step(next, lds + ((cur + kDmaAhead) & (kH32Slots - 1)) * kPeriodFloats, tid, step);
   }
   __device__ __forceinline__ void end_period(int nstores) {
+#ifdef NOF_DIAG_H32_NOWAIT  // diagnostic: the period barrier does not wait for the DMA (results garbage)
+    nstores = 31;
+#endif
     h32_barrier(2 * (kDmaAhead - 1) + nstores);
     cur = (cur + 1) & (kH32Slots - 1);
     next += kPeriodFloats;
@@ -175,16 +184,28 @@ __device__ __forceinline__ void h32_prologue_barrier() { h32_barrier(2 * (kDmaAh
 // Epilogue piece schedule inside a host chunk of NK k-steps: the 8 packed dwords' VALU, then the
 // tile's row stores, the layer's mask store (last tile), the C-operand load of the next chunk.
 __host__ __device__ constexpr int epi_valu_pos(int d, int nk) { return nk >= 16 ? d : d >> 1; }
+#ifdef NOF_DIAG_H32_NOROWS  // diagnostic: no tile-row swaps / stores (results garbage)
+__host__ __device__ constexpr int epi_rows_pos(int nk) { return 99; }
+#else
 __host__ __device__ constexpr int epi_rows_pos(int nk) { return nk >= 16 ? 8 : 4; }
+#endif
 __host__ __device__ constexpr int epi_mask_pos(int nk) { return nk >= 16 ? 9 : 5; }
 __host__ __device__ constexpr int cinit_pos(int nk) { return nk >= 16 ? 12 : nk - 1; }
 
-// byte offset of (sample x, lane half h) in a tiled [32][F] block: + 2048 t for tile t
-__device__ __forceinline__ uint32_t tile_row_off(int x, int h) { return (uint32_t)x * 64u + (uint32_t)h * 32u; }
+// Side-output tile layout ("slot layout"): a 32-sample x 32-feature fp16 tile is 2 KB = two 1-KB halves
+// s (features 16s .. 16s + 15) of 64 16-B slots; slot 2x + hh of half s holds sample x's features
+// 16s + 4hh + {0..3} (bytes 0..7) and 16s + 8 + 4hh + {0..3} (bytes 8..15):
+//   byte(x, f) = (f >> 4) * 1024 + (2x + ((f >> 2) & 1)) * 16 + ((f >> 3) & 1) * 8 + (f & 3) * 2.
+// That is what lane (x, h) holds after an epilogue (p[4s .. 4s + 3], features 8 (d >> 1) + 4h + 2 (d & 1)),
+// so each half is ONE contiguous 1-KB store per wave (the row-major tile with its two 32-B runs per
+// lane stored at 16-B granularity ran the forward 0.222 -> 0.189 ms, the backward 0.206 -> 0.177 ms
+// slower), and every 4 consecutive features of a sample stay one aligned 8-B run — the unit
+// ds_read_b64_tr_b16 transposes in the weight-gradient launch (conflict-free: a 16-lane group reads
+// 4 samples x 16 features = 128 contiguous bytes).
+__device__ __forceinline__ uint32_t slot_off(int x, int h) { return (uint32_t)x * 32u + (uint32_t)h * 16u; }
 // v_permlane32_swap of four register pairs: vdst of lanes 32..63 <-> src0 of lanes 0..31 (measured,
 // tools/probe/h32_probe.hip), in inline asm with wait states on both sides — issued by the builtin
-// right after the VALU that wrote its operands (the epilogue drain after the last layer, nothing in
-// between) it returned stale values in some lanes (nondeterministic act_h9 tiles).
+// right after the VALU that wrote its operands it returned stale values in some lanes.
 __device__ __forceinline__ void swap32x4(uint32_t (&v)[4], uint32_t (&s)[4]) {
   asm volatile(
       "s_nop 4\n\t"
@@ -192,14 +213,6 @@ __device__ __forceinline__ void swap32x4(uint32_t (&v)[4], uint32_t (&s)[4]) {
       "v_permlane32_swap_b32 %2, %6\n\tv_permlane32_swap_b32 %3, %7\n\t"
       "s_nop 4"
       : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(s[0]), "+v"(s[1]), "+v"(s[2]), "+v"(s[3]));
-}
-// A tile's 8 packed dwords (p[d] = registers 2d, 2d + 1: features 8 (d >> 1) + 4h + 2 (d & 1) + {0, 1})
-// -> the 32 contiguous bytes of the tile row that lane half h stores (features 16h .. 16h + 15).
-__device__ __forceinline__ void tile_row(const uint32_t (&p)[8], u32x4& a, u32x4& b) {
-  uint32_t r0[4] = {p[0], p[1], p[2], p[3]}, r1[4] = {p[4], p[5], p[6], p[7]};
-  swap32x4(r0, r1);
-  a = u32x4{r0[0], r0[1], r1[0], r1[1]};
-  b = u32x4{r0[2], r0[3], r1[2], r1[3]};
 }
 
 struct NoEpiH {
@@ -258,14 +271,22 @@ __device__ __forceinline__ void h32_layer(const BSrc& bsrc, f32x16 (&acc)[2], H3
   static_for<0, N>([&](auto ic) {
     constexpr int i = decltype(ic)::value, c = i / NK, kk = i % NK, pos = i % kPeriod;
     asm volatile("" ::"v"(fr[i % R]));  // fragment i has landed before more reads issue
-    if constexpr (pos < 2) ring.dma(pos, tid);
+    if constexpr (pos < 2 || (pos >= kDmaLatePos && pos < kDmaLatePos + 2)) {
+      // waves 0-3 issue the period's DMA at positions 0 / 1, their SIMD partners 4-7 at kDmaLatePos (a
+      // wave-uniform branch): the partner's MFMAs keep the pipe busy while one wave sits in the issue
+      if ((pos < 2) == ring.early) ring.dma(pos & 1, tid);
+    }
     if constexpr (i + kReadAhead < N) fr[(i + kReadAhead) % R] = ring.frag((pos + kReadAhead) % kPeriod, lane);
     __builtin_amdgcn_sched_barrier(0);
     uint32_t b[4];
     bsrc(kk, b);
     acc[c & 1] = mfma_h32(fr[i % R], b, (kk == 0 && !kBias) ? f32x16{} : acc[c & 1]);
+#ifndef NOF_DIAG_H32_NOEPI  // diagnostic: no epilogue at all (results garbage)
     if constexpr (c == 0) nst += prev.piece(Prev::kNC - 1, kk, NK);  // the previous layer's last tile (acc[1])
     else nst += epi.piece(c - 1, kk, NK);
+#else
+    if constexpr (kk == 0) asm volatile("" ::"v"(acc[(c + 1) & 1][0]));  // keeps the MFMAs alive
+#endif
     if constexpr (kBias && c + 1 < NC && kk == cinit_pos(NK)) acc[(c + 1) & 1] = cinit_load(cv, c + 1);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (pos == kBarrierPos) {  // the next period's reads start at the next position

@@ -733,28 +733,28 @@ __device__ __forceinline__ void wg_item_s(const WgItem& item, const WgProblem& P
 #pragma unroll
     for (int c = 0; c < CB; ++c) acc[r][c] = f32x16{};
   float bsum = 0.0f;  // bias partial of row tile rowt[wc] (wave columns wc < RB)
-  // transposed-read address of this lane inside a tile (halves): sample row 16 ks + 8h + q (+4 for the
-  // second read), feature column 16 (G & 1) + 4p
+  // transposed-read address of this lane inside a tile (bytes, the slot layout of mlp_h32.h): the 8-B
+  // run of features 16 (G & 1) + 4p .. + 3 of sample 16 ks + 8 (G >> 1) + q (+4 for the second read)
   const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const int toff = (8 * (G >> 1) + q) * 32 + 16 * (G & 1) + 4 * p;
+  const int toff = (G & 1) * 1024 + (8 * (G >> 1) + q) * 32 + (p & 1) * 16 + (p >> 1) * 8;
   // inline asm: through the builtin the compiler orders every transposed read behind the LDS-DMA in
   // flight (s_waitcnt vmcnt(0) before each k-step's reads); the ring's own counted waits order them
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
   // (the asm outputs are written asynchronously: nothing may copy them before the lgkmcnt wait, so each
   // read has its own output and the fragments are assembled after the wait)
   auto frag = [&](uint32_t stage_b, int tile, s16x4v& lo, s16x4v& hi) {
-    const uint32_t a = stage_b + (uint32_t)(tile * 1024 + toff) * 2u;
+    const uint32_t a = stage_b + (uint32_t)(tile * 2048 + toff);
 #if defined(NOF_DIAG_WS_NOREAD)
     lo = s16x4v{(short)a, 0, 0, 0};
     hi = lo;
 #else
     asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a));
-    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:256" : "=v"(hi) : "v"(a));
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:128" : "=v"(hi) : "v"(a));
 #endif
   };
   struct Frags { s16x4v al[RB], ah[RB], bl[CB], bh[CB]; };
   auto issue = [&](int slot, int ks, Frags& f) {  // k-step ks (samples 16 ks ..) of the block in `slot`
-    const uint32_t sb = lds_base + (uint32_t)(slot * kStage + ks * 512) * 2u;
+    const uint32_t sb = lds_base + (uint32_t)(slot * kStage) * 2u + (uint32_t)ks * 512u;  // + 16 samples x 32 B
 #pragma unroll
     for (int r = 0; r < RB; ++r) frag(sb, rowt[r], f.al[r], f.ah[r]);
 #pragma unroll

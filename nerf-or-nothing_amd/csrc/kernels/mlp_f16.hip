@@ -50,11 +50,17 @@ __device__ __forceinline__ void store_b128(__amdgpu_buffer_rsrc_t r, uint32_t vo
   asm volatile("s_nop 1" ::"v"(v) : "memory");
 }
 // one 32 x 32 fp16 tile T of a side output in the slot layout (mlp_h32.h): lane (x, h) holds sample x's
-// packed pairs p[d] (features 8 (d >> 1) + 4h + 2 (d & 1) + {0, 1}); vslot = slot_off(x, h)
+// packed pairs p[d] (features 8 (d >> 1) + 4h + 2 (d & 1) + {0, 1}); vslot = slot_off(x, h).  Half s is
+// p[4s .. 4s + 3]: one contiguous 1-KB store.
+template <int aux>
+__device__ __forceinline__ void store_half(__amdgpu_buffer_rsrc_t r, uint32_t vslot, int T, int s, uint32_t p0,
+                                           uint32_t p1, uint32_t p2, uint32_t p3) {
+  store_b128<aux>(r, vslot, 2048 * T + 1024 * s, u32x4{p0, p1, p2, p3});
+}
 template <int aux>
 __device__ __forceinline__ void store_tile(__amdgpu_buffer_rsrc_t r, uint32_t vslot, int T, const uint32_t (&p)[8]) {
-  store_b128<aux>(r, vslot, 2048 * T, u32x4{p[0], p[1], p[2], p[3]});
-  store_b128<aux>(r, vslot, 2048 * T + 1024, u32x4{p[4], p[5], p[6], p[7]});
+  store_half<aux>(r, vslot, T, 0, p[0], p[1], p[2], p[3]);
+  store_half<aux>(r, vslot, T, 1, p[4], p[5], p[6], p[7]);
 }
 __device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
   return __builtin_amdgcn_fdot2(__builtin_bit_cast(h16x2, a), __builtin_bit_cast(h16x2, b), c, false);
@@ -123,13 +129,13 @@ struct FwdEpiH {
         if (dens) zs = dot2(p, w8[T * 16 + d], zs);
       }
     if constexpr (kStore) {
-      if (kk == epi_rows_pos(NK)) {
-        uint32_t p[8];
 #pragma unroll
-        for (int d = 0; d < 8; ++d) p[d] = dst[2 * T + (d >> 2)][d & 3];
-        store_tile<kFwdAux>(blk, voff, T, p);
-        n += 2;
-      }
+      for (int sh = 0; sh < 2; ++sh)
+        if (kk == epi_half_pos(sh, NK)) {
+          const uint32_t(&q)[4] = dst[2 * T + sh];
+          store_half<kFwdAux>(blk, voff, T, sh, q[0], q[1], q[2], q[3]);
+          ++n;
+        }
       if (T == kNC - 1 && kk == epi_mask_pos(NK)) {
         store_b128<kFwdAux>(mrs, moff, mimm, u32x4{mw[0], mw[1], mw[2], mw[3]});
         ++n;
@@ -170,10 +176,12 @@ struct ViewEpiH {
         for (int c = 0; c < 3; ++c) zc[c] = dot2(p, w10[(c * 4 + T) * 16 + d], zc[c]);
       }
     if constexpr (kStore) {
-      if (kk == epi_rows_pos(NK)) {
-        store_tile<kFwdAux>(blk, voff, T, p8);
-        n += 2;
-      }
+#pragma unroll
+      for (int sh = 0; sh < 2; ++sh)
+        if (kk == epi_half_pos(sh, NK)) {
+          store_half<kFwdAux>(blk, voff, T, sh, p8[4 * sh], p8[4 * sh + 1], p8[4 * sh + 2], p8[4 * sh + 3]);
+          ++n;
+        }
       if (T == kNC - 1 && kk == epi_mask_pos(NK)) {
         store_b128<kFwdAux>(mrs, moff, 8 * 1024, u32x4{mw[0], mw[1], mw[2], mw[3]});
         ++n;
@@ -406,13 +414,13 @@ struct BwdEpiH {
         const uint32_t word = (T >> 1) == 0 ? mk.x : ((T >> 1) == 1 ? mk.y : ((T >> 1) == 2 ? mk.z : mk.w));
         dst[2 * T + (d >> 2)][d & 3] = pk_h(v0, v1) & mask_expand(word, 8 * (T & 1) + d);
       }
-    if (kk == epi_rows_pos(NK)) {
-      uint32_t p[8];
 #pragma unroll
-      for (int d = 0; d < 8; ++d) p[d] = dst[2 * T + (d >> 2)][d & 3];
-      store_tile<kBwdAux>(blk, voff, T, p);
-      n += 2;
-    }
+    for (int sh = 0; sh < 2; ++sh)
+      if (kk == epi_half_pos(sh, NK)) {
+        const uint32_t(&q)[4] = dst[2 * T + sh];
+        store_half<kBwdAux>(blk, voff, T, sh, q[0], q[1], q[2], q[3]);
+        ++n;
+      }
     return n;
   }
 };

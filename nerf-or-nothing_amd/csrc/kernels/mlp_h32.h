@@ -184,10 +184,11 @@ __device__ __forceinline__ void h32_prologue_barrier() { h32_barrier(2 * (kDmaAh
 // Epilogue piece schedule inside a host chunk of NK k-steps: the 8 packed dwords' VALU, then the
 // tile's row stores, the layer's mask store (last tile), the C-operand load of the next chunk.
 __host__ __device__ constexpr int epi_valu_pos(int d, int nk) { return nk >= 16 ? d : d >> 1; }
-#ifdef NOF_DIAG_H32_NOROWS  // diagnostic: no tile-row swaps / stores (results garbage)
-__host__ __device__ constexpr int epi_rows_pos(int nk) { return 99; }
+// tile half s (packed dwords 4s .. 4s + 3) goes out one k-step after its last dword is computed
+#ifdef NOF_DIAG_H32_NOROWS  // diagnostic: no side-output tile stores (results garbage)
+__host__ __device__ constexpr int epi_half_pos(int s, int nk) { return 99; }
 #else
-__host__ __device__ constexpr int epi_rows_pos(int nk) { return nk >= 16 ? 8 : 4; }
+__host__ __device__ constexpr int epi_half_pos(int s, int nk) { return nk >= 16 ? 4 + 4 * s : 2 + 2 * s; }
 #endif
 __host__ __device__ constexpr int epi_mask_pos(int nk) { return nk >= 16 ? 9 : 5; }
 __host__ __device__ constexpr int cinit_pos(int nk) { return nk >= 16 ? 12 : nk - 1; }

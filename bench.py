@@ -460,10 +460,13 @@ def main():
                 for m, o in zip(models, opts):
                     o.step(m.mlp.allParams, m.mlp.allGradients, nof.learning_rate_decay(k + 1))
                 if native is not None:
-                    for nd in native:
-                        nd.wait()  # failure detection: an RCCL error or a stall raises instead of hanging
+                    for nd in native:  # failure detection, one step behind (the host queues the next step
+                        nd.step_end()  # meanwhile): an RCCL error or a stall raises instead of hanging
 
             def sync_all():
+                if native is not None:
+                    for nd in native:
+                        nd.wait()  # the last step's all-reduces (bounded)
                 for d in devs:
                     torch.cuda.synchronize(d)
 

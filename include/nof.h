@@ -286,6 +286,10 @@ nof_status nof_dp_attach(nof_dp* dp, nof_mipnerf* h, void* comm_stream);
  * the communicator is aborted and NOF_ERR_RCCL returned.  Every later call on an aborted dp
  * returns NOF_ERR_RCCL (never hangs). */
 nof_status nof_dp_wait(nof_dp* dp, int32_t timeout_ms);
+/* End of a training step, one step behind: the same bounded wait for the all-reduces of the PREVIOUS
+ * call's step (this step's become the next call's), so the host can enqueue the next step while this
+ * one's exchange runs.  A final nof_dp_wait covers the last step. */
+nof_status nof_dp_step_end(nof_dp* dp, int32_t timeout_ms);
 nof_status nof_dp_abort(nof_dp* dp);
 nof_status nof_dp_destroy(nof_dp* dp);
 /* Loopback group (SURVEY.md §4 "T0 DP logic"): k <= 8 communicators of this process on ONE device

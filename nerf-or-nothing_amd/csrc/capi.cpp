@@ -310,6 +310,9 @@ nof_status nof_dp_attach(nof_dp* dp, nof_mipnerf* h, void* comm_stream) {
 nof_status nof_dp_wait(nof_dp* dp, int32_t timeout_ms) {
   return guard([&] { KEEP_DEVICE; ARG(timeout_ms >= 0); dp_wait(dp, timeout_ms); });
 }
+nof_status nof_dp_step_end(nof_dp* dp, int32_t timeout_ms) {
+  return guard([&] { KEEP_DEVICE; ARG(timeout_ms >= 0); dp_step_end(dp, timeout_ms); });
+}
 nof_status nof_dp_abort(nof_dp* dp) {
   return guard([&] { KEEP_DEVICE; dp_abort(dp); });
 }

@@ -47,6 +47,8 @@ struct nof_dp {
   std::string why;                  // reason of the abort
   hipEvent_t done = nullptr;        // recorded after the last enqueued all-reduce
   bool pending = false;
+  hipEvent_t lag = nullptr;         // dp_step_end: the previous step's last all-reduce
+  bool lag_pending = false;
   // attached (overlapped) mode
   AcceleratedNeRFUtils::AcceleratedMipNeRF* model = nullptr;
   hipStream_t comm_stream = nullptr;
@@ -91,6 +93,7 @@ static void abort_comm(nof_dp* dp, const std::string& why) {
   DPLOG("abort returned\n");
   dp->aborted = true;
   dp->pending = false;
+  dp->lag_pending = false;
   dp->why = why;
   throw Error(NOF_ERR_RCCL, why);
 }
@@ -402,20 +405,12 @@ void dp_attach(nof_dp* dp, AcceleratedMipNeRF* model, hipStream_t comm_stream) {
   model->mlp->set_bucket_hook(&bucket_hook, dp);
 }
 
-void dp_wait(nof_dp* dp, int timeout_ms) {
-  check_live(dp);
-  if (dp->loop && loop_incomplete(dp)) {  // a peer that never arrives: the loopback "missing rank"
-    const std::string why = "loopback all-reduce incomplete: a member of the group of " +
-                            std::to_string(dp->loop->k) + " never arrived";
-    dp->aborted = true;
-    dp->why = why;
-    throw Error(NOF_ERR_RCCL, why);
-  }
-  if (!dp->pending) return;
+// bounded poll of one event on the communicator's stream: an RCCL error or the time limit aborts
+static void wait_event(nof_dp* dp, hipEvent_t ev, int timeout_ms) {
   const int limit = timeout_ms > 0 ? timeout_ms : dp->timeout_ms;
   const auto t0 = Clock::now();
   for (;;) {
-    const hipError_t e = hipEventQuery(dp->done);
+    const hipError_t e = hipEventQuery(ev);
     if (e == hipSuccess) break;
     if (e != hipErrorNotReady) NOF_HIP(e);
     ncclResult_t r = ncclSuccess;
@@ -426,7 +421,40 @@ void dp_wait(nof_dp* dp, int timeout_ms) {
       abort_comm(dp, "all-reduce did not complete within " + std::to_string(limit) + " ms");
     std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
+}
+
+static void check_loopback(nof_dp* dp) {
+  if (dp->loop && loop_incomplete(dp)) {  // a peer that never arrives: the loopback "missing rank"
+    const std::string why = "loopback all-reduce incomplete: a member of the group of " +
+                            std::to_string(dp->loop->k) + " never arrived";
+    dp->aborted = true;
+    dp->why = why;
+    throw Error(NOF_ERR_RCCL, why);
+  }
+}
+
+void dp_wait(nof_dp* dp, int timeout_ms) {
+  check_live(dp);
+  check_loopback(dp);
+  // every all-reduce of a communicator is ordered on one stream: the last one done implies the lagged one
+  if (dp->pending) wait_event(dp, dp->done, timeout_ms);
   dp->pending = false;
+  dp->lag_pending = false;
+}
+
+// End of a training step, one step behind: the bounded wait covers the PREVIOUS step's
+// all-reduces, so the host can enqueue step k + 1 while step k's exchange and Adam still run; this
+// step's become the next call's (or a final dp_wait's).
+void dp_step_end(nof_dp* dp, int timeout_ms) {
+  check_live(dp);
+  check_loopback(dp);
+  if (dp->lag_pending) wait_event(dp, dp->lag, timeout_ms);
+  dp->lag_pending = false;
+  if (dp->pending) {  // the step's last all-reduce becomes the lagged one; `done` is re-recorded next step
+    std::swap(dp->done, dp->lag);
+    dp->pending = false;
+    dp->lag_pending = true;
+  }
 }
 
 void dp_abort(nof_dp* dp) {
@@ -436,6 +464,7 @@ void dp_abort(nof_dp* dp) {
   if (dp->comm) (void)ncclCommAbort(dp->comm);
   dp->aborted = true;
   dp->pending = false;
+  dp->lag_pending = false;
   dp->why = "aborted by the caller";
 }
 
@@ -457,6 +486,7 @@ void dp_destroy(nof_dp* dp) {
   }
   if (dp->comm && !dp->aborted) (void)ncclCommDestroy(dp->comm);
   if (dp->done) (void)hipEventDestroy(dp->done);
+  if (dp->lag) (void)hipEventDestroy(dp->lag);
   for (hipEvent_t e : dp->ready)
     if (e) (void)hipEventDestroy(e);
   if (dp->own_stream) (void)hipStreamDestroy(dp->comm_stream);

@@ -10,6 +10,7 @@ void dp_allreduce(nof_dp* dp, float* buf, int64_t count, hipStream_t st);
 void dp_allreduce_grads(int n, nof_dp* const* dps, AcceleratedMipNeRF* const* models, hipStream_t const* streams);
 void dp_attach(nof_dp* dp, AcceleratedMipNeRF* model, hipStream_t comm_stream);
 void dp_wait(nof_dp* dp, int timeout_ms);
+void dp_step_end(nof_dp* dp, int timeout_ms);
 void dp_abort(nof_dp* dp);
 void dp_destroy(nof_dp* dp);
 void dp_init_loopback(int k, int device, nof_dp** out);

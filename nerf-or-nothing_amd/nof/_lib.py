@@ -109,6 +109,7 @@ SIGNATURES = {
     "nof_dp_init_rank_timeout": [P, I32, I32, I32, I32, C.POINTER(P)],
     "nof_dp_attach": [P, P, P],
     "nof_dp_wait": [P, I32],
+    "nof_dp_step_end": [P, I32],
     "nof_dp_abort": [P],
     "nof_dp_init_all": [I32, C.POINTER(I32), C.POINTER(P)],
     "nof_dp_allreduce": [P, P, C.c_int64, P],

@@ -148,6 +148,13 @@ class NativeDP:
 
         call("nof_dp_wait", self._h, timeout_ms)
 
+    def step_end(self, timeout_ms: int = 0):
+        """nof_dp_step_end: the bounded wait of wait(), one step behind (the previous step's
+        all-reduces), so the host enqueues the next step meanwhile; a final wait() covers the last."""
+        from ._lib import call
+
+        call("nof_dp_step_end", self._h, timeout_ms)
+
     def abort(self):
         from ._lib import call
 

@@ -1,7 +1,7 @@
 """tools/pmc_summary.py turns rocprofv3 CSVs into the committed evidence bench.py reads: per-launch
 HBM bytes (2 * FETCH_SIZE + WRITE_SIZE, KB), MFMA busy over 1024 SIMDs x GRBM_GUI_ACTIVE / 8, the
-LDS-array busy fraction, and the lookup keys per precision mode (the fp16-block weight-gradient kernel
-is shared by f16x2 and F16, so its key follows the run's mode).  Synthetic CSVs, CPU only."""
+LDS-array busy fraction, and the lookup keys per precision mode (the F16 mode's kernels
+k_mlp_fwd_h32 / k_wgrad_s, the f16x2 mode's k_wgrad_h).  Synthetic CSVs, CPU only."""
 import csv
 import json
 import os
@@ -21,7 +21,8 @@ def _write(path, header, rows):
 
 def _run(tmp, suffix):
     src, dst = os.path.join(tmp, "src"), os.path.join(tmp, "profiles")
-    kernels = {"void nof::k_mlp_fwd16<4, true>(nof::FwdArgs)": 0.5e6, "void nof::k_wgrad_h(nof::WgradArgs)": 0.25e6}
+    kernels = {"void nof::k_mlp_fwd_h32<true>(nof::FwdArgs)": 0.5e6, "void nof::k_wgrad_s(nof::WgradArgs)": 0.25e6,
+               "void nof::k_wgrad_h(nof::WgradArgs)": 0.25e6}
     _write(os.path.join(src, "trace", "run_kernel_stats.csv"), ["Name", "Calls", "AverageNs"],
            [[k, 10, ns] for k, ns in kernels.items()])
     cyc = 2.0e9 * 0.5e-3  # 0.5 ms at 2.0 GHz
@@ -40,15 +41,15 @@ def _run(tmp, suffix):
 
 def test_f16_mode_keys_and_fractions(tmp_path):
     per, traffic, busy = _run(str(tmp_path), "_f16")
-    fwd = per["k_mlp_fwd16<4, true>"]
+    fwd = per["k_mlp_fwd_h32<true>"]
     assert fwd["hbm_bytes_per_launch"] == (2 * 1000.0 + 500.0) * 1024
     assert abs(fwd["mfma_busy"] - 0.25) < 1e-4 and abs(fwd["lds_busy"] - 0.5) < 1e-4
     assert abs(fwd["eff_clock_GHz"] - 2.0) < 1e-3  # 0.5 ms dispatch: clock reported
-    assert per["k_wgrad_h"]["eff_clock_GHz"] is None  # < 0.3 ms: GRBM quotient not trusted
-    assert set(traffic) >= {"mlp_fwd_f16", "wgrad_f16"} and "wgrad_f16x2" not in traffic
+    assert per["k_wgrad_s"]["eff_clock_GHz"] is None  # < 0.3 ms: GRBM quotient not trusted
+    assert set(traffic) >= {"mlp_fwd_f16", "wgrad_f16", "wgrad_f16x2"}
     assert busy["mlp_fwd_f16"] == fwd["mfma_busy"]
 
 
 def test_f16x2_run_keeps_its_weight_gradient_key(tmp_path):
-    _, traffic, _ = _run(str(tmp_path), "_f16x2")
-    assert "wgrad_f16x2" in traffic and "wgrad_f16" not in traffic
+    per, traffic, _ = _run(str(tmp_path), "_f16x2")
+    assert traffic["wgrad_f16x2"] == per["k_wgrad_h"]["hbm_bytes_per_launch"]

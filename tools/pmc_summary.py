@@ -72,9 +72,8 @@ json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
 # lookups read by bench.py (bench kernel-timer names; other precision modes keyed with "_<mode>")
 names = {"k_mlp_fwd16<0, true>": "mlp_fwd", "k_mlp_bwd16<0>": "mlp_bwd", "k_wgrad": "wgrad",
          "k_mlp_fwd16<2, true>": "mlp_fwd_f16x2", "k_mlp_bwd16<2>": "mlp_bwd_f16x2",
-         "k_mlp_fwd16<4, true>": "mlp_fwd_f16", "k_mlp_bwd16<4>": "mlp_bwd_f16",
-         # f16x2 and F16 share the fp16-block weight-gradient kernel: key it by the run's mode
-         "k_wgrad_h": "wgrad" + (suffix if suffix in ("_f16x2", "_f16") else "_f16x2"),
+         "k_mlp_fwd_h32<true>": "mlp_fwd_f16", "k_mlp_bwd_h32": "mlp_bwd_f16", "k_wgrad_s": "wgrad_f16",
+         "k_wgrad_h": "wgrad_f16x2",
          "k_mlp_fwd<1, true>": "mlp_fwd_split", "k_mlp_bwd<1>": "mlp_bwd_split", "k_wgrad_x3<1>": "wgrad_split",
          "k_mlp_fwd16<3, true>": "mlp_fwd_f16split", "k_mlp_bwd16<3>": "mlp_bwd_f16split",
          "k_wgrad_x3<2>": "wgrad_f16split",

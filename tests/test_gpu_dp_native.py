@@ -43,3 +43,29 @@ def test_native_dp_world1_identity(gpu):
     assert np.array_equal(nof.to_numpy(m.mlp.flat_grads()[0], (546948,)), g0)
     d1.close()
     m.close()
+
+
+def test_step_end_waits_one_step_behind(gpu):
+    """nof_dp_step_end (ADVICE r2): each call waits, boundedly, for the PREVIOUS step's all-reduces;
+    a final nof_dp_wait covers the last.  Loopback group of two on the one GPU: 1, 2 -> 3 -> 6 -> 12."""
+    import torch
+    import nof
+    from nof.dp import NativeDP
+
+    dps = NativeDP.init_loopback(2, 0)
+    ts = [torch.full((1000,), float(i + 1), device=gpu) for i in range(2)]
+    for _ in range(3):
+        for d, t in zip(dps, ts):
+            d.allreduce(t.data_ptr(), 1000)
+        for d in dps:
+            d.step_end()
+    for d in dps:
+        d.wait()
+    torch.cuda.synchronize()
+    for t in ts:
+        assert torch.equal(t, torch.full((1000,), 12.0, device=gpu))
+    dps[0].abort()
+    with pytest.raises(nof.NofError):
+        dps[0].step_end()
+    for d in dps:
+        d.close()

@@ -221,7 +221,17 @@ typedef struct nof_batch {
   float* pixels;                          /* [n][3] */
   int32_t* record_index;                  /* [n] record drawn for each ray */
 } nof_batch;
+/* The whole record file is copied into HBM, unless it exceeds half the device's free memory: then it
+ * is streamed as by nof_dataset_open_streaming. */
 nof_status nof_dataset_open(const char* path, int32_t device, nof_dataset** out);
+/* A record file resident in HBM iff it holds at most max_resident_records records; otherwise STREAMED
+ * (files larger than HBM): each nof_dataset_next reads the batch's records from the file, as
+ * BinDataset.LoadBatch does (BinDataset.cs:31-38), into pinned host memory, copies them to the device
+ * and unpacks them with the same gather — batches bit-identical to the resident dataset's — while the
+ * records of the next step of the same request (step + 1) are prefetched on a host thread. */
+nof_status nof_dataset_open_streaming(const char* path, int32_t device, int64_t max_resident_records,
+                                      nof_dataset** out);
+nof_status nof_dataset_is_streaming(nof_dataset* ds, int32_t* streaming);
 nof_status nof_dataset_from_host(const float* records /* count x 16 */, int64_t count, int32_t device,
                                  nof_dataset** out);
 nof_status nof_dataset_count(nof_dataset* ds, int64_t* count);

@@ -243,6 +243,19 @@ nof_status nof_dataset_open(const char* path, int32_t device, nof_dataset** out)
     *out = d;
   });
 }
+nof_status nof_dataset_open_streaming(const char* path, int32_t device, int64_t max_resident_records,
+                                      nof_dataset** out) {
+  return guard([&] {
+    ARG(path && out && max_resident_records >= 0);
+    KEEP_DEVICE;
+    auto* d = new nof_dataset{nullptr};
+    try { d->impl = new RayDataset(std::string(path), device, max_resident_records); } catch (...) { delete d; throw; }
+    *out = d;
+  });
+}
+nof_status nof_dataset_is_streaming(nof_dataset* ds, int32_t* streaming) {
+  return guard([&] { ARG(ds && streaming); *streaming = ds->impl->streaming() ? 1 : 0; });
+}
 nof_status nof_dataset_from_host(const float* records, int64_t count, int32_t device, nof_dataset** out) {
   return guard([&] {
     ARG(records && out);

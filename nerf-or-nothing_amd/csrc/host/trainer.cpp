@@ -1,5 +1,8 @@
 #include "trainer.h"
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -14,7 +17,7 @@ RayDataset::RayDataset(const float* host_records, int64_t count, int device) : d
   NOF_HIP(hipMemcpy(rec_.p, host_records, (size_t)count * 64, hipMemcpyHostToDevice));
 }
 
-RayDataset::RayDataset(const std::string& path, int device) : device_(device) {
+RayDataset::RayDataset(const std::string& path, int device, int64_t max_resident) : device_(device) {
   std::unique_ptr<FILE, int (*)(FILE*)> f(std::fopen(path.c_str(), "rb"), &std::fclose);
   NOF_REQUIRE(f != nullptr, "cannot open record file " + path);
   std::fseek(f.get(), 0, SEEK_END);
@@ -24,6 +27,21 @@ RayDataset::RayDataset(const std::string& path, int device) : device_(device) {
   count_ = bytes / 64;  // BinDataset.cs:15
   NOF_REQUIRE(count_ <= 0xFFFFFFFFll, "too many records");
   NOF_HIP(hipSetDevice(device));
+  bool resident;
+  if (max_resident < 0) {
+    size_t free_b = 0, total_b = 0;
+    NOF_HIP(hipMemGetInfo(&free_b, &total_b));
+    resident = (size_t)bytes <= free_b / 2;
+  } else {
+    resident = count_ <= max_resident;
+  }
+  if (!resident) {  // streaming: records stay in the file, batches are fetched per step
+    fd_ = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+    NOF_REQUIRE(fd_ >= 0, "cannot open record file " + path);
+    for (hipEvent_t& e : copied_) NOF_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    NOF_HIP(hipEventCreateWithFlags(&gathered_, hipEventDisableTiming));
+    return;
+  }
   rec_.alloc((size_t)count_ * 16);
   // stream through a pinned staging buffer (64 MB chunks): never the whole file in host memory
   const size_t chunk = 64u << 20;
@@ -37,6 +55,26 @@ RayDataset::RayDataset(const std::string& path, int device) : device_(device) {
     NOF_REQUIRE(got == want, "short read from record file");
     NOF_HIP(hipMemcpy(reinterpret_cast<char*>(rec_.p) + done, stage, want, hipMemcpyHostToDevice));
     done += want;
+  }
+}
+
+RayDataset::~RayDataset() {
+  if (prefetch_.joinable()) prefetch_.join();
+  if (fd_ >= 0) ::close(fd_);
+  for (int b = 0; b < 2; ++b) {
+    if (copied_[b]) (void)hipEventSynchronize(copied_[b]);
+    if (hrec_[b]) (void)hipHostFree(hrec_[b]);
+    if (copied_[b]) (void)hipEventDestroy(copied_[b]);
+  }
+  if (gathered_) (void)hipEventDestroy(gathered_);
+}
+
+void RayDataset::fetch(int b, int n, uint64_t seed, uint32_t step, uint32_t ray_base) {
+  float* dst = hrec_[b];
+  for (int r = 0; r < n; ++r) {  // BinDataset.LoadBatch: one 64-byte record per ray (BinDataset.cs:31-38)
+    const uint32_t idx = nof::batch_record_host(seed, step, ray_base + (uint32_t)r, count_);
+    const ssize_t got = ::pread(fd_, dst + 16 * (size_t)r, 64, (off_t)idx * 64);
+    NOF_REQUIRE(got == 64, "short read from record file");
   }
 }
 
@@ -98,6 +136,17 @@ void RayDataset::reserve(int n, hipStream_t st) {
   NOF_HIP(hipStreamSynchronize(st));  // the previous batch may still be read
   o_.alloc(3 * (size_t)n); d_.alloc(3 * (size_t)n); vd_.alloc(3 * (size_t)n); r_.alloc(n); nr_.alloc(n);
   fr_.alloc(n); lm_.alloc(n); pix_.alloc(3 * (size_t)n); idx_.alloc(n); msum_.alloc(1);
+  if (streaming()) {  // the device staging slot and the two pinned record buffers
+    if (prefetch_.joinable()) prefetch_.join();
+    pre_.valid = false;
+    NOF_HIP(hipDeviceSynchronize());  // no copy from the old pinned buffers, no gather from the old slot
+    rec_.alloc(16 * (size_t)n);
+    for (float*& h : hrec_) {
+      if (h) NOF_HIP(hipHostFree(h));
+      h = nullptr;
+      NOF_HIP(hipHostMalloc(reinterpret_cast<void**>(&h), 64 * (size_t)n, hipHostMallocDefault));
+    }
+  }
   cap_ = n;
 }
 
@@ -106,8 +155,47 @@ void RayDataset::next(int n, uint64_t seed, uint32_t step, uint32_t ray_base, hi
   NOF_REQUIRE(n > 0 && out, "bad batch request");
   NOF_HIP(hipSetDevice(device_));
   reserve(n, st);
+  int staged = 0;
+  if (streaming()) {
+    // this batch's records: the prefetch made during the previous call when it guessed this request
+    // (same n / seed / ray base, the next step), else a synchronous fetch into the other buffer
+    if (prefetch_.joinable()) prefetch_.join();
+    int b;
+    if (pre_.valid && prefetch_error_.empty() && pre_.n == n && pre_.seed == seed && pre_.step == step &&
+        pre_.ray_base == ray_base) {
+      b = pre_buf_;
+    } else {
+      b = cur_ ^ 1;
+      NOF_HIP(hipEventSynchronize(copied_[b]));  // its previous copy has left the pinned buffer
+      fetch(b, n, seed, step, ray_base);
+    }
+    pre_.valid = false;
+    prefetch_error_.clear();
+    NOF_HIP(hipStreamWaitEvent(st, gathered_, 0));  // the previous batch's gather has read the slot
+    NOF_HIP(hipMemcpyAsync(rec_.p, hrec_[b], 64 * (size_t)n, hipMemcpyHostToDevice, st));
+    NOF_HIP(hipEventRecord(copied_[b], st));
+    cur_ = b;
+    staged = 1;
+  }
   NOF_HIP(nof::launch_gather_batch(rec_.p, count_, n, seed, step, ray_base, o_.p, d_.p, vd_.p, r_.p, nr_.p, fr_.p,
-                                   lm_.p, pix_.p, idx_.p, host_msum ? msum_.p : nullptr, st));
+                                   lm_.p, pix_.p, idx_.p, host_msum ? msum_.p : nullptr, st, staged));
+  if (streaming()) {
+    NOF_HIP(hipEventRecord(gathered_, st));
+    // prefetch the likely next request (the next step of the same shard) into the other buffer while
+    // the GPU runs this step
+    const int pb = cur_ ^ 1;
+    pre_ = Key{n, seed, step + 1, ray_base, true};
+    pre_buf_ = pb;
+    prefetch_ = std::thread([this, pb, n, seed, step, ray_base] {
+      try {
+        NOF_HIP(hipSetDevice(device_));
+        NOF_HIP(hipEventSynchronize(copied_[pb]));
+        fetch(pb, n, seed, step + 1, ray_base);
+      } catch (const std::exception& e) {
+        prefetch_error_ = e.what();  // the next call fetches synchronously and reports the error
+      }
+    });
+  }
   out->n = n;
   out->origins = o_.p; out->directions = d_.p; out->viewdirs = vd_.p; out->radii = r_.p;
   out->nears = nr_.p; out->fars = fr_.p; out->loss_mults = lm_.p; out->pixels = pix_.p; out->record_index = idx_.p;

@@ -26,13 +26,14 @@ __global__ __launch_bounds__(256) void k_gather_batch(const float4* __restrict__
                                                       float* __restrict__ vd, float* __restrict__ radius,
                                                       float* __restrict__ near, float* __restrict__ far,
                                                       float* __restrict__ lm, float* __restrict__ pix,
-                                                      int* __restrict__ idx_out) {
+                                                      int* __restrict__ idx_out, int staged) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   const int r = g >> 2, q = g & 3;
   if (r >= n) return;
   const uint32_t idx = batch_record(seed, step, ray_base + (uint32_t)r, count);
   NOF_DCHECK((int64_t)idx < count, kChkGather);
-  const float4 v = rec[(size_t)idx * 4 + q];  // floats 4q .. 4q+3 of the record (BinDataset.cs:40-49)
+  // staged (streaming datasets): the host already fetched ray r's record into slot r
+  const float4 v = rec[(staged ? (size_t)r : (size_t)idx) * 4 + q];  // floats 4q .. 4q+3 (BinDataset.cs:40-49)
   switch (q) {
     case 0:  // origin xyz, direction x
       o[3 * r] = v.x; o[3 * r + 1] = v.y; o[3 * r + 2] = v.z; d[3 * r] = v.w;
@@ -63,14 +64,21 @@ __global__ __launch_bounds__(1024) void k_sum(const float* __restrict__ x, int n
   if (threadIdx.x == 0) *out = red[0];
 }
 
+uint32_t batch_record_host(uint64_t seed, uint32_t step, uint32_t gray, int64_t count) {
+  uint32_t c[4] = {0u, gray, kStreamBatch << 16, step};
+  philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  return (uint32_t)(((uint64_t)c[0] * (uint64_t)count) >> 32);
+}
+
 hipError_t launch_gather_batch(const float* records, int64_t count, int n, uint64_t seed, uint32_t step,
                                uint32_t ray_base, float* o, float* d, float* vd, float* radius, float* near,
-                               float* far, float* lm, float* pix, int* idx_out, float* lm_sum, hipStream_t st) {
+                               float* far, float* lm, float* pix, int* idx_out, float* lm_sum, hipStream_t st,
+                               int staged) {
   if (n <= 0) return hipSuccess;
   if (count <= 0 || count > 0xFFFFFFFFll) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_gather_batch, dim3((4 * n + 255) / 256), dim3(256), 0, st,
                      reinterpret_cast<const float4*>(records), count, n, seed, step, ray_base, o, d, vd, radius,
-                     near, far, lm, pix, idx_out);
+                     near, far, lm, pix, idx_out, staged);
   if (lm_sum) hipLaunchKernelGGL(k_sum, dim3(1), dim3(1024), 0, st, lm, n, lm_sum);
   return hipGetLastError();
 }

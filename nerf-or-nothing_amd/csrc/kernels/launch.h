@@ -125,7 +125,10 @@ hipError_t launch_wgrad_reduce(const WgOut* outs, int nouts, int max_elems, cons
 // ---- dataset.hip: device-resident record set -> SoA batch gather (+ optional loss-mult sum) ----
 hipError_t launch_gather_batch(const float* records, int64_t count, int n, uint64_t seed, uint32_t step,
                                uint32_t ray_base, float* o, float* d, float* vd, float* radius, float* near,
-                               float* far, float* lm, float* pix, int* idx_out, float* lm_sum, hipStream_t st);
+                               float* far, float* lm, float* pix, int* idx_out, float* lm_sum, hipStream_t st,
+                               int staged = 0);
+// the record index the gather draws for global ray `gray` (host copy of dataset.hip batch_record)
+uint32_t batch_record_host(uint64_t seed, uint32_t step, uint32_t gray, int64_t count);
 
 // ---- raygen.hip: poses (V x [R row-major | t]) (+ images [V][H][W][3]) -> 64-byte records ----
 hipError_t launch_generate_rays(const float* poses, int V, int w, int h, float focal, float near, float far, int ndc,

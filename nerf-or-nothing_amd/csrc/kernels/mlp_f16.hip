@@ -23,8 +23,14 @@ typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t h32_rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
 }
-#ifndef NOF_DIAG_H32_NTSTORE  // diagnostic: bit 0 = forward, bit 1 = backward side outputs non-temporal
-#define NOF_DIAG_H32_NTSTORE 0
+// Side outputs are whole 1-KB tile halves written once and read once by the next launch: non-temporal
+// (nt) stores.  A/B on one box (round 3, tools/ab_multi.sh, per level): default policy fwd 0.188 / bwd
+// 0.175 / wgrad 0.286 ms; nt forward only 0.161 / 0.149 / 0.291; nt backward only 0.179 / 0.157 / 0.246;
+// both 0.151 / 0.142 / 0.207 ms (step 1.43 -> 1.13 ms): the default policy leaves the 1.2 GB of tiles
+// dirty in L2 / MALL and the write-back competes with the kernels that follow.  Diagnostic override:
+// bit 0 = forward, bit 1 = backward nt.
+#ifndef NOF_DIAG_H32_NTSTORE
+#define NOF_DIAG_H32_NTSTORE 3
 #endif
 constexpr int kFwdAux = (NOF_DIAG_H32_NTSTORE & 1) ? 2 : 0;  // side-output store cache policy
 constexpr int kBwdAux = (NOF_DIAG_H32_NTSTORE & 2) ? 2 : 0;

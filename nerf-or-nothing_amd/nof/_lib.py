@@ -97,6 +97,8 @@ SIGNATURES = {
     "nof_mipnerf_render_device": [P, I32, P, P, P, P, P, I32, I32, C.POINTER(nof_render_out)],
     "nof_image_metrics": [P, P, I32, I32, F, C.POINTER(F), C.POINTER(F), P],
     "nof_dataset_open": [C.c_char_p, I32, C.POINTER(P)],
+    "nof_dataset_open_streaming": [C.c_char_p, I32, C.c_int64, C.POINTER(P)],
+    "nof_dataset_is_streaming": [P, C.POINTER(I32)],
     "nof_dataset_from_host": [P, C.c_int64, I32, C.POINTER(P)],
     "nof_dataset_count": [P, C.POINTER(C.c_int64)],
     "nof_dataset_next": [P, I32, U64, U32, U32, P, C.POINTER(nof_batch), C.POINTER(F)],

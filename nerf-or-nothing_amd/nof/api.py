@@ -405,9 +405,12 @@ class RayDataset:
     FIELDS = {"o": ("origins", 3), "d": ("directions", 3), "viewdir": ("viewdirs", 3), "radius": ("radii", 1),
               "near": ("nears", 1), "far": ("fars", 1), "lossmult": ("loss_mults", 1), "pix": ("pixels", 3)}
 
-    def __init__(self, path=None, records=None, device: int = 0, generate: dict | None = None):
-        """path: record file; records: host [N, 16] array; generate: dict(poses [V, 12], width, height,
-        focal, near, far, ndc=False, images=device tensor [V, H, W, 3] or None) -> rays made on the GPU."""
+    def __init__(self, path=None, records=None, device: int = 0, generate: dict | None = None,
+                 max_resident: int | None = None):
+        """path: record file (max_resident: HBM-resident iff at most that many records, else streamed
+        from the file per batch); records: host [N, 16] array; generate: dict(poses [V, 12], width,
+        height, focal, near, far, ndc=False, images=device tensor [V, H, W, 3] or None) -> rays made on
+        the GPU."""
         h = C.c_void_p()
         if generate is not None:
             g = dict(generate)
@@ -416,6 +419,8 @@ class RayDataset:
             call("nof_dataset_generate", poses.ctypes.data, poses.shape[0], int(g["width"]), int(g["height"]),
                  float(g["focal"]), float(g["near"]), float(g["far"]), int(bool(g.get("ndc", False))),
                  _ptr(img) if img is not None else None, device, C.byref(h))
+        elif path is not None and max_resident is not None:
+            call("nof_dataset_open_streaming", str(path).encode(), device, int(max_resident), C.byref(h))
         elif path is not None:
             call("nof_dataset_open", str(path).encode(), device, C.byref(h))
         else:
@@ -427,6 +432,12 @@ class RayDataset:
         n = C.c_int64()
         call("nof_dataset_count", self._h, C.byref(n))
         return n.value
+
+    @property
+    def streaming(self) -> bool:
+        s = C.c_int32()
+        call("nof_dataset_is_streaming", self._h, C.byref(s))
+        return bool(s.value)
 
     def next(self, n: int, seed: int, step: int, ray_base: int = 0, stream=None, with_sum: bool = True):
         """Device SoA batch {key: (ptr, shape)} (+ 'record_index') and the loss-mult sum (or None)."""

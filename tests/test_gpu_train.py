@@ -78,6 +78,41 @@ def test_dataset_file_equals_host(gpu, tmp_path):
         nof.RayDataset(tmp_path / "bad.bin")
 
 
+def test_streaming_dataset_equals_resident(gpu, tmp_path):
+    """Record files larger than HBM (BinDataset.cs:27-52 reads each batch from the file): a file of
+    5 x the residency cap is streamed — batch records read from the file into pinned memory, copied,
+    unpacked by the same gather, the next step prefetched on a host thread — and every batch is
+    bit-identical to the HBM-resident dataset's: consecutive steps (prefetch hits), a jump, a shard
+    change, a larger n (buffers regrown), on the caller's stream and on another one."""
+    import torch
+    import nof
+
+    cap = 1000
+    rec = _records(5 * cap + 17, 8)
+    path = tmp_path / "big.bin"
+    rec.tofile(path)
+    res, st = nof.RayDataset(path), nof.RayDataset(path, max_resident=cap)
+    assert not res.streaming and st.streaming and len(st) == len(rec)
+    assert not nof.RayDataset(path, max_resident=len(rec)).streaming
+    side = torch.cuda.Stream()
+    seed = 0xABCDEF12345
+    reqs = [(512, 0, 0), (512, 1, 0), (512, 2, 0), (512, 9, 0), (512, 10, 512), (900, 11, 0), (900, 12, 0), (64, 3, 7)]
+    for i, (n, step, base) in enumerate(reqs):
+        s = side.cuda_stream if i % 3 == 2 else None
+        ba, ma = res.next(n, seed, step, base, stream=s)
+        torch.cuda.synchronize()
+        fa = {k: v.copy() for k, v in _fetch(ba, n).items()}
+        bb, mb = st.next(n, seed, step, base, stream=s)
+        torch.cuda.synchronize()
+        fb = _fetch(bb, n)
+        for k in fa:
+            assert np.array_equal(fa[k], fb[k]), (i, k)
+        assert ma == mb
+        assert np.array_equal(fb["record_index"], _expected_index(seed, step, np.arange(base, base + n), len(rec)))
+    st.close()
+    res.close()
+
+
 @pytest.mark.parametrize("precision", [0, 1, 2, 3, 4])
 def test_checkpoint_resume_bit_exact(gpu, tmp_path, precision):
     import torch

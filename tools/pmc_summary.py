@@ -1,4 +1,4 @@
-"""Summarise a tools/profile_r02.sh (or profile.sh) run into profiles/<tag>_*.json/csv (committed
+"""Summarise a tools/profile_r02.sh (or ab_write.sh) run into profiles/<tag>_*.json/csv (committed
 evidence) and the lookups bench.py reads (profiles/pmc_traffic.json, profiles/pmc_mfma.json).
 
 traffic per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 B  — FETCH_SIZE (KB) reads half of a wide

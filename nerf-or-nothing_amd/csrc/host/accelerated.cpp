@@ -145,11 +145,11 @@ AcceleratedMLP::AcceleratedMLP(int deg_point, int deg_view, const nof_config& cf
   } else if (precision_ == NOF_PRECISION_F16) {  // fp16 k-step fragment streams + the fp32 tails (mlp_h32.h)
     wimg_f_.alloc(nof::kFwdH32Floats + nof::kFwdTail);
     wimg_b_.alloc(nof::kBwdH32Floats + nof::kBwdTail);
-    amax_.alloc(1);
+    amax_.alloc(cfg.num_levels);
   } else if (f16_pieces()) {  // f16 (hi, lo) slices + the fp32 tails
     wimg_f_.alloc(nof::fwd_image_split_floats<2>() + nof::kFwdTail);
     wimg_b_.alloc(nof::bwd_image_split_floats<2>() + nof::kBwdTail);
-    amax_.alloc(1);
+    amax_.alloc(cfg.num_levels);
   } else {
     wimg_f_.alloc(nof::kFwdImageFloats);
     wimg_b_.alloc(nof::kBwdImageFloats);
@@ -167,12 +167,11 @@ AcceleratedMLP::AcceleratedMLP(int deg_point, int deg_view, const nof_config& cf
     L.zhead.alloc((size_t)L.cap * 4);
     L.sigma.alloc(L.cap);
     L.rgb.alloc((size_t)L.cap * 3);
+    L.delta.alloc(8 * nb * 256 * kBlk);
+    L.delta9x.alloc(nb * nof::kD9F * kBlk);
+    NOF_HIP(hipMemset(L.delta9x.p, 0, L.delta9x.n * sizeof(float)));  // rows 132..159 stay zero
     max_M_ = std::max(max_M_, L.cap);
   }
-  const size_t nbm = (size_t)max_M_ / kBlk;
-  delta_.alloc(8 * nbm * 256 * kBlk);
-  delta9x_.alloc(nbm * nof::kD9F * kBlk);
-  NOF_HIP(hipMemset(delta9x_.p, 0, delta9x_.n * sizeof(float)));  // rows 132..159 stay zero
   numeric_.alloc(2);
   NOF_HIP(hipMemset(numeric_.p, 0, 2 * sizeof(uint32_t)));
   slab_cap_ = (size_t)(num_cu_ + 64) * 65536;
@@ -250,7 +249,7 @@ nof_mlp_debug AcceleratedMLP::debug_view(int level) const {
   nof_mlp_debug d;
   d.M = L.M;
   d.act_in = L.act_in.p; d.act_h = L.act_h.p; d.act_h9 = L.act_h9.p; d.masks = L.masks.p; d.zhead = L.zhead.p;
-  d.delta = delta_.p; d.delta9x = delta9x_.p;
+  d.delta = L.delta.p; d.delta9x = L.delta9x.p;
   return d;
 }
 
@@ -277,26 +276,20 @@ int AcceleratedMLP::bucket_spans(int b, int64_t* off, int64_t* cnt) const {
   return grad_bucket_spans(s.data(), kLayers, b, off, cnt);
 }
 
-AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M, int bucket) {
-  Level& L = lv_[level];
-  auto it = L.sched.find({M, bucket});
-  if (it != L.sched.end()) return it->second;
-  const int nblk = M / kBlk;
-  const size_t ls = (size_t)nblk * 256 * kBlk;
+AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int lv0, int lv1, int bucket) {
+  NOF_REQUIRE(lv0 >= 0 && lv0 < lv1 && lv1 <= (int)lv_.size(), "bad level range");
+  std::vector<int64_t> key{lv0, lv1, bucket};
+  for (int l = lv0; l < lv1; ++l) key.push_back(lv_[l].M);
+  auto it = sched_.find(key);
+  if (it != sched_.end()) return it->second;
+  const int nlev = lv1 - lv0;
   std::vector<nof::WgProblem> P;
   std::vector<int> pbucket;  // bucket of each problem's outputs: layers 5..10 -> 0, 0..4 -> 1
-  auto prob = [&](int layer, const float* A, int FA, int a0, int ntr, const float* B, int FB, int b0, int ntc) {
-    nof::WgProblem p{};
-    p.A = A; p.FA = FA; p.a_row0 = a0; p.ntr = ntr; p.B = B; p.FB = FB; p.b_col0 = b0; p.ntc = ntc; p.shape = 0;
-    p.ntc1 = ntc;
-    P.push_back(p);
-    pbucket.push_back(layer >= 5 ? 0 : 1);
-    return (int)P.size() - 1;
-  };
+  std::vector<int> pnblk;    // k-blocks of each problem (its level's M / 32)
   struct OutSpec { int prob, row_off, nrows, col_off, ncols; float* dst; int ld, dst_col; float* bias; };
   std::vector<OutSpec> os;
   float* G = grads_.p;
-  // operand blocks hold fp16 in the f16x2 mode (mlp_common.h ActOut): element offsets in halves there
+  // operand blocks hold fp16 in the f16 modes (mlp_common.h ActOut): element offsets in halves there
   const bool half = f16_blocks();
   auto at = [&](float* base, size_t off) -> const float* {
     return half ? reinterpret_cast<const float*>(reinterpret_cast<const uint16_t*>(base) + off) : base + off;
@@ -306,49 +299,87 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M, int bucket)
   // F16 (k_wgrad_s): the problems that share an A operand are one problem with more output columns —
   // delta_4 x [h3 | IPE] and delta_9x x [h7 | view PE | h9] — so each delta block is read once
   const bool merge = precision_ == NOF_PRECISION_F16;
-  auto extra_b = [&](int p, const float* B, int FB, int b0, int ntc) {
-    nof::WgProblem& q = P[p];
-    if (q.ntc2 == 0) { q.B2 = B; q.FB2 = FB; q.b2_col0 = b0; q.ntc2 = ntc; }
-    else { q.B3 = B; q.FB3 = FB; q.b3_col0 = b0; q.ntc3 = ntc; }
-    q.ntc += ntc;
-  };
-  int p;
-  p = prob(0, delta_.p, 256, 0, 8, L.act_in.p, nof::kInF, 0, 3);
-  os.push_back({p, 0, 256, 0, 96, Wg(0), 96, 0, Bg(0)});
-  for (int l = 1; l < 8; ++l) {
-    p = prob(l, at(delta_.p, l * ls), 256, 0, 8, at(L.act_h.p, (l - 1) * ls), 256, 0, 8);
-    os.push_back({p, 0, 256, 0, 256, Wg(l), in_[l], 0, Bg(l)});
-    if (l == 4 && merge) {
-      extra_b(p, L.act_in.p, nof::kInF, 0, 3);
-      os.push_back({p, 0, 256, 256, 96, Wg(4), in_[4], 256, nullptr});
-    } else if (l == 4) {
-      p = prob(4, at(delta_.p, l * ls), 256, 0, 8, L.act_in.p, nof::kInF, 0, 3);
-      os.push_back({p, 0, 256, 0, 96, Wg(4), in_[4], 256, nullptr});
+  // The per-level problem list is the same for every level; problem q of level lev goes to index
+  // q nlev + (lev - lv0), so a problem's items over all levels are contiguous (level order) and one
+  // output spec (WgOut) reduces them all.
+  for (int lev = lv0; lev < lv1; ++lev) {
+    Level& L = lv_[lev];
+    const int nblk = L.M / kBlk;
+    const size_t ls = (size_t)nblk * 256 * kBlk;
+    std::vector<nof::WgProblem> Pl;
+    std::vector<int> bl;
+    std::vector<OutSpec> ol;
+    auto prob = [&](int layer, const float* A, int FA, int a0, int ntr, const float* B, int FB, int b0, int ntc) {
+      nof::WgProblem q{};
+      q.A = A; q.FA = FA; q.a_row0 = a0; q.ntr = ntr; q.B = B; q.FB = FB; q.b_col0 = b0; q.ntc = ntc; q.shape = 0;
+      q.ntc1 = ntc;
+      q.level = lev;
+      Pl.push_back(q);
+      bl.push_back(layer >= 5 ? 0 : 1);
+      return (int)Pl.size() - 1;
+    };
+    auto extra_b = [&](int p, const float* B, int FB, int b0, int ntc) {
+      nof::WgProblem& q = Pl[p];
+      if (q.ntc2 == 0) { q.B2 = B; q.FB2 = FB; q.b2_col0 = b0; q.ntc2 = ntc; }
+      else { q.B3 = B; q.FB3 = FB; q.b3_col0 = b0; q.ntc3 = ntc; }
+      q.ntc += ntc;
+    };
+    float* dl = L.delta.p;
+    float* d9 = L.delta9x.p;
+    int p;
+    p = prob(0, dl, 256, 0, 8, L.act_in.p, nof::kInF, 0, 3);
+    ol.push_back({p, 0, 256, 0, 96, Wg(0), 96, 0, Bg(0)});
+    for (int l = 1; l < 8; ++l) {
+      p = prob(l, at(dl, l * ls), 256, 0, 8, at(L.act_h.p, (l - 1) * ls), 256, 0, 8);
+      ol.push_back({p, 0, 256, 0, 256, Wg(l), in_[l], 0, Bg(l)});
+      if (l == 4 && merge) {
+        extra_b(p, L.act_in.p, nof::kInF, 0, 3);
+        ol.push_back({p, 0, 256, 256, 96, Wg(4), in_[4], 256, nullptr});
+      } else if (l == 4) {
+        p = prob(4, at(dl, l * ls), 256, 0, 8, L.act_in.p, nof::kInF, 0, 3);
+        ol.push_back({p, 0, 256, 0, 96, Wg(4), in_[4], 256, nullptr});
+      }
     }
-  }
-  p = prob(9, delta9x_.p, nof::kD9F, 0, 5, at(L.act_h.p, 7 * ls), 256, 0, 8);
-  os.push_back({p, 0, 128, 0, 256, Wg(9), in_[9], 0, Bg(9)});
-  os.push_back({p, 128, 1, 0, 256, Wg(8), in_[8], 0, Bg(8)});
-  if (merge) {  // columns 256..287: the view PE tile, 288..415: h9
-    extra_b(p, L.act_in.p, nof::kInF, 96, 1);
-    extra_b(p, L.act_h9.p, 128, 0, 4);
-    os.push_back({p, 0, 128, 256, 27, Wg(9), in_[9], 256, nullptr});
-    os.push_back({p, 129, 3, 288, 128, Wg(10), in_[10], 0, Bg(10)});
-  } else {
-    p = prob(9, delta9x_.p, nof::kD9F, 0, 4, L.act_in.p, nof::kInF, 96, 1);
-    os.push_back({p, 0, 128, 0, 27, Wg(9), in_[9], 256, nullptr});
-    p = prob(10, delta9x_.p, nof::kD9F, 128, 1, L.act_h9.p, 128, 0, 4);
-    os.push_back({p, 1, 3, 0, 128, Wg(10), in_[10], 0, Bg(10)});
+    p = prob(9, d9, nof::kD9F, 0, 5, at(L.act_h.p, 7 * ls), 256, 0, 8);
+    ol.push_back({p, 0, 128, 0, 256, Wg(9), in_[9], 0, Bg(9)});
+    ol.push_back({p, 128, 1, 0, 256, Wg(8), in_[8], 0, Bg(8)});
+    if (merge) {  // columns 256..287: the view PE tile, 288..415: h9
+      extra_b(p, L.act_in.p, nof::kInF, 96, 1);
+      extra_b(p, L.act_h9.p, 128, 0, 4);
+      ol.push_back({p, 0, 128, 256, 27, Wg(9), in_[9], 256, nullptr});
+      ol.push_back({p, 129, 3, 288, 128, Wg(10), in_[10], 0, Bg(10)});
+    } else {
+      p = prob(9, d9, nof::kD9F, 0, 4, L.act_in.p, nof::kInF, 96, 1);
+      ol.push_back({p, 0, 128, 0, 27, Wg(9), in_[9], 256, nullptr});
+      p = prob(10, d9, nof::kD9F, 128, 1, L.act_h9.p, 128, 0, 4);
+      ol.push_back({p, 1, 3, 0, 128, Wg(10), in_[10], 0, Bg(10)});
+    }
+    const int nq = (int)Pl.size();
+    if (lev == lv0) {
+      P.resize((size_t)nq * nlev);
+      pbucket.resize(P.size());
+      pnblk.resize(P.size());
+      for (OutSpec o : ol) { o.prob *= nlev; os.push_back(o); }
+    }
+    NOF_REQUIRE(nq * nlev == (int)P.size(), "levels with different problem lists");
+    for (int q = 0; q < nq; ++q) {
+      const int i = q * nlev + (lev - lv0);
+      P[i] = Pl[q];
+      pbucket[i] = bl[q];
+      pnblk[i] = nblk;
+    }
   }
   if (bucket >= 0) {  // keep only this bucket's problems (and their outputs), renumbered
     std::vector<int> remap(P.size(), -1);
     std::vector<nof::WgProblem> Pb;
+    std::vector<int> nb;
     for (size_t i = 0; i < P.size(); ++i)
-      if (pbucket[i] == bucket) { remap[i] = (int)Pb.size(); Pb.push_back(P[i]); }
+      if (pbucket[i] == bucket) { remap[i] = (int)Pb.size(); Pb.push_back(P[i]); nb.push_back(pnblk[i]); }
     std::vector<OutSpec> ob;
-    for (OutSpec s : os)
-      if (remap[s.prob] >= 0) { s.prob = remap[s.prob]; ob.push_back(s); }
+    for (OutSpec o : os)
+      if (remap[o.prob] >= 0) { o.prob = remap[o.prob]; ob.push_back(o); }
     P.swap(Pb);
+    pnblk.swap(nb);
     os.swap(ob);
   }
 
@@ -382,36 +413,39 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M, int bucket)
   // marks w * total / G and (w + 1) * total / G, each rounded to the nearest block: no workgroup is
   // off by more than one block and no rounding accumulates onto the last one (the greedy fill this
   // replaces closed every workgroup short and left the sum of the shortfalls to the last: measured
-  // workgroup ends 229-324 us for a 253-us mean).
-  std::vector<int64_t> cum(P.size() + 1, 0);
-  for (size_t i = 0; i < P.size(); ++i) cum[i + 1] = cum[i] + cost[i] * nblk;
+  // workgroup ends 229-324 us for a 253-us mean).  Problems may differ in k-blocks (levels of
+  // different sample counts): a cut is a (problem, block) pair.
+  const int np = (int)P.size();
+  std::vector<int64_t> cum(np + 1, 0);
+  for (int i = 0; i < np; ++i) cum[i + 1] = cum[i] + cost[i] * pnblk[i];
   const int64_t total = cum.back();
   const int G_wg = num_cu_;
-  auto mark = [&](int w) {  // global block index of the cut before workgroup w
-    if (w >= G_wg) return (int64_t)P.size() * nblk;
+  auto mark = [&](int w) -> std::pair<int, int> {  // the cut before workgroup w
+    if (w >= G_wg) return {np, 0};
     const double x = (double)total * w / G_wg;
-    size_t pi = 0;
-    while (pi + 1 < P.size() && (double)cum[pi + 1] <= x) ++pi;
-    const int64_t kb = std::min<int64_t>(nblk, std::llround((x - (double)cum[pi]) / (double)cost[pi]));
-    return (int64_t)pi * nblk + kb;
+    int pi = 0;
+    while (pi + 1 < np && (double)cum[pi + 1] <= x) ++pi;
+    const int kb = (int)std::min<int64_t>(pnblk[pi], std::llround((x - (double)cum[pi]) / (double)cost[pi]));
+    return kb >= pnblk[pi] ? std::make_pair(pi + 1, 0) : std::make_pair(pi, kb);
   };
   std::vector<nof::WgItem> items;
   std::vector<int> item_wg;
-  std::vector<int> first_item(P.size(), -1), nitems(P.size(), 0);
+  std::vector<int> first_item(np, -1), nitems(np, 0);
   for (int w = 0; w < G_wg; ++w) {
-    int64_t g0 = mark(w);
-    const int64_t g1 = std::max(g0, mark(w + 1));
-    while (g0 < g1) {  // split the workgroup's range at problem boundaries
-      const int pi = (int)(g0 / nblk);
-      const int kb0 = (int)(g0 - (int64_t)pi * nblk);
-      const int kb1 = (int)std::min<int64_t>(nblk, g1 - (int64_t)pi * nblk);
-      nof::WgItem itm;
-      itm.prob = pi; itm.kb0 = kb0; itm.kb1 = kb1; itm.slab = (int)items.size();
-      if (first_item[pi] < 0) first_item[pi] = (int)items.size();
-      nitems[pi]++;
-      items.push_back(itm);
-      item_wg.push_back(w);
-      g0 = (int64_t)pi * nblk + kb1;
+    std::pair<int, int> a = mark(w);
+    const std::pair<int, int> b = std::max(a, mark(w + 1));
+    while (a < b) {  // split the workgroup's range at problem boundaries
+      const int pi = a.first;
+      const int kb1 = b.first == pi ? b.second : pnblk[pi];
+      if (kb1 > a.second) {
+        nof::WgItem itm;
+        itm.prob = pi; itm.kb0 = a.second; itm.kb1 = kb1; itm.slab = (int)items.size();
+        if (first_item[pi] < 0) first_item[pi] = (int)items.size();
+        nitems[pi]++;
+        items.push_back(itm);
+        item_wg.push_back(w);
+      }
+      a = kb1 >= pnblk[pi] ? std::make_pair(pi + 1, 0) : std::make_pair(pi, kb1);
     }
   }
   const int nwg = std::min(G_wg, item_wg.empty() ? 0 : item_wg.back() + 1);
@@ -434,13 +468,18 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int level, int M, int bucket)
   int max_elems = 0;
   for (const OutSpec& s : os) {
     nof::WgOut o;
-    o.item0 = first_item[s.prob]; o.nitems = nitems[s.prob];
+    o.item0 = first_item[s.prob];
+    o.nitems = 0;  // the problem's items at every level: problems s.prob .. s.prob + nlev - 1, contiguous
+    for (int l = 0; l < nlev; ++l) {
+      NOF_REQUIRE(first_item[s.prob + l] == o.item0 + o.nitems, "a problem's items are not contiguous");
+      o.nitems += nitems[s.prob + l];
+    }
     o.row_off = s.row_off; o.nrows = s.nrows; o.col_off = s.col_off; o.ncols = s.ncols;
     o.dst = s.dst; o.ld = s.ld; o.dst_col = s.dst_col; o.bias_dst = s.bias; o.prob = s.prob;
     outs.push_back(o);
-    max_elems = std::max(max_elems, s.nrows * s.ncols);
+    max_elems = std::max(max_elems, nof::wgrad_reduce_threads(s.nrows, s.ncols, s.col_off));
   }
-  Schedule& sc = L.sched[{M, bucket}];
+  Schedule& sc = sched_[key];
   sc.probs.alloc(P.size());
   sc.items.alloc(items.size());
   sc.item_ptr.alloc(item_ptr.size());
@@ -473,6 +512,42 @@ void AcceleratedMLP::run_wgrad(Schedule& sc, int accumulate) {
   te(kTWgradReduce);
 }
 
+void AcceleratedMLP::run_backward(int level, const float* color_grad, const float* density_grad) {
+  Level& L = lv_[level];
+  nof::BwdArgs b{};
+  b.M = L.M;
+  b.split = precision_;
+  if (f16_pieces()) {  // the level's power-of-two delta scale
+    NOF_HIP(nof::launch_delta_amax(density_grad, color_grad, L.M, amax_.p + level, st_, numeric_.p));
+    b.amax = amax_.p + level;
+  }
+  b.dsigma = density_grad; b.drgb = color_grad; b.zhead = L.zhead.p;
+  b.masks = L.masks.p;
+  b.wimg_b = wimg_b_.p;
+  b.delta = L.delta.p; b.delta9x = L.delta9x.p;
+  tb(kTMlpBwd);
+  NOF_HIP(nof::launch_mlp_bwd(b, st_));
+  te(kTMlpBwd);
+}
+
+// the weight gradients of levels [lv0, lv1) (their dX chains done): one scheduled launch + reduce, or
+// with the bucket hook kBuckets of them in reverse layer order, the hook fired after each
+float* const* AcceleratedMLP::wgrad_levels(int lv0, int lv1, int accumulate, bool buckets) {
+  if (!buckets) {
+    run_wgrad(schedule(lv0, lv1), accumulate);
+  } else {
+    // reverse layer order: the hook's all-reduce of layers 5..10 overlaps the layer-0..4 launch
+    for (int bk = 0; bk < kBuckets; ++bk) {
+      run_wgrad(schedule(lv0, lv1, bk), accumulate);
+      int64_t off[2], cnt[2];
+      const int ns = bucket_spans(bk, off, cnt);
+      TraceRange hr("nof:gradient_bucket_hook");
+      hook_(hook_user_, bk, ns, off, cnt);
+    }
+  }
+  return grad_views_.data();
+}
+
 float* const* AcceleratedMLP::get_gradient(const float* color_grad, const float* density_grad, int level,
                                            uint32_t flags) {
   NOF_REQUIRE(level >= 0 && level < (int)lv_.size(), "level out of range");
@@ -483,38 +558,28 @@ float* const* AcceleratedMLP::get_gradient(const float* color_grad, const float*
   const bool buckets = (flags & NOF_GRAD_PUBLISH) && hook_;
   // build every schedule this call needs before the first launch (a schedule may grow the slabs,
   // which synchronises the stream)
-  Schedule* whole = buckets ? nullptr : &schedule(level, L.M);
-  Schedule* part[kBuckets] = {};
-  if (buckets)
-    for (int b = 0; b < kBuckets; ++b) part[b] = &schedule(level, L.M, b);
-  nof::BwdArgs b{};
-  b.M = L.M;
-  b.split = precision_;
-  if (f16_pieces()) {
-    NOF_HIP(nof::launch_delta_amax(density_grad, color_grad, L.M, amax_.p, st_, numeric_.p));
-    b.amax = amax_.p;
+  if (!buckets) (void)schedule(level, level + 1);
+  else
+    for (int b = 0; b < kBuckets; ++b) (void)schedule(level, level + 1, b);
+  run_backward(level, color_grad, density_grad);
+  return wgrad_levels(level, level + 1, (level > 0 || (flags & NOF_GRAD_ACCUMULATE)) ? 1 : 0, buckets);
+}
+
+float* const* AcceleratedMLP::get_gradient_levels(const float* const* color_grads, const float* const* density_grads,
+                                                  uint32_t flags) {
+  const int nl = (int)lv_.size();
+  NOF_REQUIRE(color_grads && density_grads, "null output gradients");
+  for (int l = 0; l < nl; ++l) {
+    NOF_REQUIRE(lv_[l].M > 0, "get_gradient before get_output for a level");
+    NOF_REQUIRE(color_grads[l] && density_grads[l], "null output gradients");
   }
-  b.dsigma = density_grad; b.drgb = color_grad; b.zhead = L.zhead.p;
-  b.masks = L.masks.p;
-  b.wimg_b = wimg_b_.p;
-  b.delta = delta_.p; b.delta9x = delta9x_.p;
-  tb(kTMlpBwd);
-  NOF_HIP(nof::launch_mlp_bwd(b, st_));
-  te(kTMlpBwd);
-  const int accumulate = (level > 0 || (flags & NOF_GRAD_ACCUMULATE)) ? 1 : 0;
-  if (!buckets) {
-    run_wgrad(*whole, accumulate);
-  } else {
-    // reverse layer order: the hook's all-reduce of layers 5..10 overlaps the layer-0..4 launch
-    for (int bk = 0; bk < kBuckets; ++bk) {
-      run_wgrad(*part[bk], accumulate);
-      int64_t off[2], cnt[2];
-      const int ns = bucket_spans(bk, off, cnt);
-      TraceRange hr("nof:gradient_bucket_hook");
-      hook_(hook_user_, bk, ns, off, cnt);
-    }
-  }
-  return grad_views_.data();
+  NOF_REQUIRE((flags & ~(uint32_t)(NOF_GRAD_ACCUMULATE | NOF_GRAD_PUBLISH)) == 0, "unknown gradient flags");
+  const bool buckets = (flags & NOF_GRAD_PUBLISH) && hook_;
+  if (!buckets) (void)schedule(0, nl);
+  else
+    for (int b = 0; b < kBuckets; ++b) (void)schedule(0, nl, b);
+  for (int l = 0; l < nl; ++l) run_backward(l, color_grads[l], density_grads[l]);
+  return wgrad_levels(0, nl, (flags & NOF_GRAD_ACCUMULATE) ? 1 : 0, buckets);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -579,8 +644,7 @@ float* const* AcceleratedMipNeRF::run(int n, const float* o, const float* d, con
                                       nof_output_grad_fn cb, void* user, uint32_t flags) {
   static const char* const kFwd[] = {"nof:level0_forward", "nof:level1_forward", "nof:level2_forward",
                                      "nof:level3_forward"};
-  static const char* const kBwd[] = {"nof:level0_backward", "nof:level1_backward", "nof:level2_backward",
-                                     "nof:level3_backward"};
+  static const char* const kBwd[] = {"nof:backward"};
   const int L = cfg_.num_levels;
   TraceRange step_range("nof:get_gradient");
   mlp->pack_weights();
@@ -617,11 +681,14 @@ float* const* AcceleratedMipNeRF::run(int n, const float* o, const float* d, con
                                    st_));
     timer.end(kTRenderBwd);
   }
+  // MNcpp:135-142 (level 0 overwrites unless accumulating, later levels add): every level's dX chain,
+  // then one weight-gradient launch over both levels' operands
   float* const* grads = nullptr;
-  for (int lv = 0; lv < L; ++lv) {  // MNcpp:135-142; level 0 overwrites unless accumulating
-    const uint32_t f = (lv == 0 ? (flags & NOF_GRAD_ACCUMULATE) : 0u) | (lv == L - 1 ? (flags & NOF_GRAD_PUBLISH) : 0u);
-    TraceRange lr(kBwd[lv & 3]);
-    grads = mlp->get_gradient(drgb_[lv].p, dsig_[lv].p, lv, f);
+  {
+    TraceRange lr(kBwd[0]);
+    std::vector<const float*> cg(L), dg(L);
+    for (int lv = 0; lv < L; ++lv) { cg[lv] = drgb_[lv].p; dg[lv] = dsig_[lv].p; }
+    grads = mlp->get_gradient_levels(cg.data(), dg.data(), flags);
   }
   last_n_ = n;
   last_fused_ = cb == nullptr;

@@ -111,6 +111,11 @@ class AcceleratedMLP {
   // call that completes the step's gradient: with a bucket hook set, its weight gradients run as
   // kBuckets launches in reverse layer order and the hook fires after each one is enqueued.
   float* const* get_gradient(const float* color_grad, const float* density_grad, int level, uint32_t flags = 0);
+  // Every level's gradient in one call (the fused training step): each level's dX chain into its own
+  // delta blocks, then ONE weight-gradient launch and ONE ordered reduce over all levels' operands
+  // (level 0's sums first, then level 1's: the arithmetic of the per-level calls).  Same flags.
+  float* const* get_gradient_levels(const float* const* color_grads, const float* const* density_grads,
+                                    uint32_t flags);
   static constexpr int kBuckets = 2;
   void set_bucket_hook(nof_grad_bucket_fn fn, void* user) { hook_ = fn; hook_user_ = user; }
   bool has_bucket_hook() const { return hook_ != nullptr; }
@@ -148,14 +153,17 @@ class AcceleratedMLP {
   struct Level {
     int cap = 0, M = 0, n = 0, S = 0;
     DevBuf<float> act_in, act_h, act_h9, zhead, sigma, rgb;
+    DevBuf<float> delta, delta9x;  // the level's dX-chain outputs (the weight gradients' A operands)
     DevBuf<uint32_t> masks;
-    std::map<std::pair<int, int>, Schedule> sched;  // by (M, bucket)
   };
   void run_forward(int level, const nof::FwdArgs& a);
-  // weight-gradient schedule of `level` at M samples: bucket -1 = every problem, b >= 0 = the
-  // problems whose outputs belong to bucket b (see bucket_spans)
-  Schedule& schedule(int level, int M, int bucket = -1);
+  void run_backward(int level, const float* color_grad, const float* density_grad);
+  // weight-gradient schedule of levels [lv0, lv1) at their current sample counts: bucket -1 = every
+  // problem, b >= 0 = the problems whose outputs belong to bucket b (see bucket_spans)
+  Schedule& schedule(int lv0, int lv1, int bucket = -1);
+  std::map<std::vector<int64_t>, Schedule> sched_;  // by (lv0, lv1, bucket, M of each level)
   void run_wgrad(Schedule& sc, int accumulate);
+  float* const* wgrad_levels(int lv0, int lv1, int accumulate, bool buckets);
   nof_grad_bucket_fn hook_ = nullptr;
   void* hook_user_ = nullptr;
   void tb(int id) { if (timer) timer->begin(id); }
@@ -178,8 +186,8 @@ class AcceleratedMLP {
   std::vector<float*> param_views_, grad_views_;
   std::vector<Level> lv_;
   int max_M_ = 0;
-  DevBuf<float> delta_, delta9x_, slabs_, bias_slabs_;
-  DevBuf<uint32_t> amax_;  // f16x2: bits of max |dsigma|, |drgb| of the level in flight (delta scale)
+  DevBuf<float> slabs_, bias_slabs_;
+  DevBuf<uint32_t> amax_;  // f16 modes: per level, bits of max |dsigma|, |drgb| (the level's delta scale)
   DevBuf<uint32_t> numeric_;
   size_t slab_cap_ = 0;
 };

@@ -95,8 +95,11 @@ struct WgProblem {
   int ntc1;              // tiles of B (ntc = ntc1 + ntc2 + ntc3)
   const float* B2; int FB2, b2_col0, ntc2;
   const float* B3; int FB3, b3_col0, ntc3;
+  int level;             // the MLP level whose operands these are (the reduce's per-level delta scale)
 };
 struct WgItem { int prob, kb0, kb1; int slab; };  // slab = index into slab_off[]
+// k_wgrad_reduce threads an output needs (max_elems of launch_wgrad_reduce = the max over outputs)
+int wgrad_reduce_threads(int nrows, int ncols, int col_off);
 struct WgOut {
   int item0, nitems;        // contiguous items of the problem
   int row_off, nrows, col_off, ncols;

@@ -982,9 +982,16 @@ hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const in
   return launch_wgrad_split<1>(probs, items, item_ptr, num_wg, slab_off, slabs, bias_slabs, st);
 }
 
-// One thread per 4 consecutive output elements (a float4 of every slab when the output's columns
-// come in fours, 4 scalar elements otherwise), each summed over the problem's item slabs in item order
-// — the same bits as one element per thread, with 4x the bytes per load in flight.
+// Thread t sums 4 consecutive output elements (a float4 of every slab) when the output's columns come
+// in fours, element t otherwise, over the problem's item slabs in item order (the host sizes the grid:
+// wgrad_reduce_threads).  Items are grouped by level (two-level launches): each level's sum is scaled by
+// its delta scale (f16 modes) and added in level order — the arithmetic of one reduce per level.
+__host__ __device__ inline bool reduce_vec(int ncols, int col_off) { return (ncols & 3) == 0 && (col_off & 3) == 0; }
+int wgrad_reduce_threads(int nrows, int ncols, int col_off) {
+  const int ne = nrows * ncols;
+  return std::max(reduce_vec(ncols, col_off) ? (ne + 3) / 4 : ne, nrows);
+}
+
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const WgOut* __restrict__ outs, const WgItem* __restrict__ items,
                                                       const WgProblem* __restrict__ probs,
                                                       const int64_t* __restrict__ slab_off,
@@ -992,49 +999,73 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const WgOut* __restrict__ 
                                                       const float* __restrict__ bias_slabs, int accumulate,
                                                       const uint32_t* __restrict__ amax) {
   const WgOut o = outs[blockIdx.y];
-  const float inv = amax ? delta_scale(amax, true) : 1.0f;  // f16x2 / F16: undo the delta scaling (exact)
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int ld = probs[o.prob].ntc * 32;
   const int ne = o.nrows * o.ncols;
   constexpr int kU = 8;  // item slabs in flight per step
-  if (4 * t < ne) {
-    if ((o.ncols & 3) == 0 && (o.col_off & 3) == 0) {
-      const int rr = (4 * t) / o.ncols, cc = 4 * t - rr * o.ncols;
-      const size_t off = (size_t)(o.row_off + rr) * ld + o.col_off + cc;  // 16-B aligned (ld % 32 == 0)
+  auto level_of = [&](int k) { return probs[items[o.item0 + k].prob].level; };
+  auto inv_of = [&](int lev) { return amax ? delta_scale(amax + lev, true) : 1.0f; };  // exact powers of 2
+  const bool vec = reduce_vec(o.ncols, o.col_off);
+  if (vec ? 4 * t < ne : t < ne) {
+    const int e = vec ? 4 * t : t;
+    const int rr = e / o.ncols, cc = e - rr * o.ncols;
+    const size_t off = (size_t)(o.row_off + rr) * ld + o.col_off + cc;  // 16-B aligned when vec (ld % 32 == 0)
+    float* dst = o.dst + (size_t)rr * o.ld + o.dst_col + cc;
+    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    bool first = true;
+    for (int k = 0; k < o.nitems;) {
+      const int lev = level_of(k);
+      int k1 = k + 1;
+      while (k1 < o.nitems && level_of(k1) == lev) ++k1;
       f32x4 s = {0.0f, 0.0f, 0.0f, 0.0f};
-      int k = 0;
-      for (; k + kU <= o.nitems; k += kU) {
-        f32x4 v[kU];
+      if (vec) {
+        for (; k + kU <= k1; k += kU) {
+          f32x4 v[kU];
 #pragma unroll
-        for (int u = 0; u < kU; ++u)
-          v[u] = *reinterpret_cast<const f32x4*>(slabs + slab_off[items[o.item0 + k + u].slab] + off);
+          for (int u = 0; u < kU; ++u)
+            v[u] = *reinterpret_cast<const f32x4*>(slabs + slab_off[items[o.item0 + k + u].slab] + off);
 #pragma unroll
-        for (int u = 0; u < kU; ++u) s += v[u];
+          for (int u = 0; u < kU; ++u) s += v[u];
+        }
+        for (; k < k1; ++k) s += *reinterpret_cast<const f32x4*>(slabs + slab_off[items[o.item0 + k].slab] + off);
+      } else {
+        for (; k + kU <= k1; k += kU) {
+          float v[kU];
+#pragma unroll
+          for (int u = 0; u < kU; ++u) v[u] = slabs[slab_off[items[o.item0 + k + u].slab] + off];
+#pragma unroll
+          for (int u = 0; u < kU; ++u) s[0] += v[u];
+        }
+        for (; k < k1; ++k) s[0] += slabs[slab_off[items[o.item0 + k].slab] + off];
       }
-      for (; k < o.nitems; ++k) s += *reinterpret_cast<const f32x4*>(slabs + slab_off[items[o.item0 + k].slab] + off);
-      float* dst = o.dst + (size_t)rr * o.ld + o.dst_col + cc;
+      const float inv = inv_of(lev);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float v = s[j] * inv;
-        dst[j] = accumulate ? dst[j] + v : v;
+        acc[j] = first ? (accumulate ? dst[vec ? j : 0] + v : v) : acc[j] + v;
       }
+      first = false;
+    }
+    if (vec) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dst[j] = acc[j];
     } else {
-      for (int e = 4 * t; e < 4 * t + 4 && e < ne; ++e) {
-        const int rr = e / o.ncols, cc = e - rr * o.ncols;
-        const size_t off = (size_t)(o.row_off + rr) * ld + o.col_off + cc;
-        float s = 0.0f;
-        for (int k = 0; k < o.nitems; ++k) s += slabs[slab_off[items[o.item0 + k].slab] + off];
-        float* dst = o.dst + (size_t)rr * o.ld + o.dst_col + cc;
-        s *= inv;
-        *dst = accumulate ? *dst + s : s;
-      }
+      dst[0] = acc[0];
     }
   }
   if (o.bias_dst && t < o.nrows) {
-    float s = 0.0f;
-    for (int k = 0; k < o.nitems; ++k) s += bias_slabs[(size_t)items[o.item0 + k].slab * 256 + o.row_off + t];
-    s *= inv;
-    o.bias_dst[t] = accumulate ? o.bias_dst[t] + s : s;
+    float acc = 0.0f;
+    bool first = true;
+    for (int k = 0; k < o.nitems;) {
+      const int lev = level_of(k);
+      float s = 0.0f;
+      for (; k < o.nitems && level_of(k) == lev; ++k)
+        s += bias_slabs[(size_t)items[o.item0 + k].slab * 256 + o.row_off + t];
+      const float v = s * inv_of(lev);
+      acc = first ? (accumulate ? o.bias_dst[t] + v : v) : acc + v;
+      first = false;
+    }
+    o.bias_dst[t] = acc;
   }
 }
 
@@ -1057,8 +1088,7 @@ hipError_t launch_wgrad_reduce(const WgOut* outs, int nouts, int max_elems, cons
                                const WgProblem* probs, const int64_t* slab_off, const float* slabs,
                                const float* bias_slabs, int accumulate, const uint32_t* amax, hipStream_t st) {
   if (nouts <= 0) return hipSuccess;
-  const int threads = std::max((max_elems + 3) / 4, 256);  // >= nrows (the bias sums)
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3((threads + 255) / 256, nouts), dim3(256), 0, st, outs, items, probs,
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((max_elems + 255) / 256, nouts), dim3(256), 0, st, outs, items, probs,
                      slab_off, slabs, bias_slabs, accumulate, amax);
   return hipGetLastError();
 }

@@ -64,6 +64,7 @@ def test_timer_pool_bounded(gpu):
     for _ in range(steps):
         m.get_gradient_device(n, d["o"], d["d"], d["radius"], d["near"], d["far"], d["lossmult"], d["pix"], float(n))
     t = m.read_timing()
-    assert t["mlp_fwd"][1] == 2 * steps and t["wgrad"][1] == 2 * steps and t["pack"][1] == steps
+    # one weight-gradient launch per step covers both levels
+    assert t["mlp_fwd"][1] == 2 * steps and t["wgrad"][1] == steps and t["pack"][1] == steps
     assert all(ms > 0 for ms, cnt in t.values() if cnt)
     m.close()

@@ -400,9 +400,11 @@ struct BwdEpiH {
   float dzs;
   __device__ __forceinline__ BwdEpiH(const f32x16 (&a)[2], uint32_t (&d)[16][4], uint32_t voff_)
       : acc(a), dst(d), voff(voff_) {}
-  __device__ __forceinline__ void begin(const void* blk_, const uint32_t* mask, const float* w8_, float dzs_) {
+  // mask: the layer's ReLU mask words, loaded one layer ahead by the caller (a load issued here would
+  // be waited for one chunk later together with every store issued before it: vmcnt retires in order)
+  __device__ __forceinline__ void begin(const void* blk_, const uint4& mask, const float* w8_, float dzs_) {
     blk = h32_rsrc(blk_);
-    mk = *reinterpret_cast<const uint4*>(mask);
+    mk = mask;
     w8 = w8_;
     dzs = dzs_;
   }
@@ -498,6 +500,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   f32x16 acc[2];
   const size_t lstride = (size_t)nblk * kBlk * kWidth;
   const _Float16* delta = reinterpret_cast<const _Float16*>(a.delta) + (size_t)m0 * kWidth;
+  auto mask_of = [&](int l) { return *reinterpret_cast<const uint4*>(masks_blk + l * 256); };
   BwdEpiH eX(acc, X, vrow), eY(acc, Y, vrow);
   NoEpiH none;
   auto srcX = [&](int kk, uint32_t (&b)[4]) {
@@ -509,17 +512,20 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
     for (int e = 0; e < 4; ++e) b[e] = Y[kk][e];
   };
   // dh7 = W9[:, :256]^T delta9 + w8 dz_s ; delta7
-  eY.begin(delta + 7 * lstride, masks_blk + 7 * 256, lds + kW8 + 16 * h, dzs);
+  uint4 mk_next = mask_of(6);  // every later layer's mask words are loaded one layer before its begin()
+  eY.begin(delta + 7 * lstride, mask_of(7), lds + kW8 + 16 * h, dzs);
   h32_layer<8, 8, false>(srcX, acc, ring, eY, none, nullptr, tid, lane);
   // dh_{l-1} = W_l[:, :256]^T delta_l ; delta_{l-1}, l = 7..2 in pairs, then l = 1
   for (int it = 0; it < 3; ++it) {
     const int l = kDepth - 1 - 2 * it;
-    eX.begin(delta + (l - 1) * lstride, masks_blk + (l - 1) * 256, nullptr, 0.0f);
+    eX.begin(delta + (l - 1) * lstride, mk_next, nullptr, 0.0f);
+    mk_next = mask_of(l - 2);
     h32_layer<16, 8, false>(srcY, acc, ring, eX, eY, nullptr, tid, lane);
-    eY.begin(delta + (l - 2) * lstride, masks_blk + (l - 2) * 256, nullptr, 0.0f);
+    eY.begin(delta + (l - 2) * lstride, mk_next, nullptr, 0.0f);
+    mk_next = mask_of(l - 3);
     h32_layer<16, 8, false>(srcX, acc, ring, eY, eX, nullptr, tid, lane);
   }
-  eX.begin(delta, masks_blk, nullptr, 0.0f);
+  eX.begin(delta, mk_next, nullptr, 0.0f);
   h32_layer<16, 8, false>(srcY, acc, ring, eX, eY, nullptr, tid, lane);
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk) eX.piece(7, kk, 16);  // delta0's last tile

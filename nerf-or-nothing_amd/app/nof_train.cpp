@@ -3,7 +3,8 @@
 // It is what a C# maintainer's Program.cs becomes over P/Invoke, compiled with a
 // plain C++ compiler against libnof.so:
 //
-//   BinDataset(path)                       -> nof_dataset_open (records resident in HBM)
+//   BinDataset(path)                       -> nof_dataset_open (records resident in HBM; streamed from the
+//                                             file past --max-resident records: nof_dataset_open_streaming)
 //   new AcceleratedMipNeRF()               -> nof_mipnerf_create (nof_config_default + --precision)
 //   new AcceleratedAdamOptimizer(sizes)    -> nof_adam_create(nof_mipnerf_layer_sizes)
 //   new AcceleratedGradientCalculator(N)   -> nof_gradcalc_create          (--host-api)
@@ -52,6 +53,7 @@ struct Args {
   bool loopback = false;  // --dp loopback: the gpus replicas on --device, a loopback group
   bool attach = false;    // bucketed all-reduce through the gradient-bucket hook
   int micro = 0;          // micro-batch rays (0: the whole shard)
+  long long max_resident = -1;  // >= 0: stream the record file when it holds more records than this
   bool host_api = false;
   uint64_t seed = 0x5EED0000ull;
   // Config (TrainState.cs:54-58)
@@ -64,7 +66,7 @@ struct Args {
                "usage: nof_train --records FILE [--steps K] [--batch N] [--precision f32|split|f16x2|f16split|f16]\n"
                "                 [--print-every P] [--save-every S --ckpt-dir DIR] [--resume CKPT] [--host-api]\n"
                "                 [--seed X] [--device D | --gpus N [--dp rccl|loopback] [--attach]] [--micro-batch M]\n"
-               "                 [--dump-params FILE]\n");
+               "                 [--dump-params FILE] [--max-resident RECORDS]\n");
   std::exit(code);
 }
 
@@ -91,6 +93,7 @@ Args parse(int argc, char** argv) {
     else if (k == "--host-api") a.host_api = true;
     else if (k == "--attach") a.attach = true;
     else if (k == "--micro-batch") a.micro = std::atoi(val());
+    else if (k == "--max-resident") a.max_resident = std::atoll(val());
     else if (k == "--dp") {
       const std::string d = val();
       if (d == "loopback") a.loopback = true;
@@ -195,7 +198,10 @@ int main(int argc, char** argv) {
     Replica& R = rs[r];
     R.device = a.gpus > 0 && !a.loopback ? r : a.device;
     CHECK(nof_set_device(R.device));
-    CHECK(nof_dataset_open(a.records.c_str(), R.device, &R.ds));  // BinDataset, resident on every device
+    if (a.max_resident >= 0)  // BinDataset streamed from the file when larger than the residency cap
+      CHECK(nof_dataset_open_streaming(a.records.c_str(), R.device, a.max_resident, &R.ds));
+    else
+      CHECK(nof_dataset_open(a.records.c_str(), R.device, &R.ds));  // BinDataset, resident on every device
     nof_config_default(&R.cfg);
     R.cfg.device = R.device;
     R.cfg.max_rays = micro;

@@ -46,6 +46,8 @@ def test_native_driver_matches_python_trainer(gpu, tmp_path):
     # the single-process data-parallel path (nof_dp_init_all + grouped all-reduce + nof_dp_wait) on
     # this box's one device: a world-1 all-reduce is the identity
     out_dp = _run(*common, "--steps", 4, "--gpus", 1, "--dump-params", tmp_path / "p_dp.bin")
+    # the record file streamed (4000 records against a residency cap of 1000): the same batches
+    out_st = _run(*common, "--steps", 4, "--max-resident", 1000, "--dump-params", tmp_path / "p_st.bin")
     p_dev = np.fromfile(tmp_path / "p_dev.bin", np.float32)
     p_host = np.fromfile(tmp_path / "p_host.bin", np.float32)
     assert p_dev.shape == (P,)
@@ -60,12 +62,13 @@ def test_native_driver_matches_python_trainer(gpu, tmp_path):
     p_py = nof.to_numpy(tr.model.mlp.flat_params()[0], (P,))
     assert np.array_equal(p_dev, p_py)      # the compiled driver == the Python driver, bit for bit
     assert np.array_equal(np.fromfile(tmp_path / "p_dp.bin", np.float32), p_py)
+    assert np.array_equal(np.fromfile(tmp_path / "p_st.bin", np.float32), p_py)
     # the reference's callback flow: the same step except that GetGradient sums the loss multipliers
     # on the host in ray order (MNcpp:61-65) where the device batch sums them on the GPU — one rounding
     # of 1/sum m apart, so equal to fp32 accuracy rather than bitwise
     assert np.linalg.norm(p_host.astype(np.float64) - p_py) <= 1e-6 * np.linalg.norm(p_py.astype(np.float64))
 
-    for out in (out_dev, out_host, out_dp):  # "Step {step}/{MaxSteps}, Loss: {loss}" (Program.cs:44)
+    for out in (out_dev, out_host, out_dp, out_st):  # "Step {step}/{MaxSteps}, Loss: {loss}" (Program.cs:44)
         got = {int(s): float(v) for s, v in re.findall(r"Step (\d+)/1000000, Loss: (\S+)", out)}
         assert sorted(got) == [2, 4]
         for s, v in got.items():

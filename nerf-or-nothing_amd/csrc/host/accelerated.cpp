@@ -188,6 +188,11 @@ std::vector<int> AcceleratedMLP::get_layer_sizes() const {
 void AcceleratedMLP::pack_weights() {
   nof::PackArgs pa;
   for (int l = 0; l < kLayers; ++l) { pa.woff[l] = woff_[l]; pa.boff[l] = boff_[l]; }
+  if (f16_pieces()) {  // the step's delta-scale maxima start at 0 (no memset launch per level)
+    pa.zero = amax_.p;
+    pa.nzero = (int)lv_.size();
+    amax_cleared_ = (1u << lv_.size()) - 1u;
+  }
   tb(kTPack);
   if (precision_ == NOF_PRECISION_F16)
     NOF_HIP(nof::launch_pack_weights_h32(params_.p, pa, wimg_f_.p, wimg_b_.p, st_));
@@ -518,7 +523,9 @@ void AcceleratedMLP::run_backward(int level, const float* color_grad, const floa
   b.M = L.M;
   b.split = precision_;
   if (f16_pieces()) {  // the level's power-of-two delta scale
-    NOF_HIP(nof::launch_delta_amax(density_grad, color_grad, L.M, amax_.p + level, st_, numeric_.p));
+    const bool cleared = (amax_cleared_ >> level) & 1u;  // by this step's pack launch, not used since
+    amax_cleared_ &= ~(1u << level);
+    NOF_HIP(nof::launch_delta_amax(density_grad, color_grad, L.M, amax_.p + level, st_, numeric_.p, cleared));
     b.amax = amax_.p + level;
   }
   b.dsigma = density_grad; b.drgb = color_grad; b.zhead = L.zhead.p;

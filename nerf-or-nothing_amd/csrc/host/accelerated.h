@@ -188,6 +188,7 @@ class AcceleratedMLP {
   int max_M_ = 0;
   DevBuf<float> slabs_, bias_slabs_;
   DevBuf<uint32_t> amax_;  // f16 modes: per level, bits of max |dsigma|, |drgb| (the level's delta scale)
+  uint32_t amax_cleared_ = 0;  // levels whose amax word the last pack launch zeroed and no pass used yet
   DevBuf<uint32_t> numeric_;
   size_t slab_cap_ = 0;
 };

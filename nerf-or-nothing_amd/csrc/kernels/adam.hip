@@ -164,6 +164,7 @@ __global__ void k_pack_weights_x3(const float* __restrict__ P_, PackArgs pa, flo
   constexpr int kChunks = split_slice_floats<P>() / 4;  // fragments of 16 B per slice
   const float* __restrict__ Pp = P_;
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid < pa.nzero) pa.zero[gid] = 0u;
   const int64_t nfc = (int64_t)kFwdSlices * kChunks, nbc = (int64_t)kBwdSlices * kChunks;
   if (gid < nfc + nbc) {
     const bool fwd = gid < nfc;
@@ -218,6 +219,7 @@ hipError_t launch_pack_weights_x3(const float* params, const PackArgs& pa, float
 __global__ void k_pack_weights_h32(const float* __restrict__ P, PackArgs pa, float* __restrict__ wf,
                                    float* __restrict__ wb) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid < pa.nzero) pa.zero[gid] = 0u;
   const int64_t nfc = (int64_t)(kFwdFrags + kStreamPad) * 64, nbc = (int64_t)(kBwdFrags + kStreamPad) * 64;
   if (gid < nfc + nbc) {
     const bool fwd = gid < nfc;

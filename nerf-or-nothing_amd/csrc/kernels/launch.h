@@ -75,7 +75,7 @@ hipError_t launch_mlp_bwd(const BwdArgs& a, hipStream_t st);
 // f16x2 mode: *amax = bits of max(|dsigma|, |drgb|) over M samples (clears *amax first); nonfinite
 // (optional): word 1 set to 1 when an input is not finite
 hipError_t launch_delta_amax(const float* dsigma, const float* drgb, int M, uint32_t* amax, hipStream_t st,
-                             uint32_t* nonfinite = nullptr);
+                             uint32_t* nonfinite = nullptr, bool cleared = false);  // cleared: *amax is 0 already
 // fp32-precision kernels (v_mfma_f32_16x16x4_f32, two waves per SIMD): mlp_fwd16.hip / mlp_bwd16.hip
 hipError_t launch_mlp_fwd16(const FwdArgs& a, hipStream_t st);
 hipError_t launch_mlp_bwd16(const BwdArgs& a, hipStream_t st);
@@ -146,7 +146,10 @@ constexpr int kLoopMax = 8;
 hipError_t launch_loopback_sum(int k, float* const* bufs, int64_t n, hipStream_t st);
 hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v, float lr, float inv1, float inv2,
                        hipStream_t st);
-struct PackArgs { int woff[11]; int boff[11]; };
+struct PackArgs {
+  int woff[11]; int boff[11];
+  uint32_t* zero = nullptr; int nzero = 0;  // words the pack launch also clears (the f16 modes' delta-scale maxima)
+};
 hipError_t launch_pack_weights(const float* params, const PackArgs& pa, float* wimg_f, float* wimg_b, hipStream_t st);
 // split images: precision 1 (bf16 hi/mid/lo) or 2 (f16 hi/lo)
 hipError_t launch_pack_weights_h32(const float* params, const PackArgs& pa, float* wimg_f, float* wimg_b,

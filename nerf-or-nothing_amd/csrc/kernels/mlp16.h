@@ -144,7 +144,6 @@ struct BlkStore16H {
 // gradient operands in fp32), fp16 blocks (P = 2); all nt
 template <int P, bool kBwd> struct Store16 { typedef BlkStore16 T; typedef float E; };
 template <bool kBwd> struct Store16<2, kBwd> { typedef BlkStore16H<true> T; typedef _Float16 E; };
-template <bool kBwd> struct Store16<4, kBwd> { typedef BlkStore16H<true> T; typedef _Float16 E; };  // F16
 template <class E>
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t blk_rsrc_t(E* blk) {
   return __builtin_amdgcn_make_buffer_rsrc(blk, (short)0, 0x7fffffff, 0x00020000);
@@ -236,8 +235,8 @@ __device__ __forceinline__ void put_tile(float (&bin)[16][4], int t, const float
 // kVmPerPart = vector-memory ops one tile issues (4: fp32 tiles), for the counted slice barrier.  fp16
 // tiles issue 2 (store_pairs): with the 3-slot ring the count of 4 then lets exactly the previous slice's
 // stores stay in flight too (they follow the DMA the barrier must retire), but a 4-slot ring, whose
-// barrier also retires the slice's own DMA, needs the exact 2 (an F16 4-slot ring raced on 4, round 2;
-// the exact count in the 3-slot path forces the previous slice's stores out: F16 step +1 %, A/B).
+// barrier also retires the slice's own DMA, needs the exact 2 (a 4-slot fp16 ring raced on 4, round 2;
+// the exact count in the 3-slot path forces the previous slice's stores out: step +1 %, A/B).
 struct NoEpi16 {
   static constexpr int kVmPerPart = 0;
   __device__ __forceinline__ void operator()(int) {}
@@ -337,21 +336,18 @@ __device__ __forceinline__ void mlp_layer16(const float (&bin)[16][4], const flo
 // (k_pack_weights_x3<2>) holds, per 16-row tile rt and piece p, the 16-B A fragment of lane (g, j):
 // W[16 rt + j][base + 16 (i >> 2) + 4g + (i & 3)], i = 0..7 (chunk (16 p + rt) 64 + lane: one
 // contiguous ds_read_b128 per fragment; piece-major, so the hi pieces are the slice's first 16 KB).
-// kProd = 1 streams only that half: 2 DMA steps per slice instead of 4.  A group = one row-tile pair x 3 products (lo.hi, hi.lo,
+// A group = one row-tile pair x 3 products (lo.hi, hi.lo,
 // hi.hi) interleaved over the pair's two accumulators; the next pair's fragments are read one group
 // ahead; the 4 DMA steps of slice t + 2 ride groups 0..3; epilogue tiles 2t + 2, 2t + 3 run after them.
-// kProd = 1 (F16): the hi.hi product alone — only the hi A fragments are read, the lo pieces the
-// epilogues leave in `bin` go unused.
-template <int NT_B, int NT_I, int OT, class Epi, int kProd = 3>
+template <int NT_B, int NT_I, int OT, class Epi>
 __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16],
                                              float* lds, int& cur, const float*& wsrc, bool last_in_schedule, int tid,
                                              int lane, Epi& epi, const float* cinit) {
   typedef SplitMode<2> SM;
   static_assert(OT % 2 == 0 && OT <= 16, "row tiles come in pairs");
-  static_assert(kProd == 1 || kProd == SM::NPROD, "hi.hi alone or all three products");
-  constexpr int kPieces = kProd == 1 ? 1 : 2;     // A fragment pieces read per row tile
-  constexpr int kPP0 = SM::NPROD - kProd;         // first product (SM::pa / pb order; the last is hi.hi)
-  constexpr int kDmaSteps = kProd == 1 ? 2 : 4;   // 8-KB steps per slice: the hi half, or all of it
+  constexpr int kPieces = 2;    // A fragment pieces read per row tile (hi, lo)
+  constexpr int kPP0 = 0;       // first product (SM::pa / pb order; the last is hi.hi)
+  constexpr int kDmaSteps = 4;  // 8-KB steps per slice
   constexpr int kSlots = ring16_slots<2>();
   constexpr int NG = OT / 2;  // groups per slice
   constexpr int kE1 = NG > 4 ? 4 : NG - 1;
@@ -429,15 +425,13 @@ __device__ __forceinline__ void mlp_layer16h(const float (&bin)[16][4], const fl
   }
 }
 
-// precision dispatch: P = 0 fp32 16x16x4, P = 2 / 3 fp16 (hi, lo) pieces on 16x16x32, P = 4 fp16 hi.hi
+// precision dispatch: P = 0 fp32 16x16x4, P = 2 / 3 fp16 (hi, lo) pieces on 16x16x32
 template <int P, int NT_B, int NT_I, int OT, class Epi>
 __device__ __forceinline__ void layer16(const float (&bin)[16][4], const float* ipe_lds, f32x4 (&acc)[16], float* lds,
                                         int& cur, const float*& wsrc, bool last_in_schedule, int tid, int lane,
                                         Epi& epi, const float* cinit = nullptr) {
   if constexpr (P == 2 || P == 3)
     mlp_layer16h<NT_B, NT_I, OT>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi, cinit);
-  else if constexpr (P == 4)
-    mlp_layer16h<NT_B, NT_I, OT, Epi, 1>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane, epi, cinit);
   else
     mlp_layer16<NT_B, NT_I, OT, ring16_slots<P>()>(bin, ipe_lds, acc, lds, cur, wsrc, last_in_schedule, tid, lane,
                                                    epi, cinit);

@@ -194,8 +194,8 @@ __global__ void k_delta_amax(const float* __restrict__ dsigma, const float* __re
 }
 
 hipError_t launch_delta_amax(const float* dsigma, const float* drgb, int M, uint32_t* amax, hipStream_t st,
-                             uint32_t* nonfinite) {
-  hipError_t e = hipMemsetAsync(amax, 0, sizeof(uint32_t), st);
+                             uint32_t* nonfinite, bool cleared) {
+  hipError_t e = cleared ? hipSuccess : hipMemsetAsync(amax, 0, sizeof(uint32_t), st);
   if (e != hipSuccess || M <= 0) return e;
   const int blocks = std::min(256, (4 * M + 255) / 256);
   hipLaunchKernelGGL(k_delta_amax, dim3(blocks), dim3(256), 0, st, dsigma, drgb, M, amax, nonfinite);

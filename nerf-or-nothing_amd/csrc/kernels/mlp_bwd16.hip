@@ -160,7 +160,6 @@ hipError_t launch_mlp_bwd16(const BwdArgs& a, hipStream_t st) {
   const int nblk = a.M / kBlk;
   if (a.split == 2) hipLaunchKernelGGL(k_mlp_bwd16<2>, dim3((nblk + 3) / 4), dim3(kMlp16Threads), 0, st, a);
   else if (a.split == 3) hipLaunchKernelGGL(k_mlp_bwd16<3>, dim3((nblk + 3) / 4), dim3(kMlp16Threads), 0, st, a);
-  else if (a.split == 4) hipLaunchKernelGGL(k_mlp_bwd16<4>, dim3((nblk + 3) / 4), dim3(kMlp16Threads), 0, st, a);
   else hipLaunchKernelGGL(k_mlp_bwd16<0>, dim3((nblk + 3) / 4), dim3(kMlp16Threads), 0, st, a);
   return hipGetLastError();
 }

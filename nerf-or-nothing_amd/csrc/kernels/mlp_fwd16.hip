@@ -78,7 +78,7 @@ struct FwdEpi16 {
 };
 
 // P: 0 = fp32 (16x16x4 fp32 MFMA, fp32 activation blocks), 2 = f16x2 (16x16x32 f16, fp16 blocks),
-// 3 = F32_F16SPLIT (16x16x32 f16, fp32 blocks), 4 = F16 (one hi.hi product, fp16 blocks)
+// 3 = F32_F16SPLIT (16x16x32 f16, fp32 blocks); the F16 mode runs mlp_f16.hip
 template <int P, bool store>  // store: side outputs for the backward pass (off for inference)
 __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
   typedef typename Store16<P, false>::T ST;
@@ -253,9 +253,6 @@ hipError_t launch_mlp_fwd16(const FwdArgs& a, hipStream_t st) {
   if (a.split == 2) {
     if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd16<2, false>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((k_mlp_fwd16<2, true>), grid, block, 0, st, a);
-  } else if (a.split == 4) {
-    if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd16<4, false>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((k_mlp_fwd16<4, true>), grid, block, 0, st, a);
   } else if (a.split == 3) {  // the inference variant is <2, false>'s arithmetic with nothing stored
     if (a.no_store) hipLaunchKernelGGL((k_mlp_fwd16<2, false>), grid, block, 0, st, a);
     else hipLaunchKernelGGL((k_mlp_fwd16<3, true>), grid, block, 0, st, a);

@@ -475,8 +475,11 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int lv0, int lv1, int bucket)
     nof::WgOut o;
     o.item0 = first_item[s.prob];
     o.nitems = 0;  // the problem's items at every level: problems s.prob .. s.prob + nlev - 1, contiguous
+    NOF_REQUIRE(nlev <= nof::kWgMaxLevels, "too many levels");
+    o.nlev = nlev;
     for (int l = 0; l < nlev; ++l) {
       NOF_REQUIRE(first_item[s.prob + l] == o.item0 + o.nitems, "a problem's items are not contiguous");
+      o.lev_items[l] = nitems[s.prob + l];
       o.nitems += nitems[s.prob + l];
     }
     o.row_off = s.row_off; o.nrows = s.nrows; o.col_off = s.col_off; o.ncols = s.ncols;

@@ -100,8 +100,11 @@ struct WgProblem {
 struct WgItem { int prob, kb0, kb1; int slab; };  // slab = index into slab_off[]
 // k_wgrad_reduce threads an output needs (max_elems of launch_wgrad_reduce = the max over outputs)
 int wgrad_reduce_threads(int nrows, int ncols, int col_off);
+constexpr int kWgMaxLevels = 4;
 struct WgOut {
-  int item0, nitems;        // contiguous items of the problem
+  int item0, nitems;        // contiguous items of the problem (item i writes slab i)
+  int lev_items[kWgMaxLevels];  // of which level 0's come first, then level 1's, ... (the reduce's grouping)
+  int nlev;
   int row_off, nrows, col_off, ncols;
   float* dst; int ld, dst_col;
   float* bias_dst;          // null: no bias

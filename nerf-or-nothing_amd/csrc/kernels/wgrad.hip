@@ -1003,7 +1003,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const WgOut* __restrict__ 
   const int ld = probs[o.prob].ntc * 32;
   const int ne = o.nrows * o.ncols;
   constexpr int kU = 8;  // item slabs in flight per step
-  auto level_of = [&](int k) { return probs[items[o.item0 + k].prob].level; };
+  const int64_t* so = slab_off + o.item0;  // item i writes slab i: no item-table indirection
   auto inv_of = [&](int lev) { return amax ? delta_scale(amax + lev, true) : 1.0f; };  // exact powers of 2
   const bool vec = reduce_vec(o.ncols, o.col_off);
   if (vec ? 4 * t < ne : t < ne) {
@@ -1012,39 +1012,35 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const WgOut* __restrict__ 
     const size_t off = (size_t)(o.row_off + rr) * ld + o.col_off + cc;  // 16-B aligned when vec (ld % 32 == 0)
     float* dst = o.dst + (size_t)rr * o.ld + o.dst_col + cc;
     f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-    bool first = true;
-    for (int k = 0; k < o.nitems;) {
-      const int lev = level_of(k);
-      int k1 = k + 1;
-      while (k1 < o.nitems && level_of(k1) == lev) ++k1;
+    int k = 0;
+    for (int lev = 0; lev < o.nlev; ++lev) {
+      const int k1 = k + o.lev_items[lev];
       f32x4 s = {0.0f, 0.0f, 0.0f, 0.0f};
       if (vec) {
         for (; k + kU <= k1; k += kU) {
           f32x4 v[kU];
 #pragma unroll
-          for (int u = 0; u < kU; ++u)
-            v[u] = *reinterpret_cast<const f32x4*>(slabs + slab_off[items[o.item0 + k + u].slab] + off);
+          for (int u = 0; u < kU; ++u) v[u] = *reinterpret_cast<const f32x4*>(slabs + so[k + u] + off);
 #pragma unroll
           for (int u = 0; u < kU; ++u) s += v[u];
         }
-        for (; k < k1; ++k) s += *reinterpret_cast<const f32x4*>(slabs + slab_off[items[o.item0 + k].slab] + off);
+        for (; k < k1; ++k) s += *reinterpret_cast<const f32x4*>(slabs + so[k] + off);
       } else {
         for (; k + kU <= k1; k += kU) {
           float v[kU];
 #pragma unroll
-          for (int u = 0; u < kU; ++u) v[u] = slabs[slab_off[items[o.item0 + k + u].slab] + off];
+          for (int u = 0; u < kU; ++u) v[u] = slabs[so[k + u] + off];
 #pragma unroll
           for (int u = 0; u < kU; ++u) s[0] += v[u];
         }
-        for (; k < k1; ++k) s[0] += slabs[slab_off[items[o.item0 + k].slab] + off];
+        for (; k < k1; ++k) s[0] += slabs[so[k] + off];
       }
       const float inv = inv_of(lev);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float v = s[j] * inv;
-        acc[j] = first ? (accumulate ? dst[vec ? j : 0] + v : v) : acc[j] + v;
+        acc[j] = lev == 0 ? (accumulate ? dst[vec ? j : 0] + v : v) : acc[j] + v;
       }
-      first = false;
     }
     if (vec) {
 #pragma unroll
@@ -1055,15 +1051,13 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const WgOut* __restrict__ 
   }
   if (o.bias_dst && t < o.nrows) {
     float acc = 0.0f;
-    bool first = true;
-    for (int k = 0; k < o.nitems;) {
-      const int lev = level_of(k);
+    int k = 0;
+    for (int lev = 0; lev < o.nlev; ++lev) {
       float s = 0.0f;
-      for (; k < o.nitems && level_of(k) == lev; ++k)
-        s += bias_slabs[(size_t)items[o.item0 + k].slab * 256 + o.row_off + t];
+      for (const int k1 = k + o.lev_items[lev]; k < k1; ++k)
+        s += bias_slabs[(size_t)(o.item0 + k) * 256 + o.row_off + t];
       const float v = s * inv_of(lev);
-      acc = first ? (accumulate ? o.bias_dst[t] + v : v) : acc + v;
-      first = false;
+      acc = lev == 0 ? (accumulate ? o.bias_dst[t] + v : v) : acc + v;
     }
     o.bias_dst[t] = acc;
   }

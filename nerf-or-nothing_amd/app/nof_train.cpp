@@ -119,6 +119,9 @@ Args parse(int argc, char** argv) {
   if (a.micro < 0 || (a.micro > 0 && shard % a.micro)) usage(2);
   if ((a.loopback || a.attach) && a.gpus == 0) usage(2);
   if (a.host_api && (a.micro || a.attach)) usage(2);  // the reference's flow: one call per shard
+  // one process driving several RCCL ranks all-reduces them in one group (nof_dp_train_step refuses
+  // attached RCCL communicators at n > 1); the bucket hook is for one rank per process or loopback
+  if (a.attach && a.gpus > 1 && !a.loopback) usage(2);
   return a;
 }
 

@@ -501,6 +501,7 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int lv0, int lv1, int bucket)
   sc.nouts = (int)outs.size();
   sc.max_elems = max_elems;
   sc.num_wg = nwg;
+  sc.lv0 = lv0;
   return sc;
 }
 
@@ -516,7 +517,7 @@ void AcceleratedMLP::run_wgrad(Schedule& sc, int accumulate) {
   tb(kTWgradReduce);
   NOF_HIP(nof::launch_wgrad_reduce(sc.outs.p, sc.nouts, sc.max_elems, sc.items.p, sc.probs.p, sc.slab_off.p,
                                    slabs_.p, bias_slabs_.p, accumulate,
-                                   f16_pieces() ? amax_.p : nullptr, st_));
+                                   f16_pieces() ? amax_.p + sc.lv0 : nullptr, st_));
   te(kTWgradReduce);
 }
 

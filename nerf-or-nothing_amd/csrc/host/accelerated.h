@@ -149,6 +149,7 @@ class AcceleratedMLP {
     DevBuf<int64_t> slab_off;
     DevBuf<nof::WgOut> outs;
     int nouts = 0, max_elems = 0, num_wg = 0;
+    int lv0 = 0;  // first level: the reduce's delta-scale words are amax_ + lv0 + (level - lv0)
   };
   struct Level {
     int cap = 0, M = 0, n = 0, S = 0;

@@ -436,8 +436,10 @@ static void check_loopback(nof_dp* dp) {
 void dp_wait(nof_dp* dp, int timeout_ms) {
   check_live(dp);
   check_loopback(dp);
-  // every all-reduce of a communicator is ordered on one stream: the last one done implies the lagged one
+  // every all-reduce of a communicator is ordered on one stream: the last one done implies the lagged
+  // one; after dp_step_end the step's last all-reduce is the lagged event, and this wait covers it
   if (dp->pending) wait_event(dp, dp->done, timeout_ms);
+  else if (dp->lag_pending) wait_event(dp, dp->lag, timeout_ms);
   dp->pending = false;
   dp->lag_pending = false;
 }
@@ -534,7 +536,17 @@ void dp_train_step(int n, nof_dp* const* dps, AcceleratedMipNeRF* const* models,
     for (int r = 0; r < n; ++r)
       NOF_REQUIRE((dps[r]->model != nullptr) == attached && (!attached || dps[r]->model == models[r]),
                   "attach every replica's communicator to its model, or none");
+    // one host thread driving n RCCL ranks must issue every rank's collective inside ONE group; the
+    // bucket hook issues (and settles) each rank's bucket as that rank's backward publishes it, so
+    // rank 0 would wait for peers this thread has not launched yet: grouped all-reduce only
+    NOF_REQUIRE(!(attached && n > 1 && !dps[0]->loop),
+                "attached (bucketed) mode drives one RCCL rank per process; several devices in one process "
+                "use the grouped all-reduce (do not attach)");
   }
+  // a dataset's batch buffers are reused by every next() call: replica r + 1's gather would overwrite
+  // what replica r's gradient kernels still read
+  for (int r = 0; r < n; ++r)
+    for (int q = r + 1; q < n; ++q) NOF_REQUIRE(datasets[r] != datasets[q], "every replica needs its own dataset");
   NOF_REQUIRE(global_batch > 0 && global_batch % world == 0, "the global batch must divide into equal shards");
   const int shard = global_batch / world;
   const int micro = micro_batch > 0 ? std::min(micro_batch, shard) : shard;

@@ -139,6 +139,7 @@ void RayDataset::reserve(int n, hipStream_t st) {
   if (streaming()) {  // the device staging slot and the two pinned record buffers
     if (prefetch_.joinable()) prefetch_.join();
     pre_.valid = false;
+    cur_key_.valid = false;
     NOF_HIP(hipDeviceSynchronize());  // no copy from the old pinned buffers, no gather from the old slot
     rec_.alloc(16 * (size_t)n);
     for (float*& h : hrec_) {
@@ -157,24 +158,32 @@ void RayDataset::next(int n, uint64_t seed, uint32_t step, uint32_t ray_base, hi
   reserve(n, st);
   int staged = 0;
   if (streaming()) {
-    // this batch's records: the prefetch made during the previous call when it guessed this request
-    // (same n / seed / ray base, the next step), else a synchronous fetch into the other buffer
+    // this batch's records: the buffer fetched by the previous call when this is the same request again
+    // (nof_dp_train_step's two passes over one shard), the prefetch made during the previous call when
+    // it guessed this request (same n / seed / ray base, the next step), else a synchronous fetch into
+    // the other buffer
     if (prefetch_.joinable()) prefetch_.join();
+    const Key want{n, seed, step, ray_base, true};
+    const bool reuse = cur_key_.same(want);
     int b;
-    if (pre_.valid && prefetch_error_.empty() && pre_.n == n && pre_.seed == seed && pre_.step == step &&
-        pre_.ray_base == ray_base) {
+    if (reuse) {
+      b = cur_;
+    } else if (prefetch_error_.empty() && pre_.same(want)) {
       b = pre_buf_;
     } else {
       b = cur_ ^ 1;
       NOF_HIP(hipEventSynchronize(copied_[b]));  // its previous copy has left the pinned buffer
       fetch(b, n, seed, step, ray_base);
     }
-    pre_.valid = false;
-    prefetch_error_.clear();
+    if (!reuse) {  // the other buffer was consumed or overwritten
+      pre_.valid = false;
+      prefetch_error_.clear();
+    }
     NOF_HIP(hipStreamWaitEvent(st, gathered_, 0));  // the previous batch's gather has read the slot
     NOF_HIP(hipMemcpyAsync(rec_.p, hrec_[b], 64 * (size_t)n, hipMemcpyHostToDevice, st));
     NOF_HIP(hipEventRecord(copied_[b], st));
     cur_ = b;
+    cur_key_ = want;
     staged = 1;
   }
   NOF_HIP(nof::launch_gather_batch(rec_.p, count_, n, seed, step, ray_base, o_.p, d_.p, vd_.p, r_.p, nr_.p, fr_.p,
@@ -182,19 +191,22 @@ void RayDataset::next(int n, uint64_t seed, uint32_t step, uint32_t ray_base, hi
   if (streaming()) {
     NOF_HIP(hipEventRecord(gathered_, st));
     // prefetch the likely next request (the next step of the same shard) into the other buffer while
-    // the GPU runs this step
+    // the GPU runs this step, unless that buffer already holds it
     const int pb = cur_ ^ 1;
-    pre_ = Key{n, seed, step + 1, ray_base, true};
-    pre_buf_ = pb;
-    prefetch_ = std::thread([this, pb, n, seed, step, ray_base] {
-      try {
-        NOF_HIP(hipSetDevice(device_));
-        NOF_HIP(hipEventSynchronize(copied_[pb]));
-        fetch(pb, n, seed, step + 1, ray_base);
-      } catch (const std::exception& e) {
-        prefetch_error_ = e.what();  // the next call fetches synchronously and reports the error
-      }
-    });
+    const Key nk{n, seed, step + 1, ray_base, true};
+    if (!(pre_.same(nk) && pre_buf_ == pb && prefetch_error_.empty())) {
+      pre_ = nk;
+      pre_buf_ = pb;
+      prefetch_ = std::thread([this, pb, n, seed, step, ray_base] {
+        try {
+          NOF_HIP(hipSetDevice(device_));
+          NOF_HIP(hipEventSynchronize(copied_[pb]));
+          fetch(pb, n, seed, step + 1, ray_base);
+        } catch (const std::exception& e) {
+          prefetch_error_ = e.what();  // the next call fetches synchronously and reports the error
+        }
+      });
+    }
   }
   out->n = n;
   out->origins = o_.p; out->directions = d_.p; out->viewdirs = vd_.p; out->radii = r_.p;

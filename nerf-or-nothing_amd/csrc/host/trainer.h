@@ -45,7 +45,14 @@ class RayDataset {
   hipEvent_t copied_[2] = {nullptr, nullptr};
   hipEvent_t gathered_ = nullptr;  // after the last gather from the staging slot
   int cur_ = 0, pre_buf_ = 1;
-  struct Key { int n; uint64_t seed; uint32_t step, ray_base; bool valid; } pre_{0, 0, 0, 0, false};
+  struct Key {
+    int n; uint64_t seed; uint32_t step, ray_base; bool valid;
+    bool same(const Key& o) const {
+      return valid && o.valid && n == o.n && seed == o.seed && step == o.step && ray_base == o.ray_base;
+    }
+  };
+  Key pre_{0, 0, 0, 0, false};
+  Key cur_key_{0, 0, 0, 0, false};  // the records held by pinned buffer cur_
   std::thread prefetch_;
   std::string prefetch_error_;
   int cap_ = 0;

@@ -69,3 +69,28 @@ def test_step_end_waits_one_step_behind(gpu):
         dps[0].step_end()
     for d in dps:
         d.close()
+
+
+def test_wait_after_step_end_covers_the_last_step(gpu):
+    """after nof_dp_step_end the step's all-reduce is the LAGGED one; a final nof_dp_wait must
+    still wait for it (boundedly).  The all-reduce sits behind a ~0.5 s spin on the stream, so a wait with a
+    50 ms limit has to time out and fail loudly instead of returning at once."""
+    import torch
+    import nof
+    from nof.dp import NativeDP
+
+    dps = NativeDP.init_loopback(2, 0)
+    ts = [torch.full((1000,), float(i + 1), device=gpu) for i in range(2)]
+    torch.cuda._sleep(1_000_000_000)  # ~0.5 s of GPU clock ticks ahead of the all-reduce on the null stream
+    for d, t in zip(dps, ts):
+        d.allreduce(t.data_ptr(), 1000)
+    for d in dps:
+        d.step_end()  # no earlier step: returns at once; this step becomes the lagged one
+    with pytest.raises(nof.NofError):
+        dps[0].wait(50)
+    torch.cuda.synchronize()
+    dps[1].wait(60000)  # the other member's lagged all-reduce has completed by now
+    for t in ts:
+        assert torch.equal(t, torch.full((1000,), 3.0, device=gpu))
+    for d in dps:
+        d.close()

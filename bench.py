@@ -57,6 +57,11 @@ PEAK_HBM_GBS = 8000.0
 # dz_sigma 1 and dz_rgb 3 = 2180 (the stored blocks add 33 zero rows: not counted)
 WGRAD_VALUES = 2299 + 2180
 WGRAD_BYTES_PER_VALUE = {"f32": 4, "split": 4, "f16x2": 2, "f16split": 4, "f16": 2}
+# algorithmic HBM bytes per sample per level of the F16 MLP kernels (mlp_f16.hip, fp16 blocks):
+#   forward writes act_in 128 x 2 + h0..h7 8 x 256 x 2 + h9 128 x 2 + ReLU masks 9 x 32 + zhead 16 + sigma,
+#   rgb 16 = 4928; backward writes delta 8 x 256 x 2 + delta9x 132 x 2 = 4360 and reads the masks 288,
+#   zhead 16, dsigma / drgb 16 = 4680; weight gradients read every stored operand once (WGRAD_VALUES x 2)
+KERNEL_BYTES_PER_SAMPLE = {"f16": {"mlp_fwd": 4928, "mlp_bwd": 4680, "wgrad": WGRAD_VALUES * 2}}
 INTEGRATOR_FWD_B = lambda S: S * (12 + 4 + 4) + (S + 1) * 4 + 12 + 12  # rgb, sigma, w | t | d | C  (3100 @128)
 INTEGRATOR_BWD_B = lambda S: 12 + S * (12 + 4) + (S + 1) * 4 + 12 + S * (12 + 4)  # 4636 @128
 
@@ -535,15 +540,24 @@ def main():
                 m.close()
         return dt, timing, psnr, in_sync
 
-    def summarize(prec, dt, timing, sh=shard):
-        ms_step = dt * 1e3 / a.steps
-        M = [sh * s for s in samples]
+    def summarize(prec, dt, timing, sh=shard, smp=None, steps=None):
+        steps = steps or a.steps
+        ms_step = dt * 1e3 / steps
+        M = [sh * s for s in (smp or samples)]
         flop = {"mlp_fwd": 2 * MACS_FWD * sum(M), "mlp_bwd": 2 * MACS_DX * sum(M), "wgrad": 2 * MACS_DW * sum(M)}
         kernels = {}
         for name, (ms, cnt) in timing.items():
             if cnt:
-                kernels[name] = {"ms_per_step": round(ms / a.steps, 4), "launches_per_step": cnt // a.steps,
+                kernels[name] = {"ms_per_step": round(ms / steps, 4), "launches_per_step": cnt // steps,
                                  "avg_launch_ms": round(ms / cnt, 4)}
+        # algorithmic HBM bytes of the MLP kernels where they are an HBM stream as much as an MFMA
+        # workload (the F16 mode): achieved GB/s beside the MFMA fraction of each
+        for k, bps in KERNEL_BYTES_PER_SAMPLE.get(prec, {}).items():
+            if k in kernels:
+                b_launch = bps * sum(M) / kernels[k]["launches_per_step"]
+                gbs = b_launch / (kernels[k]["avg_launch_ms"] * 1e-3) / 1e9
+                kernels[k].update({"bytes_per_launch": b_launch, "achieved_gbs": round(gbs, 1),
+                                   "hbm_frac": round(gbs / PEAK_HBM_GBS, 4)})
         dom = max((k for k in flop if k in kernels), key=lambda k: kernels[k]["ms_per_step"])
         fl_launch = flop[dom] / kernels[dom]["launches_per_step"]
         achieved = fl_launch / (kernels[dom]["avg_launch_ms"] * 1e-3) / 1e12
@@ -602,6 +616,22 @@ def main():
         cfg4 = {"workload": "BASELINE configs[3] on 1 GPU: 65536-ray global batch x 128+128 samples, 8 micro-batches "
                             "of 8192 rays accumulated, one Adam step", "value": round(65536 * c_steps / c_dt, 1),
                 "unit": "rays/s", "ms_per_step": round(c_dt * 1e3 / c_steps, 3), "steps": c_steps, "warmup": 1}
+
+    cfg3 = None
+    if lead and world == 1 and G == 1 and a.scene == "blender" and samples == [128, 128] and not a.no_alt:
+        # BASELINE configs[2]: mip-NeRF coarse + fine with 64 + 128 hierarchical samples (the coarse level
+        # stratified, the fine level resampled from it), same batch, same mode, its own live roofline
+        c3_smp = [64, 128]
+        c3_dt, c3_timing, c3_psnr, _ = measure(a.precision, smp=c3_smp)
+        c3_ms, c3_kernels, c3_roof = summarize(a.precision, c3_dt, c3_timing, smp=c3_smp)
+        c3_tf = 2 * (MACS_FWD + MACS_DX + MACS_DW) * shard * sum(c3_smp) / (c3_ms * 1e-3) / 1e12
+        cfg3 = {"workload": f"BASELINE configs[2]: {B}-ray batches x 64+128 hierarchical samples (mip-NeRF "
+                            f"coarse + fine), 8x256 MLP fwd/bwd + Adam", "value": round(B * a.steps / c3_dt, 1),
+                "unit": "rays/s", "ms_per_step": round(c3_ms, 4), "steps": a.steps, "warmup": a.warmup,
+                "precision": a.precision, "dtype": DTYPES[a.precision], **c3_roof,
+                "roofline_step": {"bound": "mfma", "achieved": round(c3_tf, 2), "peak": PEAKS[a.precision],
+                                  "unit": "TFLOP/s", "frac": round(c3_tf / PEAKS[a.precision], 4)},
+                "kernels": c3_kernels, "psnr_fine": round(c3_psnr, 3)}
 
     cfg5 = None
     if a.scene == "blender" and not a.no_config5:
@@ -675,6 +705,8 @@ def main():
                 result["rehearsal"] = f"{backend}: {world} ranks on {torch.cuda.device_count()} GPU(s), not a scaling run"
         if llff:
             result["llff_1gpu"] = llff
+        if cfg3:
+            result["config3"] = cfg3
         if cfg4:
             result["config4_1gpu"] = cfg4
         if cfg5:
@@ -683,10 +715,19 @@ def main():
             result["alt_precision"] = []
             for aprec, adt, atiming, apsnr, _ in alts:
                 ams, akernels, aroof = summarize(aprec, adt, atiming)
-                result["alt_precision"].append({
-                    "precision": aprec, "dtype": DTYPES[aprec], "value": round(B * a.steps / adt, 1),
-                    "unit": "rays/s", "ms_per_step": round(ams, 4), **aroof,
-                    "kernels": {k: v["avg_launch_ms"] for k, v in akernels.items()}, "psnr_fine": round(apsnr, 3)})
+                entry = {"precision": aprec, "dtype": DTYPES[aprec], "value": round(B * a.steps / adt, 1),
+                         "unit": "rays/s", "ms_per_step": round(ams, 4), **aroof,
+                         "kernels": {k: v["avg_launch_ms"] for k, v in akernels.items()}, "psnr_fine": round(apsnr, 3)}
+                if aprec in KERNEL_BYTES_PER_SAMPLE:  # each MLP kernel: MFMA fraction and achieved GB/s
+                    fl = {"mlp_fwd": MACS_FWD, "mlp_bwd": MACS_DX, "wgrad": MACS_DW}
+                    entry["kernel_rooflines"] = {
+                        k: {"avg_launch_ms": v["avg_launch_ms"],
+                            "mfma_frac": round(2 * fl[k] * B * sum(samples) / v["launches_per_step"]
+                                               / (v["avg_launch_ms"] * 1e-3) / 1e12 / PEAKS[aprec], 4),
+                            "achieved_gbs": v["achieved_gbs"], "hbm_frac": v["hbm_frac"],
+                            "bytes_per_launch": v["bytes_per_launch"]}
+                        for k, v in akernels.items() if "achieved_gbs" in v}
+                result["alt_precision"].append(entry)
         if world == 1 and G == 1 and a.scene == "blender" and B <= 8192:
             result["api_path_pcie"] = api_path(torch, nof, synth, dev, B, samples, a.precision)
             result["render_1gpu"] = render_throughput(torch, nof, synth, dev, a.precision, samples=tuple(samples))

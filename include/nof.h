@@ -56,6 +56,12 @@ typedef struct nof_config {
   uint64_t seed;                          /* Philox key (reference: time(nullptr), MNcpp:44) */
   void* stream;                           /* hipStream_t, NULL = default stream */
   int32_t precision;                      /* NOF_PRECISION_*: MLP contraction arithmetic (build extension) */
+  int32_t grad_buckets;                   /* 0: the weight-gradient split-K items are cut for the whole launch;
+                                             1: cut per all-reduce bucket (layers 5..10 | 0..4), the cut the
+                                             bucketed (attached, overlapped) launches use, so an unbucketed and
+                                             a bucketed step sum every gradient element in the same order and a
+                                             data-parallel run is bitwise the same attached or not.  Installing
+                                             a gradient-bucket hook (nof_dp_attach) selects 1 (build extension) */
 } nof_config;
 
 /* MLP contraction arithmetic.  Every mode holds operands and accumulators in fp32 between the

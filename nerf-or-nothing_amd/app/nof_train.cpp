@@ -210,6 +210,9 @@ int main(int argc, char** argv) {
     R.cfg.max_rays = micro;
     R.cfg.seed = a.seed;
     R.cfg.precision = a.precision;
+    // data-parallel runs cut the weight-gradient items per all-reduce bucket: attached (bucketed,
+    // overlapped) and grouped all-reduces then give bitwise-identical parameters
+    R.cfg.grad_buckets = G > 1 ? 1 : 0;
     CHECK(nof_mipnerf_create(&R.cfg, &R.model));
     int32_t sizes[64], nsizes = 0;
     CHECK(nof_mipnerf_layer_sizes(R.model, sizes, 64, &nsizes));

@@ -96,6 +96,7 @@ void nof_config_default(nof_config* c) {
   c->seed = 0x5EED0000ull;
   c->stream = nullptr;
   c->precision = NOF_PRECISION_F32;
+  c->grad_buckets = 0;
 }
 
 const char* nof_last_error(void) { return g_err.c_str(); }

@@ -117,6 +117,7 @@ AcceleratedMLP::AcceleratedMLP(int deg_point, int deg_view, const nof_config& cf
   hipDeviceProp_t prop;
   NOF_HIP(hipGetDeviceProperties(&prop, cfg.device));
   num_cu_ = prop.multiProcessorCount;
+  aligned_ = cfg.grad_buckets != 0;
 
   // layer dims (get_layer_sizes MLPcpp:131-154)
   const int W = 256, Wc = 128, pos = 96, dir = 27;
@@ -283,7 +284,7 @@ int AcceleratedMLP::bucket_spans(int b, int64_t* off, int64_t* cnt) const {
 
 AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int lv0, int lv1, int bucket) {
   NOF_REQUIRE(lv0 >= 0 && lv0 < lv1 && lv1 <= (int)lv_.size(), "bad level range");
-  std::vector<int64_t> key{lv0, lv1, bucket};
+  std::vector<int64_t> key{lv0, lv1, bucket, aligned_ ? 1 : 0};
   for (int l = lv0; l < lv1; ++l) key.push_back(lv_[l].M);
   auto it = sched_.find(key);
   if (it != sched_.end()) return it->second;
@@ -388,7 +389,7 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int lv0, int lv1, int bucket)
     os.swap(ob);
   }
 
-  // cost per k-block, calibrated against per-item timings (NOF_DIAG_WG_TIME builds,
+  // cost per k-block, calibrated against per-item timings (stamps builds, make STAMPS=1,
   // tools/diag_item_time.py).  fp32 (k_wgrad, MFMA-bound): wgrad_block_cost.  f16x2 (k_wgrad_h, an
   // HBM stream): the bytes, 10 (ntr + ntc) — 1.57 / 1.11 / 1.28 / 0.49 us per block measured for the
   // 16 / 11 / 13 / 5-tile problems — and the one-column (4,1) problem 0.60 us (two active waves and
@@ -420,48 +421,79 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int lv0, int lv1, int bucket)
   // replaces closed every workgroup short and left the sum of the shortfalls to the last: measured
   // workgroup ends 229-324 us for a 253-us mean).  Problems may differ in k-blocks (levels of
   // different sample counts): a cut is a (problem, block) pair.
+  // The sequence is cut as ONE group (the default) or, bucket-aligned (aligned_), as one group per
+  // all-reduce bucket, workgroup w then taking its piece of every group: a bucket launch cuts its
+  // group exactly so, hence an unbucketed and a bucketed step form the same items.
   const int np = (int)P.size();
-  std::vector<int64_t> cum(np + 1, 0);
-  for (int i = 0; i < np; ++i) cum[i + 1] = cum[i] + cost[i] * pnblk[i];
-  const int64_t total = cum.back();
+  std::vector<std::vector<int>> groups;
+  if (aligned_ && bucket < 0) {
+    groups.resize(kBuckets);
+    for (int i = 0; i < np; ++i) groups[pbucket[i]].push_back(i);
+  } else {
+    groups.resize(1);
+    for (int i = 0; i < np; ++i) groups[0].push_back(i);
+  }
   const int G_wg = num_cu_;
-  auto mark = [&](int w) -> std::pair<int, int> {  // the cut before workgroup w
-    if (w >= G_wg) return {np, 0};
-    const double x = (double)total * w / G_wg;
-    int pi = 0;
-    while (pi + 1 < np && (double)cum[pi + 1] <= x) ++pi;
-    const int kb = (int)std::min<int64_t>(pnblk[pi], std::llround((x - (double)cum[pi]) / (double)cost[pi]));
-    return kb >= pnblk[pi] ? std::make_pair(pi + 1, 0) : std::make_pair(pi, kb);
-  };
-  std::vector<nof::WgItem> items;
-  std::vector<int> item_wg;
-  std::vector<int> first_item(np, -1), nitems(np, 0);
-  for (int w = 0; w < G_wg; ++w) {
-    std::pair<int, int> a = mark(w);
-    const std::pair<int, int> b = std::max(a, mark(w + 1));
-    while (a < b) {  // split the workgroup's range at problem boundaries
-      const int pi = a.first;
-      const int kb1 = b.first == pi ? b.second : pnblk[pi];
-      if (kb1 > a.second) {
-        nof::WgItem itm;
-        itm.prob = pi; itm.kb0 = a.second; itm.kb1 = kb1; itm.slab = (int)items.size();
-        if (first_item[pi] < 0) first_item[pi] = (int)items.size();
-        nitems[pi]++;
-        items.push_back(itm);
-        item_wg.push_back(w);
+  std::vector<std::vector<nof::WgItem>> wg_items(G_wg);
+  for (const std::vector<int>& grp : groups) {
+    const int ng = (int)grp.size();
+    if (ng == 0) continue;
+    std::vector<int64_t> cum(ng + 1, 0);
+    for (int j = 0; j < ng; ++j) cum[j + 1] = cum[j] + cost[grp[j]] * pnblk[grp[j]];
+    const int64_t total = cum.back();
+    auto mark = [&](int w) -> std::pair<int, int> {  // the cut before workgroup w: (group position, block)
+      if (w >= G_wg) return {ng, 0};
+      const double x = (double)total * w / G_wg;
+      int pj = 0;
+      while (pj + 1 < ng && (double)cum[pj + 1] <= x) ++pj;
+      const int nb = pnblk[grp[pj]];
+      const int kb = (int)std::min<int64_t>(nb, std::llround((x - (double)cum[pj]) / (double)cost[grp[pj]]));
+      return kb >= nb ? std::make_pair(pj + 1, 0) : std::make_pair(pj, kb);
+    };
+    for (int w = 0; w < G_wg; ++w) {
+      std::pair<int, int> a = mark(w);
+      const std::pair<int, int> b = std::max(a, mark(w + 1));
+      while (a < b) {  // split the workgroup's range at problem boundaries
+        const int pj = a.first, nb = pnblk[grp[pj]];
+        const int kb1 = b.first == pj ? b.second : nb;
+        if (kb1 > a.second) {
+          nof::WgItem itm;
+          itm.prob = grp[pj]; itm.kb0 = a.second; itm.kb1 = kb1; itm.slab = -1;
+          wg_items[w].push_back(itm);
+        }
+        a = kb1 >= nb ? std::make_pair(pj + 1, 0) : std::make_pair(pj, kb1);
       }
-      a = kb1 >= pnblk[pi] ? std::make_pair(pi + 1, 0) : std::make_pair(pi, kb1);
     }
   }
-  const int nwg = std::min(G_wg, item_wg.empty() ? 0 : item_wg.back() + 1);
+  // slabs numbered problem-major (k-blocks ascending within a problem): the reduce sums a problem's
+  // slabs first_item .. first_item + nitems - 1 in that order, whichever workgroup wrote them
+  std::vector<std::pair<std::pair<int, int>, nof::WgItem*>> order;
+  for (auto& v : wg_items)
+    for (nof::WgItem& it : v) order.push_back({{it.prob, it.kb0}, &it});
+  std::sort(order.begin(), order.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+  std::vector<int> first_item(np, -1), nitems(np, 0);
+  std::vector<int> slab_prob(order.size());
+  for (size_t i = 0; i < order.size(); ++i) {
+    nof::WgItem& it = *order[i].second;
+    it.slab = (int)i;
+    slab_prob[i] = it.prob;
+    if (first_item[it.prob] < 0) first_item[it.prob] = (int)i;
+    nitems[it.prob]++;
+  }
+  std::vector<nof::WgItem> items;
+  int nwg = 0;
+  for (int w = 0; w < G_wg; ++w)
+    if (!wg_items[w].empty()) nwg = w + 1;
   std::vector<int> item_ptr(nwg + 1, 0);
-  for (int w : item_wg) item_ptr[w + 1]++;
-  for (int w = 0; w < nwg; ++w) item_ptr[w + 1] += item_ptr[w];
-  std::vector<int64_t> slab_off(items.size());
+  for (int w = 0; w < nwg; ++w) {
+    for (const nof::WgItem& it : wg_items[w]) items.push_back(it);
+    item_ptr[w + 1] = (int)items.size();
+  }
+  std::vector<int64_t> slab_off(items.size());  // by slab index
   int64_t so = 0;
-  for (size_t i = 0; i < items.size(); ++i) {
+  for (size_t i = 0; i < slab_prob.size(); ++i) {
     slab_off[i] = so;
-    so += (int64_t)P[items[i].prob].ntr * 32 * P[items[i].prob].ntc * 32;
+    so += (int64_t)P[slab_prob[i]].ntr * 32 * P[slab_prob[i]].ntc * 32;
   }
   if ((size_t)so > slab_cap_ || items.size() * 256 > bias_slabs_.n) {  // grow (schedules are built once per M)
     NOF_HIP(hipStreamSynchronize(st_));

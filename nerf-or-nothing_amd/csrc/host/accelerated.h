@@ -117,7 +117,13 @@ class AcceleratedMLP {
   float* const* get_gradient_levels(const float* const* color_grads, const float* const* density_grads,
                                     uint32_t flags);
   static constexpr int kBuckets = 2;
-  void set_bucket_hook(nof_grad_bucket_fn fn, void* user) { hook_ = fn; hook_user_ = user; }
+  // a hook selects the bucket-aligned weight-gradient partition (nof_config.grad_buckets) for every
+  // launch of this model, so its unbucketed launches (earlier micro-batches) sum like the bucketed ones
+  void set_bucket_hook(nof_grad_bucket_fn fn, void* user) {
+    hook_ = fn;
+    hook_user_ = user;
+    aligned_ = fn != nullptr || cfg_.grad_buckets != 0;
+  }
   bool has_bucket_hook() const { return hook_ != nullptr; }
   // arena spans (offset, count) of bucket b: 0 = W5..W10; 1 = W0..W4 and every bias
   int bucket_spans(int b, int64_t* off, int64_t* cnt) const;
@@ -166,6 +172,7 @@ class AcceleratedMLP {
   void run_wgrad(Schedule& sc, int accumulate);
   float* const* wgrad_levels(int lv0, int lv1, int accumulate, bool buckets);
   nof_grad_bucket_fn hook_ = nullptr;
+  bool aligned_ = false;  // weight-gradient items cut per all-reduce bucket (nof_config.grad_buckets)
   void* hook_user_ = nullptr;
   void tb(int id) { if (timer) timer->begin(id); }
   void te(int id) { if (timer) timer->end(id); }

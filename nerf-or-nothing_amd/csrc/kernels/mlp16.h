@@ -80,10 +80,7 @@ __device__ __forceinline__ constexpr int feat16(int t, int g, int r) { return 16
 // forward's store_short pairs measured 3 % slower as nt; since its tiles go out as dwords
 // (BlkStore16H::store_pairs) nt is neutral for the forward and the weight-gradient launch runs 7 %
 // faster (f16x2 step -2.3 %), so every block store is nt.
-#ifndef NOF_DIAG_STORE_NT  // diagnostic override (tools/ab_write.sh: 0 = default policy)
-#define NOF_DIAG_STORE_NT 2
-#endif
-constexpr int kStoreNT = NOF_DIAG_STORE_NT;  // aux bit of the buffer-store builtins: nt
+constexpr int kStoreNT = 2;  // aux bit of the buffer-store builtins: nt
 struct BlkStore16 {
   static constexpr bool kHalf = false;
   uint32_t voff[4];

@@ -27,20 +27,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t h32_rsrc(const void* p) {
 // (nt) stores.  A/B on one box (round 3, tools/ab_multi.sh, per level): default policy fwd 0.188 / bwd
 // 0.175 / wgrad 0.286 ms; nt forward only 0.161 / 0.149 / 0.291; nt backward only 0.179 / 0.157 / 0.246;
 // both 0.151 / 0.142 / 0.207 ms (step 1.43 -> 1.13 ms): the default policy leaves the 1.2 GB of tiles
-// dirty in L2 / MALL and the write-back competes with the kernels that follow.  Diagnostic override:
-// bit 0 = forward, bit 1 = backward nt.
-#ifndef NOF_DIAG_H32_NTSTORE
-#define NOF_DIAG_H32_NTSTORE 3
-#endif
-constexpr int kFwdAux = (NOF_DIAG_H32_NTSTORE & 1) ? 2 : 0;  // side-output store cache policy
-constexpr int kBwdAux = (NOF_DIAG_H32_NTSTORE & 2) ? 2 : 0;
+// dirty in L2 / MALL and the write-back competes with the kernels that follow.
+constexpr int kFwdAux = 2;  // side-output store cache policy: nt
+constexpr int kBwdAux = 2;
 template <int aux>
 __device__ __forceinline__ void store_b64(__amdgpu_buffer_rsrc_t r, uint32_t voff, int imm, uint32_t lo, uint32_t hi) {
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-#ifdef NOF_DIAG_H32_NOSTORE  // diagnostic: no side-output stores (keeps one dependency so nothing is dead)
-  if (lo == 0x7fff1234u && hi == 0x1234u) __builtin_amdgcn_raw_buffer_store_b64((u32x2{lo, hi}), r, (int)voff, imm, aux);
-  return;
-#endif
   __builtin_amdgcn_raw_buffer_store_b64((u32x2{lo, hi}), r, (int)voff, imm, aux);
 }
 // 16-B store: the data registers stay untouched for two wait states after the store issues — measured:
@@ -48,10 +40,6 @@ __device__ __forceinline__ void store_b64(__amdgpu_buffer_rsrc_t r, uint32_t vof
 // (nondeterministic act_h9 tiles; the compiler inserted no wait state for this >8-byte store-data hazard)
 template <int aux>
 __device__ __forceinline__ void store_b128(__amdgpu_buffer_rsrc_t r, uint32_t voff, int imm, const u32x4& v) {
-#ifdef NOF_DIAG_H32_NOSTORE
-  asm volatile("" ::"v"(v));
-  return;
-#endif
   __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, imm, aux);
   asm volatile("s_nop 1" ::"v"(v) : "memory");
 }

@@ -24,11 +24,11 @@
 // element j is taken to be feature kfeat(kk, h, j) = 16 kk + 8 (j >> 2) + 4h + (j & 3) — and the packed
 // weight fragments (k_pack_weights_h32) follow that order.
 //
-// Weights stream through a 4-slot LDS ring of 16-KB periods (16 one-KB k-step fragments) by
+// Weights stream through an 8-slot LDS ring of 16-KB periods (16 one-KB k-step fragments) by
 // LDS-DMA; every layer is a whole number of periods, so the DMA / barrier schedule is the same in
-// every layer: period P + 2 is fetched at positions 0 and 1 of period P (into the slot period P - 2
-// left), and the barrier ending period P waits for period P + 1 with a counted vmcnt that lets the
-// period's own DMA and side-output stores stay in flight.
+// every layer: period P + kDmaAhead (6) is fetched during period P (into the slot period P - 2 left),
+// and the barrier ending period P waits for period P + 1 with a counted vmcnt that lets the later
+// periods' DMA and this period's side-output stores stay in flight.
 //
 // Side outputs: activation / delta buffers are [M/32 blocks][F/32 tiles] of 2-KB fp16 tiles in the
 // slot layout below (slot_off) — exactly the epilogue's registers, two contiguous 1-KB stores per tile
@@ -99,9 +99,6 @@ __device__ __forceinline__ uint32_t relu_pk(uint32_t p) {
 // shift one mask bit per half into w: w = 2w + min(relu'd half, 1) (inline asm: the compiler turns the
 // packed min into two compares, two selects and a perm)
 __device__ __forceinline__ uint32_t mask_shift(uint32_t w, uint32_t relu) {
-#ifdef NOF_DIAG_H32_NOMASK  // diagnostic: no mask bits (results garbage)
-  return w ^ relu;
-#endif
   uint32_t b, r;
   asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(b) : "v"(relu));
   asm("v_pk_mad_u16 %0, %1, 2, %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(w), "v"(b));
@@ -131,17 +128,10 @@ __device__ __forceinline__ void h32_barrier(int n) {
   }
 #undef NOF_H32_BAR
 }
-#ifdef NOF_DIAG_H32_NOBAR  // diagnostic: the period barrier without s_barrier
-#define h32_barrier(n) asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
-#endif
 
 // The weight ring.  `next` = stream position of period P + kDmaAhead while period P is consumed from
 // slot `cur`.
-#ifdef NOF_DIAG_H32_NOSTAGGER
-constexpr int kDmaLatePos = 0;
-#else
 constexpr int kDmaLatePos = 8;
-#endif
 struct H32Ring {
   float* lds;
   const float* next;
@@ -160,15 +150,9 @@ struct H32Ring {
     early = kDmaLatePos == 0 || __builtin_amdgcn_readfirstlane(tid >> 6) < 4;
   }
   __device__ __forceinline__ void dma(int step, int tid) {
-#ifdef NOF_DIAG_H32_NODMA  // diagnostic builds only (timings; results are garbage)
-    return;
-#endif
     slice16_dma_step(next, lds + ((cur + kDmaAhead) & (kH32Slots - 1)) * kPeriodFloats, tid, step);
   }
   __device__ __forceinline__ void end_period(int nstores) {
-#ifdef NOF_DIAG_H32_NOWAIT  // diagnostic: the period barrier does not wait for the DMA (results garbage)
-    nstores = 31;
-#endif
     h32_barrier(2 * (kDmaAhead - 1) + nstores);
     cur = (cur + 1) & (kH32Slots - 1);
     next += kPeriodFloats;
@@ -185,11 +169,7 @@ __device__ __forceinline__ void h32_prologue_barrier() { h32_barrier(2 * (kDmaAh
 // tile's row stores, the layer's mask store (last tile), the C-operand load of the next chunk.
 __host__ __device__ constexpr int epi_valu_pos(int d, int nk) { return nk >= 16 ? d : d >> 1; }
 // tile half s (packed dwords 4s .. 4s + 3) goes out one k-step after its last dword is computed
-#ifdef NOF_DIAG_H32_NOROWS  // diagnostic: no side-output tile stores (results garbage)
-__host__ __device__ constexpr int epi_half_pos(int s, int nk) { return 99; }
-#else
 __host__ __device__ constexpr int epi_half_pos(int s, int nk) { return nk >= 16 ? 4 + 4 * s : 2 + 2 * s; }
-#endif
 __host__ __device__ constexpr int epi_mask_pos(int nk) { return nk >= 16 ? 9 : 5; }
 __host__ __device__ constexpr int cinit_pos(int nk) { return nk >= 16 ? 12 : nk - 1; }
 
@@ -282,12 +262,8 @@ __device__ __forceinline__ void h32_layer(const BSrc& bsrc, f32x16 (&acc)[2], H3
     uint32_t b[4];
     bsrc(kk, b);
     acc[c & 1] = mfma_h32(fr[i % R], b, (kk == 0 && !kBias) ? f32x16{} : acc[c & 1]);
-#ifndef NOF_DIAG_H32_NOEPI  // diagnostic: no epilogue at all (results garbage)
     if constexpr (c == 0) nst += prev.piece(Prev::kNC - 1, kk, NK);  // the previous layer's last tile (acc[1])
     else nst += epi.piece(c - 1, kk, NK);
-#else
-    if constexpr (kk == 0) asm volatile("" ::"v"(acc[(c + 1) & 1][0]));  // keeps the MFMAs alive
-#endif
     if constexpr (kBias && c + 1 < NC && kk == cinit_pos(NK)) acc[(c + 1) & 1] = cinit_load(cv, c + 1);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (pos == kBarrierPos) {  // the next period's reads start at the next position

@@ -14,6 +14,7 @@
 #include "common.h"
 #include "launch.h"
 #include "mlp_common.h"
+#include "stamps.h"
 
 namespace nof {
 
@@ -179,38 +180,6 @@ __device__ __forceinline__ void wg_item(const WgItem& item, const WgProblem& P, 
   __syncthreads();  // LDS ring reused by the next item
 }
 
-#ifdef NOF_DIAG_WG_TIME  // per-workgroup wall-clock start/end of the last k_wgrad / k_wgrad_h launch
-__device__ unsigned long long g_wg_times[2][1024][2];
-#define NOF_WG_T0(k) const unsigned long long wg_t0_ = wall_clock64();
-#define NOF_WG_T1(k)                                                                   \
-  __syncthreads();                                                                     \
-  if (threadIdx.x == 0 && blockIdx.x < 1024) {                                         \
-    g_wg_times[k][blockIdx.x][0] = wg_t0_;                                             \
-    g_wg_times[k][blockIdx.x][1] = wall_clock64();                                     \
-  }
-__device__ unsigned long long g_item_times[2][4096][4];  // t0, t1, problem, k-blocks
-#define NOF_IT_T0(k) const unsigned long long it_t0_ = wall_clock64();
-#define NOF_IT_T1(k)                                                                 \
-  if (threadIdx.x == 0 && it < 4096) {                                               \
-    g_item_times[k][it][0] = it_t0_;                                                 \
-    g_item_times[k][it][1] = wall_clock64();                                         \
-    g_item_times[k][it][2] = item.prob | (blockIdx.x << 16);                         \
-    g_item_times[k][it][3] = item.kb1 - item.kb0;                                    \
-  }
-extern "C" int nof_diag_item_times(unsigned long long* host, int kernel) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_item_times), sizeof(unsigned long long) * 16384,
-                                  sizeof(unsigned long long) * 16384 * kernel, hipMemcpyDeviceToHost);
-}
-extern "C" int nof_diag_wg_times(unsigned long long* host, int kernel) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wg_times), sizeof(unsigned long long) * 2048,
-                                  sizeof(unsigned long long) * 2048 * kernel, hipMemcpyDeviceToHost);
-}
-#else
-#define NOF_WG_T0(k)
-#define NOF_WG_T1(k)
-#define NOF_IT_T0(k)
-#define NOF_IT_T1(k)
-#endif
 
 __global__ __launch_bounds__(kWgThreads, 1) void k_wgrad(const WgProblem* __restrict__ probs,
                                                          const WgItem* __restrict__ items,
@@ -720,11 +689,7 @@ __device__ __forceinline__ void wg_item_s(const WgItem& item, const WgProblem& P
 #pragma unroll
     for (int i = 0; i < ND; ++i) {
       const char* src = tsrc[i] + (int64_t)k * tstr[i] + lane * 16;
-#ifndef NOF_DIAG_WS_NODMA
       __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(stage + tdst[i]), 16, 0, kWsAux);
-#else
-      asm volatile("" ::"s"(src), "s"(stage + tdst[i]));
-#endif
     }
   };
   f32x16 acc[RB][CB];
@@ -744,13 +709,8 @@ __device__ __forceinline__ void wg_item_s(const WgItem& item, const WgProblem& P
   // read has its own output and the fragments are assembled after the wait)
   auto frag = [&](uint32_t stage_b, int tile, s16x4v& lo, s16x4v& hi) {
     const uint32_t a = stage_b + (uint32_t)(tile * 2048 + toff);
-#if defined(NOF_DIAG_WS_NOREAD)
-    lo = s16x4v{(short)a, 0, 0, 0};
-    hi = lo;
-#else
     asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a));
     asm volatile("ds_read_b64_tr_b16 %0, %1 offset:128" : "=v"(hi) : "v"(a));
-#endif
   };
   struct Frags { s16x4v al[RB], ah[RB], bl[CB], bh[CB]; };
   auto issue = [&](int slot, int ks, Frags& f) {  // k-step ks (samples 16 ks ..) of the block in `slot`
@@ -779,11 +739,7 @@ __device__ __forceinline__ void wg_item_s(const WgItem& item, const WgProblem& P
     for (int r = 0; r < RB; ++r)
 #pragma unroll
       for (int c = 0; c < CB; ++c)
-#ifdef NOF_DIAG_WS_NOMFMA
-        acc[r][c][0] += (float)fa[r][0] * (float)fb[c][1];
-#else
         acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[r], fb[c], acc[r][c], 0, 0, 0);
-#endif
     // bias partials: row sums of delta, row tile rowt[wc] on wave column wc (spread over the four SIMDs;
     // a wave-uniform select, no branch): four packed dot products with ones per k-step
     if (wc < RB) {
@@ -923,7 +879,7 @@ int wgrad_shape(int ntr, int ntc, int* cost2) {
   return best;
 }
 
-// Calibrated k_wgrad cost of one k-block (per-item timings of NOF_DIAG_WG_TIME builds,
+// Calibrated k_wgrad cost of one k-block (per-item timings of stamps builds, make STAMPS=1,
 // tools/diag_item_time.py: 7.82 / 3.08 / 4.99 / 1.00 us per block for the (8,8) / (8,3) / (5,8) /
 // (4,1),(1,4) tile problems): the busiest SIMD's MFMA tiles, 2-5 % dearer per tile for the narrow
 // shapes (more fragment reads per MFMA), or the staging latency that bounds the 1-tile-wide problems.

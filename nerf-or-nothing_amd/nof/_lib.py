@@ -36,7 +36,7 @@ class nof_config(C.Structure):
         ("skip_layer", C.c_int32), ("min_deg_point", C.c_int32), ("max_deg_point", C.c_int32),
         ("deg_view", C.c_int32), ("randomized", C.c_int32), ("white_bkgd", C.c_int32),
         ("resample_padding", C.c_float), ("coarse_loss_mult", C.c_float),
-        ("seed", C.c_uint64), ("stream", C.c_void_p), ("precision", C.c_int32),
+        ("seed", C.c_uint64), ("stream", C.c_void_p), ("precision", C.c_int32), ("grad_buckets", C.c_int32),
     ]
 
 

@@ -9,7 +9,8 @@ micro-batch accumulation and the one-call nof_dp_train_step all run for real bef
   * after Adam every replica holds bitwise-identical parameters;
   * nof_dp_train_step at N = 1 == the Python Trainer bit for bit, and at K = 2 == the same step
     emulated in Python (two shard gradients added by torch, Adam) bit for bit;
-  * bin/nof_train --gpus 2 --dp loopback [--attach] [--micro-batch] == --gpus 1 to fp32 accuracy.
+  * bin/nof_train --gpus 2 --dp loopback [--micro-batch] == --gpus 1 to fp32 accuracy, and --attach ==
+    the grouped all-reduce bit for bit (bucket-aligned weight-gradient items, nof_config.grad_buckets).
 """
 import os
 import subprocess
@@ -35,11 +36,11 @@ def _records(n, seed):
     return synth.pack_records(r)
 
 
-def _models(k, max_rays, precision=0):
+def _models(k, max_rays, precision=0, grad_buckets=0):
     import nof
 
-    ms = [nof.AcceleratedMipNeRF(seed=SEED, max_rays=max_rays, num_samples=SAMPLES, precision=precision)
-          for _ in range(k)]
+    ms = [nof.AcceleratedMipNeRF(seed=SEED, max_rays=max_rays, num_samples=SAMPLES, precision=precision,
+                                 grad_buckets=grad_buckets) for _ in range(k)]
     return ms, [nof.AcceleratedAdamOptimizer(m.GetLayerSizes(), m.config) for m in ms]
 
 
@@ -167,8 +168,10 @@ def test_train_step_loopback_k2_matches_emulation(gpu, micro, attach):
     sh = B // K
     mb = micro or sh
     ds_py = nof.RayDataset(records=_records(3000, 9))
-    ms_py, ad_py = _models(K, mb)
-    ms, ad = _models(K, mb)
+    # bucket-aligned weight-gradient items (nof_config.grad_buckets; an attached model selects them): the
+    # unbucketed emulation then sums every gradient element exactly as the bucketed launches do
+    ms_py, ad_py = _models(K, mb, grad_buckets=1)
+    ms, ad = _models(K, mb, grad_buckets=1)
     dss = [nof.RayDataset(records=_records(3000, 9)) for _ in range(K)]
     dps = NativeDP.init_loopback(K, 0)
     if attach:
@@ -198,12 +201,7 @@ def test_train_step_loopback_k2_matches_emulation(gpu, micro, attach):
                 o.step(m.mlp.allParams, m.mlp.allGradients, lr)
             torch.cuda.synchronize()
             for r in range(K):
-                want = _flat(ms_py[r], "p")
-                got = _flat(ms[r], "p")
-                if attach:  # the bucketed weight-gradient launches sum the split-K partials in another order
-                    assert rel_l2(got, want) <= 1e-6
-                else:
-                    assert np.array_equal(got, want), f"replica {r} step {step}"
+                assert np.array_equal(_flat(ms[r], "p"), _flat(ms_py[r], "p")), f"replica {r} step {step}"
             assert np.array_equal(_flat(ms[0], "p"), _flat(ms[1], "p"))
     finally:
         for d in dps:
@@ -214,17 +212,24 @@ def test_train_step_loopback_k2_matches_emulation(gpu, micro, attach):
             m.close()
 
 
-@pytest.mark.parametrize("extra", [[], ["--attach"], ["--micro-batch", 64]])
-def test_native_driver_loopback_equals_one_replica(gpu, tmp_path, extra):
+@pytest.mark.parametrize("micro", [[], ["--micro-batch", 64]])
+def test_native_driver_loopback_equals_one_replica(gpu, tmp_path, micro):
+    """--gpus 2 --dp loopback == --gpus 1 to fp32 accuracy (the shards' sums add in another order), and
+    --attach (bucketed all-reduce through the hook) == the grouped all-reduce BIT FOR BIT: a data-parallel
+    driver cuts the weight-gradient items per bucket (nof_config.grad_buckets)."""
     path = tmp_path / "train.bin"
     _records(4000, 13).tofile(path)
     common = [EXE, "--records", path, "--batch", 256, "--seed", 77, "--print-every", 0, "--steps", 3]
     run = lambda *a: subprocess.run([str(x) for x in (*common, *a)], capture_output=True, text=True, timeout=120)
     one = run("--gpus", 1, "--dump-params", tmp_path / "p1.bin")
     assert one.returncode == 0, one.stderr[-2000:]
-    two = run("--gpus", 2, "--dp", "loopback", *extra, "--dump-params", tmp_path / "p2.bin")
-    assert two.returncode == 0, two.stderr[-2000:]
-    assert "parameters identical on 2 devices" in two.stdout  # the driver's own replica check
     p1 = np.fromfile(tmp_path / "p1.bin", np.float32)
-    p2 = np.fromfile(tmp_path / "p2.bin", np.float32)
-    assert rel_l2(p2, p1) <= 1e-6
+    p2 = {}
+    for mode in ("grouped", "attach"):
+        extra = list(micro) + (["--attach"] if mode == "attach" else [])
+        two = run("--gpus", 2, "--dp", "loopback", *extra, "--dump-params", tmp_path / f"p2{mode}.bin")
+        assert two.returncode == 0, two.stderr[-2000:]
+        assert "parameters identical on 2 devices" in two.stdout  # the driver's own replica check
+        p2[mode] = np.fromfile(tmp_path / f"p2{mode}.bin", np.float32)
+        assert rel_l2(p2[mode], p1) <= 1e-6
+    assert np.array_equal(p2["attach"], p2["grouped"]), "attached and grouped data parallelism differ"

@@ -1,0 +1,80 @@
+"""Timing experiments on modified kernels, built from a PATCHED COPY of the product tree (the product
+sources carry no diagnostic switches).
+
+    python tools/diag/variant.py NAME EDIT [EDIT ...]   ->  build_diag/NAME/nerf-or-nothing_amd/lib/libnof.so
+    NOF_LIB=$PWD/build_diag/NAME/nerf-or-nothing_amd/lib/libnof.so python bench.py ...
+
+Each EDIT names a list of exact string replacements (EDITS below); an edit whose anchor no longer
+occurs exactly once fails loudly instead of building something else.  Most edits REMOVE work (weight
+DMA, side-output stores, epilogues, MFMAs): their results are garbage and only their timings mean
+anything (tools/ab_multi.sh, tools/diag_lib.sh).
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+K = "csrc/kernels/"
+
+EDITS = {
+    # F16 forward / backward (mlp_h32.h, mlp_f16.hip)
+    "h32_nodma": [(K + "mlp_h32.h",
+                   "    slice16_dma_step(next, lds + ((cur + kDmaAhead) & (kH32Slots - 1)) * kPeriodFloats, tid, step);",
+                   "    (void)step; (void)tid;")],
+    "h32_nostore": [(K + "mlp_f16.hip",
+                     "  __builtin_amdgcn_raw_buffer_store_b64((u32x2{lo, hi}), r, (int)voff, imm, aux);",
+                     "  if (lo == 0x7fff1234u && hi == 0x1234u) __builtin_amdgcn_raw_buffer_store_b64((u32x2{lo, hi}), r, (int)voff, imm, aux);"),
+                    (K + "mlp_f16.hip",
+                     "  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, imm, aux);\n  asm volatile(\"s_nop 1\" ::\"v\"(v) : \"memory\");",
+                     "  asm volatile(\"\" ::\"v\"(v));")],
+    "h32_noepi": [(K + "mlp_h32.h",
+                   "    if constexpr (c == 0) nst += prev.piece(Prev::kNC - 1, kk, NK);  // the previous layer's last tile (acc[1])\n"
+                   "    else nst += epi.piece(c - 1, kk, NK);",
+                   "    if constexpr (kk == 0) asm volatile(\"\" ::\"v\"(acc[(c + 1) & 1][0]));")],
+    "h32_nostagger": [(K + "mlp_h32.h", "constexpr int kDmaLatePos = 8;", "constexpr int kDmaLatePos = 0;")],
+    # side-output store cache policy: default instead of nt (fp32 / fp16-block kernels and F16)
+    "store_default": [(K + "mlp16.h", "constexpr int kStoreNT = 2;", "constexpr int kStoreNT = 0;"),
+                      (K + "mlp_f16.hip", "constexpr int kFwdAux = 2;", "constexpr int kFwdAux = 0;"),
+                      (K + "mlp_f16.hip", "constexpr int kBwdAux = 2;", "constexpr int kBwdAux = 0;")],
+    # F16 weight gradients (k_wgrad_s)
+    "ws_nodma": [(K + "wgrad.hip",
+                  "      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(stage + tdst[i]), 16, 0, kWsAux);",
+                  "      asm volatile(\"\" ::\"s\"(src), \"s\"(stage + tdst[i]));")],
+    "ws_noread": [(K + "wgrad.hip",
+                   "    asm volatile(\"ds_read_b64_tr_b16 %0, %1\" : \"=v\"(lo) : \"v\"(a));\n"
+                   "    asm volatile(\"ds_read_b64_tr_b16 %0, %1 offset:128\" : \"=v\"(hi) : \"v\"(a));",
+                   "    lo = s16x4v{(short)a, 0, 0, 0};\n    hi = lo;")],
+    "ws_nomfma": [(K + "wgrad.hip",
+                   "        acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[r], fb[c], acc[r][c], 0, 0, 0);",
+                   "        acc[r][c][0] += (float)fa[r][0] * (float)fb[c][1];")],
+}
+
+
+def build(name, edits):
+    dst = os.path.join(ROOT, "build_diag", name)
+    if os.path.exists(dst):
+        shutil.rmtree(dst)
+    pkg = os.path.join(dst, "nerf-or-nothing_amd")
+    os.makedirs(pkg)
+    shutil.copytree(os.path.join(ROOT, "include"), os.path.join(dst, "include"))
+    shutil.copytree(os.path.join(ROOT, "nerf-or-nothing_amd", "csrc"), os.path.join(pkg, "csrc"))
+    shutil.copy(os.path.join(ROOT, "nerf-or-nothing_amd", "Makefile"), pkg)
+    for e in edits:
+        for rel, old, new in EDITS[e]:
+            p = os.path.join(pkg, rel)
+            s = open(p).read()
+            if s.count(old) != 1:
+                raise SystemExit(f"edit {e}: anchor occurs {s.count(old)} times in {rel}")
+            open(p, "w").write(s.replace(old, new))
+    jobs = str(min(16, os.cpu_count() or 8))
+    subprocess.check_call(["make", "-j", jobs, "-C", pkg, "lib/libnof.so"], stdout=subprocess.DEVNULL)
+    out = os.path.join(pkg, "lib", "libnof.so")
+    print(out)
+    return out
+
+
+if __name__ == "__main__":
+    if len(sys.argv) < 3 or any(e not in EDITS for e in sys.argv[2:]):
+        raise SystemExit(__doc__ + "\nedits: " + ", ".join(EDITS))
+    build(sys.argv[1], sys.argv[2:])

@@ -1,7 +1,7 @@
-"""Diagnostic (NOF_DIAG_WG_TIME builds): per-item durations of the last weight-gradient launch,
+"""Diagnostic (stamps builds: make STAMPS=1 -> lib/libnof_stamps.so): per-item durations of the last weight-gradient launch,
 fitted per problem as overhead + cost per k-block (calibration data for the host's item schedule),
 and the slowest workgroups with their items and XCD (blockIdx % 8).
-usage: NOF_LIB=.../libnof_wgt.so python tools/diag_item_time.py f32|f16x2|f16"""
+usage: NOF_LIB=$PWD/nerf-or-nothing_amd/lib/libnof_stamps.so python tools/diag_item_time.py f32|f16x2|f16"""
 import ctypes as C, os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

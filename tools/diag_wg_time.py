@@ -1,6 +1,6 @@
-"""Diagnostic (NOF_DIAG_WG_TIME builds): per-workgroup start/end spread of the last weight-gradient
+"""Diagnostic (stamps builds: make STAMPS=1 -> lib/libnof_stamps.so): per-workgroup start/end spread of the last weight-gradient
 launch — how well the host's cost-balanced item schedule finishes all CUs together.
-usage: NOF_LIB=.../libnof_wgt.so python tools/diag_wg_time.py f32|f16x2"""
+usage: NOF_LIB=$PWD/nerf-or-nothing_amd/lib/libnof_stamps.so python tools/diag_wg_time.py f32|f16x2"""
 import ctypes as C, os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -1,7 +1,7 @@
 """Timing experiments on modified kernels, built from a PATCHED COPY of the product tree (the product
 sources carry no diagnostic switches).
 
-    python tools/diag/variant.py NAME EDIT [EDIT ...]   ->  build_diag/NAME/nerf-or-nothing_amd/lib/libnof.so
+    python tools/diag/variant.py NAME [EDIT ...]   ->  build_diag/NAME/nerf-or-nothing_amd/lib/libnof.so
     NOF_LIB=$PWD/build_diag/NAME/nerf-or-nothing_amd/lib/libnof.so python bench.py ...
 
 Each EDIT names a list of exact string replacements (EDITS below); an edit whose anchor no longer
@@ -118,6 +118,6 @@ def build(name, edits):
 
 
 if __name__ == "__main__":
-    if len(sys.argv) < 3 or any(e not in EDITS for e in sys.argv[2:]):
+    if len(sys.argv) < 2 or any(e not in EDITS for e in sys.argv[2:]):
         raise SystemExit(__doc__ + "\nedits: " + ", ".join(EDITS))
     build(sys.argv[1], sys.argv[2:])

@@ -82,6 +82,7 @@ hipError_t launch_mlp_bwd16(const BwdArgs& a, hipStream_t st);
 // F16 mode (mlp_h32.h, mlp_f16.hip): 32 samples per wave on 32x32x16 f16, row-chunk-outer layers;
 // activations / deltas as row-major [M][F] fp16, wimg / wimg_b the h32 images
 hipError_t launch_mlp_fwd_h32(const FwdArgs& a, hipStream_t st);
+int device_cus();  // compute units of the current device (persistent grids)
 hipError_t launch_mlp_bwd_h32(const BwdArgs& a, hipStream_t st);
 
 // ---- wgrad.hip: weight/bias gradients as one scheduled split-K launch + ordered reduce ------

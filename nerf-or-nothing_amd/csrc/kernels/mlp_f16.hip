@@ -191,27 +191,113 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   constexpr int kDirb = kBias + 8 * 256;          // per-wave view-direction bias [8][128]
   constexpr int kW8 = kDirb + kH32Waves * 128;    // packed w8 [8][2][8]
   constexpr int kW10 = kW8 + 128;                 // packed W10 [3][4][2][8]
-  __shared__ __attribute__((aligned(16))) float lds[kW10 + 192];
+  constexpr int kW9d = kW10 + 192;                // W9[:, 256:283] transposed [27][128], then b9 [128]
+  __shared__ __attribute__((aligned(16))) float lds[kW9d + (kDirIn + 1) * 128];
   const int tid = threadIdx.x, lane = tid & 63, x = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nblk = a.M / kBlk;
-  const int blk_raw = blockIdx.x * kH32Waves + wave;
-  const int blk = blk_raw < nblk ? blk_raw : nblk - 1;  // tail waves duplicate the last block
-  const int m0 = blk * kBlk, ray = m0 / a.S;
-  const int m = m0 + x;
-  NOF_DCHECK(a.M % kBlk == 0 && a.S % kBlk == 0 && blk >= 0 && blk < nblk, kChkMlpBlock);
+  const int ngroups = (nblk + kH32Waves - 1) / kH32Waves;  // 256 samples (8 blocks) per group
+  NOF_DCHECK(a.M % kBlk == 0 && a.S % kBlk == 0, kChkMlpBlock);
   const float* tail = a.wimg + kFwdH32Floats;
 
   H32Ring ring;
   ring.lds = lds;
-  ring.prologue(a.wimg, tid);  // periods 0 and 1 in flight while the encodings are computed
+  ring.prologue(a.wimg, kFwdFrags * kFragFloats, tid);  // the first periods land while the encodings run
+
+  // ---- LDS tables, the same for every group: trunk biases, packed w8 / W10 -------------------------
+  for (int i = tid; i < 2048 / 4; i += kH32Threads)
+    *reinterpret_cast<f32x4*>(lds + kBias + 4 * i) = *reinterpret_cast<const f32x4*>(tail + kFwdTailBias + 4 * i);
+  if (tid < 128 + 192) {  // packed pairs of features 32T + 8(d >> 1) + 4hh + 2(d & 1) + {0, 1}
+    const bool is8 = tid < 128;  // w8 [T][hh][d] | W10 [c][T][hh][d]
+    const int i = is8 ? tid : tid - 128;
+    const int d = i & 7, hh = (i >> 3) & 1, T = (i >> 4) & (is8 ? 7 : 3), c = is8 ? 0 : i >> 6;
+    const int f = 32 * T + 8 * (d >> 1) + 4 * hh + 2 * (d & 1);
+    const float* src = is8 ? tail + kFwdTailW8 : tail + kFwdTailW10 + c * 128;
+    reinterpret_cast<uint32_t*>(lds + (is8 ? kW8 : kW10))[i] = pk_h(src[f], src[f + 1]);
+  }
+  // the view layer's direction columns, feature-major so that the 64 lanes of a wave (64 outputs) read 64
+  // consecutive words: every group's direction bias from LDS, not from global memory (a global load would
+  // wait, in vmcnt order, for the weight DMA in flight)
+  for (int i = tid; i < (kDirIn + 1) * 128; i += kH32Threads) {
+    const int k = i >> 7, o = i & 127;
+    lds[kW9d + i] = k < kDirIn ? tail[kFwdTailW9d + o * 32 + k] : tail[kFwdTailBias + 9 * 256 + o];
+  }
+  const uint32_t vrow = slot_off(x, h);  // (sample x, lane half h): its 16-B slot in a tile half
+  const uint32_t moff = (uint32_t)lane * 16u;
+  const size_t lstride = (size_t)nblk * kBlk * kWidth;  // halves per act_h layer
+  const float* bias_h = lds + kBias + 4 * h;
+  const uint32_t* w8h = reinterpret_cast<const uint32_t*>(lds + kW8) + 8 * h;
+  // VMEM instructions a group issues outside the layers (ring.add_ops: a lower bound): the act_in tiles (8)
+  // and, after the first group, its predecessor's last view tile (two halves and the mask) and heads (sigma,
+  // rgb — perhaps one store —, zhead)
+  constexpr int kFirstOps = kStore ? 8 : 0;
+  constexpr int kGroupOps = kStore ? 8 + 3 + 3 : 2;
+
+  // Persistent: workgroup b runs groups b, b + G, ...; the weight ring streams on across groups (it wraps
+  // to the stream start), so only the first group waits for a ring fill and builds the tables.
+  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+  const bool first = g == (int)blockIdx.x;
+  const int blk_raw = g * kH32Waves + wave;
+  const int blk = blk_raw < nblk ? blk_raw : nblk - 1;  // tail waves duplicate the last block
+  const int m0 = blk * kBlk, ray = m0 / a.S;
+  const int m = m0 + x;
+  NOF_DCHECK(blk >= 0 && blk < nblk, kChkMlpBlock);
+  float d3[3];
+  d3[0] = a.dirs[3 * ray]; d3[1] = a.dirs[3 * ray + 1]; d3[2] = a.dirs[3 * ray + 2];
+  const void* masks_blk = a.masks + (size_t)blk * kMaskSlots * 256;
+  const __amdgpu_buffer_rsrc_t rin = h32_rsrc(reinterpret_cast<const _Float16*>(a.act_in) + (size_t)m0 * kInF);
+  // ---- view PE of the wave's ray: lane k < 27 evaluates feature k, every lane reads them back as scalars;
+  // first the direction bias and the act_in view-PE tile (pe dies before the IPE's registers go live)
+  {
+    const int kl = lane < kDirIn ? lane : 0;
+    const float pe_l = a.encoded ? a.enc_dir[(size_t)ray * kDirIn + kl] : dir_feature(kl, d3);
+    float pe[kDirIn];
+#pragma unroll
+    for (int k = 0; k < kDirIn; ++k) pe[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pe_l), k));
+    // (the memory clobber also keeps the table's loads inside the loop: hoisted out of it, its 3 456
+    // values would stay live across every group and spill)
+    if (first) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the W9 / b9 table written
+    else asm volatile("" ::: "memory");
+    float* dirb = lds + kDirb + wave * 128;  // b9 + W9[:, 256:283] . PE(d) (LDS; read by this wave only)
+#pragma unroll
+    for (int rep = 0; rep < 2; ++rep) {
+      const int o = lane + 64 * rep;
+      // the table through opaque reads: as plain loads the compiler keeps them live far beyond this use
+      // (256 VGPRs and 42 spilled)
+      const uint32_t base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(lds + kW9d + o);
+      float wv[kDirIn + 1];
+#pragma unroll
+      for (int k = 0; k <= kDirIn; ++k) asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(wv[k]) : "v"(base), "i"(k * 512));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // the reads' outputs are written asynchronously: each is (re)defined here, after the wait, so no copy
+      // of one can be scheduled before it has landed
+#pragma unroll
+      for (int k = 0; k <= kDirIn; ++k) asm volatile("" : "+v"(wv[k]));
+      float s = wv[kDirIn];
+#pragma unroll
+      for (int k = 0; k < kDirIn; ++k) s = __builtin_fmaf(wv[k], pe[k], s);
+      dirb[o] = s;
+    }
+    if constexpr (kStore) {  // act_in tile 3: view PE 96..122, zeros
+      uint32_t w[8];
+#pragma unroll
+      for (int d = 0; d < 8; ++d) {  // tile 3 feature 8 (d >> 1) + 4h + 2 (d & 1) + u = view PE feature of that index
+        float v[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int f0 = 8 * (d >> 1) + 2 * (d & 1) + u, f1 = f0 + 4;  // lane half h = 0 / 1
+          v[u] = h ? (f1 < kDirIn ? pe[f1 < kDirIn ? f1 : 0] : 0.0f) : (f0 < kDirIn ? pe[f0 < kDirIn ? f0 : 0] : 0.0f);
+        }
+        w[d] = pk_h(v[0], v[1]);
+      }
+      store_tile<kFwdAux>(rin, vrow, 3, w);
+    }
+  }
 
   // ---- encodings: lane h computes canonical IPE features 48h .. 48h + 47 of its sample -----------
   // packed pairs: ix[kk][e] = features c = kfeat(kk, 0, 2e) + {0, 1} (the B-fragment half h' = 0),
   // iy[kk][e] the half h' = 1, for k-steps 3h + kk
   uint32_t ix[3][4], iy[3][4];
-  float d3[3];
-  d3[0] = a.dirs[3 * ray]; d3[1] = a.dirs[3 * ray + 1]; d3[2] = a.dirs[3 * ray + 2];
   if (!a.encoded) {
     const float o3[3] = {a.origins[3 * ray], a.origins[3 * ray + 1], a.origins[3 * ray + 2]};
     const float* tr = a.t + (size_t)ray * (a.S + 1) + (m0 - ray * a.S) + x;
@@ -243,16 +329,6 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
         iy[kk][e] = pk_h(ep[c1], ep[c1 + 1]);
       }
   }
-  // view PE of the wave's ray: lane k < 27 evaluates feature k, every lane reads them back as scalars
-  const int kl = lane < kDirIn ? lane : 0;
-  const float pe_l = a.encoded ? a.enc_dir[(size_t)ray * kDirIn + kl] : dir_feature(kl, d3);
-  float pe[kDirIn];
-#pragma unroll
-  for (int k = 0; k < kDirIn; ++k) pe[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pe_l), k));
-
-  const uint32_t vrow = slot_off(x, h);  // (sample x, lane half h): its 16-B slot in a tile half
-  const uint32_t moff = (uint32_t)lane * 16u;
-  const void* masks_blk = a.masks + (size_t)blk * kMaskSlots * 256;
   // the B fragments of layers 0 / 4: k-steps 0..2 from the lane half h = 0, 3..5 from h = 1 — one
   // permlane32 swap per packed dword moves each half's other-h' pairs across (tools/probe/h32_probe.hip)
   uint32_t ipe[6][4];
@@ -265,57 +341,18 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
       ipe[kk + 3][e] = iy[kk][e];
     }
   }
-  if constexpr (kStore) {  // act_in: IPE 0..95 (k-steps 2t, 2t + 1 = the halves of tile t), view PE 96..122, zeros
-    const __amdgpu_buffer_rsrc_t r = h32_rsrc(reinterpret_cast<const _Float16*>(a.act_in) + (size_t)m0 * kInF);
+  if constexpr (kStore) {  // act_in: IPE 0..95 (k-steps 2t, 2t + 1 = the halves of tile t)
 #pragma unroll
     for (int k = 0; k < 6; ++k)
-      store_b128<kFwdAux>(r, vrow, (k >> 1) * 2048 + (k & 1) * 1024, u32x4{ipe[k][0], ipe[k][1], ipe[k][2], ipe[k][3]});
-    uint32_t w[8];
-#pragma unroll
-    for (int d = 0; d < 8; ++d) {  // tile 3 feature 8 (d >> 1) + 4h + 2 (d & 1) + u = view PE feature of that index
-      float v[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int f0 = 8 * (d >> 1) + 2 * (d & 1) + u, f1 = f0 + 4;  // lane half h = 0 / 1
-        v[u] = h ? (f1 < kDirIn ? pe[f1 < kDirIn ? f1 : 0] : 0.0f) : (f0 < kDirIn ? pe[f0 < kDirIn ? f0 : 0] : 0.0f);
-      }
-      w[d] = pk_h(v[0], v[1]);
-    }
-    store_tile<kFwdAux>(r, vrow, 3, w);
+      store_b128<kFwdAux>(rin, vrow, (k >> 1) * 2048 + (k & 1) * 1024, u32x4{ipe[k][0], ipe[k][1], ipe[k][2], ipe[k][3]});
   }
 
-  // ---- LDS tables: trunk biases, the wave's view-direction bias, packed w8 / W10 -------------------
-  for (int i = tid; i < 2048 / 4; i += kH32Threads)
-    *reinterpret_cast<f32x4*>(lds + kBias + 4 * i) = *reinterpret_cast<const f32x4*>(tail + kFwdTailBias + 4 * i);
-  {
-    float* dirb = lds + kDirb + wave * 128;
-#pragma unroll
-    for (int rep = 0; rep < 2; ++rep) {  // b9 + W9[:, 256:283] . PE(d)
-      const int o = lane + 64 * rep;
-      float s = tail[kFwdTailBias + 9 * 256 + o];
-      const float* w9 = tail + kFwdTailW9d + o * 32;
-#pragma unroll
-      for (int k = 0; k < kDirIn; ++k) s = __builtin_fmaf(w9[k], pe[k], s);
-      dirb[o] = s;
-    }
-  }
-  if (tid < 128 + 192) {  // packed pairs of features 32T + 8(d >> 1) + 4hh + 2(d & 1) + {0, 1}
-    const bool is8 = tid < 128;  // w8 [T][hh][d] | W10 [c][T][hh][d]
-    const int i = is8 ? tid : tid - 128;
-    const int d = i & 7, hh = (i >> 3) & 1, T = (i >> 4) & (is8 ? 7 : 3), c = is8 ? 0 : i >> 6;
-    const int f = 32 * T + 8 * (d >> 1) + 4 * hh + 2 * (d & 1);
-    const float* src = is8 ? tail + kFwdTailW8 : tail + kFwdTailW10 + c * 128;
-    reinterpret_cast<uint32_t*>(lds + (is8 ? kW8 : kW10))[i] = pk_h(src[f], src[f + 1]);
-  }
-  h32_prologue_barrier();  // tables written (lgkmcnt), periods 0 and 1 landed
+  if (first) h32_prologue_barrier();  // tables written (lgkmcnt), the first periods landed
 
   // ---- layers -------------------------------------------------------------------------------------
   f32x16 acc[2];
   uint32_t X[16][4], Y[16][4];
-  const size_t lstride = (size_t)nblk * kBlk * kWidth;  // halves per act_h layer
   const _Float16* act_h = reinterpret_cast<const _Float16*>(a.act_h) + (size_t)m0 * kWidth;
-  const float* bias_h = lds + kBias + 4 * h;
-  const uint32_t* w8h = reinterpret_cast<const uint32_t*>(lds + kW8) + 8 * h;
   uint32_t mwX[4], mwY[4], mwV[4], p8[8];
   FwdEpiH<kStore> eX(acc, X, mwX, vrow, moff), eY(acc, Y, mwY, vrow, moff);
   NoEpiH none;
@@ -336,6 +373,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
     for (int e = 0; e < 4; ++e) b[e] = kk < 16 ? Y[kk < 16 ? kk : 0][e] : ipe[kk >= 16 ? kk - 16 : 0][e];
   };
   eX.begin(act_h, masks_blk, 0, w8h, false);
+  ring.add_ops(first ? kFirstOps : kGroupOps);
   h32_layer<6, 8, true>(srcI, acc, ring, eX, none, bias_h, tid, lane);
   for (int it = 0; it < 2; ++it) {  // layers 1..3, (4), 5..7
     const int la = 1 + 4 * it;
@@ -371,6 +409,10 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
     for (int c = 0; c < 3; ++c) a.rgb[(size_t)m * 3 + c] = sigmoid_f(zc[c]) * kRgbScale - kRgbPadding;
     if constexpr (kStore) reinterpret_cast<f32x4*>(a.zhead)[m] = f32x4{zs, zc[0], zc[1], zc[2]};
   }
+  // the inference forward (no side outputs: the evaluation render) runs one group per workgroup — as a
+  // loop its live ranges spill at 256 VGPRs
+  if constexpr (!kStore) break;
+  }  // groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's trailing DMAs land before the LDS is released
 }
 
@@ -423,42 +465,66 @@ struct BwdEpiH {
 
 __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   constexpr int kW8 = kH32RingFloats;  // fp32 w8 in D-register order [8][2][16]
-  __shared__ __attribute__((aligned(16))) float lds[kW8 + 256];
+  constexpr int kW10 = kW8 + 256;      // fp32 W10 [3][128]
+  __shared__ __attribute__((aligned(16))) float lds[kW10 + 3 * 128];
   const int tid = threadIdx.x, lane = tid & 63, x = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nblk = a.M / kBlk;
-  const int blk_raw = blockIdx.x * kH32Waves + wave;
-  const int blk = blk_raw < nblk ? blk_raw : nblk - 1;
-  const int m0 = blk * kBlk, m = m0 + x;
-  NOF_DCHECK(a.M % kBlk == 0 && blk >= 0 && blk < nblk, kChkMlpBlock);
+  const int ngroups = (nblk + kH32Waves - 1) / kH32Waves;
+  NOF_DCHECK(a.M % kBlk == 0, kChkMlpBlock);
   const float* tail = a.wimg_b + kBwdH32Floats;
-  const uint32_t* masks_blk = a.masks + (size_t)blk * kMaskSlots * 256 + lane * 4;
 
   H32Ring ring;
   ring.lds = lds;
-  ring.prologue(a.wimg_b, tid);
-  if (tid < 256) {
+  ring.prologue(a.wimg_b, kBwdFrags * kFragFloats, tid);
+  if (tid < 256) {  // the tables, the same for every group
     const int T = tid >> 5, hh = (tid >> 4) & 1, r = tid & 15;
     lds[kW8 + tid] = tail[kBwdTailW8 + 32 * T + 8 * (r >> 2) + 4 * hh + (r & 3)];
   }
+  if (tid < 96) *reinterpret_cast<f32x4*>(lds + kW10 + 4 * tid) = *reinterpret_cast<const f32x4*>(tail + kBwdTailW10 + 4 * tid);
+  const uint32_t vrow = slot_off(x, h);
+  const size_t lstride = (size_t)nblk * kBlk * kWidth;
+  const float sc = delta_scale(a.amax, false);
+  // VMEM instructions a group issues outside the layers (ring.add_ops: a lower bound): the delta9x tiles
+  // (8 halves + the heads' 8 bytes) and, after the first group, its predecessor's last delta0 tile (two
+  // halves); the loads are not counted (the dsigma / drgb loads may be merged)
+  constexpr int kFirstOps = 9;
+  constexpr int kGroupOps = 9 + 2;
+
+  // Persistent: workgroup b runs groups b, b + G, ...; the weight ring streams on across groups.
+  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+  const bool first = g == (int)blockIdx.x;
+  const int blk_raw = g * kH32Waves + wave;
+  const int blk = blk_raw < nblk ? blk_raw : nblk - 1;
+  const int m0 = blk * kBlk, m = m0 + x;
+  NOF_DCHECK(blk >= 0 && blk < nblk, kChkMlpBlock);
+  const uint32_t* masks_blk = a.masks + (size_t)blk * kMaskSlots * 256 + lane * 4;
+  auto mask_of = [&](int l) { return *reinterpret_cast<const uint4*>(masks_blk + l * 256); };
 
   // ---- heads (MNcs:410-415), scaled by the level's power of two ---------------------------------------
+  // every load of the group first (the masks of layers 9, 7 and 6 too): vmcnt retires in issue order, so
+  // a load issued behind the delta9x stores would wait for them
   const f32x4 zh = reinterpret_cast<const f32x4*>(a.zhead)[m];
-  const float sc = delta_scale(a.amax, false);
-  const float dzs = a.dsigma[m] * sigmoid_f(zh[0] + kDensityBias) * sc;
+  const float ds_m = a.dsigma[m];
+  float dr[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) dr[c] = a.drgb[(size_t)m * 3 + c];
+  const uint4 mk9 = mask_of(8);
+  const uint4 mk7 = mask_of(7);
+  uint4 mk_next = mask_of(6);  // every later layer's mask words are loaded one layer before its begin()
+  const float dzs = ds_m * sigmoid_f(zh[0] + kDensityBias) * sc;
   float dzc[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const float s = sigmoid_f(zh[1 + c]);
-    dzc[c] = a.drgb[(size_t)m * 3 + c] * (s * (1.0f - s)) * kRgbScale * sc;
+    dzc[c] = dr[c] * (s * (1.0f - s)) * kRgbScale * sc;
   }
   // ---- delta9 = (W10^T dz_rgb) * relu'(layer 9) -> the B fragments of dh7, and delta9x ------------------
   uint32_t X[16][4], Y[16][4];
-  const uint32_t vrow = slot_off(x, h);
   const __amdgpu_buffer_rsrc_t d9 = h32_rsrc(reinterpret_cast<const _Float16*>(a.delta9x) + (size_t)m0 * kD9F);
   {
-    const uint4 mk9 = *reinterpret_cast<const uint4*>(masks_blk + 8 * 256);
-    const float* w10 = tail + kBwdTailW10;
+    if (first) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the W10 table written
+    const float* w10 = lds + kW10;
 #pragma unroll
     for (int T = 0; T < 4; ++T) {
       float v[16];
@@ -483,12 +549,10 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
     }
     if (h == 0) store_b64<kBwdAux>(d9, vrow, 4 * 2048, pk_h(dzs, dzc[0]), pk_h(dzc[1], dzc[2]));  // features 128..131
   }
-  h32_prologue_barrier();  // w8 table written, periods 0 and 1 landed
+  if (first) h32_prologue_barrier();  // w8 table written, the first periods landed
 
   f32x16 acc[2];
-  const size_t lstride = (size_t)nblk * kBlk * kWidth;
   const _Float16* delta = reinterpret_cast<const _Float16*>(a.delta) + (size_t)m0 * kWidth;
-  auto mask_of = [&](int l) { return *reinterpret_cast<const uint4*>(masks_blk + l * 256); };
   BwdEpiH eX(acc, X, vrow), eY(acc, Y, vrow);
   NoEpiH none;
   auto srcX = [&](int kk, uint32_t (&b)[4]) {
@@ -500,8 +564,8 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
     for (int e = 0; e < 4; ++e) b[e] = Y[kk][e];
   };
   // dh7 = W9[:, :256]^T delta9 + w8 dz_s ; delta7
-  uint4 mk_next = mask_of(6);  // every later layer's mask words are loaded one layer before its begin()
-  eY.begin(delta + 7 * lstride, mask_of(7), lds + kW8 + 16 * h, dzs);
+  eY.begin(delta + 7 * lstride, mk7, lds + kW8 + 16 * h, dzs);
+  ring.add_ops(first ? kFirstOps : kGroupOps);
   h32_layer<8, 8, false>(srcX, acc, ring, eY, none, nullptr, tid, lane);
   // dh_{l-1} = W_l[:, :256]^T delta_l ; delta_{l-1}, l = 7..2 in pairs, then l = 1
   for (int it = 0; it < 3; ++it) {
@@ -517,19 +581,30 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   h32_layer<16, 8, false>(srcY, acc, ring, eX, eY, nullptr, tid, lane);
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk) eX.piece(7, kk, 16);  // delta0's last tile
+  }  // groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+int device_cus() {  // compute units of the current device (cached per device)
+  static int cus[64] = {};
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return 256;
+  if (!cus[d] && hipDeviceGetAttribute(&cus[d], hipDeviceAttributeMultiprocessorCount, d) != hipSuccess) cus[d] = 256;
+  return cus[d];
 }
 
 hipError_t launch_mlp_fwd_h32(const FwdArgs& a, hipStream_t st) {
   const int nblk = a.M / kBlk;
-  const dim3 grid((nblk + kH32Waves - 1) / kH32Waves), block(kH32Threads);
-  if (a.no_store) hipLaunchKernelGGL(k_mlp_fwd_h32<false>, grid, block, 0, st, a);
+  const int ngroups = (nblk + kH32Waves - 1) / kH32Waves;
+  const dim3 grid(std::min(ngroups, device_cus())), block(kH32Threads);  // persistent: one workgroup per CU
+  if (a.no_store) hipLaunchKernelGGL(k_mlp_fwd_h32<false>, dim3(ngroups), block, 0, st, a);
   else hipLaunchKernelGGL(k_mlp_fwd_h32<true>, grid, block, 0, st, a);
   return hipGetLastError();
 }
 hipError_t launch_mlp_bwd_h32(const BwdArgs& a, hipStream_t st) {
   const int nblk = a.M / kBlk;
-  hipLaunchKernelGGL(k_mlp_bwd_h32, dim3((nblk + kH32Waves - 1) / kH32Waves), dim3(kH32Threads), 0, st, a);
+  const int ngroups = (nblk + kH32Waves - 1) / kH32Waves;
+  hipLaunchKernelGGL(k_mlp_bwd_h32, dim3(std::min(ngroups, device_cus())), dim3(kH32Threads), 0, st, a);
   return hipGetLastError();
 }
 

@@ -110,21 +110,22 @@ __device__ __forceinline__ uint32_t mask_expand(uint32_t w, int k) {
   return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s16x2, m) >> (s16x2{15, 15}));
 }
 
-// End of a ring period P: this wave's DMA of period P + 1 has landed once at most n VMEM ops are
-// outstanding — n = the ops issued after it: the DMA steps of periods P + 2 .. P + kDmaAhead (two each)
-// and this period's stores (a lower bound: the earlier periods' stores are older than some of those
-// DMAs and only make the true count larger); every wave's LDS reads of the period are done; then the
-// workgroup barrier.
+// End of a ring period P: this wave's DMA of period P + 1 (issued during period P - 5) has landed once at
+// most n VMEM ops are outstanding, n = the ops issued after it: the DMA of periods P + 2 .. P + kDmaAhead
+// (two each) and every store or load this wave issued in periods P - 4 .. P (the ring counts them,
+// H32Ring::end_period); every wave's LDS reads of the period are done; then the workgroup barrier.
 __device__ __forceinline__ void h32_barrier(int n) {
 #define NOF_H32_BAR(N) \
   case N: asm volatile("s_waitcnt vmcnt(" #N ")\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
-  switch (n < 0 ? 0 : (n > 31 ? 31 : n)) {
+  switch (n < 0 ? 0 : (n > 47 ? 47 : n)) {
     NOF_H32_BAR(0) NOF_H32_BAR(1) NOF_H32_BAR(2) NOF_H32_BAR(3) NOF_H32_BAR(4) NOF_H32_BAR(5) NOF_H32_BAR(6)
     NOF_H32_BAR(7) NOF_H32_BAR(8) NOF_H32_BAR(9) NOF_H32_BAR(10) NOF_H32_BAR(11) NOF_H32_BAR(12) NOF_H32_BAR(13)
     NOF_H32_BAR(14) NOF_H32_BAR(15) NOF_H32_BAR(16) NOF_H32_BAR(17) NOF_H32_BAR(18) NOF_H32_BAR(19) NOF_H32_BAR(20)
     NOF_H32_BAR(21) NOF_H32_BAR(22) NOF_H32_BAR(23) NOF_H32_BAR(24) NOF_H32_BAR(25) NOF_H32_BAR(26) NOF_H32_BAR(27)
-    NOF_H32_BAR(28) NOF_H32_BAR(29) NOF_H32_BAR(30)
-    default: asm volatile("s_waitcnt vmcnt(31)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    NOF_H32_BAR(28) NOF_H32_BAR(29) NOF_H32_BAR(30) NOF_H32_BAR(31) NOF_H32_BAR(32) NOF_H32_BAR(33) NOF_H32_BAR(34)
+    NOF_H32_BAR(35) NOF_H32_BAR(36) NOF_H32_BAR(37) NOF_H32_BAR(38) NOF_H32_BAR(39) NOF_H32_BAR(40) NOF_H32_BAR(41)
+    NOF_H32_BAR(42) NOF_H32_BAR(43) NOF_H32_BAR(44) NOF_H32_BAR(45) NOF_H32_BAR(46)
+    default: asm volatile("s_waitcnt vmcnt(47)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); break;
   }
 #undef NOF_H32_BAR
 }
@@ -135,11 +136,19 @@ constexpr int kDmaLatePos = 8;
 struct H32Ring {
   float* lds;
   const float* next;
+  const float* start;  // the stream (a whole number of periods): the DMA wraps from its end to its start,
+  const float* stop;   // so a persistent kernel streams the next group's first periods without a pause
   int cur;
   bool early;  // waves 0-3 (wave-uniform): DMA at positions 0 / 1, else at kDmaLatePos
+  // VMEM stores / loads this wave issued in the current period (ops) and in the four before it (h0 the
+  // latest): all of them are younger than the DMA the period's barrier waits for, so it leaves them in
+  // flight — a barrier that waited for them would wait for stores issued periods ago to reach memory
+  int ops, h0, h1, h2, h3;
   // periods 0 .. kDmaAhead - 1 into slots 0 .. kDmaAhead - 1; the caller's barrier then waits for the
   // first two (prologue_wait)
-  __device__ __forceinline__ void prologue(const float* stream, int tid) {
+  __device__ __forceinline__ void prologue(const float* stream, int stream_floats, int tid) {
+    start = stream;
+    stop = stream + stream_floats;
 #pragma unroll
     for (int p = 0; p < kDmaAhead; ++p) {
       slice16_dma_step(stream + p * kPeriodFloats, lds + p * kPeriodFloats, tid, 0);
@@ -147,15 +156,26 @@ struct H32Ring {
     }
     next = stream + kDmaAhead * kPeriodFloats;
     cur = 0;
+    ops = h0 = h1 = h2 = h3 = 0;
     early = kDmaLatePos == 0 || __builtin_amdgcn_readfirstlane(tid >> 6) < 4;
   }
   __device__ __forceinline__ void dma(int step, int tid) {
     slice16_dma_step(next, lds + ((cur + kDmaAhead) & (kH32Slots - 1)) * kPeriodFloats, tid, step);
   }
+  // VMEM instructions issued outside h32_layer's own count (a group's prologue): a lower bound
+  __device__ __forceinline__ void add_ops(int n) { ops += n; }
   __device__ __forceinline__ void end_period(int nstores) {
-    h32_barrier(2 * (kDmaAhead - 1) + nstores);
+    const int now = ops + nstores;
+    h32_barrier(2 * (kDmaAhead - 1) + now + h0 + h1 + h2 + h3);
+    static_assert(kDmaAhead == 6, "the ring keeps the VMEM counts of kDmaAhead - 2 earlier periods");
+    h3 = h2;
+    h2 = h1;
+    h1 = h0;
+    h0 = now;
+    ops = 0;
     cur = (cur + 1) & (kH32Slots - 1);
     next += kPeriodFloats;
+    if (next == stop) next = start;
   }
   __device__ __forceinline__ f16x8 frag(int i, int lane) const {  // fragment i (0..15) of the current period
     return reinterpret_cast<const f16x8*>(lds + cur * kPeriodFloats + i * kFragFloats)[lane];

@@ -656,14 +656,22 @@ __device__ __forceinline__ void wg_item_s(const WgItem& item, const WgProblem& P
   // this wave's 1-KB DMA pieces c = 8i + wave: tile c >> 1, half c & 1 (clamped: the surplus
   // instructions of narrower problems repeat the last piece, an L2 hit) — block-kb0 source and bytes
   // per block, all wave-uniform
+  // Second halves (features 16..31) land with their two 128-B quarters of every 256 B swapped: lane L
+  // of the piece fetches global chunk L ^ 8, so half-byte j in LDS holds byte j ^ 128.  The transposed
+  // reads of a 32-lane group take 128 B from each half of a tile at the same offset; with the swap the two
+  // halves' reads fall on disjoint banks (unswapped they hit the same 32 banks: 2-way conflicts on every
+  // read, SQ_LDS_BANK_CONFLICT = half of SQ_LDS_IDX_ACTIVE in round 3).
   const char* tsrc[ND];
   int64_t tstr[ND];
   int tdst[ND];
+  bool todd[ND];
+  const int lo_even = lane * 16, lo_odd = (lane ^ 8) * 16;
 #pragma unroll
   for (int i = 0; i < ND; ++i) {
     const int c = min(i * 8 + wave, 2 * T - 1);
     int t = c >> 1;
     tdst[i] = c * 512;
+    todd[i] = c & 1;
     const float* base;
     int F, row0;
     if (t < P.ntr) {
@@ -688,7 +696,7 @@ __device__ __forceinline__ void wg_item_s(const WgItem& item, const WgProblem& P
     _Float16* stage = lds + slot * kStage;
 #pragma unroll
     for (int i = 0; i < ND; ++i) {
-      const char* src = tsrc[i] + (int64_t)k * tstr[i] + lane * 16;
+      const char* src = tsrc[i] + (int64_t)k * tstr[i] + (todd[i] ? lo_odd : lo_even);
       __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(stage + tdst[i]), 16, 0, kWsAux);
     }
   };
@@ -701,7 +709,9 @@ __device__ __forceinline__ void wg_item_s(const WgItem& item, const WgProblem& P
   // transposed-read address of this lane inside a tile (bytes, the slot layout of mlp_h32.h): the 8-B
   // run of features 16 (G & 1) + 4p .. + 3 of sample 16 ks + 8 (G >> 1) + q (+4 for the second read)
   const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const int toff = (G & 1) * 1024 + (8 * (G >> 1) + q) * 32 + (p & 1) * 16 + (p >> 1) * 8;
+  const int toff = (G & 1) * 1024 + (8 * (G >> 1) + q) * 32 + (p & 1) * 16 + (p >> 1) * 8;  // bit 7 clear
+  // the second half's quarters swapped (above): its reads of logical bytes b and b + 128 go to b + 128 and b
+  const uint32_t sw1 = (G & 1) ? 128u : 0u, sw2 = 128u - sw1;
   // inline asm: through the builtin the compiler orders every transposed read behind the LDS-DMA in
   // flight (s_waitcnt vmcnt(0) before each k-step's reads); the ring's own counted waits order them
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
@@ -709,8 +719,8 @@ __device__ __forceinline__ void wg_item_s(const WgItem& item, const WgProblem& P
   // read has its own output and the fragments are assembled after the wait)
   auto frag = [&](uint32_t stage_b, int tile, s16x4v& lo, s16x4v& hi) {
     const uint32_t a = stage_b + (uint32_t)(tile * 2048 + toff);
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a));
-    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:128" : "=v"(hi) : "v"(a));
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a + sw1));
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(a + sw2));
   };
   struct Frags { s16x4v al[RB], ah[RB], bl[CB], bh[CB]; };
   auto issue = [&](int slot, int ks, Frags& f) {  // k-step ks (samples 16 ks ..) of the block in `slot`

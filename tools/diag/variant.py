@@ -39,42 +39,48 @@ EDITS = {
         (K + "mlp_f16.hip", "namespace nof {\n\ntypedef _Float16 h16x2",
          "namespace nof {\n__device__ unsigned long long g_h32_stamps[2][8192][16];\n"
          "extern \"C\" int nof_diag_h32_stamps(unsigned long long* host, int kernel) {\n"
-         "  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_h32_stamps), sizeof(unsigned long long) * 81920,\n"
+         "  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_h32_stamps), sizeof(unsigned long long) * 131072,\n"
          "                                  sizeof(unsigned long long) * 131072 * kernel, hipMemcpyDeviceToHost);\n}\n"
          "#define H32_ST(i) st_[i] = __builtin_amdgcn_s_memtime();\n"
-         "#define H32_FLUSH(k) if (tid == 0 && blockIdx.x < 8192) { st_[14] = rt0_; st_[15] = __builtin_amdgcn_s_memrealtime(); "
-         "for (int q_ = 0; q_ < 16; ++q_) g_h32_stamps[k][blockIdx.x][q_] = st_[q_]; }\n\ntypedef _Float16 h16x2"),
+         "#define H32_FLUSH(k) if (tid == 0 && g < 8192) { st_[13] = blockIdx.x; st_[14] = rt0_; "
+         "st_[15] = __builtin_amdgcn_s_memrealtime(); for (int q_ = 0; q_ < 16; ++q_) g_h32_stamps[k][g][q_] = st_[q_]; }\n"
+         "\ntypedef _Float16 h16x2"),
+        # forward
         (K + "mlp_f16.hip", "  const float* tail = a.wimg + kFwdH32Floats;\n",
-         "  const float* tail = a.wimg + kFwdH32Floats;\n  unsigned long long st_[16] = {};\n"
-         "  const unsigned long long rt0_ = __builtin_amdgcn_s_memrealtime();\n  H32_ST(0)\n"),
-        (K + "mlp_f16.hip", "  // view PE of the wave's ray: lane k < 27 evaluates feature k",
-         "  H32_ST(7)\n  // view PE of the wave's ray: lane k < 27 evaluates feature k"),
-        (K + "mlp_f16.hip", "  // ---- LDS tables: trunk biases, the wave's view-direction bias, packed w8 / W10",
-         "  H32_ST(8)\n  // ---- LDS tables: trunk biases, the wave's view-direction bias, packed w8 / W10"),
-        (K + "mlp_f16.hip", "  h32_prologue_barrier();  // tables written (lgkmcnt), periods 0 and 1 landed\n",
-         "  H32_ST(9)\n  h32_prologue_barrier();  // tables written (lgkmcnt), periods 0 and 1 landed\n  H32_ST(1)\n"),
-        (K + "mlp_f16.hip", "  // ---- delta9 = (W10^T dz_rgb)", "  H32_ST(7)\n  // ---- delta9 = (W10^T dz_rgb)"),
-        (K + "mlp_f16.hip", "  h32_prologue_barrier();  // w8 table written, periods 0 and 1 landed\n",
-         "  H32_ST(9)\n  h32_prologue_barrier();  // w8 table written, periods 0 and 1 landed\n  H32_ST(1)\n"),
-
-        (K + "mlp_f16.hip", "  h32_layer<6, 8, true>(srcI, acc, ring, eX, none, bias_h, tid, lane);\n",
-         "  h32_layer<6, 8, true>(srcI, acc, ring, eX, none, bias_h, tid, lane);\n  H32_ST(2)\n"),
+         "  const float* tail = a.wimg + kFwdH32Floats;\n  unsigned long long st_[16] = {}, rt0_ = 0;\n"),
+        (K + "mlp_f16.hip", "  NOF_DCHECK(blk >= 0 && blk < nblk, kChkMlpBlock);\n  float d3[3];",
+         "  NOF_DCHECK(blk >= 0 && blk < nblk, kChkMlpBlock);\n  rt0_ = __builtin_amdgcn_s_memrealtime();\n  H32_ST(0)\n  float d3[3];"),
+        (K + "mlp_f16.hip", "  // ---- encodings: lane h computes", "  H32_ST(7)\n  // ---- encodings: lane h computes"),
+        (K + "mlp_f16.hip", "  // the B fragments of layers 0 / 4", "  H32_ST(8)\n  // the B fragments of layers 0 / 4"),
+        (K + "mlp_f16.hip", "  if (first) h32_prologue_barrier();  // tables written (lgkmcnt), the first periods landed\n",
+         "  H32_ST(9)\n  if (first) h32_prologue_barrier();  // tables written (lgkmcnt), the first periods landed\n  H32_ST(1)\n"),
+        (K + "mlp_f16.hip", "  else h32_layer<6, 8, true, kGroupOps>(srcI, acc, ring, eX, none, bias_h, tid, lane);\n",
+         "  else h32_layer<6, 8, true, kGroupOps>(srcI, acc, ring, eX, none, bias_h, tid, lane);\n  H32_ST(2)\n"),
         (K + "mlp_f16.hip", "  h32_layer<16, 4, true>(srcY, acc, ring, eV, eY, lds + kDirb + wave * 128 + 4 * h, tid, lane);\n",
          "  H32_ST(3)\n  h32_layer<16, 4, true>(srcY, acc, ring, eV, eY, lds + kDirb + wave * 128 + 4 * h, tid, lane);\n  H32_ST(4)\n"),
-        (K + "mlp_f16.hip", "  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // the ring's trailing DMAs land before the LDS is released\n",
-         "  H32_ST(5)\n  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // the ring's trailing DMAs land before the LDS is released\n"
-         "  H32_ST(6)\n  H32_FLUSH(0)\n"),
+        (K + "mlp_f16.hip", "  }  // groups\n  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // the ring's trailing DMAs",
+         "  H32_ST(5)\n  H32_FLUSH(0)\n  }  // groups\n  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // the ring's trailing DMAs"),
+        # backward
         (K + "mlp_f16.hip", "  const float* tail = a.wimg_b + kBwdH32Floats;\n",
-         "  const float* tail = a.wimg_b + kBwdH32Floats;\n  unsigned long long st_[16] = {};\n"
-         "  const unsigned long long rt0_ = __builtin_amdgcn_s_memrealtime();\n  H32_ST(0)\n"),
-        (K + "mlp_f16.hip", "  h32_layer<8, 8, false>(srcX, acc, ring, eY, none, nullptr, tid, lane);\n",
-         "  h32_layer<8, 8, false>(srcX, acc, ring, eY, none, nullptr, tid, lane);\n  H32_ST(2)\n"),
+         "  const float* tail = a.wimg_b + kBwdH32Floats;\n  unsigned long long st_[16] = {}, rt0_ = 0;\n"),
+        (K + "mlp_f16.hip", "  auto mask_of = [&](int l) { return *reinterpret_cast<const uint4*>(masks_blk + l * 256); };\n",
+         "  auto mask_of = [&](int l) { return *reinterpret_cast<const uint4*>(masks_blk + l * 256); };\n"
+         "  rt0_ = __builtin_amdgcn_s_memrealtime();\n  H32_ST(0)\n"),
+        (K + "mlp_f16.hip", "  // ---- delta9 = (W10^T dz_rgb)", "  H32_ST(7)\n  // ---- delta9 = (W10^T dz_rgb)"),
+        (K + "mlp_f16.hip", "  if (first) h32_prologue_barrier();  // w8 table written, the first periods landed\n",
+         "  H32_ST(9)\n  if (first) h32_prologue_barrier();  // w8 table written, the first periods landed\n  H32_ST(1)\n"),
+        (K + "mlp_f16.hip", "  else h32_layer<8, 8, false, kGroupOps>(srcX, acc, ring, eY, none, nullptr, tid, lane);\n",
+         "  else h32_layer<8, 8, false, kGroupOps>(srcX, acc, ring, eY, none, nullptr, tid, lane);\n  H32_ST(2)\n"),
         (K + "mlp_f16.hip", "  eX.begin(delta, mk_next, nullptr, 0.0f);\n  h32_layer<16, 8, false>(srcY, acc, ring, eX, eY, nullptr, tid, lane);\n",
          "  eX.begin(delta, mk_next, nullptr, 0.0f);\n  H32_ST(3)\n  h32_layer<16, 8, false>(srcY, acc, ring, eX, eY, nullptr, tid, lane);\n  H32_ST(4)\n"),
-        (K + "mlp_f16.hip", "  for (int kk = 0; kk < 16; ++kk) eX.piece(7, kk, 16);  // delta0's last tile\n  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n",
-         "  for (int kk = 0; kk < 16; ++kk) eX.piece(7, kk, 16);  // delta0's last tile\n  H32_ST(5)\n"
-         "  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n  H32_ST(6)\n  H32_FLUSH(1)\n"),
+        (K + "mlp_f16.hip", "  }  // groups\n  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n}",
+         "  H32_ST(5)\n  H32_FLUSH(1)\n  }  // groups\n  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n}"),
     ],
+    "h32_prio": [(K + "mlp_f16.hip", "  ring.prologue(a.wimg, kFwdFrags * kFragFloats, tid);",
+                  "  ring.prologue(a.wimg, kFwdFrags * kFragFloats, tid);\n  if (wave >= 4) __builtin_amdgcn_s_setprio(1);"),
+                 (K + "mlp_f16.hip", "  ring.prologue(a.wimg_b, kBwdFrags * kFragFloats, tid);",
+                  "  ring.prologue(a.wimg_b, kBwdFrags * kFragFloats, tid);\n  if (wave >= 4) __builtin_amdgcn_s_setprio(1);")],
+    "h32_ra3": [(K + "mlp_h32.h", "constexpr int kReadAhead = 2;", "constexpr int kReadAhead = 3;")],
     "h32_nostagger": [(K + "mlp_h32.h", "constexpr int kDmaLatePos = 8;", "constexpr int kDmaLatePos = 0;")],
     # side-output store cache policy: default instead of nt (fp32 / fp16-block kernels and F16)
     "store_default": [(K + "mlp16.h", "constexpr int kStoreNT = 2;", "constexpr int kStoreNT = 0;"),
@@ -85,8 +91,8 @@ EDITS = {
                   "      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(stage + tdst[i]), 16, 0, kWsAux);",
                   "      asm volatile(\"\" ::\"s\"(src), \"s\"(stage + tdst[i]));")],
     "ws_noread": [(K + "wgrad.hip",
-                   "    asm volatile(\"ds_read_b64_tr_b16 %0, %1\" : \"=v\"(lo) : \"v\"(a));\n"
-                   "    asm volatile(\"ds_read_b64_tr_b16 %0, %1 offset:128\" : \"=v\"(hi) : \"v\"(a));",
+                   "    asm volatile(\"ds_read_b64_tr_b16 %0, %1\" : \"=v\"(lo) : \"v\"(a + sw1));\n"
+                   "    asm volatile(\"ds_read_b64_tr_b16 %0, %1\" : \"=v\"(hi) : \"v\"(a + sw2));",
                    "    lo = s16x4v{(short)a, 0, 0, 0};\n    hi = lo;")],
     "ws_nomfma": [(K + "wgrad.hip",
                    "        acc[r][c] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[r], fb[c], acc[r][c], 0, 0, 0);",

@@ -56,6 +56,12 @@ __device__ __forceinline__ void store_tile(__amdgpu_buffer_rsrc_t r, uint32_t vs
   store_half<aux>(r, vslot, T, 0, p[0], p[1], p[2], p[3]);
   store_half<aux>(r, vslot, T, 1, p[4], p[5], p[6], p[7]);
 }
+// a wave-uniform float by a scalar load (the caller waits: lgkmcnt, and redefines the result after it)
+__device__ __forceinline__ float sload_f32(const float* p) {
+  float v;
+  asm volatile("s_load_dword %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
+  return v;
+}
 __device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
   return __builtin_amdgcn_fdot2(__builtin_bit_cast(h16x2, a), __builtin_bit_cast(h16x2, b), c, false);
 }
@@ -200,7 +206,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   NOF_DCHECK(a.M % kBlk == 0 && a.S % kBlk == 0, kChkMlpBlock);
   const float* tail = a.wimg + kFwdH32Floats;
 
-  H32Ring ring;
+  H32Ring<kFwdDmaLate> ring;
   ring.lds = lds;
   ring.prologue(a.wimg, kFwdFrags * kFragFloats, tid);  // the first periods land while the encodings run
 
@@ -233,6 +239,39 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   constexpr int kFirstOps = kStore ? 8 : 0;
   constexpr int kGroupOps = kStore ? 8 + 3 + 3 : 2;
 
+  // A group's ray and sample inputs (direction, origin, radius, the sample's two t) are loaded during the
+  // previous group's view layer (loads wait, in vmcnt order, behind every older store and DMA: issued at
+  // the group start they would wait for the whole ring's DMA in flight); the first group's here.
+  // The ray's values are wave-uniform: scalar loads (lgkmcnt, not ordered behind vector memory), kept in
+  // SGPRs; the two t per lane are vector loads.
+  struct RayIn { float d3[3], o3[3], rad, t0, t1; };
+  auto load_in = [&](int gg) {
+    RayIn r;
+    const int b = min(gg * kH32Waves + wave, nblk - 1), mm0 = b * kBlk;
+    const int ry = __builtin_amdgcn_readfirstlane(mm0 / a.S);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) r.d3[k] = sload_f32(a.dirs + 3 * ry + k);
+    if (!a.encoded) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) r.o3[k] = sload_f32(a.origins + 3 * ry + k);
+      r.rad = sload_f32(a.radii + ry);
+      const float* tr = a.t + (size_t)ry * (a.S + 1) + (mm0 - ry * a.S) + x;
+      r.t0 = tr[0];
+      r.t1 = tr[1];
+    } else {
+      r.o3[0] = r.o3[1] = r.o3[2] = r.rad = r.t0 = r.t1 = 0.0f;
+    }
+    return r;
+  };
+  // the scalar loads' destinations are written asynchronously: each is (re)defined after this wait
+  auto settle_in = [&](RayIn& r) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < 3; ++k) asm volatile("" : "+s"(r.d3[k]), "+s"(r.o3[k]));
+    asm volatile("" : "+s"(r.rad));
+  };
+  RayIn in = load_in(blockIdx.x);
+
   // Persistent: workgroup b runs groups b, b + G, ...; the weight ring streams on across groups (it wraps
   // to the stream start), so only the first group waits for a ring fill and builds the tables.
   for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
@@ -242,8 +281,8 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   const int m0 = blk * kBlk, ray = m0 / a.S;
   const int m = m0 + x;
   NOF_DCHECK(blk >= 0 && blk < nblk, kChkMlpBlock);
-  float d3[3];
-  d3[0] = a.dirs[3 * ray]; d3[1] = a.dirs[3 * ray + 1]; d3[2] = a.dirs[3 * ray + 2];
+  settle_in(in);
+  const float d3[3] = {in.d3[0], in.d3[1], in.d3[2]};
   const void* masks_blk = a.masks + (size_t)blk * kMaskSlots * 256;
   const __amdgpu_buffer_rsrc_t rin = h32_rsrc(reinterpret_cast<const _Float16*>(a.act_in) + (size_t)m0 * kInF);
   // ---- view PE of the wave's ray: lane k < 27 evaluates feature k, every lane reads them back as scalars;
@@ -299,10 +338,8 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   // iy[kk][e] the half h' = 1, for k-steps 3h + kk
   uint32_t ix[3][4], iy[3][4];
   if (!a.encoded) {
-    const float o3[3] = {a.origins[3 * ray], a.origins[3 * ray + 1], a.origins[3 * ray + 2]};
-    const float* tr = a.t + (size_t)ray * (a.S + 1) + (m0 - ray * a.S) + x;
     float mean[3], cov[3];
-    frustum_gaussian(tr[0], tr[1], o3, d3, a.radii[ray], mean, cov);
+    frustum_gaussian(in.t0, in.t1, in.o3, d3, in.rad, mean, cov);
     float mu_h[3], nv_h[3];
     const float sh = h ? 256.0f : 1.0f;  // 2^(8h)
 #pragma unroll
@@ -392,6 +429,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   // ---- view layer 9: relu(W9[:, :256] h7 + dirbias), the RGB head (layer 10) in its epilogue ----------
   ViewEpiH<kStore> eV(acc, mwV, p8, vrow, moff, reinterpret_cast<const _Float16*>(a.act_h9) + (size_t)m0 * kWidthCond,
                       masks_blk, reinterpret_cast<const uint32_t*>(lds + kW10) + 8 * h);
+  if (g + (int)gridDim.x < ngroups) in = load_in(g + gridDim.x);  // the next group's inputs (see load_in)
   h32_layer<16, 4, true>(srcY, acc, ring, eV, eY, lds + kDirb + wave * 128 + 4 * h, tid, lane);
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk) eV.piece(3, kk, 16);  // the last view tile: nothing left to hide it under
@@ -474,7 +512,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   NOF_DCHECK(a.M % kBlk == 0, kChkMlpBlock);
   const float* tail = a.wimg_b + kBwdH32Floats;
 
-  H32Ring ring;
+  H32Ring<kBwdDmaLate> ring;
   ring.lds = lds;
   ring.prologue(a.wimg_b, kBwdFrags * kFragFloats, tid);
   if (tid < 256) {  // the tables, the same for every group

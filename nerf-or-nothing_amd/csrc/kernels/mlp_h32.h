@@ -132,18 +132,24 @@ __device__ __forceinline__ void h32_barrier(int n) {
 
 // The weight ring.  `next` = stream position of period P + kDmaAhead while period P is consumed from
 // slot `cur`.
-constexpr int kDmaLatePos = 8;
+// Positions (k-steps of a period) of a wave's two DMA steps: waves 0-3 at 0 / 1, their SIMD partners
+// 4-7 at kLate / kLate + 1 (H32Ring<kLate>; kLate = 0: no stagger).  Measured with the persistent
+// kernels (tools/ab_multi.sh, two boxes, two rounds each): the forward 2.5-2.8 % faster without the
+// stagger (0.1545 vs 0.159 ms), the backward 1 % faster with it at 8 (0.140 vs 0.1416 ms).
+constexpr int kFwdDmaLate = 0, kBwdDmaLate = 8;
+template <int kLate>
 struct H32Ring {
   float* lds;
   const float* next;
   const float* start;  // the stream (a whole number of periods): the DMA wraps from its end to its start,
   const float* stop;   // so a persistent kernel streams the next group's first periods without a pause
   int cur;
-  bool early;  // waves 0-3 (wave-uniform): DMA at positions 0 / 1, else at kDmaLatePos
+  bool early;  // waves 0-3 (wave-uniform)
   // VMEM stores / loads this wave issued in the current period (ops) and in the four before it (h0 the
   // latest): all of them are younger than the DMA the period's barrier waits for, so it leaves them in
   // flight — a barrier that waited for them would wait for stores issued periods ago to reach memory
   int ops, h0, h1, h2, h3;
+  static constexpr int kLatePos = kLate;
   // periods 0 .. kDmaAhead - 1 into slots 0 .. kDmaAhead - 1; the caller's barrier then waits for the
   // first two (prologue_wait)
   __device__ __forceinline__ void prologue(const float* stream, int stream_floats, int tid) {
@@ -157,7 +163,7 @@ struct H32Ring {
     next = stream + kDmaAhead * kPeriodFloats;
     cur = 0;
     ops = h0 = h1 = h2 = h3 = 0;
-    early = kDmaLatePos == 0 || __builtin_amdgcn_readfirstlane(tid >> 6) < 4;
+    early = kLate == 0 || __builtin_amdgcn_readfirstlane(tid >> 6) < 4;
   }
   __device__ __forceinline__ void dma(int step, int tid) {
     slice16_dma_step(next, lds + ((cur + kDmaAhead) & (kH32Slots - 1)) * kPeriodFloats, tid, step);
@@ -257,8 +263,8 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-template <int NK, int NC, bool kBias, class BSrc, class Epi, class Prev>
-__device__ __forceinline__ void h32_layer(const BSrc& bsrc, f32x16 (&acc)[2], H32Ring& ring, Epi& epi, Prev& prev,
+template <int NK, int NC, bool kBias, class BSrc, class Ring, class Epi, class Prev>
+__device__ __forceinline__ void h32_layer(const BSrc& bsrc, f32x16 (&acc)[2], Ring& ring, Epi& epi, Prev& prev,
                                           const float* cv, int tid, int lane) {
   static_assert((NK * NC) % kPeriod == 0, "a layer is a whole number of ring periods");
   static_assert(NC % 2 == 0 && Prev::kNC % 2 == 0, "the pending last tile of a layer sits in acc[1]");
@@ -272,10 +278,10 @@ __device__ __forceinline__ void h32_layer(const BSrc& bsrc, f32x16 (&acc)[2], H3
   static_for<0, N>([&](auto ic) {
     constexpr int i = decltype(ic)::value, c = i / NK, kk = i % NK, pos = i % kPeriod;
     asm volatile("" ::"v"(fr[i % R]));  // fragment i has landed before more reads issue
-    if constexpr (pos < 2 || (pos >= kDmaLatePos && pos < kDmaLatePos + 2)) {
-      // waves 0-3 issue the period's DMA at positions 0 / 1, their SIMD partners 4-7 at kDmaLatePos (a
-      // wave-uniform branch): the partner's MFMAs keep the pipe busy while one wave sits in the issue
-      if ((pos < 2) == ring.early) ring.dma(pos & 1, tid);
+    constexpr int kLate = Ring::kLatePos;
+    if constexpr (pos < 2 || (pos >= kLate && pos < kLate + 2)) {
+      // a wave-uniform branch when staggered: the partner's MFMAs keep the pipe busy while one wave issues
+      if (kLate == 0 || (pos < 2) == ring.early) ring.dma(pos & 1, tid);
     }
     if constexpr (i + kReadAhead < N) fr[(i + kReadAhead) % R] = ring.frag((pos + kReadAhead) % kPeriod, lane);
     __builtin_amdgcn_sched_barrier(0);

@@ -81,7 +81,13 @@ EDITS = {
                  (K + "mlp_f16.hip", "  ring.prologue(a.wimg_b, kBwdFrags * kFragFloats, tid);",
                   "  ring.prologue(a.wimg_b, kBwdFrags * kFragFloats, tid);\n  if (wave >= 4) __builtin_amdgcn_s_setprio(1);")],
     "h32_ra3": [(K + "mlp_h32.h", "constexpr int kReadAhead = 2;", "constexpr int kReadAhead = 3;")],
-    "h32_nostagger": [(K + "mlp_h32.h", "constexpr int kDmaLatePos = 8;", "constexpr int kDmaLatePos = 0;")],
+    "h32_dma08": [(K + "mlp_h32.h", "constexpr int kDmaPos0 = 0, kDmaPos1 = 1;", "constexpr int kDmaPos0 = 0, kDmaPos1 = 8;")],
+    "h32_st812": [(K + "mlp_h32.h",
+                   "__host__ __device__ constexpr int epi_half_pos(int s, int nk) { return nk >= 16 ? 4 + 4 * s : 2 + 2 * s; }",
+                   "__host__ __device__ constexpr int epi_half_pos(int s, int nk) { return nk >= 16 ? 8 + 4 * s : 2 + 2 * s; }")],
+    "h32_st513": [(K + "mlp_h32.h",
+                   "__host__ __device__ constexpr int epi_half_pos(int s, int nk) { return nk >= 16 ? 4 + 4 * s : 2 + 2 * s; }",
+                   "__host__ __device__ constexpr int epi_half_pos(int s, int nk) { return nk >= 16 ? 5 + 8 * s : 2 + 2 * s; }")],
     # side-output store cache policy: default instead of nt (fp32 / fp16-block kernels and F16)
     "store_default": [(K + "mlp16.h", "constexpr int kStoreNT = 2;", "constexpr int kStoreNT = 0;"),
                       (K + "mlp_f16.hip", "constexpr int kFwdAux = 2;", "constexpr int kFwdAux = 0;"),

@@ -315,7 +315,12 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
     split2<PM>(v[0], v[1], e0);
     split2<PM>(v[2], v[3], e1);
     const int t = row >> 5, xr = row & 31;
-    V4* dst = reinterpret_cast<V4*>(img) + (((t * 64 + (lc >> 1) * 32 + xr) * 2) + (lc & 1));
+    // fragment lane (h, xr) = 32 h + xr, its 16-B chunk XOR 4 when h = 1: the 8-B writes of a 16-lane group
+    // (4 rows x both halves) then fall on disjoint banks (unswizzled the halves, 512 B apart, collided:
+    // SQ_LDS_BANK_CONFLICT 28 % of SQ_LDS_IDX_ACTIVE); the reads apply the same XOR (a permutation inside
+    // every 8 lanes: still conflict-free)
+    const int h2 = lc >> 1;
+    V4* dst = reinterpret_cast<V4*>(img) + (((t * 64 + h2 * 32 + (xr ^ (4 * h2))) * 2) + (lc & 1));
 #pragma unroll
     for (int p = 0; p < NP; ++p) dst[p * 8 * 64 * 2] = __builtin_shufflevector(e0[p], e1[p], 0, 1, 2, 3);
   };
@@ -341,7 +346,7 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
   // nobody reads rather than branching.
   auto step = [&](int k, const X3Raw<NCH>& nx) {
     const bool live = k + 1 < K;
-    const V8* FA = reinterpret_cast<const V8*>(lds + (k & 1) * 2 * kX3Frag) + (lane & 63);
+    const V8* FA = reinterpret_cast<const V8*>(lds + (k & 1) * 2 * kX3Frag) + ((lane & 63) ^ ((lane >> 3) & 4));
     const V8* FB = FA + kX3Frag / 4;
     Frag<PM> fb[CB], fa;
     // first row group's fragments in the order its MFMAs consume them (lo.hi, hi.lo, mid.mid, ...):

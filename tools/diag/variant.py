@@ -76,6 +76,8 @@ EDITS = {
         (K + "mlp_f16.hip", "  }  // groups\n  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n}",
          "  H32_ST(5)\n  H32_FLUSH(1)\n  }  // groups\n  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n}"),
     ],
+    "h32_nomask": [(K + "mlp_h32.h", "__device__ __forceinline__ uint32_t mask_shift(uint32_t w, uint32_t relu) {\n  uint32_t b, r;",
+                    "__device__ __forceinline__ uint32_t mask_shift(uint32_t w, uint32_t relu) {\n  return w ^ relu;\n  uint32_t b, r;")],
     "h32_prio": [(K + "mlp_f16.hip", "  ring.prologue(a.wimg, kFwdFrags * kFragFloats, tid);",
                   "  ring.prologue(a.wimg, kFwdFrags * kFragFloats, tid);\n  if (wave >= 4) __builtin_amdgcn_s_setprio(1);"),
                  (K + "mlp_f16.hip", "  ring.prologue(a.wimg_b, kBwdFrags * kFragFloats, tid);",

@@ -56,10 +56,12 @@ __device__ __forceinline__ void store_tile(__amdgpu_buffer_rsrc_t r, uint32_t vs
   store_half<aux>(r, vslot, T, 0, p[0], p[1], p[2], p[3]);
   store_half<aux>(r, vslot, T, 1, p[4], p[5], p[6], p[7]);
 }
-// a wave-uniform float by a scalar load (the caller waits: lgkmcnt, and redefines the result after it)
+// a wave-uniform float by a scalar load that waits for itself: an inline-asm load's output is taken as
+// written when the statement ends, so a load left in flight across statements can have its register copied
+// (or spilled) before the data lands, and the late write clobber a register reused in between
 __device__ __forceinline__ float sload_f32(const float* p) {
   float v;
-  asm volatile("s_load_dword %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
+  asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
   return v;
 }
 __device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
@@ -198,7 +200,8 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   constexpr int kW8 = kDirb + kH32Waves * 128;    // packed w8 [8][2][8]
   constexpr int kW10 = kW8 + 128;                 // packed W10 [3][4][2][8]
   constexpr int kW9d = kW10 + 192;                // W9[:, 256:283] transposed [27][128], then b9 [128]
-  __shared__ __attribute__((aligned(16))) float lds[kW9d + (kDirIn + 1) * 128];
+  constexpr int kTin = kW9d + (kDirIn + 1) * 128;  // per-wave group inputs [8][64] (in_dma)
+  __shared__ __attribute__((aligned(16))) float lds[kTin + kH32Waves * 64];
   const int tid = threadIdx.x, lane = tid & 63, x = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nblk = a.M / kBlk;
@@ -239,38 +242,58 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   constexpr int kFirstOps = kStore ? 8 : 0;
   constexpr int kGroupOps = kStore ? 8 + 3 + 3 : 2;
 
-  // A group's ray and sample inputs (direction, origin, radius, the sample's two t) are loaded during the
-  // previous group's view layer (loads wait, in vmcnt order, behind every older store and DMA: issued at
-  // the group start they would wait for the whole ring's DMA in flight); the first group's here.
-  // The ray's values are wave-uniform: scalar loads (lgkmcnt, not ordered behind vector memory), kept in
-  // SGPRs; the two t per lane are vector loads.
-  struct RayIn { float d3[3], o3[3], rad, t0, t1; };
-  auto load_in = [&](int gg) {
-    RayIn r;
+  // A group's inputs — the 33 t of each wave's 32 samples and its ray's direction, origin and radius — go
+  // into the wave's LDS slot by LDS-DMA (in_dma: [0, 33) t, [40, 43) direction, [44, 47) origin, 48 radius)
+  // a trunk layer + the view layer ahead (the first group's before the loop): landed, in vmcnt order, by
+  // the ring barriers six periods later, and read back opaquely at the group start (read_in).  A vector
+  // load issued at the group start would wait, in vmcnt order, behind every older store and the whole
+  // ring's DMA in flight; a plain LDS read after an LDS-DMA gets a full vmcnt(0) drain from the compiler.
+  constexpr int kInOps = 4;
+  auto in_dma = [&](int gg) {
     const int b = min(gg * kH32Waves + wave, nblk - 1), mm0 = b * kBlk;
     const int ry = __builtin_amdgcn_readfirstlane(mm0 / a.S);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) r.d3[k] = sload_f32(a.dirs + 3 * ry + k);
-    if (!a.encoded) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) r.o3[k] = sload_f32(a.origins + 3 * ry + k);
-      r.rad = sload_f32(a.radii + ry);
-      const float* tr = a.t + (size_t)ry * (a.S + 1) + (mm0 - ry * a.S) + x;
-      r.t0 = tr[0];
-      r.t1 = tr[1];
-    } else {
-      r.o3[0] = r.o3[1] = r.o3[2] = r.rad = r.t0 = r.t1 = 0.0f;
+    float* slot = lds + kTin + wave * 64;
+    uint32_t l4 = (uint32_t)min(lane, kBlk) * 4u;  // (recomputed opaquely: hoisted out of the loop it stays live)
+    asm volatile("" : "+v"(l4));
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(h32_rsrc(a.t + (size_t)ry * (a.S + 1) + (mm0 - ry * a.S)), (lptr_t)slot, 4,
+                                             l4, 0, 0, 0);
+    if (lane < 3) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(h32_rsrc(a.dirs + 3 * ry), (lptr_t)(slot + 40), 4, l4, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(h32_rsrc(a.origins + 3 * ry), (lptr_t)(slot + 44), 4, l4, 0, 0, 0);
+      if (lane == 0) __builtin_amdgcn_raw_ptr_buffer_load_lds(h32_rsrc(a.radii + ry), (lptr_t)(slot + 48), 4, l4, 0, 0, 0);
     }
+  };
+  struct GroupIn { float t0, t1, d3[3], o3[3], rad; };
+  auto read_in = [&]() {  // sample x's two t, the ray's values (wave-uniform: to SGPRs)
+    const uint32_t sa = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(lds + kTin + wave * 64);
+    f32x2 tt;
+    float v[7];
+    asm volatile(
+        "ds_read2_b32 %0, %8 offset1:1\n\t"
+        "ds_read_b32 %1, %9 offset:160\n\tds_read_b32 %2, %9 offset:164\n\tds_read_b32 %3, %9 offset:168\n\t"
+        "ds_read_b32 %4, %9 offset:176\n\tds_read_b32 %5, %9 offset:180\n\tds_read_b32 %6, %9 offset:184\n\t"
+        "ds_read_b32 %7, %9 offset:192\n\ts_waitcnt lgkmcnt(0)"
+        : "=&v"(tt), "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6])
+        : "v"(sa + 4u * (uint32_t)x), "v"(sa));
+    GroupIn r;
+    r.t0 = tt[0];
+    r.t1 = tt[1];
+    const auto u = [](float f) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(f))); };
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      r.d3[k] = u(v[k]);
+      r.o3[k] = u(v[3 + k]);
+    }
+    r.rad = u(v[6]);
     return r;
   };
-  // the scalar loads' destinations are written asynchronously: each is (re)defined after this wait
-  auto settle_in = [&](RayIn& r) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // the heads' biases (b8, b10), wave-uniform scalars for every group: loaded by the heads from global
+  // memory they would wait, in vmcnt order, for the view layer's stores and the weight DMA in flight
+  float hb[4];
+  hb[0] = sload_f32(tail + kFwdTailBias + 8 * 256);
 #pragma unroll
-    for (int k = 0; k < 3; ++k) asm volatile("" : "+s"(r.d3[k]), "+s"(r.o3[k]));
-    asm volatile("" : "+s"(r.rad));
-  };
-  RayIn in = load_in(blockIdx.x);
+  for (int c = 0; c < 3; ++c) hb[1 + c] = sload_f32(tail + kFwdTailBias + 10 * 256 + c);
+  if (!a.encoded) in_dma(blockIdx.x);
 
   // Persistent: workgroup b runs groups b, b + G, ...; the weight ring streams on across groups (it wraps
   // to the stream start), so only the first group waits for a ring fill and builds the tables.
@@ -281,7 +304,11 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   const int m0 = blk * kBlk, ray = m0 / a.S;
   const int m = m0 + x;
   NOF_DCHECK(blk >= 0 && blk < nblk, kChkMlpBlock);
-  settle_in(in);
+  GroupIn in = {};
+  if (!a.encoded) {
+    if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the first group's inputs (later: the ring barriers)
+    in = read_in();
+  }
   const float d3[3] = {in.d3[0], in.d3[1], in.d3[2]};
   const void* masks_blk = a.masks + (size_t)blk * kMaskSlots * 256;
   const __amdgpu_buffer_rsrc_t rin = h32_rsrc(reinterpret_cast<const _Float16*>(a.act_in) + (size_t)m0 * kInF);
@@ -289,7 +316,15 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   // first the direction bias and the act_in view-PE tile (pe dies before the IPE's registers go live)
   {
     const int kl = lane < kDirIn ? lane : 0;
-    const float pe_l = a.encoded ? a.enc_dir[(size_t)ray * kDirIn + kl] : dir_feature(kl, d3);
+    // (the encoded load's value redefined inside its branch: waited for at the join, the wait — a full
+    // vmcnt drain — would run in the other path too)
+    float pe_l;
+    if (a.encoded) {
+      pe_l = a.enc_dir[(size_t)ray * kDirIn + kl];
+      asm volatile("" : "+v"(pe_l));
+    } else {
+      pe_l = dir_feature(kl, d3);
+    }
     float pe[kDirIn];
 #pragma unroll
     for (int k = 0; k < kDirIn; ++k) pe[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pe_l), k));
@@ -305,13 +340,20 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
       // (256 VGPRs and 42 spilled)
       const uint32_t base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(lds + kW9d + o);
       float wv[kDirIn + 1];
+      // 14 reads and their wait per statement: an asm output is taken as written when its statement ends
+      static_assert(kDirIn + 1 == 28, "two statements of 14 reads");
+#define NOF_RD(I, J) "ds_read_b32 %" #I ", %14 offset:" #J "\n\t"
 #pragma unroll
-      for (int k = 0; k <= kDirIn; ++k) asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(wv[k]) : "v"(base), "i"(k * 512));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      // the reads' outputs are written asynchronously: each is (re)defined here, after the wait, so no copy
-      // of one can be scheduled before it has landed
-#pragma unroll
-      for (int k = 0; k <= kDirIn; ++k) asm volatile("" : "+v"(wv[k]));
+      for (int q = 0; q < 2; ++q)
+        asm volatile(NOF_RD(0, 0) NOF_RD(1, 512) NOF_RD(2, 1024) NOF_RD(3, 1536) NOF_RD(4, 2048) NOF_RD(5, 2560)
+                     NOF_RD(6, 3072) NOF_RD(7, 3584) NOF_RD(8, 4096) NOF_RD(9, 4608) NOF_RD(10, 5120) NOF_RD(11, 5632)
+                     NOF_RD(12, 6144) NOF_RD(13, 6656) "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(wv[14 * q]), "=&v"(wv[14 * q + 1]), "=&v"(wv[14 * q + 2]), "=&v"(wv[14 * q + 3]),
+                       "=&v"(wv[14 * q + 4]), "=&v"(wv[14 * q + 5]), "=&v"(wv[14 * q + 6]), "=&v"(wv[14 * q + 7]),
+                       "=&v"(wv[14 * q + 8]), "=&v"(wv[14 * q + 9]), "=&v"(wv[14 * q + 10]), "=&v"(wv[14 * q + 11]),
+                       "=&v"(wv[14 * q + 12]), "=&v"(wv[14 * q + 13])
+                     : "v"(base + q * 14 * 512));
+#undef NOF_RD
       float s = wv[kDirIn];
 #pragma unroll
       for (int k = 0; k < kDirIn; ++k) s = __builtin_fmaf(wv[k], pe[k], s);
@@ -365,6 +407,10 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
         ix[kk][e] = pk_h(ep[c0], ep[c0 + 1]);
         iy[kk][e] = pk_h(ep[c1], ep[c1 + 1]);
       }
+#pragma unroll
+    for (int kk = 0; kk < 3; ++kk)  // (as pe_l above: waited for in this branch)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(ix[kk][e]), "+v"(iy[kk][e]));
   }
   // the B fragments of layers 0 / 4: k-steps 0..2 from the lane half h = 0, 3..5 from h = 1 — one
   // permlane32 swap per packed dword moves each half's other-h' pairs across (tools/probe/h32_probe.hip)
@@ -419,6 +465,10 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
     eX.begin(act_h + (la + 1) * lstride, masks_blk, la + 1, w8h, false);
     h32_layer<16, 8, true>(srcY, acc, ring, eX, eY, bias_h + (la + 1) * 256, tid, lane);
     eY.begin(act_h + (la + 2) * lstride, masks_blk, la + 2, w8h, la + 2 == kDepth - 1);  // + density (layer 8)
+    if (kStore && it == 1 && !a.encoded && g + (int)gridDim.x < ngroups) {  // 12 periods ahead of read_in
+      in_dma(g + gridDim.x);
+      ring.add_ops(kInOps);
+    }
     h32_layer<16, 8, true>(srcX, acc, ring, eY, eX, bias_h + (la + 2) * 256, tid, lane);
     if (it == 0) {
       eX.begin(act_h + kSkip * lstride, masks_blk, kSkip, w8h, false);
@@ -429,7 +479,6 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   // ---- view layer 9: relu(W9[:, :256] h7 + dirbias), the RGB head (layer 10) in its epilogue ----------
   ViewEpiH<kStore> eV(acc, mwV, p8, vrow, moff, reinterpret_cast<const _Float16*>(a.act_h9) + (size_t)m0 * kWidthCond,
                       masks_blk, reinterpret_cast<const uint32_t*>(lds + kW10) + 8 * h);
-  if (g + (int)gridDim.x < ngroups) in = load_in(g + gridDim.x);  // the next group's inputs (see load_in)
   h32_layer<16, 4, true>(srcY, acc, ring, eV, eY, lds + kDirb + wave * 128 + 4 * h, tid, lane);
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk) eV.piece(3, kk, 16);  // the last view tile: nothing left to hide it under
@@ -437,10 +486,10 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   // ---- heads: sigma = softplus(z_s - 1), rgb = sigmoid(z_c) 1.002 - 0.001 (MNcs:307-309) -------------
   float zs = eY.zs;
   zs += __shfl_xor(zs, 32, 64);
-  zs += tail[kFwdTailBias + 8 * 256];
+  zs += hb[0];
   float zc[3];
 #pragma unroll
-  for (int c = 0; c < 3; ++c) zc[c] = eV.zc[c] + __shfl_xor(eV.zc[c], 32, 64) + tail[kFwdTailBias + 10 * 256 + c];
+  for (int c = 0; c < 3; ++c) zc[c] = eV.zc[c] + __shfl_xor(eV.zc[c], 32, 64) + hb[1 + c];
   if (h == 0) {
     a.sigma[m] = softplus_f(zs + kDensityBias);
 #pragma unroll
@@ -483,9 +532,14 @@ struct BwdEpiH {
       if (kk == epi_valu_pos(d, NK)) {
         float v0 = acc[T & 1][2 * d], v1 = acc[T & 1][2 * d + 1];
         if (w8) {
-          const float2 w = *reinterpret_cast<const float2*>(w8 + T * 32 + 2 * d);
-          v0 = __builtin_fmaf(w.x, dzs, v0);
-          v1 = __builtin_fmaf(w.y, dzs, v1);
+          // an opaque read that waits for itself: as a plain LDS load the compiler cannot tell it from
+          // the ring's LDS-DMA destination and puts a full s_waitcnt vmcnt(0) before it — draining every
+          // store and weight DMA in flight, twice per tile of the layer
+          const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)w8;
+          f32x2 w;
+          asm volatile("ds_read_b64 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)" : "=v"(w) : "v"(la), "i"(4 * (T * 32 + 2 * d)));
+          v0 = __builtin_fmaf(w[0], dzs, v0);
+          v1 = __builtin_fmaf(w[1], dzs, v1);
         }
         const uint32_t word = (T >> 1) == 0 ? mk.x : ((T >> 1) == 1 ? mk.y : ((T >> 1) == 2 ? mk.z : mk.w));
         dst[2 * T + (d >> 2)][d & 3] = pk_h(v0, v1) & mask_expand(word, 8 * (T & 1) + d);
@@ -504,7 +558,10 @@ struct BwdEpiH {
 __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   constexpr int kW8 = kH32RingFloats;  // fp32 w8 in D-register order [8][2][16]
   constexpr int kW10 = kW8 + 256;      // fp32 W10 [3][128]
-  __shared__ __attribute__((aligned(16))) float lds[kW10 + 3 * 128];
+  // per-wave group inputs (bwd_in_dma): masks of layers 8 and 7 [64 lanes][4], zhead [32][4], drgb [32][3],
+  // dsigma [32]
+  constexpr int kIn = kW10 + 3 * 128, kInFloats = 256 + 256 + 128 + 96 + 32;
+  __shared__ __attribute__((aligned(16))) float lds[kIn + kH32Waves * kInFloats];
   const int tid = threadIdx.x, lane = tid & 63, x = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nblk = a.M / kBlk;
@@ -529,26 +586,58 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   constexpr int kFirstOps = 9;
   constexpr int kGroupOps = 9 + 2;
 
+  // A group's inputs (the heads' gradients, the layer-9 and layer-7 masks) go into the wave's LDS slot by
+  // five LDS-DMAs issued at the previous group's last layer (the first group's before the loop): landed in
+  // vmcnt order by the ring barriers eight periods later, and read back opaquely at the group start.  As
+  // vector loads issued at the group start they waited, in vmcnt order, behind the previous group's last
+  // stores and the ring's DMA in flight (a drain per group); a plain LDS read after an LDS-DMA gets a full
+  // vmcnt(0) from the compiler.
+  float* const in_slot = lds + kIn + wave * kInFloats;
+  auto in_dma = [&](int gg) {
+    const int b = min(gg * kH32Waves + wave, nblk - 1), mm0 = b * kBlk;
+    // (the lane offsets recomputed here, opaquely: hoisted out of the group loop they are spilled, and a
+    // scratch reload's wait is a full vmcnt drain)
+    uint32_t l16 = (uint32_t)lane * 16u, l4 = (uint32_t)lane * 4u;
+    asm volatile("" : "+v"(l16), "+v"(l4));
+    const __amdgpu_buffer_rsrc_t rm = h32_rsrc(a.masks + (size_t)b * kMaskSlots * 256);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, (lptr_t)in_slot, 16, l16, 8 * 1024, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, (lptr_t)(in_slot + 256), 16, l16, 7 * 1024, 0, 0);
+    if (lane < kBlk) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(h32_rsrc(a.zhead + (size_t)mm0 * 4), (lptr_t)(in_slot + 512), 16, l16, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(h32_rsrc(a.dsigma + mm0), (lptr_t)(in_slot + 736), 4, l4, 0, 0, 0);
+    }
+    if (lane < kBlk * 3 / 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(h32_rsrc(a.drgb + (size_t)mm0 * 3), (lptr_t)(in_slot + 640), 16, l16, 0, 0, 0);
+  };
+  constexpr int kInOps = 5;
+  in_dma(blockIdx.x);
+
   // Persistent: workgroup b runs groups b, b + G, ...; the weight ring streams on across groups.
   for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
   const bool first = g == (int)blockIdx.x;
   const int blk_raw = g * kH32Waves + wave;
   const int blk = blk_raw < nblk ? blk_raw : nblk - 1;
-  const int m0 = blk * kBlk, m = m0 + x;
+  const int m0 = blk * kBlk;
   NOF_DCHECK(blk >= 0 && blk < nblk, kChkMlpBlock);
   const uint32_t* masks_blk = a.masks + (size_t)blk * kMaskSlots * 256 + lane * 4;
   auto mask_of = [&](int l) { return *reinterpret_cast<const uint4*>(masks_blk + l * 256); };
 
   // ---- heads (MNcs:410-415), scaled by the level's power of two ---------------------------------------
-  // every load of the group first (the masks of layers 9, 7 and 6 too): vmcnt retires in issue order, so
-  // a load issued behind the delta9x stores would wait for them
-  const f32x4 zh = reinterpret_cast<const f32x4*>(a.zhead)[m];
-  const float ds_m = a.dsigma[m];
-  float dr[3];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) dr[c] = a.drgb[(size_t)m * 3 + c];
-  const uint4 mk9 = mask_of(8);
-  const uint4 mk7 = mask_of(7);
+  if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the first group's inputs (later: the ring barriers)
+  u32x4 mk9v, mk7v;
+  f32x4 zh;
+  float dr[3], ds_m;
+  {
+    const auto la = [](const float* p) { return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)p; };
+    asm volatile(
+        "ds_read_b128 %0, %7\n\tds_read_b128 %1, %7 offset:1024\n\tds_read_b128 %2, %8 offset:2048\n\t"
+        "ds_read_b32 %3, %9 offset:2560\n\tds_read_b32 %4, %9 offset:2564\n\tds_read_b32 %5, %9 offset:2568\n\t"
+        "ds_read_b32 %6, %10 offset:2944\n\ts_waitcnt lgkmcnt(0)"
+        : "=&v"(mk9v), "=&v"(mk7v), "=&v"(zh), "=&v"(dr[0]), "=&v"(dr[1]), "=&v"(dr[2]), "=&v"(ds_m)
+        : "v"(la(in_slot + lane * 4)), "v"(la(in_slot + x * 4)), "v"(la(in_slot + x * 3)), "v"(la(in_slot + x)));
+  }
+  const uint4 mk9 = {mk9v[0], mk9v[1], mk9v[2], mk9v[3]};
+  const uint4 mk7 = {mk7v[0], mk7v[1], mk7v[2], mk7v[3]};
   uint4 mk_next = mask_of(6);  // every later layer's mask words are loaded one layer before its begin()
   const float dzs = ds_m * sigmoid_f(zh[0] + kDensityBias) * sc;
   float dzc[3];
@@ -616,6 +705,10 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
     h32_layer<16, 8, false>(srcX, acc, ring, eY, eX, nullptr, tid, lane);
   }
   eX.begin(delta, mk_next, nullptr, 0.0f);
+  if (g + (int)gridDim.x < ngroups) {
+    in_dma(g + gridDim.x);
+    ring.add_ops(kInOps);
+  }
   h32_layer<16, 8, false>(srcY, acc, ring, eX, eY, nullptr, tid, lane);
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk) eX.piece(7, kk, 16);  // delta0's last tile

@@ -48,14 +48,14 @@ EDITS = {
         # forward
         (K + "mlp_f16.hip", "  const float* tail = a.wimg + kFwdH32Floats;\n",
          "  const float* tail = a.wimg + kFwdH32Floats;\n  unsigned long long st_[16] = {}, rt0_ = 0;\n"),
-        (K + "mlp_f16.hip", "  NOF_DCHECK(blk >= 0 && blk < nblk, kChkMlpBlock);\n  float d3[3];",
-         "  NOF_DCHECK(blk >= 0 && blk < nblk, kChkMlpBlock);\n  rt0_ = __builtin_amdgcn_s_memrealtime();\n  H32_ST(0)\n  float d3[3];"),
+        (K + "mlp_f16.hip", "  NOF_DCHECK(blk >= 0 && blk < nblk, kChkMlpBlock);\n  GroupIn in = {};",
+         "  NOF_DCHECK(blk >= 0 && blk < nblk, kChkMlpBlock);\n  rt0_ = __builtin_amdgcn_s_memrealtime();\n  H32_ST(0)\n  GroupIn in = {};"),
         (K + "mlp_f16.hip", "  // ---- encodings: lane h computes", "  H32_ST(7)\n  // ---- encodings: lane h computes"),
         (K + "mlp_f16.hip", "  // the B fragments of layers 0 / 4", "  H32_ST(8)\n  // the B fragments of layers 0 / 4"),
         (K + "mlp_f16.hip", "  if (first) h32_prologue_barrier();  // tables written (lgkmcnt), the first periods landed\n",
          "  H32_ST(9)\n  if (first) h32_prologue_barrier();  // tables written (lgkmcnt), the first periods landed\n  H32_ST(1)\n"),
-        (K + "mlp_f16.hip", "  else h32_layer<6, 8, true, kGroupOps>(srcI, acc, ring, eX, none, bias_h, tid, lane);\n",
-         "  else h32_layer<6, 8, true, kGroupOps>(srcI, acc, ring, eX, none, bias_h, tid, lane);\n  H32_ST(2)\n"),
+        (K + "mlp_f16.hip", "  h32_layer<6, 8, true>(srcI, acc, ring, eX, none, bias_h, tid, lane);\n",
+         "  h32_layer<6, 8, true>(srcI, acc, ring, eX, none, bias_h, tid, lane);\n  H32_ST(2)\n"),
         (K + "mlp_f16.hip", "  h32_layer<16, 4, true>(srcY, acc, ring, eV, eY, lds + kDirb + wave * 128 + 4 * h, tid, lane);\n",
          "  H32_ST(3)\n  h32_layer<16, 4, true>(srcY, acc, ring, eV, eY, lds + kDirb + wave * 128 + 4 * h, tid, lane);\n  H32_ST(4)\n"),
         (K + "mlp_f16.hip", "  }  // groups\n  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // the ring's trailing DMAs",
@@ -69,10 +69,10 @@ EDITS = {
         (K + "mlp_f16.hip", "  // ---- delta9 = (W10^T dz_rgb)", "  H32_ST(7)\n  // ---- delta9 = (W10^T dz_rgb)"),
         (K + "mlp_f16.hip", "  if (first) h32_prologue_barrier();  // w8 table written, the first periods landed\n",
          "  H32_ST(9)\n  if (first) h32_prologue_barrier();  // w8 table written, the first periods landed\n  H32_ST(1)\n"),
-        (K + "mlp_f16.hip", "  else h32_layer<8, 8, false, kGroupOps>(srcX, acc, ring, eY, none, nullptr, tid, lane);\n",
-         "  else h32_layer<8, 8, false, kGroupOps>(srcX, acc, ring, eY, none, nullptr, tid, lane);\n  H32_ST(2)\n"),
-        (K + "mlp_f16.hip", "  eX.begin(delta, mk_next, nullptr, 0.0f);\n  h32_layer<16, 8, false>(srcY, acc, ring, eX, eY, nullptr, tid, lane);\n",
-         "  eX.begin(delta, mk_next, nullptr, 0.0f);\n  H32_ST(3)\n  h32_layer<16, 8, false>(srcY, acc, ring, eX, eY, nullptr, tid, lane);\n  H32_ST(4)\n"),
+        (K + "mlp_f16.hip", "  h32_layer<8, 8, false>(srcX, acc, ring, eY, none, nullptr, tid, lane);\n",
+         "  h32_layer<8, 8, false>(srcX, acc, ring, eY, none, nullptr, tid, lane);\n  H32_ST(2)\n"),
+        (K + "mlp_f16.hip", "  h32_layer<16, 8, false>(srcY, acc, ring, eX, eY, nullptr, tid, lane);\n#pragma unroll\n  for (int kk = 0; kk < 16; ++kk) eX.piece(7, kk, 16);",
+         "  H32_ST(3)\n  h32_layer<16, 8, false>(srcY, acc, ring, eX, eY, nullptr, tid, lane);\n  H32_ST(4)\n#pragma unroll\n  for (int kk = 0; kk < 16; ++kk) eX.piece(7, kk, 16);"),
         (K + "mlp_f16.hip", "  }  // groups\n  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n}",
          "  H32_ST(5)\n  H32_FLUSH(1)\n  }  // groups\n  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n}"),
     ],
@@ -83,7 +83,8 @@ EDITS = {
                  (K + "mlp_f16.hip", "  ring.prologue(a.wimg_b, kBwdFrags * kFragFloats, tid);",
                   "  ring.prologue(a.wimg_b, kBwdFrags * kFragFloats, tid);\n  if (wave >= 4) __builtin_amdgcn_s_setprio(1);")],
     "h32_ra3": [(K + "mlp_h32.h", "constexpr int kReadAhead = 2;", "constexpr int kReadAhead = 3;")],
-    "h32_dma08": [(K + "mlp_h32.h", "constexpr int kDmaPos0 = 0, kDmaPos1 = 1;", "constexpr int kDmaPos0 = 0, kDmaPos1 = 8;")],
+    # the weight-DMA stagger (waves 4-7 at k-step kLate): forward staggered at 8, backward not
+    "h32_stagger": [(K + "mlp_h32.h", "constexpr int kFwdDmaLate = 0, kBwdDmaLate = 8;", "constexpr int kFwdDmaLate = 8, kBwdDmaLate = 0;")],
     "h32_st812": [(K + "mlp_h32.h",
                    "__host__ __device__ constexpr int epi_half_pos(int s, int nk) { return nk >= 16 ? 4 + 4 * s : 2 + 2 * s; }",
                    "__host__ __device__ constexpr int epi_half_pos(int s, int nk) { return nk >= 16 ? 8 + 4 * s : 2 + 2 * s; }")],

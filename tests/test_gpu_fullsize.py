@@ -158,3 +158,43 @@ def test_config4_shard_vs_oracle(gpu, oracle):
     _gpu_step(model, r, gpu, msum, lo, n)
     _compare_step(oracle, model, sub, samples, seed, step, base + lo, msum, 0)
     model.close()
+
+
+@pytest.mark.parametrize("precision", [4, 0])
+def test_persistent_groups_with_partial_tail(gpu, oracle, precision):
+    """1025 rays x 128+128: 4 100 sample blocks = 513 groups of 8 per level, so on a 256-CU part the F16
+    kernels' persistent workgroup 0 runs three groups (0, 256, 512) and the last is partial (4 blocks, its
+    other waves duplicate the last block); the next groups' inputs are prefetched across group boundaries.
+    Per-sample outputs do not depend on the grouping: the last 8 rays' forward outputs and integrator
+    adjoint equal, bitwise, those of an 8-ray batch of the same rays (same global ids, same loss-mult sum,
+    same parameters), and match the oracle's own forward within the mode's tolerance."""
+    import nof
+
+    n, samples, tail = 1025, (128, 128), 8
+    seed, step, base = 0x5EED0007, 3, 4096
+    r = _rays("blender", n, seed=77)
+    msum = float(np.sum(r["lossmult"], dtype=np.float32))
+    model = nof.AcceleratedMipNeRF(seed=5, max_rays=n, num_samples=samples, precision=precision)
+    model.set_rng(seed, step, base)
+    _gpu_step(model, r, gpu, msum)
+    full = [model.level_numpy(l) for l in range(2)]
+    _check_t(oracle, full, r, samples, seed, step, base)
+    lo = n - tail
+    params = nof.to_numpy(model.mlp.flat_params()[0], (546948,)).copy()
+    small = nof.AcceleratedMipNeRF(seed=5, max_rays=tail, num_samples=samples, precision=precision)
+    small.set_rng(seed, step, base + lo)
+    _gpu_step(small, r, gpu, msum, lo, n)
+    part = [small.level_numpy(l) for l in range(2)]
+    for l in range(2):
+        for k in PER_RAY + ("t",):
+            assert np.array_equal(full[l][k][lo:], part[l][k]), f"{k} level {l}: grouping changed the result"
+    sub = {k: v[lo:] for k, v in r.items()}
+    ref = oracle.step(oracle.Spec(), params, sub, samples=samples, seed=seed, step_idx=step, ray_base=base + lo,
+                      loss_mult_sum=msum, t_override={1: full[1]["t"][lo:]}, nthreads=NTHREADS,
+                      want=tuple(ORACLE_KEY.values()))
+    for l in range(2):
+        for k in PER_RAY:
+            e = rel_l2(full[l][k][lo:], ref[ORACLE_KEY[k]][l])
+            assert e < TOLS[precision], f"{k} level {l} (rays {lo}..{n - 1}): rel L2 {e:.3g}"
+    small.close()
+    model.close()

@@ -6,7 +6,7 @@
 //   dma:    2 x 1-KB LDS-DMA pieces of the 1-MB weight stream (L2 / MALL resident) into an 8-slot ring,
 //           fetched 6 periods ahead, one counted-vmcnt barrier per period;
 //   mfma:   16 v_mfma_f32_32x32x16_f16, the A fragment of each read from the ring slot (one per k-step).
-// mode bits: 1 = stores, 2 = dma, 4 = mfma.  Prints us per launch and the store rate.
+// mode bits: 1 = stores, 2 = dma, 4 = mfma, 8 = the DMA as global_load_lds_dwordx4 (per-lane address).  Prints us per launch and the store rate.
 // hipcc --offload-arch=gfx950 -O3 -std=c++17 h32_mix_probe.hip -o h32_mix_probe
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -28,8 +28,12 @@ __global__ __launch_bounds__(512, 1) void k_mix(const float* __restrict__ wstrea
   auto dma = [&](int per, int step) {  // period `per` (mod the stream) into its slot, half `step`
     const int p = per % kPeriods;
     float* dst = lds + (per % kSlots) * kPeriodFloats;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lptr_t)(dst + (512 * step + 64 * wave) * 4), 16, tid * 16,
-                                             p * kPeriodFloats * 4 + step * 512 * 16, 0, 0);
+    if constexpr (MODE & 8)  // global_load_lds_dwordx4 (per-lane address) instead of the buffer form
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(wstream + p * kPeriodFloats + step * 512 * 4 + tid * 4),
+                                       (lptr_t)(dst + (512 * step + 64 * wave) * 4), 16, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lptr_t)(dst + (512 * step + 64 * wave) * 4), 16, tid * 16,
+                                               p * kPeriodFloats * 4 + step * 512 * 16, 0, 0);
   };
   if constexpr (MODE & 2)
     for (int p = 0; p < kAhead; ++p) { dma(p, 0); dma(p, 1); }
@@ -102,5 +106,8 @@ int main() {
   run(k_mix<5>, "stores+mfma", 5);
   run(k_mix<6>, "dma+mfma", 6);
   run(k_mix<7>, "stores+dma+mfma", 7);
+  run(k_mix<10>, "gdma", 10);
+  run(k_mix<14>, "gdma+mfma", 14);
+  run(k_mix<15>, "stores+gdma+mfma", 15);
   return 0;
 }

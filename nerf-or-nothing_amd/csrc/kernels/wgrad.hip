@@ -987,25 +987,29 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const WgOut* __restrict__ 
     for (int lev = 0; lev < o.nlev; ++lev) {
       const int k1 = k + o.lev_items[lev];
       f32x4 s = {0.0f, 0.0f, 0.0f, 0.0f};
+      // kU slabs in flight, the last round guarded (uniform conditions), summed in item order
       if (vec) {
-        for (; k + kU <= k1; k += kU) {
+        for (; k < k1; k += kU) {
           f32x4 v[kU];
 #pragma unroll
-          for (int u = 0; u < kU; ++u) v[u] = *reinterpret_cast<const f32x4*>(slabs + so[k + u] + off);
+          for (int u = 0; u < kU; ++u)
+            if (k + u < k1) v[u] = *reinterpret_cast<const f32x4*>(slabs + so[k + u] + off);
 #pragma unroll
-          for (int u = 0; u < kU; ++u) s += v[u];
+          for (int u = 0; u < kU; ++u)
+            if (k + u < k1) s += v[u];
         }
-        for (; k < k1; ++k) s += *reinterpret_cast<const f32x4*>(slabs + so[k] + off);
       } else {
-        for (; k + kU <= k1; k += kU) {
+        for (; k < k1; k += kU) {
           float v[kU];
 #pragma unroll
-          for (int u = 0; u < kU; ++u) v[u] = slabs[so[k + u] + off];
+          for (int u = 0; u < kU; ++u)
+            if (k + u < k1) v[u] = slabs[so[k + u] + off];
 #pragma unroll
-          for (int u = 0; u < kU; ++u) s[0] += v[u];
+          for (int u = 0; u < kU; ++u)
+            if (k + u < k1) s[0] += v[u];
         }
-        for (; k < k1; ++k) s[0] += slabs[so[k] + off];
       }
+      k = k1;
       const float inv = inv_of(lev);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -1025,8 +1029,19 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const WgOut* __restrict__ 
     int k = 0;
     for (int lev = 0; lev < o.nlev; ++lev) {
       float s = 0.0f;
-      for (const int k1 = k + o.lev_items[lev]; k < k1; ++k)
-        s += bias_slabs[(size_t)(o.item0 + k) * 256 + o.row_off + t];
+      const int k1 = k + o.lev_items[lev];
+      // kU partials in flight, summed in item order (as one at a time, the same bits): a single load per
+      // step made this chain — one HBM/MALL latency per item of the output — the reduce's critical path
+      for (; k < k1; k += kU) {
+        float v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+          if (k + u < k1) v[u] = bias_slabs[(size_t)(o.item0 + k + u) * 256 + o.row_off + t];
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+          if (k + u < k1) s += v[u];
+      }
+      k = k1;
       const float v = s * inv_of(lev);
       acc = lev == 0 ? (accumulate ? o.bias_dst[t] + v : v) : acc + v;
     }

@@ -975,6 +975,12 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const WgOut* __restrict__ 
   const int ne = o.nrows * o.ncols;
   constexpr int kU = 8;  // item slabs in flight per step
   const int64_t* so = slab_off + o.item0;  // item i writes slab i: no item-table indirection
+  // the output's slab offsets staged in LDS once (as scalar loads inside the k loop each round of
+  // partials waited for its offsets first); an output with more items reads the rest from memory
+  __shared__ int64_t s_off[256];
+  if ((int)threadIdx.x < o.nitems) s_off[threadIdx.x] = so[threadIdx.x];
+  __syncthreads();
+  auto slab = [&](int k) { return k < 256 ? s_off[k] : so[k]; };
   auto inv_of = [&](int lev) { return amax ? delta_scale(amax + lev, true) : 1.0f; };  // exact powers of 2
   const bool vec = reduce_vec(o.ncols, o.col_off);
   if (vec ? 4 * t < ne : t < ne) {
@@ -993,7 +999,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const WgOut* __restrict__ 
           f32x4 v[kU];
 #pragma unroll
           for (int u = 0; u < kU; ++u)
-            if (k + u < k1) v[u] = *reinterpret_cast<const f32x4*>(slabs + so[k + u] + off);
+            if (k + u < k1) v[u] = *reinterpret_cast<const f32x4*>(slabs + slab(k + u) + off);
 #pragma unroll
           for (int u = 0; u < kU; ++u)
             if (k + u < k1) s += v[u];
@@ -1003,7 +1009,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const WgOut* __restrict__ 
           float v[kU];
 #pragma unroll
           for (int u = 0; u < kU; ++u)
-            if (k + u < k1) v[u] = slabs[so[k + u] + off];
+            if (k + u < k1) v[u] = slabs[slab(k + u) + off];
 #pragma unroll
           for (int u = 0; u < kU; ++u)
             if (k + u < k1) s[0] += v[u];

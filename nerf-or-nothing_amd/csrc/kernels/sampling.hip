@@ -49,16 +49,42 @@ __global__ __launch_bounds__(64) void k_sample_pdf(int n, int B, const float* __
                                                    int32_t* __restrict__ idx_out) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* wb = smem;           // [B]   blurred weights, then pdf
-  float* cdf = smem + B;      // [B+1]
+  float* cdf = smem + B;      // [B+1] (first the input weights, staged)
+  float* trs = smem + 2 * B + 1;  // [B+1] the ray's input t row, staged
   __shared__ float s_wsum;
   const int r = blockIdx.x;
   const int lane = threadIdx.x;
   const float* wr = w + (size_t)r * B;
+  const float* tr = t_in + (size_t)r * (B + 1);
+  // the weights and the t row staged in LDS by loads all issued before the first is waited for (as
+  // per-element global reads — three dependent ones per blur element, two per sample — the chain of
+  // load latencies was most of this kernel's time)
+  {
+    constexpr int kR = 9;  // B + 1 <= 576 staged by the unrolled loads; longer rows by the loop below
+    float v[kR], u[kR];
+#pragma unroll
+    for (int j = 0; j < kR; ++j) {
+      const int i = lane + 64 * j;
+      if (i < B) v[j] = wr[i];
+      if (i <= B) u[j] = tr[i];
+    }
+#pragma unroll
+    for (int j = 0; j < kR; ++j) {
+      const int i = lane + 64 * j;
+      if (i < B) cdf[i] = v[j];
+      if (i <= B) trs[i] = u[j];
+    }
+    for (int i = lane + 64 * kR; i <= B; i += 64) {
+      if (i < B) cdf[i] = wr[i];
+      trs[i] = tr[i];
+    }
+  }
+  __syncthreads();
   // blur-pool: wmax[i] = max(pad[i], pad[i+1]); wb[i] = .5(wmax[i] + wmax[i+1]) + padding (MH:646-661)
   for (int i = lane; i < B; i += 64) {
-    const float w0 = wr[i];
-    const float wl = i == 0 ? w0 : wr[i - 1];
-    const float wh = i == B - 1 ? w0 : wr[i + 1];
+    const float w0 = cdf[i];
+    const float wl = i == 0 ? w0 : cdf[i - 1];
+    const float wh = i == B - 1 ? w0 : cdf[i + 1];
     const float m0 = fmaxf(wl, w0);
     const float m1 = fmaxf(w0, wh);
     wb[i] = 0.5f * (m0 + m1) + padding;
@@ -92,7 +118,6 @@ __global__ __launch_bounds__(64) void k_sample_pdf(int n, int B, const float* __
   __syncthreads();
   const int ns = S_out + 1;
   const float s1 = 1.0f / (float)ns;
-  const float* tr = t_in + (size_t)r * (B + 1);
   for (int s = lane; s < ns; s += 64) {
     float u;
     if (randomized) {
@@ -107,7 +132,7 @@ __global__ __launch_bounds__(64) void k_sample_pdf(int n, int B, const float* __
       if (cdf[mid] <= u) lo = mid; else hi = mid - 1;
     }
     NOF_DCHECK(lo >= 0 && lo < B, kChkSampleIdx);  // a bin of the input t row
-    const float b0 = tr[lo], b1 = tr[lo + 1], c0 = cdf[lo], c1 = cdf[lo + 1];
+    const float b0 = trs[lo], b1 = trs[lo + 1], c0 = cdf[lo], c1 = cdf[lo + 1];
     const float denom = c1 - c0;
     float tt = denom > 0.0f ? (u - c0) / denom : 0.0f;
     tt = fminf(fmaxf(tt, 0.0f), 1.0f);
@@ -165,7 +190,7 @@ hipError_t launch_sample_pdf(int n, int S_in, const float* t_in, const float* w,
                              int randomized, uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base,
                              float* t_out, int32_t* idx_out, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  const size_t shm = sizeof(float) * (2 * S_in + 1);
+  const size_t shm = sizeof(float) * (3 * S_in + 2);
   hipLaunchKernelGGL(k_sample_pdf, dim3(n), dim3(64), shm, st, n, S_in, t_in, w, S_out, padding, randomized, seed,
                      step, level, ray_base, t_out, idx_out);
   return hipGetLastError();

@@ -42,6 +42,18 @@ __global__ void k_sample_stratified(int n, int S, const float* __restrict__ near
 }
 
 // One 64-lane workgroup per ray.  LDS: wb[B] then cdf[B+1].
+// the sequential fp32 cdf of a pdf row (lane 0).  pdf and cdf are disjoint LDS rows: restrict lets the
+// compiler issue the pdf reads ahead of the cdf writes (else each read waits for the previous write)
+__device__ __forceinline__ void cdf_chain(const float* __restrict__ pdf, float* __restrict__ cdf, int B) {
+  cdf[0] = 0.0f;
+  float run = 0.0f;
+  for (int i = 0; i < B - 1; ++i) {
+    run = run + pdf[i];
+    cdf[i + 1] = fminf(1.0f, run);
+  }
+  cdf[B] = 1.0f;
+}
+
 __global__ __launch_bounds__(64) void k_sample_pdf(int n, int B, const float* __restrict__ t_in,
                                                    const float* __restrict__ w, int S_out, float padding,
                                                    int randomized, uint64_t seed, uint32_t step, uint32_t level,
@@ -107,13 +119,7 @@ __global__ __launch_bounds__(64) void k_sample_pdf(int n, int B, const float* __
   for (int i = lane; i < B; i += 64) wb[i] = wb[i] / wsum;   // pdf
   __syncthreads();
   if (lane == 0) {  // sequential fp32 cumsum: a parallel scan would change the rounding
-    cdf[0] = 0.0f;
-    float run = 0.0f;
-    for (int i = 0; i < B - 1; ++i) {
-      run = run + wb[i];
-      cdf[i + 1] = fminf(1.0f, run);
-    }
-    cdf[B] = 1.0f;
+    cdf_chain(wb, cdf, B);
   }
   __syncthreads();
   const int ns = S_out + 1;

@@ -93,7 +93,7 @@ EDITS = {
                    "__host__ __device__ constexpr int epi_half_pos(int s, int nk) { return nk >= 16 ? 5 + 8 * s : 2 + 2 * s; }")],
     # resampler phases removed (timings only): the double weight sum, the cdf cumsum, the sample loop
     "pdf_nosum": [(K + "sampling.hip", "    for (int i = 0; i < B; ++i) acc += (double)wb[i];", "    acc = (double)wb[0];")],
-    "pdf_nocdf": [(K + "sampling.hip", "    for (int i = 0; i < B - 1; ++i) {\n      run = run + wb[i];", "    for (int i = 0; i < 0; ++i) {\n      run = run + wb[i];")],
+    "pdf_nocdf": [(K + "sampling.hip", "  for (int i = 0; i < B - 1; ++i) {\n    run = run + pdf[i];", "  for (int i = 0; i < 0; ++i) {\n    run = run + pdf[i];")],
     "pdf_nosample": [(K + "sampling.hip", "  for (int s = lane; s < ns; s += 64) {\n    float u;", "  for (int s = lane; s < 0; s += 64) {\n    float u;")],
     # side-output store cache policy: default instead of nt (fp32 / fp16-block kernels and F16)
     "store_default": [(K + "mlp16.h", "constexpr int kStoreNT = 2;", "constexpr int kStoreNT = 0;"),

@@ -103,6 +103,7 @@ static void check_cfg(const nof_config& c) {
                   c.precision == NOF_PRECISION_F16X2 || c.precision == NOF_PRECISION_F32_F16SPLIT ||
                   c.precision == NOF_PRECISION_F16,
               "unknown precision mode");
+  NOF_REQUIRE(c.grad_buckets == 0 || c.grad_buckets == 1, "grad_buckets must be 0 or 1");
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -197,6 +197,7 @@ void RayDataset::next(int n, uint64_t seed, uint32_t step, uint32_t ray_base, hi
     if (!(pre_.same(nk) && pre_buf_ == pb && prefetch_error_.empty())) {
       pre_ = nk;
       pre_buf_ = pb;
+      prefetch_error_.clear();  // an earlier prefetch's error belongs to that request, not to this one
       prefetch_ = std::thread([this, pb, n, seed, step, ray_base] {
         try {
           NOF_HIP(hipSetDevice(device_));

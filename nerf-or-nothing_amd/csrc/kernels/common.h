@@ -124,7 +124,7 @@ __device__ inline float softplus_f(float x) { return x > 20.0f ? x : log1pf(expf
 __device__ inline float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 constexpr float kRgbPadding = 0.001f;
-constexpr float kRgbScale = 1.0f + 2.0f * 0.001f;  // (1 + 2*RgbPadding), MNcs:308
+constexpr float kRgbScale = 1.0f + 2.0f * 0.001f;  // (1 + 2*RgbPadding), MNcs:22,151
 constexpr float kDensityBias = -1.0f;              // MNcs:20
 constexpr float kHalfPi = 3.14159274f * 0.5f;      // MathF.PI * 0.5f, MH:446
 

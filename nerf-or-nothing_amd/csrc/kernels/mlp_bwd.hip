@@ -7,7 +7,7 @@
 // masks come from the forward's packed bits, and every delta_l is written once in the
 // block-swizzled [F][32] layout for the deterministic weight-gradient GEMMs (wgrad.hip).
 // Gradient routing per D11: dh7 = W8^T dz_s + W9[:, :256]^T delta9 ; dh3 = W4[:, :256]^T delta4.
-// Heads per MNcs:410-415 with the sigmoid' written as s(1-s) (overflow-safe, D28).
+// Heads per MNcs:23-28,184-189 with the sigmoid' written as s(1-s) (overflow-safe, D28).
 #include <algorithm>
 
 #include "common.h"
@@ -88,7 +88,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_bwd(BwdArgs a) {
 
   first_slice_dma<P>(a.wimg_b, lds, tid);
 
-  // ---- heads (MNcs:410-415) ------------------------------------------------------------
+  // ---- heads (MNcs:23-28,184-189) ------------------------------------------------------------
   const f32x4 zh = reinterpret_cast<const f32x4*>(a.zhead)[m];
   float dzs = a.dsigma[m] * sigmoid_f(zh[0] + kDensityBias);
   float dzc[3];

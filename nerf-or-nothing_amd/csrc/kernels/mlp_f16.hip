@@ -5,12 +5,14 @@
 // Replaces, for this mode, cast_rays (AF:292-317), encode_input_data (AF:187-221), the 11 per-layer
 // launches of AcceleratedMLP::get_output (MLPcpp:214-255: get_neuron_output*, AF:36-90) and of
 // AcceleratedMLP::get_gradient's dX part (MLPcpp:256-321: backpropagate_neuron*, AF:91-182).
-// Semantics per MLP.CallCached (MLPcs:112-136), the C# heads (MNcs:307-309, D23) and their
-// derivatives (MNcs:410-415, D28); gradient routing per D11 (dh7 = W8^T dz_s + W9[:, :256]^T delta9,
+// Semantics per MLP.CallCached (MLPcs:112-136), the C# heads (MNcs:19-22,151-152, D23) and their
+// derivatives (MNcs:23-28,184-189, D28); gradient routing per D11 (dh7 = W8^T dz_s + W9[:, :256]^T delta9,
 // dh3 = W4[:, :256]^T delta4).  Numerics: every product is one fp16 x fp16 MFMA term accumulated in
 // fp32 (weights and activations rounded to fp16, deltas power-of-two scaled then rounded), the IPE
 // from a double-float range reduction and the hardware sin / exp2 (the encodings are rounded to fp16
 // before any product, so their ~1e-7 error is below that rounding).
+#include <atomic>
+
 #include "common.h"
 #include "geometry.h"
 #include "launch.h"
@@ -253,10 +255,13 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
     const int b = min(gg * kH32Waves + wave, nblk - 1), mm0 = b * kBlk;
     const int ry = __builtin_amdgcn_readfirstlane(mm0 / a.S);
     float* slot = lds + kTin + wave * 64;
-    uint32_t l4 = (uint32_t)min(lane, kBlk) * 4u;  // (recomputed opaquely: hoisted out of the loop it stays live)
+    uint32_t l4 = (uint32_t)lane * 4u;  // (recomputed opaquely: hoisted out of the loop it stays live)
     asm volatile("" : "+v"(l4));
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(h32_rsrc(a.t + (size_t)ry * (a.S + 1) + (mm0 - ry * a.S)), (lptr_t)slot, 4,
-                                             l4, 0, 0, 0);
+    // lanes 0..32 only: the 33 t land in slot[0, 33) and nothing of this DMA overlaps the ray values at
+    // slot[40, 49), which their own DMAs below write (no ordering between the DMAs is assumed)
+    if (lane <= kBlk)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(h32_rsrc(a.t + (size_t)ry * (a.S + 1) + (mm0 - ry * a.S)), (lptr_t)slot,
+                                               4, l4, 0, 0, 0);
     if (lane < 3) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(h32_rsrc(a.dirs + 3 * ry), (lptr_t)(slot + 40), 4, l4, 0, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(h32_rsrc(a.origins + 3 * ry), (lptr_t)(slot + 44), 4, l4, 0, 0, 0);
@@ -483,7 +488,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk) eV.piece(3, kk, 16);  // the last view tile: nothing left to hide it under
 
-  // ---- heads: sigma = softplus(z_s - 1), rgb = sigmoid(z_c) 1.002 - 0.001 (MNcs:307-309) -------------
+  // ---- heads: sigma = softplus(z_s - 1), rgb = sigmoid(z_c) 1.002 - 0.001 (MNcs:19-22,151-152) -------------
   float zs = eY.zs;
   zs += __shfl_xor(zs, 32, 64);
   zs += hb[0];
@@ -622,7 +627,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   const uint32_t* masks_blk = a.masks + (size_t)blk * kMaskSlots * 256 + lane * 4;
   auto mask_of = [&](int l) { return *reinterpret_cast<const uint4*>(masks_blk + l * 256); };
 
-  // ---- heads (MNcs:410-415), scaled by the level's power of two ---------------------------------------
+  // ---- heads (MNcs:23-28,184-189), scaled by the level's power of two ---------------------------------------
   if (first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the first group's inputs (later: the ring barriers)
   u32x4 mk9v, mk7v;
   f32x4 zh;
@@ -716,12 +721,16 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-int device_cus() {  // compute units of the current device (cached per device)
-  static int cus[64] = {};
+int device_cus() {  // compute units of the current device (cached per device; any host thread may ask)
+  static std::atomic<int> cus[64] = {};
   int d = 0;
   if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return 256;
-  if (!cus[d] && hipDeviceGetAttribute(&cus[d], hipDeviceAttributeMultiprocessorCount, d) != hipSuccess) cus[d] = 256;
-  return cus[d];
+  int n = cus[d].load(std::memory_order_relaxed);
+  if (!n) {  // concurrent first calls store the same value
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || n <= 0) n = 256;
+    cus[d].store(n, std::memory_order_relaxed);
+  }
+  return n;
 }
 
 hipError_t launch_mlp_fwd_h32(const FwdArgs& a, hipStream_t st) {

@@ -4,7 +4,7 @@
 // Replaces cast_rays (AF:292-317), encode_input_data (AF:187-221) and the 11 per-layer
 // launches of AcceleratedMLP::get_output (MLPcpp:214-255: get_neuron_output*, AF:36-90) with
 // one launch per level.  Semantics per MLP.CallCached (MLPcs:112-136) and the C# heads
-// (MNcs:307-309, D23): sigma = softplus(z_s - 1), rgb = sigmoid(z_c) * 1.002 - 0.001.
+// (MNcs:19-22,151-152, D23): sigma = softplus(z_s - 1), rgb = sigmoid(z_c) * 1.002 - 0.001.
 //
 // Per wave (16 samples of one ray): the 24 IPE features of its lanes computed in registers (the B
 // operand of layer 0 and of the skip layer: kept in registers beside the fp32 4-slot weight ring,

@@ -106,7 +106,7 @@ struct Spec {
 
 // Config constants the reference hard-codes as float (MNcs:19-22, TrainState.cs:69).
 static const float kRgbPadding = 0.001f;
-static const float kRgbScale = 1.0f + 2.0f * 0.001f;  // (1 + 2*RgbPadding) in fp32 (MNcs:308)
+static const float kRgbScale = 1.0f + 2.0f * 0.001f;  // (1 + 2*RgbPadding) in fp32 (MNcs:22,151)
 static const float kDensityBias = -1.0f;
 static const float kHalfPi = 3.14159274f * 0.5f;      // MathF.PI * 0.5f (MH:446)
 
@@ -489,10 +489,10 @@ static void step(const Spec& sp, const float* P, const StepIO& io) {
         mlp_forward_sample<T>(sp, P, enc.data(), dpe.data(), c, mk);
         flipsp[tid][lv] += c.flips;
         zs[lv][k] = c.zs;
-        sig[lv][k] = softplus<T>(c.zs + (T)kDensityBias);                       // MNcs:309
+        sig[lv][k] = softplus<T>(c.zs + (T)kDensityBias);                       // MNcs:19-20,152
         for (int j = 0; j < 3; ++j) {
           zc[lv][3 * k + j] = c.zc[j];
-          rgb[lv][3 * k + j] = sigm<T>(c.zc[j]) * (T)kRgbScale - (T)kRgbPadding;    // MNcs:307-308
+          rgb[lv][3 * k + j] = sigm<T>(c.zc[j]) * (T)kRgbScale - (T)kRgbPadding;    // MNcs:21-22,151
         }
       }
       render_ray<T>(S, sig[lv].data(), rgb[lv].data(), tl[lv].data(), d, io.white, Cl[lv].data(), w[lv].data(), al[lv].data(), tr[lv].data());
@@ -519,7 +519,7 @@ static void step(const Spec& sp, const float* P, const StepIO& io) {
       if (io.drgb_out && io.drgb_out[lv]) std::memcpy((T*)io.drgb_out[lv] + (size_t)r * 3 * S, dc.data(), sizeof(T) * 3 * S);
       if (io.grads) {
         for (int k = 0; k < S; ++k) {
-          // activation gradients MNcs:410-415 (sigmoid' written as s(1-s), D28-style overflow safety)
+          // activation gradients MNcs:23-28,184-189 (sigmoid' written as s(1-s), D28-style overflow safety)
           const T dzs = ds[k] * sigm<T>(zs[lv][k] + (T)kDensityBias);
           T dzc[3];
           for (int j = 0; j < 3; ++j) {

@@ -162,15 +162,21 @@ def test_config4_shard_vs_oracle(gpu, oracle):
 
 @pytest.mark.parametrize("precision", [4, 0])
 def test_persistent_groups_with_partial_tail(gpu, oracle, precision):
-    """1025 rays x 128+128: 4 100 sample blocks = 513 groups of 8 per level, so on a 256-CU part the F16
-    kernels' persistent workgroup 0 runs three groups (0, 256, 512) and the last is partial (4 blocks, its
-    other waves duplicate the last block); the next groups' inputs are prefetched across group boundaries.
+    """4 x CUs + 1 rays x 128+128 (1025 on a 256-CU part): 4 n sample blocks = 2 CUs + 1 groups of 8 per
+    level, so the F16 kernels' persistent workgroup 0 (one per CU) runs three groups (0, CUs, 2 CUs) and the
+    last is partial (4 blocks, its other waves duplicate the last block); the next groups' inputs are
+    prefetched across group boundaries.
     Per-sample outputs do not depend on the grouping: the last 8 rays' forward outputs and integrator
     adjoint equal, bitwise, those of an 8-ray batch of the same rays (same global ids, same loss-mult sum,
     same parameters), and match the oracle's own forward within the mode's tolerance."""
     import nof
 
-    n, samples, tail = 1025, (128, 128), 8
+    import torch
+
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    n, samples, tail = 4 * cus + 1, (128, 128), 8
+    groups = -(-(n * samples[0] // 32) // 8)
+    assert groups == 2 * cus + 1 and (n * samples[0] // 32) % 8 == 4, "three groups on workgroup 0, the last partial"
     seed, step, base = 0x5EED0007, 3, 4096
     r = _rays("blender", n, seed=77)
     msum = float(np.sum(r["lossmult"], dtype=np.float32))

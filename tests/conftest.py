@@ -36,6 +36,17 @@ def gpu():
     return torch.device("cuda", 0)
 
 
+# The F16 mode's gradient bound (NOF_PRECISION_F16), per gradient tensor, relative L2 against an
+# fp64 oracle that makes its OWN ReLU decisions.  Its forward rounds weights and activations to fp16 before
+# every product, so units with |z| within fp16 rounding of 0 gate the other way than fp64 does; each such
+# flip moves every gradient below that unit, most of all W0's (the deepest delta times the fp16 IPE).
+# Measured (GPUTEST r05): W0 3.3e-3 at config 2 (1024 x 128+128), 4.9e-3 at configs[4]'s per-GPU shape
+# (512 LLFF rays x 256+256), 3.1e-3 on the two-ray golden fixture; the median tensor 5e-4, the whole
+# arena 2.9e-4.  With the GPU's ReLU decisions adopted the gradients are within 2e-3 (measured 5.3e-4);
+# the forward outputs and the integrator adjoint are within 2e-3 without adoption.
+F16_GRAD_TOL = 1e-2
+
+
 def rel_l2(a, b):
     import numpy as np
 

@@ -62,7 +62,17 @@ typedef struct nof_config {
                                              a bucketed step sum every gradient element in the same order and a
                                              data-parallel run is bitwise the same attached or not.  Installing
                                              a gradient-bucket hook (nof_dp_attach) selects 1 (build extension) */
+  int32_t lindisp;                        /* 0: t linear in depth; 1: linear in disparity (MipNerfModel.LinDisp,
+                                             MNcs:14, SampleAlongRay MH:618-620); default 0 */
+  int32_t ray_shape;                      /* NOF_RAY_CONICAL (MNcs:15, MH:391-402) or NOF_RAY_CYLINDRICAL
+                                             (CylinderToGaussian MH:403-409); default conical */
 } nof_config;
+/* The struct grows at its end only (grad_buckets, then lindisp / ray_shape were appended): a binding
+ * compiled against an older header passes a shorter struct.  nof_config_size() is sizeof(nof_config) of
+ * this library; a binding checks it against its own struct size before passing one. */
+size_t nof_config_size(void);
+
+enum { NOF_RAY_CONICAL = 0, NOF_RAY_CYLINDRICAL = 1 };
 
 /* MLP contraction arithmetic.  Every mode holds operands and accumulators in fp32 between the
  * MFMAs; they differ in how the MFMAs form products.
@@ -410,14 +420,14 @@ nof_status nof_stream_sync(void* stream);
  * encode_input_data AF:187-221, volumetric_rendering AF:318-344, volumetric_rendering_gradient
  * AF:362-402 (g = dL/dC given, or fused from pixels when dev_g == NULL). */
 nof_status nof_kernel_sample_stratified(int32_t n, int32_t samples, const float* nears, const float* fars,
-                                        int32_t randomized, uint64_t seed, uint32_t step, uint32_t level,
-                                        uint32_t ray_base, float* t_out, void* stream);
+                                        int32_t randomized, int32_t lindisp, uint64_t seed, uint32_t step,
+                                        uint32_t level, uint32_t ray_base, float* t_out, void* stream);
 nof_status nof_kernel_sample_pdf(int32_t n, int32_t samples_in, const float* t_in, const float* weights,
                                  int32_t samples_out, float padding, int32_t randomized, uint64_t seed,
                                  uint32_t step, uint32_t level, uint32_t ray_base, float* t_out, int32_t* idx_out,
                                  void* stream);
 nof_status nof_kernel_cast(int32_t n, int32_t samples, const float* t, const float* origins, const float* dirs,
-                           const float* radii, float* means, float* covs, void* stream);
+                           const float* radii, int32_t ray_shape, float* means, float* covs, void* stream);
 nof_status nof_kernel_encode(int32_t n, int32_t samples, const float* means, const float* covs, const float* dirs,
                              float* enc_pos, float* enc_dir, void* stream);
 nof_status nof_kernel_render(int32_t n, int32_t samples, const float* density, const float* rgb, const float* t,

@@ -97,7 +97,11 @@ void nof_config_default(nof_config* c) {
   c->stream = nullptr;
   c->precision = NOF_PRECISION_F32;
   c->grad_buckets = 0;
+  c->lindisp = 0;
+  c->ray_shape = NOF_RAY_CONICAL;
 }
+
+size_t nof_config_size(void) { return sizeof(nof_config); }
 
 const char* nof_last_error(void) { return g_err.c_str(); }
 const char* nof_version(void) { return "nerf-or-nothing_amd 0.1 (gfx950)"; }
@@ -550,11 +554,12 @@ nof_status nof_stream_sync(void* stream) { return guard([&] { NOF_HIP(hipStreamS
 
 // ---- individual kernels ---------------------------------------------------------------------
 nof_status nof_kernel_sample_stratified(int32_t n, int32_t S, const float* nears, const float* fars, int32_t rnd,
-                                        uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base, float* t,
-                                        void* stream) {
+                                        int32_t lindisp, uint64_t seed, uint32_t step, uint32_t level,
+                                        uint32_t ray_base, float* t, void* stream) {
   return guard([&] {
-    ARG(n >= 0 && S > 0 && nears && fars && t);
-    NOF_HIP(nof::launch_sample_stratified(n, S, nears, fars, rnd, seed, step, level, ray_base, t, (hipStream_t)stream));
+    ARG(n >= 0 && S > 0 && nears && fars && t && (lindisp == 0 || lindisp == 1));
+    NOF_HIP(nof::launch_sample_stratified(n, S, nears, fars, rnd, seed, step, level, ray_base, t, (hipStream_t)stream,
+                                          lindisp));
   });
 }
 nof_status nof_kernel_sample_pdf(int32_t n, int32_t S_in, const float* t_in, const float* w, int32_t S_out,
@@ -567,10 +572,11 @@ nof_status nof_kernel_sample_pdf(int32_t n, int32_t S_in, const float* t_in, con
   });
 }
 nof_status nof_kernel_cast(int32_t n, int32_t S, const float* t, const float* o, const float* d, const float* r,
-                           float* mean, float* cov, void* stream) {
+                           int32_t ray_shape, float* mean, float* cov, void* stream) {
   return guard([&] {
-    ARG(n >= 0 && S > 0 && t && o && d && r && mean && cov);
-    NOF_HIP(nof::launch_cast(n, S, t, o, d, r, mean, cov, (hipStream_t)stream));
+    ARG(n >= 0 && S > 0 && t && o && d && r && mean && cov &&
+        (ray_shape == NOF_RAY_CONICAL || ray_shape == NOF_RAY_CYLINDRICAL));
+    NOF_HIP(nof::launch_cast(n, S, t, o, d, r, mean, cov, (hipStream_t)stream, ray_shape));
   });
 }
 nof_status nof_kernel_encode(int32_t n, int32_t S, const float* mean, const float* cov, const float* d, float* ep,

@@ -104,6 +104,8 @@ static void check_cfg(const nof_config& c) {
                   c.precision == NOF_PRECISION_F16,
               "unknown precision mode");
   NOF_REQUIRE(c.grad_buckets == 0 || c.grad_buckets == 1, "grad_buckets must be 0 or 1");
+  NOF_REQUIRE(c.lindisp == 0 || c.lindisp == 1, "lindisp must be 0 or 1");
+  NOF_REQUIRE(c.ray_shape == NOF_RAY_CONICAL || c.ray_shape == NOF_RAY_CYLINDRICAL, "unknown ray_shape");
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -194,6 +196,7 @@ void AcceleratedMLP::pack_weights() {
     pa.zero = amax_.p;
     pa.nzero = (int)lv_.size();
     amax_cleared_ = (1u << lv_.size()) - 1u;
+    amax_given_ = 0u;
   }
   tb(kTPack);
   if (precision_ == NOF_PRECISION_F16)
@@ -202,6 +205,13 @@ void AcceleratedMLP::pack_weights() {
     NOF_HIP(nof::launch_pack_weights_x3(params_.p, pa, wimg_f_.p, wimg_b_.p, f16_pieces() ? 2 : 1, st_));
   else NOF_HIP(nof::launch_pack_weights(params_.p, pa, wimg_f_.p, wimg_b_.p, st_));
   te(kTPack);
+}
+
+uint32_t* AcceleratedMLP::claim_delta_amax(int level) {
+  if (!f16_pieces() || level < 0 || level >= (int)lv_.size() || !((amax_cleared_ >> level) & 1u)) return nullptr;
+  amax_cleared_ &= ~(1u << level);
+  amax_given_ |= 1u << level;
+  return amax_.p + level;
 }
 
 void AcceleratedMLP::run_forward(int level, const nof::FwdArgs& a0) {
@@ -230,6 +240,7 @@ void AcceleratedMLP::forward_fused(int level, int n, int samples, const float* t
   nof::FwdArgs a{};
   a.M = M; a.S = samples; a.encoded = 0;
   a.no_store = inference ? 1 : 0;
+  a.cylinder = cfg_.ray_shape == NOF_RAY_CYLINDRICAL ? 1 : 0;
   a.t = t; a.origins = origins; a.dirs = dirs; a.radii = radii;
   run_forward(level, a);
 }
@@ -554,21 +565,42 @@ void AcceleratedMLP::run_wgrad(Schedule& sc, int accumulate) {
   te(kTWgradReduce);
 }
 
-void AcceleratedMLP::run_backward(int level, const float* color_grad, const float* density_grad) {
+nof::BwdArgs AcceleratedMLP::bwd_args(int level, const float* color_grad, const float* density_grad) {
   Level& L = lv_[level];
   nof::BwdArgs b{};
   b.M = L.M;
   b.split = precision_;
   if (f16_pieces()) {  // the level's power-of-two delta scale
-    const bool cleared = (amax_cleared_ >> level) & 1u;  // by this step's pack launch, not used since
-    amax_cleared_ &= ~(1u << level);
-    NOF_HIP(nof::launch_delta_amax(density_grad, color_grad, L.M, amax_.p + level, st_, numeric_.p, cleared));
+    if ((amax_given_ >> level) & 1u) {  // filled by the integrator adjoint (claim_delta_amax)
+      amax_given_ &= ~(1u << level);
+    } else {
+      const bool cleared = (amax_cleared_ >> level) & 1u;  // by this step's pack launch, not used since
+      amax_cleared_ &= ~(1u << level);
+      NOF_HIP(nof::launch_delta_amax(density_grad, color_grad, L.M, amax_.p + level, st_, numeric_.p, cleared));
+    }
     b.amax = amax_.p + level;
   }
   b.dsigma = density_grad; b.drgb = color_grad; b.zhead = L.zhead.p;
   b.masks = L.masks.p;
   b.wimg_b = wimg_b_.p;
   b.delta = L.delta.p; b.delta9x = L.delta9x.p;
+  return b;
+}
+
+void AcceleratedMLP::run_backward(int level, const float* color_grad, const float* density_grad) {
+  const nof::BwdArgs b = bwd_args(level, color_grad, density_grad);
+  tb(kTMlpBwd);
+  NOF_HIP(nof::launch_mlp_bwd(b, st_));
+  te(kTMlpBwd);
+}
+
+// F16: two levels' dX chains as ONE persistent launch (level 0's groups, then level 1's; the same
+// arithmetic per group as two launches)
+void AcceleratedMLP::run_backward2(int level, const float* const* color_grads, const float* const* density_grads) {
+  nof::BwdArgs b = bwd_args(level, color_grads[0], density_grads[0]);
+  const nof::BwdArgs b1 = bwd_args(level + 1, color_grads[1], density_grads[1]);
+  b.M1 = b1.M; b.dsigma1 = b1.dsigma; b.drgb1 = b1.drgb; b.zhead1 = b1.zhead; b.amax1 = b1.amax;
+  b.masks1 = b1.masks; b.delta1 = b1.delta; b.delta9x1 = b1.delta9x;
   tb(kTMlpBwd);
   NOF_HIP(nof::launch_mlp_bwd(b, st_));
   te(kTMlpBwd);
@@ -622,7 +654,10 @@ float* const* AcceleratedMLP::get_gradient_levels(const float* const* color_grad
   if (!buckets) (void)schedule(0, nl);
   else
     for (int b = 0; b < kBuckets; ++b) (void)schedule(0, nl, b);
-  for (int l = 0; l < nl; ++l) run_backward(l, color_grads[l], density_grads[l]);
+  int l = 0;
+  if (precision_ == NOF_PRECISION_F16)  // levels in pairs: one persistent backward launch per pair
+    for (; l + 1 < nl; l += 2) run_backward2(l, color_grads + l, density_grads + l);
+  for (; l < nl; ++l) run_backward(l, color_grads[l], density_grads[l]);
   return wgrad_levels(0, nl, (flags & NOF_GRAD_ACCUMULATE) ? 1 : 0, buckets);
 }
 
@@ -698,7 +733,7 @@ float* const* AcceleratedMipNeRF::run(int n, const float* o, const float* d, con
     timer.begin(kTSample);
     if (lv == 0) {
       NOF_HIP(nof::launch_sample_stratified(n, S, nears, fars, cfg_.randomized, seed_, step_, 0, ray_base_,
-                                            t_[0].p, st_));
+                                            t_[0].p, st_, cfg_.lindisp));
     } else {
       NOF_HIP(nof::launch_sample_pdf(n, cfg_.num_samples[lv - 1], t_[lv - 1].p, w_[lv - 1].p, S,
                                      cfg_.resample_padding, cfg_.randomized, seed_, step_, (uint32_t)lv, ray_base_,
@@ -711,19 +746,38 @@ float* const* AcceleratedMipNeRF::run(int n, const float* o, const float* d, con
                                    w_[lv].p, st_, nullptr, nullptr, mlp->numeric_flags()));
     timer.end(kTRenderFwd);
   }
-  for (int lv = 0; lv < L; ++lv) {  // MNcpp:125-134
-    const int S = cfg_.num_samples[lv];
-    const float lam = lv < L - 1 ? cfg_.coarse_loss_mult : 1.0f;
-    const float* g = nullptr;
-    if (cb) {
-      g = reinterpret_cast<const float*>(cb(user, (uint64_t)(uintptr_t)C_[lv].p, lv, msum, (uint64_t)(uintptr_t)lm));
-      NOF_REQUIRE(g != nullptr, "output-gradient callback returned null");
+  // MNcpp:125-134: the loss gradient and the integrator adjoint of every level (with the f16 modes' delta
+  // maxima), levels of equal sample count in one launch when no callback supplies dL/dC, else one level
+  // at a time after its callback
+  {
+    nof::RenderBwdArgs ra{};
+    ra.n = n; ra.d = d; ra.white = cfg_.white_bkgd; ra.pix = pix; ra.lossmult = lm; ra.msum = msum;
+    ra.nonfinite = mlp->numeric_flags();
+    int nb = 0;
+    auto flush = [&]() {
+      if (!nb) return;
+      timer.begin(kTRenderBwd);
+      NOF_HIP(nof::launch_render_bwd(ra, nb, st_));
+      timer.end(kTRenderBwd);
+      nb = 0;
+    };
+    for (int lv = 0; lv < L; ++lv) {
+      const int S = cfg_.num_samples[lv];
+      const float* g = nullptr;
+      if (cb) {
+        g = reinterpret_cast<const float*>(cb(user, (uint64_t)(uintptr_t)C_[lv].p, lv, msum, (uint64_t)(uintptr_t)lm));
+        NOF_REQUIRE(g != nullptr, "output-gradient callback returned null");
+      }
+      if (nb && (cb || S != ra.S || nb == nof::kRenderMaxLevels)) flush();
+      ra.S = S;
+      nof::RenderBwdLevel& R = ra.lv[nb++];
+      R.sigma = mlp->density(lv); R.rgb = mlp->rgb(lv); R.t = t_[lv].p; R.C = C_[lv].p; R.g_ext = g;
+      R.lam = lv < L - 1 ? cfg_.coarse_loss_mult : 1.0f;
+      R.dsigma = dsig_[lv].p; R.drgb = drgb_[lv].p; R.loss_rays = cb ? nullptr : loss_rays_[lv].p;
+      R.amax = mlp->claim_delta_amax(lv);
+      if (cb) flush();
     }
-    timer.begin(kTRenderBwd);
-    NOF_HIP(nof::launch_render_bwd(n, S, mlp->density(lv), mlp->rgb(lv), t_[lv].p, d, cfg_.white_bkgd, C_[lv].p, g,
-                                   pix, lm, msum, lam, dsig_[lv].p, drgb_[lv].p, cb ? nullptr : loss_rays_[lv].p,
-                                   st_));
-    timer.end(kTRenderBwd);
+    flush();
   }
   // MNcpp:135-142 (level 0 overwrites unless accumulating, later levels add): every level's dX chain,
   // then one weight-gradient launch over both levels' operands
@@ -749,7 +803,8 @@ void AcceleratedMipNeRF::Render(int n, const float* o, const float* d, const flo
   for (int lv = 0; lv < L; ++lv) {  // MNcs:40-95
     const int S = cfg_.num_samples[lv];
     if (lv == 0) {
-      NOF_HIP(nof::launch_sample_stratified(n, S, nears, fars, randomized, seed_, step_, 0, ray_base_, t_[0].p, st_));
+      NOF_HIP(nof::launch_sample_stratified(n, S, nears, fars, randomized, seed_, step_, 0, ray_base_, t_[0].p, st_,
+                                            cfg_.lindisp));
     } else {
       NOF_HIP(nof::launch_sample_pdf(n, cfg_.num_samples[lv - 1], t_[lv - 1].p, w_[lv - 1].p, S,
                                      cfg_.resample_padding, randomized, seed_, step_, (uint32_t)lv, ray_base_,

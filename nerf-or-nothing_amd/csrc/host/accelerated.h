@@ -146,6 +146,10 @@ class AcceleratedMLP {
   nof_mlp_debug debug_view(int level) const;
   // non-finite flags: [0] forward (set by the owner's integrator), [1] output gradients (f16x2 scaling)
   uint32_t* numeric_flags() const { return numeric_.p; }
+  // The fused step's integrator adjoint takes a level's delta-scale maximum (f16 modes) from the values
+  // it writes: the level's amax word to fill (zeroed by this step's pack launch), or null when the mode
+  // has none or the word is not fresh; the level's backward then skips its k_delta_amax pass.
+  uint32_t* claim_delta_amax(int level);
 
  private:
   struct Schedule {
@@ -164,7 +168,9 @@ class AcceleratedMLP {
     DevBuf<uint32_t> masks;
   };
   void run_forward(int level, const nof::FwdArgs& a);
+  nof::BwdArgs bwd_args(int level, const float* color_grad, const float* density_grad);  // (+ its amax pass)
   void run_backward(int level, const float* color_grad, const float* density_grad);
+  void run_backward2(int level, const float* const* color_grads, const float* const* density_grads);
   // weight-gradient schedule of levels [lv0, lv1) at their current sample counts: bucket -1 = every
   // problem, b >= 0 = the problems whose outputs belong to bucket b (see bucket_spans)
   Schedule& schedule(int lv0, int lv1, int bucket = -1);
@@ -197,6 +203,7 @@ class AcceleratedMLP {
   DevBuf<float> slabs_, bias_slabs_;
   DevBuf<uint32_t> amax_;  // f16 modes: per level, bits of max |dsigma|, |drgb| (the level's delta scale)
   uint32_t amax_cleared_ = 0;  // levels whose amax word the last pack launch zeroed and no pass used yet
+  uint32_t amax_given_ = 0;    // levels whose amax word a claim_delta_amax caller fills (no k_delta_amax)
   DevBuf<uint32_t> numeric_;
   size_t slab_cap_ = 0;
 };

@@ -1,5 +1,6 @@
 // fp32 geometry with the reference's exact operation order (contraction disabled):
-// conical frustum -> Gaussian (ConicalFrustumToGaussian MH:391-402, cast_rays AF:292-317)
+// conical frustum (or cylinder) -> Gaussian (ConicalFrustumToGaussian MH:391-402, CylinderToGaussian
+// MH:403-409, cast_rays AF:292-317)
 // and the integrated positional encoding (IntegratedPositionalEncoding MH:429-449).
 // These feed bit-exactness contracts, so every expression mirrors oracle/oracle.cpp.
 #pragma once
@@ -7,18 +8,26 @@
 
 namespace nof {
 
+// cylinder (RayShape.Cylindrical, MNcs:15): CylinderToGaussian MH:403-409 instead
 __device__ inline void frustum_gaussian(float t0, float t1, const float o[3], const float d[3], float radius,
-                                        float mean[3], float cov[3]) {
+                                        float mean[3], float cov[3], bool cylinder = false) {
 #pragma clang fp contract(off)
   const float dms = fmaxf(1e-10f, (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
-  const float mu = (t0 + t1) / 2.0f;
-  const float hw = (t1 - t0) / 2.0f;
-  const float mu2 = mu * mu;
-  const float hw2 = hw * hw;
-  const float den = 3.0f * mu2 + hw2;
-  const float tmean = mu + (2.0f * mu * hw2) / den;
-  const float tvar = hw2 / 3.0f - (4.0f / 15.0f) * (hw2 * hw2 * (12.0f * mu2 - hw2)) / (den * den);
-  const float rvar = radius * radius * (mu2 / 4.0f + (5.0f / 12.0f) * hw2 - (4.0f / 15.0f) * (hw2 * hw2) / den);
+  float tmean, tvar, rvar;
+  if (cylinder) {  // MH:405-407
+    tmean = (t0 + t1) / 2.0f;
+    rvar = radius * radius / 4.0f;
+    tvar = (t1 - t0) * (t1 - t0) / 12.0f;
+  } else {
+    const float mu = (t0 + t1) / 2.0f;
+    const float hw = (t1 - t0) / 2.0f;
+    const float mu2 = mu * mu;
+    const float hw2 = hw * hw;
+    const float den = 3.0f * mu2 + hw2;
+    tmean = mu + (2.0f * mu * hw2) / den;
+    tvar = hw2 / 3.0f - (4.0f / 15.0f) * (hw2 * hw2 * (12.0f * mu2 - hw2)) / (den * den);
+    rvar = radius * radius * (mu2 / 4.0f + (5.0f / 12.0f) * hw2 - (4.0f / 15.0f) * (hw2 * hw2) / den);
+  }
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     mean[j] = d[j] * tmean + o[j];

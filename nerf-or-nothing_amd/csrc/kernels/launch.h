@@ -17,14 +17,16 @@ uint32_t check_unit_dataset(bool clear);
 hipError_t launch_check_selftest(hipStream_t st);  // fails kChkSelfTest on purpose
 
 // ---- sampling.hip (get_sample_t_vals AF:222-242, get_resampled_t_vals AF:246-291) ----------
+// lindisp: t linear in disparity (SampleAlongRay MH:618-620) instead of depth
 hipError_t launch_sample_stratified(int n, int S, const float* nears, const float* fars, int randomized,
                                     uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base, float* t,
-                                    hipStream_t st);
+                                    hipStream_t st, int lindisp = 0);
 hipError_t launch_sample_pdf(int n, int S_in, const float* t_in, const float* w, int S_out, float padding,
                              int randomized, uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base,
                              float* t_out, int32_t* idx_out, hipStream_t st);
+// ray_shape 1: cylinders (CylinderToGaussian MH:403-409) instead of conical frustums
 hipError_t launch_cast(int n, int S, const float* t, const float* o, const float* d, const float* radius,
-                       float* mean, float* cov, hipStream_t st);
+                       float* mean, float* cov, hipStream_t st, int ray_shape = 0);
 hipError_t launch_encode(int n, int S, const float* mean, const float* cov, const float* d, float* enc_pos,
                          float* enc_dir, hipStream_t st);
 
@@ -40,6 +42,24 @@ hipError_t launch_render_bwd(int n, int S, const float* sigma, const float* rgb,
                              int white, const float* C, const float* g_ext, const float* pix,
                              const float* lossmult, float loss_mult_sum, float lam, float* dsigma, float* drgb,
                              float* loss_rays, hipStream_t st);
+// Several levels of S samples per ray in one launch (the fused step's loss gradient + adjoint of every
+// level): lv[l] the level's inputs / outputs; lv[l].amax (optional, zero on entry) receives the bits of
+// max(|dsigma|, |drgb|) over the level (launch_delta_amax's value), a.nonfinite word 1 its non-finite flag.
+constexpr int kRenderMaxLevels = 4;
+struct RenderBwdLevel {
+  const float *sigma, *rgb, *t, *C, *g_ext;
+  float lam;
+  float *dsigma, *drgb, *loss_rays;
+  uint32_t* amax;
+};
+struct RenderBwdArgs {
+  int n, S, white;
+  const float *d, *pix, *lossmult;
+  float msum;
+  uint32_t* nonfinite;
+  RenderBwdLevel lv[kRenderMaxLevels];
+};
+hipError_t launch_render_bwd(const RenderBwdArgs& a, int nlev, hipStream_t st);
 hipError_t launch_output_gradient(int n, const float* C, const float* pix, const float* lossmult,
                                   float loss_mult_sum, float lam, float* g, hipStream_t st);
 
@@ -48,6 +68,7 @@ struct FwdArgs {
   int M, S, encoded;
   int no_store;                            // 1: inference only, skip the backward's side outputs
   int split;                               // MLP precision: 0 fp32, 1 bf16x3 split, 2 f16x2 (mlp_common.h)
+  int cylinder;                            // fused encoding: cylinders (MH:403-409) instead of conical frustums
   const float *t, *origins, *dirs, *radii;  // fused-encoding inputs
   const float *enc_pos, *enc_dir;          // encoded inputs (API path): [M][96], [n][27]
   const float* wimg;                       // packed forward image (slices + tail)
@@ -70,6 +91,12 @@ struct BwdArgs {
   const float* wimg_b;                     // packed backward image (slices + tail)
   float* delta;    // [8][M/32][256][32]
   float* delta9x;  // [M/32][160][32]
+  // F16 (k_mlp_bwd_h32) only: a second level's dX chain in the same launch (M1 > 0), its 256-sample groups
+  // after the first level's — one persistent launch per step instead of one per level
+  int M1;
+  const float *dsigma1, *drgb1, *zhead1;
+  const uint32_t *amax1, *masks1;
+  float *delta1, *delta9x1;
 };
 hipError_t launch_mlp_bwd(const BwdArgs& a, hipStream_t st);
 // f16x2 mode: *amax = bits of max(|dsigma|, |drgb|) over M samples (clears *amax first); nonfinite

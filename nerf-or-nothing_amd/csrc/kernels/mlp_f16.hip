@@ -386,7 +386,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   uint32_t ix[3][4], iy[3][4];
   if (!a.encoded) {
     float mean[3], cov[3];
-    frustum_gaussian(in.t0, in.t1, in.o3, d3, in.rad, mean, cov);
+    frustum_gaussian(in.t0, in.t1, in.o3, d3, in.rad, mean, cov, a.cylinder != 0);
     float mu_h[3], nv_h[3];
     const float sh = h ? 256.0f : 1.0f;  // 2^(8h)
 #pragma unroll
@@ -569,10 +569,33 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   __shared__ __attribute__((aligned(16))) float lds[kIn + kH32Waves * kInFloats];
   const int tid = threadIdx.x, lane = tid & 63, x = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nblk = a.M / kBlk;
-  const int ngroups = (nblk + kH32Waves - 1) / kH32Waves;
-  NOF_DCHECK(a.M % kBlk == 0, kChkMlpBlock);
+  // level 0's groups 0 .. ng0 - 1, then level 1's (a.M1 > 0): the ring streams on across the level boundary
+  const int nblk0 = a.M / kBlk, nblk1 = a.M1 / kBlk;
+  const int ng0 = (nblk0 + kH32Waves - 1) / kH32Waves;
+  const int ngroups = ng0 + (nblk1 + kH32Waves - 1) / kH32Waves;
+  NOF_DCHECK(a.M % kBlk == 0 && a.M1 % kBlk == 0, kChkMlpBlock);
   const float* tail = a.wimg_b + kBwdH32Floats;
+  // the level of group gg and its block b (the tail group's waves past the level's end duplicate its last
+  // block): wave-uniform values, selected per group
+  struct GrpLv {
+    int nblk, blk;
+    const float *dsigma, *drgb, *zhead;
+    const uint32_t* masks;
+    float *delta, *delta9x;
+  };
+  auto grp = [&](int gg) {
+    GrpLv v;
+    const bool second = gg >= ng0;
+    v.nblk = second ? nblk1 : nblk0;
+    v.blk = min((second ? gg - ng0 : gg) * kH32Waves + wave, v.nblk - 1);
+    v.dsigma = second ? a.dsigma1 : a.dsigma;
+    v.drgb = second ? a.drgb1 : a.drgb;
+    v.zhead = second ? a.zhead1 : a.zhead;
+    v.masks = second ? a.masks1 : a.masks;
+    v.delta = second ? a.delta1 : a.delta;
+    v.delta9x = second ? a.delta9x1 : a.delta9x;
+    return v;
+  };
 
   H32Ring<kBwdDmaLate> ring;
   ring.lds = lds;
@@ -583,8 +606,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   }
   if (tid < 96) *reinterpret_cast<f32x4*>(lds + kW10 + 4 * tid) = *reinterpret_cast<const f32x4*>(tail + kBwdTailW10 + 4 * tid);
   const uint32_t vrow = slot_off(x, h);
-  const size_t lstride = (size_t)nblk * kBlk * kWidth;
-  const float sc = delta_scale(a.amax, false);
+  const float sc0 = delta_scale(a.amax, false), sc1 = a.M1 > 0 ? delta_scale(a.amax1, false) : 1.0f;
   // VMEM instructions a group issues outside the layers (ring.add_ops: a lower bound): the delta9x tiles
   // (8 halves + the heads' 8 bytes) and, after the first group, its predecessor's last delta0 tile (two
   // halves); the loads are not counted (the dsigma / drgb loads may be merged)
@@ -599,20 +621,22 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   // vmcnt(0) from the compiler.
   float* const in_slot = lds + kIn + wave * kInFloats;
   auto in_dma = [&](int gg) {
-    const int b = min(gg * kH32Waves + wave, nblk - 1), mm0 = b * kBlk;
-    // (the lane offsets recomputed here, opaquely: hoisted out of the group loop they are spilled, and a
-    // scratch reload's wait is a full vmcnt drain)
-    uint32_t l16 = (uint32_t)lane * 16u, l4 = (uint32_t)lane * 4u;
-    asm volatile("" : "+v"(l16), "+v"(l4));
-    const __amdgpu_buffer_rsrc_t rm = h32_rsrc(a.masks + (size_t)b * kMaskSlots * 256);
+    const GrpLv v = grp(gg);
+    const int b = v.blk, mm0 = b * kBlk;
+    // (the lane offsets recomputed here from a lane id the compiler cannot hoist or reuse: kept live across
+    // the group loop they are spilled, and a scratch reload's wait is a full vmcnt drain)
+    uint32_t id;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(id));
+    const uint32_t l16 = id * 16u, l4 = id * 4u;
+    const __amdgpu_buffer_rsrc_t rm = h32_rsrc(v.masks + (size_t)b * kMaskSlots * 256);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, (lptr_t)in_slot, 16, l16, 8 * 1024, 0, 0);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, (lptr_t)(in_slot + 256), 16, l16, 7 * 1024, 0, 0);
     if (lane < kBlk) {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(h32_rsrc(a.zhead + (size_t)mm0 * 4), (lptr_t)(in_slot + 512), 16, l16, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(h32_rsrc(a.dsigma + mm0), (lptr_t)(in_slot + 736), 4, l4, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(h32_rsrc(v.zhead + (size_t)mm0 * 4), (lptr_t)(in_slot + 512), 16, l16, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(h32_rsrc(v.dsigma + mm0), (lptr_t)(in_slot + 736), 4, l4, 0, 0, 0);
     }
     if (lane < kBlk * 3 / 4)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(h32_rsrc(a.drgb + (size_t)mm0 * 3), (lptr_t)(in_slot + 640), 16, l16, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(h32_rsrc(v.drgb + (size_t)mm0 * 3), (lptr_t)(in_slot + 640), 16, l16, 0, 0, 0);
   };
   constexpr int kInOps = 5;
   in_dma(blockIdx.x);
@@ -620,11 +644,13 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   // Persistent: workgroup b runs groups b, b + G, ...; the weight ring streams on across groups.
   for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
   const bool first = g == (int)blockIdx.x;
-  const int blk_raw = g * kH32Waves + wave;
-  const int blk = blk_raw < nblk ? blk_raw : nblk - 1;
+  const GrpLv lv = grp(g);
+  const int blk = lv.blk;
   const int m0 = blk * kBlk;
-  NOF_DCHECK(blk >= 0 && blk < nblk, kChkMlpBlock);
-  const uint32_t* masks_blk = a.masks + (size_t)blk * kMaskSlots * 256 + lane * 4;
+  const size_t lstride = (size_t)lv.nblk * kBlk * kWidth;
+  const float sc = g >= ng0 ? sc1 : sc0;
+  NOF_DCHECK(blk >= 0 && blk < lv.nblk, kChkMlpBlock);
+  const uint32_t* masks_blk = lv.masks + (size_t)blk * kMaskSlots * 256 + lane * 4;
   auto mask_of = [&](int l) { return *reinterpret_cast<const uint4*>(masks_blk + l * 256); };
 
   // ---- heads (MNcs:23-28,184-189), scaled by the level's power of two ---------------------------------------
@@ -653,7 +679,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   }
   // ---- delta9 = (W10^T dz_rgb) * relu'(layer 9) -> the B fragments of dh7, and delta9x ------------------
   uint32_t X[16][4], Y[16][4];
-  const __amdgpu_buffer_rsrc_t d9 = h32_rsrc(reinterpret_cast<const _Float16*>(a.delta9x) + (size_t)m0 * kD9F);
+  const __amdgpu_buffer_rsrc_t d9 = h32_rsrc(reinterpret_cast<const _Float16*>(lv.delta9x) + (size_t)m0 * kD9F);
   {
     if (first) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the W10 table written
     const float* w10 = lds + kW10;
@@ -684,7 +710,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   if (first) h32_prologue_barrier();  // w8 table written, the first periods landed
 
   f32x16 acc[2];
-  const _Float16* delta = reinterpret_cast<const _Float16*>(a.delta) + (size_t)m0 * kWidth;
+  const _Float16* delta = reinterpret_cast<const _Float16*>(lv.delta) + (size_t)m0 * kWidth;
   BwdEpiH eX(acc, X, vrow), eY(acc, Y, vrow);
   NoEpiH none;
   auto srcX = [&](int kk, uint32_t (&b)[4]) {
@@ -742,8 +768,7 @@ hipError_t launch_mlp_fwd_h32(const FwdArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 hipError_t launch_mlp_bwd_h32(const BwdArgs& a, hipStream_t st) {
-  const int nblk = a.M / kBlk;
-  const int ngroups = (nblk + kH32Waves - 1) / kH32Waves;
+  const int ngroups = (a.M / kBlk + kH32Waves - 1) / kH32Waves + (a.M1 / kBlk + kH32Waves - 1) / kH32Waves;
   hipLaunchKernelGGL(k_mlp_bwd_h32, dim3(std::min(ngroups, device_cus())), dim3(kH32Threads), 0, st, a);
   return hipGetLastError();
 }

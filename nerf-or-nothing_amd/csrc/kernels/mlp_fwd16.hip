@@ -112,7 +112,7 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_fwd16(FwdArgs a) {
     const float o3[3] = {a.origins[3 * ray], a.origins[3 * ray + 1], a.origins[3 * ray + 2]};
     const float* tr = a.t + (size_t)ray * (a.S + 1) + s0 + j;
     float mean[3], cov[3];
-    frustum_gaussian(tr[0], tr[1], o3, d3, a.radii[ray], mean, cov);
+    frustum_gaussian(tr[0], tr[1], o3, d3, a.radii[ray], mean, cov, a.cylinder != 0);
 #pragma unroll
     for (int t = 0; t < 6; ++t)
 #pragma unroll

@@ -150,58 +150,84 @@ __global__ __launch_bounds__(256) void k_render_fwd(int n, int S, const float* _
 
 // dL/dc_k = g w_k ;  dL/dsigma_k = delta_k |d| [T_{k+1} e_k - sum_{j>k} w_j e_j],  e_k = g.c_k - G
 // (the C# recursion MH:565-596 in closed form; G = g.1 under a white background).
+// One launch covers the levels of RenderBwdArgs (blockIdx.y = level, all with S samples per ray).  With
+// lv.amax set, the level's delta-scale maximum max(|dsigma|, |drgb|) (the f16 modes' k_delta_amax,
+// mlp_bwd.hip) is taken here from the values just computed, one atomicMax of the float bits per block
+// (max is order-free: the same bits as the separate pass), *amax zero on entry.
 template <int PER>
-__global__ __launch_bounds__(256) void k_render_bwd(int n, int S, const float* __restrict__ sigma,
-                                                    const float* __restrict__ rgb, const float* __restrict__ t,
-                                                    const float* __restrict__ d, int white,
-                                                    const float* __restrict__ C, const float* __restrict__ g_ext,
-                                                    const float* __restrict__ pix, const float* __restrict__ lossmult,
-                                                    float msum, float lam, float* __restrict__ dsigma,
-                                                    float* __restrict__ drgb, float* __restrict__ loss_rays) {
+__global__ __launch_bounds__(256) void k_render_bwd(RenderBwdArgs a) {
+  const RenderBwdLevel& L = a.lv[blockIdx.y];
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= n) return;
-  RayState<PER> rs;
-  ray_alpha_T<PER>(S, r, lane, sigma, t, d, rs);
-  float g0, g1, g2;
-  if (g_ext) {
-    g0 = g_ext[3 * r]; g1 = g_ext[3 * r + 1]; g2 = g_ext[3 * r + 2];
-  } else {  // AF:356-358 order: 2*m/sum*(C-p)*lambda
-    const float m = lossmult[r];
-    const float s = 2.0f * m / msum;
-    const float e0 = C[3 * r] - pix[3 * r], e1 = C[3 * r + 1] - pix[3 * r + 1], e2 = C[3 * r + 2] - pix[3 * r + 2];
-    g0 = s * e0 * lam; g1 = s * e1 * lam; g2 = s * e2 * lam;
-    if (loss_rays && lane == 0) loss_rays[r] = lam * m * ((e0 * e0 + e1 * e1) + e2 * e2) / msum;
-  }
-  const float G = white ? (g0 + g1 + g2) : 0.0f;
-  const int k0 = lane * PER;
-  float cr[3 * PER], dc[3 * PER], ds[PER];
-  vload<3 * PER, kRgbAlign<PER>>(rgb + ((size_t)r * S + k0) * 3, cr);
-  float wk[PER], ek[PER];
-  float ls = 0.0f;
+  const bool live = r < a.n;  // wave-uniform (every wave reaches the block's amax barrier)
+  float vmax = 0.0f;
+  bool bad = false;
+  if (live) {
+    RayState<PER> rs;
+    ray_alpha_T<PER>(a.S, r, lane, L.sigma, L.t, a.d, rs);
+    float g0, g1, g2;
+    if (L.g_ext) {
+      g0 = L.g_ext[3 * r]; g1 = L.g_ext[3 * r + 1]; g2 = L.g_ext[3 * r + 2];
+    } else {  // AF:356-358 order: 2*m/sum*(C-p)*lambda
+      const float m = a.lossmult[r];
+      const float s = 2.0f * m / a.msum;
+      const float e0 = L.C[3 * r] - a.pix[3 * r], e1 = L.C[3 * r + 1] - a.pix[3 * r + 1], e2 = L.C[3 * r + 2] - a.pix[3 * r + 2];
+      g0 = s * e0 * L.lam; g1 = s * e1 * L.lam; g2 = s * e2 * L.lam;
+      if (L.loss_rays && lane == 0) L.loss_rays[r] = L.lam * m * ((e0 * e0 + e1 * e1) + e2 * e2) / a.msum;
+    }
+    const float G = a.white ? (g0 + g1 + g2) : 0.0f;
+    const int k0 = lane * PER;
+    float cr[3 * PER], dc[3 * PER], ds[PER];
+    vload<3 * PER, kRgbAlign<PER>>(L.rgb + ((size_t)r * a.S + k0) * 3, cr);
+    float wk[PER], ek[PER];
+    float ls = 0.0f;
 #pragma unroll
-  for (int p = 0; p < PER; ++p) {
-    wk[p] = rs.a[p] * rs.T[p];
-    ek[p] = (g0 * cr[3 * p] + g1 * cr[3 * p + 1]) + g2 * cr[3 * p + 2] - G;
-    dc[3 * p] = g0 * wk[p]; dc[3 * p + 1] = g1 * wk[p]; dc[3 * p + 2] = g2 * wk[p];
-    ls += wk[p] * ek[p];
-  }
-  vstore<3 * PER, kRgbAlign<PER>>(drgb + ((size_t)r * S + k0) * 3, dc);
-  float inc = ls;  // inclusive suffix sum over lanes
+    for (int p = 0; p < PER; ++p) {
+      wk[p] = rs.a[p] * rs.T[p];
+      ek[p] = (g0 * cr[3 * p] + g1 * cr[3 * p + 1]) + g2 * cr[3 * p + 2] - G;
+      dc[3 * p] = g0 * wk[p]; dc[3 * p + 1] = g1 * wk[p]; dc[3 * p + 2] = g2 * wk[p];
+      ls += wk[p] * ek[p];
+    }
+    vstore<3 * PER, kRgbAlign<PER>>(L.drgb + ((size_t)r * a.S + k0) * 3, dc);
+    float inc = ls;  // inclusive suffix sum over lanes
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const float y = __shfl_down(inc, o, 64);
-    if (lane + o < 64) inc += y;
-  }
-  float after = __shfl_down(inc, 1, 64);  // sum over lanes > lane
-  if (lane == 63) after = 0.0f;
+    for (int o = 1; o < 64; o <<= 1) {
+      const float y = __shfl_down(inc, o, 64);
+      if (lane + o < 64) inc += y;
+    }
+    float after = __shfl_down(inc, 1, 64);  // sum over lanes > lane
+    if (lane == 63) after = 0.0f;
 #pragma unroll
-  for (int p = PER - 1; p >= 0; --p) {
-    const float Tn = rs.T[p] * (1.0f - rs.a[p]);
-    ds[p] = (Tn * ek[p] - after) * (rs.tv[p + 1] - rs.tv[p]) * rs.dl;
-    after += wk[p] * ek[p];
+    for (int p = PER - 1; p >= 0; --p) {
+      const float Tn = rs.T[p] * (1.0f - rs.a[p]);
+      ds[p] = (Tn * ek[p] - after) * (rs.tv[p + 1] - rs.tv[p]) * rs.dl;
+      after += wk[p] * ek[p];
+    }
+    vstore<PER, PER>(L.dsigma + (size_t)r * a.S + k0, ds);
+    if (L.amax) {  // fmaxf drops NaN: non-finite values are flagged separately (k_delta_amax's rule)
+#pragma unroll
+      for (int q = 0; q < 3 * PER; ++q) {
+        const float x = fabsf(dc[q]);
+        bad |= !__builtin_isfinite(x);
+        vmax = fmaxf(vmax, x);
+      }
+#pragma unroll
+      for (int p = 0; p < PER; ++p) {
+        const float x = fabsf(ds[p]);
+        bad |= !__builtin_isfinite(x);
+        vmax = fmaxf(vmax, x);
+      }
+    }
   }
-  vstore<PER, PER>(dsigma + (size_t)r * S + k0, ds);
+  if (L.amax) {  // block-uniform
+    if (bad && a.nonfinite) a.nonfinite[1] = 1u;  // plain store of a constant: racing writers agree
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) vmax = fmaxf(vmax, __shfl_xor(vmax, o, 64));
+    __shared__ float wmax[4];
+    if (lane == 0) wmax[threadIdx.x >> 6] = vmax;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicMax(L.amax, __float_as_uint(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]))));
+  }
 }
 
 __global__ void k_output_gradient(int n, const float* __restrict__ C, const float* __restrict__ pix,
@@ -232,15 +258,25 @@ hipError_t launch_render_fwd(int n, int S, const float* sigma, const float* rgb,
   return hipGetLastError();
 }
 
+hipError_t launch_render_bwd(const RenderBwdArgs& a, int nlev, hipStream_t st) {
+  if (a.n <= 0 || nlev <= 0) return hipSuccess;
+  if (nlev > kRenderMaxLevels) return hipErrorInvalidValue;
+  const dim3 grid((a.n + 3) / 4, nlev), block(256);
+  const int S = a.S;
+  NOF_RENDER_DISPATCH(S, hipLaunchKernelGGL(k_render_bwd<PER>, grid, block, 0, st, a));
+  return hipGetLastError();
+}
+
 hipError_t launch_render_bwd(int n, int S, const float* sigma, const float* rgb, const float* t, const float* d,
                              int white, const float* C, const float* g_ext, const float* pix,
                              const float* lossmult, float loss_mult_sum, float lam, float* dsigma, float* drgb,
                              float* loss_rays, hipStream_t st) {
-  if (n <= 0) return hipSuccess;
-  const dim3 grid((n + 3) / 4), block(256);
-  NOF_RENDER_DISPATCH(S, hipLaunchKernelGGL(k_render_bwd<PER>, grid, block, 0, st, n, S, sigma, rgb, t, d, white, C,
-                                            g_ext, pix, lossmult, loss_mult_sum, lam, dsigma, drgb, loss_rays));
-  return hipGetLastError();
+  RenderBwdArgs a{};
+  a.n = n; a.S = S; a.d = d; a.white = white; a.pix = pix; a.lossmult = lossmult; a.msum = loss_mult_sum;
+  RenderBwdLevel& L = a.lv[0];
+  L.sigma = sigma; L.rgb = rgb; L.t = t; L.C = C; L.g_ext = g_ext; L.lam = lam;
+  L.dsigma = dsigma; L.drgb = drgb; L.loss_rays = loss_rays;
+  return launch_render_bwd(a, 1, st);
 }
 
 hipError_t launch_output_gradient(int n, const float* C, const float* pix, const float* lossmult,

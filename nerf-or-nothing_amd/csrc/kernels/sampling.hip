@@ -14,27 +14,29 @@
 
 namespace nof {
 
-__device__ inline float lin_t(int k, int S, float nr, float fr) {
+// t_k linear in depth (MH:622) or, lindisp, in disparity (MH:618-620: 1 / (1/near (1 - s) + 1/far s))
+__device__ inline float lin_t(int k, int S, float nr, float fr, bool lindisp) {
   const float tv = (float)k / (float)S;
-  return nr * (1.0f - tv) + fr * tv;
+  return lindisp ? 1.0f / (1.0f / nr * (1.0f - tv) + 1.0f / fr * tv) : nr * (1.0f - tv) + fr * tv;
 }
 
 // One thread per t-value: t_i = lower_i + (upper_i - lower_i) * u_i, lower=[t0,mids], upper=[mids,tS] (D3).
 __global__ void k_sample_stratified(int n, int S, const float* __restrict__ nears, const float* __restrict__ fars,
-                                    int randomized, uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base,
-                                    float* __restrict__ t) {
+                                    int randomized, int lindisp, uint64_t seed, uint32_t step, uint32_t level,
+                                    uint32_t ray_base, float* __restrict__ t) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= n * (S + 1)) return;
   const int r = gid / (S + 1);
   const int i = gid - r * (S + 1);
   const float nr = nears[r], fr = fars[r];
   float ti;
+  const bool ld = lindisp != 0;
   if (!randomized) {
-    ti = lin_t(i, S, nr, fr);
+    ti = lin_t(i, S, nr, fr, ld);
   } else {
-    const float li = lin_t(i, S, nr, fr);
-    const float lower = i == 0 ? li : 0.5f * (lin_t(i - 1, S, nr, fr) + li);
-    const float upper = i == S ? li : 0.5f * (li + lin_t(i + 1, S, nr, fr));
+    const float li = lin_t(i, S, nr, fr, ld);
+    const float lower = i == 0 ? li : 0.5f * (lin_t(i - 1, S, nr, fr, ld) + li);
+    const float upper = i == S ? li : 0.5f * (li + lin_t(i + 1, S, nr, fr, ld));
     const float u = philox_uniform(seed, step, level, kStreamStratified, ray_base + (uint32_t)r, (uint32_t)i);
     ti = lower + (upper - lower) * u;
   }
@@ -149,8 +151,8 @@ __global__ __launch_bounds__(64) void k_sample_pdf(int n, int B, const float* __
 
 // cast_rays (AF:292-317) as a standalone kernel for the encoded-input API path / parity tests.
 __global__ void k_cast(int n, int S, const float* __restrict__ t, const float* __restrict__ o,
-                       const float* __restrict__ d, const float* __restrict__ radius, float* __restrict__ mean,
-                       float* __restrict__ cov) {
+                       const float* __restrict__ d, const float* __restrict__ radius, int cylinder,
+                       float* __restrict__ mean, float* __restrict__ cov) {
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= n * S) return;
   const int r = gid / S;
@@ -158,7 +160,7 @@ __global__ void k_cast(int n, int S, const float* __restrict__ t, const float* _
   const float oo[3] = {o[3 * r], o[3 * r + 1], o[3 * r + 2]};
   const float dd[3] = {d[3 * r], d[3 * r + 1], d[3 * r + 2]};
   float mu[3], cv[3];
-  frustum_gaussian(t[(size_t)r * (S + 1) + k], t[(size_t)r * (S + 1) + k + 1], oo, dd, radius[r], mu, cv);
+  frustum_gaussian(t[(size_t)r * (S + 1) + k], t[(size_t)r * (S + 1) + k + 1], oo, dd, radius[r], mu, cv, cylinder != 0);
   for (int j = 0; j < 3; ++j) { mean[(size_t)gid * 3 + j] = mu[j]; cov[(size_t)gid * 3 + j] = cv[j]; }
 }
 
@@ -184,11 +186,11 @@ __global__ void k_encode(int n, int S, const float* __restrict__ mean, const flo
 
 hipError_t launch_sample_stratified(int n, int S, const float* nears, const float* fars, int randomized,
                                     uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base, float* t,
-                                    hipStream_t st) {
+                                    hipStream_t st, int lindisp) {
   const int total = n * (S + 1);
   if (total <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_sample_stratified, dim3((total + 255) / 256), dim3(256), 0, st, n, S, nears, fars, randomized,
-                     seed, step, level, ray_base, t);
+                     lindisp, seed, step, level, ray_base, t);
   return hipGetLastError();
 }
 
@@ -203,10 +205,10 @@ hipError_t launch_sample_pdf(int n, int S_in, const float* t_in, const float* w,
 }
 
 hipError_t launch_cast(int n, int S, const float* t, const float* o, const float* d, const float* radius,
-                       float* mean, float* cov, hipStream_t st) {
+                       float* mean, float* cov, hipStream_t st, int ray_shape) {
   const int total = n * S;
   if (total <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_cast, dim3((total + 255) / 256), dim3(256), 0, st, n, S, t, o, d, radius, mean, cov);
+  hipLaunchKernelGGL(k_cast, dim3((total + 255) / 256), dim3(256), 0, st, n, S, t, o, d, radius, ray_shape, mean, cov);
   return hipGetLastError();
 }
 

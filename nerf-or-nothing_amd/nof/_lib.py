@@ -37,6 +37,7 @@ class nof_config(C.Structure):
         ("deg_view", C.c_int32), ("randomized", C.c_int32), ("white_bkgd", C.c_int32),
         ("resample_padding", C.c_float), ("coarse_loss_mult", C.c_float),
         ("seed", C.c_uint64), ("stream", C.c_void_p), ("precision", C.c_int32), ("grad_buckets", C.c_int32),
+        ("lindisp", C.c_int32), ("ray_shape", C.c_int32),
     ]
 
 
@@ -77,6 +78,7 @@ SIGNATURES = {
     "nof_config_default": [C.POINTER(nof_config)],
     "nof_last_error": [],
     "nof_version": [],
+    "nof_config_size": [],
     "nof_mipnerf_create": [C.POINTER(nof_config), C.POINTER(P)],
     "nof_mipnerf_destroy": [P],
     "nof_mipnerf_get_gradient": [P, I32, P, P, P, P, P, P, OUTPUT_GRAD_FN, P, C.POINTER(PP)],
@@ -153,15 +155,16 @@ SIGNATURES = {
     "nof_memcpy_d2d": [P, P, C.c_size_t, P],
     "nof_memset": [P, C.c_int, C.c_size_t],
     "nof_stream_sync": [P],
-    "nof_kernel_sample_stratified": [I32, I32, P, P, I32, U64, U32, U32, U32, P, P],
+    "nof_kernel_sample_stratified": [I32, I32, P, P, I32, I32, U64, U32, U32, U32, P, P],
     "nof_kernel_sample_pdf": [I32, I32, P, P, I32, F, I32, U64, U32, U32, U32, P, P, P],
-    "nof_kernel_cast": [I32, I32, P, P, P, P, P, P, P],
+    "nof_kernel_cast": [I32, I32, P, P, P, P, I32, P, P, P],
     "nof_kernel_encode": [I32, I32, P, P, P, P, P, P],
     "nof_kernel_render": [I32, I32, P, P, P, P, I32, P, P, P],
     "nof_kernel_render_grad": [I32, I32, P, P, P, P, I32, P, P, P, P, F, F, P, P, P],
     "nof_kernel_adam": [C.c_int64, P, P, P, P, F, I32, P],
 }
 _RESTYPE = {"nof_config_default": None, "nof_last_error": C.c_char_p, "nof_version": C.c_char_p,
+            "nof_config_size": C.c_size_t,
             "nof_lr_decay": C.c_float}
 
 _lib = None
@@ -189,6 +192,9 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = _RESTYPE.get(name, C.c_int32)
+        if L.nof_config_size() != C.sizeof(nof_config):  # the struct this binding passes must be the library's
+            raise RuntimeError(f"nof_config: the library expects {L.nof_config_size()} bytes, this binding "
+                               f"passes {C.sizeof(nof_config)} (include/nof.h and nof/_lib.py disagree)")
         _lib = L
     return _lib
 

@@ -117,13 +117,14 @@ template <class T> static inline T sigm(T x) { return T(1) / (T(1) + std::exp(-x
 // Geometry, fp32 exact op order
 // ---------------------------------------------------------------------------
 // Stratified sampling, mip-NeRF rule (D3): lower=[t0,mids], upper=[mids,tS], S+1 uniforms.
-// SampleAlongRay MH:611-631 (linear-in-depth branch MH:622, jitter MH:625-629).
+// SampleAlongRay MH:611-631: linear in depth (MH:622) or, with LinDisp (MNcs:14), linear in disparity
+// (MH:618-620: 1 / (1/near (1 - s) + 1/far s), the C# evaluation order); jitter MH:625-629.
 static void sample_stratified_ray(int S, float near_, float far_, bool randomized, uint64_t seed,
-                                  uint32_t step, uint32_t level, uint32_t ray, float* t /*S+1*/) {
+                                  uint32_t step, uint32_t level, uint32_t ray, float* t /*S+1*/, bool lindisp = false) {
   std::vector<float> lin(S + 1), mids(S);
   for (int i = 0; i <= S; ++i) {
     const float tv = (float)i / (float)S;
-    lin[i] = near_ * (1.0f - tv) + far_ * tv;
+    lin[i] = lindisp ? 1.0f / (1.0f / near_ * (1.0f - tv) + 1.0f / far_ * tv) : near_ * (1.0f - tv) + far_ * tv;
   }
   if (!randomized) { for (int i = 0; i <= S; ++i) t[i] = lin[i]; return; }
   for (int i = 0; i < S; ++i) mids[i] = 0.5f * (lin[i] + lin[i + 1]);
@@ -188,20 +189,28 @@ static void sample_pdf_ray(int S_in, const float* t_in /*S_in+1*/, const float* 
   }
 }
 
-// ConicalFrustumToGaussian MH:391-402 + LiftGaussian(diag) MH:367-379 + CastRay MH:410-428
-// (D21: S Gaussians from S+1 t-values, as AF:298-299).
-static void cast_ray(int S, const float* t, const float* o, const float* d, float radius, float* mean, float* cov) {
+// ConicalFrustumToGaussian MH:391-402 (or, RayShape.Cylindrical (MNcs:15), CylinderToGaussian MH:403-409)
+// + LiftGaussian(diag) MH:367-379 + CastRay MH:410-428 (D21: S Gaussians from S+1 t-values, as AF:298-299).
+static void cast_ray(int S, const float* t, const float* o, const float* d, float radius, float* mean, float* cov,
+                     bool cylinder = false) {
   const float dms = std::max(1e-10f, (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
   for (int k = 0; k < S; ++k) {
     const float t0 = t[k], t1 = t[k + 1];
-    const float mu = (t0 + t1) / 2.0f;
-    const float hw = (t1 - t0) / 2.0f;
-    const float mu2 = mu * mu;
-    const float hw2 = hw * hw;
-    const float den = 3.0f * mu2 + hw2;
-    const float tmean = mu + (2.0f * mu * hw2) / den;
-    const float tvar = hw2 / 3.0f - (4.0f / 15.0f) * (hw2 * hw2 * (12.0f * mu2 - hw2)) / (den * den);
-    const float rvar = radius * radius * (mu2 / 4.0f + (5.0f / 12.0f) * hw2 - (4.0f / 15.0f) * (hw2 * hw2) / den);
+    float tmean, tvar, rvar;
+    if (cylinder) {  // MH:405-407
+      tmean = (t0 + t1) / 2.0f;
+      rvar = radius * radius / 4.0f;
+      tvar = (t1 - t0) * (t1 - t0) / 12.0f;
+    } else {
+      const float mu = (t0 + t1) / 2.0f;
+      const float hw = (t1 - t0) / 2.0f;
+      const float mu2 = mu * mu;
+      const float hw2 = hw * hw;
+      const float den = 3.0f * mu2 + hw2;
+      tmean = mu + (2.0f * mu * hw2) / den;
+      tvar = hw2 / 3.0f - (4.0f / 15.0f) * (hw2 * hw2 * (12.0f * mu2 - hw2)) / (den * den);
+      rvar = radius * radius * (mu2 / 4.0f + (5.0f / 12.0f) * hw2 - (4.0f / 15.0f) * (hw2 * hw2) / den);
+    }
     for (int j = 0; j < 3; ++j) {
       mean[k * 3 + j] = d[j] * tmean + o[j];
       const float dd = d[j] * d[j];
@@ -435,6 +444,7 @@ struct StepIO {
   void* loss;              // T  scalar
   int nthreads;
   int64_t* mask_flips;     // [level] adopted ReLU decisions != the oracle's own (optional)
+  bool lindisp, cylinder;  // LinDisp / RayShape.Cylindrical (MNcs:14-15; default false / conical)
 };
 
 template <class T>
@@ -466,7 +476,8 @@ static void step(const Spec& sp, const float* P, const StepIO& io) {
       const int S = io.S[lv];
       tl[lv].resize(S + 1);
       if (lv == 0) {
-        sample_stratified_ray(S, io.near_[r], io.far_[r], io.randomized, io.seed, io.step, 0, io.ray_base + r, tl[0].data());
+        sample_stratified_ray(S, io.near_[r], io.far_[r], io.randomized, io.seed, io.step, 0, io.ray_base + r, tl[0].data(),
+                              io.lindisp);
       } else if (io.t_override && io.t_override[lv]) {
         std::memcpy(tl[lv].data(), io.t_override[lv] + (size_t)r * (S + 1), sizeof(float) * (S + 1));
       } else {
@@ -476,7 +487,7 @@ static void step(const Spec& sp, const float* P, const StepIO& io) {
         sample_pdf_ray(Sp, tl[lv - 1].data(), wf.data(), S, io.padding, io.randomized, io.seed, io.step, lv, io.ray_base + r, tl[lv].data(), nullptr);
       }
       std::vector<float> mean(3 * S), cov(3 * S);
-      cast_ray(S, tl[lv].data(), o, d, io.radius[r], mean.data(), cov.data());
+      cast_ray(S, tl[lv].data(), o, d, io.radius[r], mean.data(), cov.data(), io.cylinder);
       sig[lv].resize(S); rgb[lv].resize(3 * S); w[lv].resize(S); al[lv].resize(S); tr[lv].resize(S);
       zs[lv].resize(S); zc[lv].resize(3 * S); cache[lv].resize(S); Cl[lv].resize(3);
       std::vector<T> enc(sp.pos_in);
@@ -564,9 +575,10 @@ void orc_layer_sizes(const orc_spec* s, int32_t* out /*2L*/) {
 }
 
 void orc_sample_stratified(int32_t n, int32_t S, const float* nears, const float* fars, int32_t randomized,
-                           uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base, float* t) {
+                           uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base, float* t, int32_t lindisp) {
   for (int r = 0; r < n; ++r)
-    sample_stratified_ray(S, nears[r], fars[r], randomized != 0, seed, step, level, ray_base + r, t + (size_t)r * (S + 1));
+    sample_stratified_ray(S, nears[r], fars[r], randomized != 0, seed, step, level, ray_base + r, t + (size_t)r * (S + 1),
+                          lindisp != 0);
 }
 
 void orc_sample_pdf(int32_t n, int32_t S_in, const float* t_in, const float* w, int32_t S_out, float padding,
@@ -577,9 +589,11 @@ void orc_sample_pdf(int32_t n, int32_t S_in, const float* t_in, const float* w, 
                    level, ray_base + r, t_out + (size_t)r * (S_out + 1), idx ? idx + (size_t)r * (S_out + 1) : nullptr);
 }
 
-void orc_cast(int32_t n, int32_t S, const float* t, const float* o, const float* d, const float* radius, float* mean, float* cov) {
+void orc_cast(int32_t n, int32_t S, const float* t, const float* o, const float* d, const float* radius, float* mean, float* cov,
+              int32_t ray_shape) {
   for (int r = 0; r < n; ++r)
-    cast_ray(S, t + (size_t)r * (S + 1), o + 3 * r, d + 3 * r, radius[r], mean + (size_t)r * S * 3, cov + (size_t)r * S * 3);
+    cast_ray(S, t + (size_t)r * (S + 1), o + 3 * r, d + 3 * r, radius[r], mean + (size_t)r * S * 3, cov + (size_t)r * S * 3,
+             ray_shape == 1);
 }
 
 void orc_encode_f64(const orc_spec* s, int64_t m, const float* mean, const float* cov, double* enc) {
@@ -653,6 +667,7 @@ struct orc_step_args {
   void* const* dsigma_out; void* const* drgb_out; void* grads; void* loss;
   int32_t nthreads;
   int64_t* mask_flips;
+  int32_t lindisp, ray_shape;  // appended (0, 0 = the reference defaults)
 };
 
 static StepIO cvt(const orc_step_args* a) {
@@ -665,6 +680,8 @@ static StepIO cvt(const orc_step_args* a) {
   io.rgb_out = a->rgb_out; io.dsigma_out = a->dsigma_out; io.drgb_out = a->drgb_out; io.grads = a->grads; io.loss = a->loss;
   io.nthreads = a->nthreads;
   io.mask_flips = a->mask_flips;
+  io.lindisp = a->lindisp != 0;
+  io.cylinder = a->ray_shape == 1;
   return io;
 }
 

@@ -41,6 +41,7 @@ class OrcStepArgs(C.Structure):
         ("dsigma_out", C.POINTER(C.c_void_p)), ("drgb_out", C.POINTER(C.c_void_p)),
         ("grads", C.c_void_p), ("loss", C.c_void_p), ("nthreads", C.c_int32),
         ("mask_flips", C.c_void_p),
+        ("lindisp", C.c_int32), ("ray_shape", C.c_int32),
     ]
 
 
@@ -80,10 +81,10 @@ def _load():
     lib.orc_param_count.restype = C.c_int64
     lib.orc_layer_sizes.argtypes = [sp, i32p]
     lib.orc_sample_stratified.argtypes = [C.c_int32, C.c_int32, f32p, f32p, C.c_int32, C.c_uint64, C.c_uint32,
-                                          C.c_uint32, C.c_uint32, f32p]
+                                          C.c_uint32, C.c_uint32, f32p, C.c_int32]
     lib.orc_sample_pdf.argtypes = [C.c_int32, C.c_int32, f32p, f32p, C.c_int32, C.c_float, C.c_int32, C.c_uint64,
                                    C.c_uint32, C.c_uint32, C.c_uint32, f32p, i32p]
-    lib.orc_cast.argtypes = [C.c_int32, C.c_int32, f32p, f32p, f32p, f32p, f32p, f32p]
+    lib.orc_cast.argtypes = [C.c_int32, C.c_int32, f32p, f32p, f32p, f32p, f32p, f32p, C.c_int32]
     lib.orc_encode_f64.argtypes = [sp, C.c_int64, f32p, f32p, f64p]
     lib.orc_dir_pe_f64.argtypes = [sp, C.c_int32, f32p, f64p]
     lib.orc_mlp_forward_f64.argtypes = [sp, f32p, C.c_int64, f64p, f64p, f64p, f64p, C.c_void_p]
@@ -150,11 +151,12 @@ def glorot_init(spec: Spec, seed: int) -> np.ndarray:
 
 
 # --- geometry (fp32 spec) ---------------------------------------------------------------------
-def sample_stratified(nears, fars, S, randomized=True, seed=0, step=0, level=0, ray_base=0):
+def sample_stratified(nears, fars, S, randomized=True, seed=0, step=0, level=0, ray_base=0, lindisp=False):
+    """SampleAlongRay (MH:611-631): t linear in depth, or in disparity with lindisp (MNcs:14, MH:618-620)."""
     nears, fars = _f32(nears), _f32(fars)
     n = nears.shape[0]
     t = np.zeros((n, S + 1), np.float32)
-    lib().orc_sample_stratified(n, S, nears, fars, int(randomized), seed, step, level, ray_base, t)
+    lib().orc_sample_stratified(n, S, nears, fars, int(randomized), seed, step, level, ray_base, t, int(lindisp))
     return t
 
 
@@ -167,13 +169,14 @@ def sample_pdf(t_in, w, S_out, padding=0.01, randomized=True, seed=0, step=0, le
     return t, idx
 
 
-def cast(t, o, d, radius):
+def cast(t, o, d, radius, ray_shape=0):
+    """CastRay (MH:410-428): conical frustums (ray_shape 0, MH:391-402) or cylinders (1, MH:403-409)."""
     t, o, d, radius = _f32(t), _f32(o), _f32(d), _f32(radius)
     n, S1 = t.shape
     S = S1 - 1
     mean = np.zeros((n, S, 3), np.float32)
     cov = np.zeros((n, S, 3), np.float32)
-    lib().orc_cast(n, S, t, o, d, radius, mean, cov)
+    lib().orc_cast(n, S, t, o, d, radius, mean, cov, int(ray_shape))
     return mean, cov
 
 
@@ -237,7 +240,7 @@ def render_grad(g, sigma, rgb, t, d, white=True):
 def step(spec: Spec, P, rays: dict, samples=(128, 128), seed=0, step_idx=0, ray_base=0, randomized=True,
          white=True, padding=0.01, coarse_mult=0.1, loss_mult_sum=0.0, t_override=None, relu_mask=None,
          dtype=np.float64,
-         nthreads=None, want=("t", "w", "C", "sigma", "rgb", "dsigma", "drgb", "grads")):
+         nthreads=None, want=("t", "w", "C", "sigma", "rgb", "dsigma", "drgb", "grads"), lindisp=False, ray_shape=0):
     """Oracle training step (MipNerfModel.GetGradient, MNcs:99-200).
 
     ``rays``: dict of float32 arrays o[n,3], d[n,3], radius[n], near[n], far[n], lossmult[n], pix[n,3].
@@ -271,6 +274,7 @@ def step(spec: Spec, P, rays: dict, samples=(128, 128), seed=0, step_idx=0, ray_
     args.randomized, args.white = int(randomized), int(white)
     args.padding, args.coarse_mult, args.loss_mult_sum = padding, coarse_mult, loss_mult_sum
     args.seed, args.step, args.ray_base = seed, step_idx, ray_base
+    args.lindisp, args.ray_shape = int(lindisp), int(ray_shape)
     args.o, args.d = inputs["o"].ctypes.data, inputs["d"].ctypes.data
     args.radius, args.near_, args.far_ = inputs["radius"].ctypes.data, inputs["near"].ctypes.data, inputs["far"].ctypes.data
     args.lossmult, args.pix = inputs["lossmult"].ctypes.data, inputs["pix"].ctypes.data

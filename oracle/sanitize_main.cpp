@@ -20,12 +20,13 @@ struct orc_step_args {
   void* const* dsigma_out; void* const* drgb_out; void* grads; void* loss;
   int32_t nthreads;
   int64_t* mask_flips;
+  int32_t lindisp, ray_shape;
 };
 extern "C" {
 int64_t orc_param_count(const orc_spec* s);
 void orc_layer_sizes(const orc_spec* s, int32_t* out);
 void orc_sample_stratified(int32_t n, int32_t S, const float* nears, const float* fars, int32_t randomized,
-                           uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base, float* t);
+                           uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base, float* t, int32_t lindisp);
 void orc_sample_pdf(int32_t n, int32_t S_in, const float* t_in, const float* w, int32_t S_out, float padding,
                     int32_t randomized, uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base,
                     float* t_out, int32_t* idx);
@@ -47,7 +48,8 @@ static bool finite(const std::vector<T>& v) {
 }
 
 template <class T>
-static void run_step(const orc_spec& sp, int n, int S0, int S1, bool masked, bool f64) {
+static void run_step(const orc_spec& sp, int n, int S0, int S1, bool masked, bool f64, int lindisp = 0,
+                     int ray_shape = 0) {
   const int64_t P = orc_param_count(&sp);
   std::vector<float> params(P);
   orc_glorot_init(&sp, 7, params.data());
@@ -77,7 +79,7 @@ static void run_step(const orc_spec& sp, int n, int S0, int S1, bool masked, boo
   int64_t flips[2] = {0, 0};  // per level
   orc_step_args a{n, 2, S, 1, 1, 0.01f, 0.1f, msum, 42, 3, 5, o.data(), d.data(), r.data(), nr.data(), fr.data(),
                   lm.data(), pix.data(), nullptr, nullptr, t_out, w_out, C_out, s_out, rgb_out, ds_out, dr_out,
-                  G.data(), &loss, 1, flips};
+                  G.data(), &loss, 1, flips, lindisp, ray_shape};
   if (f64) orc_step_f64(&sp, params.data(), &a);
   else orc_step_f32(&sp, params.data(), &a);
   check(finite(G) && finite(C1) && finite(ds1) && finite(dr0) && std::isfinite((double)loss), "step outputs finite");
@@ -105,13 +107,14 @@ int main() {
   run_step<float>(ref, 3, 128, 64, false, false);
   run_step<float>(small, 4, 64, 64, true, false);
   run_step<double>(ref, 1, 512, 512, false, true);
+  run_step<double>(ref, 2, 64, 64, false, true, 1, 1);  // LinDisp sampling, cylindrical Gaussians
   // the resampler on a ray with all-zero weights (uniform pdf after padding) and on one sample pair
   std::vector<float> tin = {2.0f, 3.0f, 4.0f, 5.0f, 6.0f}, w(4, 0.0f), tout(9);
   std::vector<int32_t> idx(9);
   orc_sample_pdf(1, 4, tin.data(), w.data(), 8, 0.01f, 1, 9, 1, 1, 0, tout.data(), idx.data());
   for (int k = 0; k < 9; ++k) check(idx[k] >= 0 && idx[k] < 4 && std::isfinite(tout[k]), "pdf on zero weights");
   std::vector<float> t1(3), nears{2.0f}, fars{6.0f};
-  orc_sample_stratified(1, 2, nears.data(), fars.data(), 1, 5, 2, 0, 0, t1.data());
+  orc_sample_stratified(1, 2, nears.data(), fars.data(), 1, 5, 2, 0, 0, t1.data(), 0);
   check(t1[0] <= t1[1] && t1[1] <= t1[2], "stratified S=2");
   std::printf("oracle sanitizer run: %s\n", fails ? "FAILED" : "ok");
   return fails ? 1 : 0;

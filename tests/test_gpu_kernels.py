@@ -43,15 +43,18 @@ def rays(n, seed=0):
 
 
 @pytest.mark.parametrize("S", [64, 128, 256, 512])
-def test_sample_stratified_bitexact(gpu, oracle, S):
+@pytest.mark.parametrize("lindisp", [0, 1])
+@pytest.mark.parametrize("rnd", [1, 0])
+def test_sample_stratified_bitexact(gpu, oracle, S, lindisp, rnd):
+    """t linear in depth, and with LinDisp (MNcs:14, MH:618-620) linear in disparity; jittered or not"""
     import nof
 
     r = rays(37, seed=1)
     t = empty((37, S + 1), gpu)
-    nof._lib.call("nof_kernel_sample_stratified", 37, S, T(r["near"], gpu).data_ptr(), T(r["far"], gpu).data_ptr(), 1,
-                  0xABCDEF12345, 7, 0, 1000, t.data_ptr(), None)
+    nof._lib.call("nof_kernel_sample_stratified", 37, S, T(r["near"], gpu).data_ptr(), T(r["far"], gpu).data_ptr(), rnd,
+                  lindisp, 0xABCDEF12345, 7, 0, 1000, t.data_ptr(), None)
     sync()
-    ref = oracle.sample_stratified(r["near"], r["far"], S, True, 0xABCDEF12345, 7, 0, 1000)
+    ref = oracle.sample_stratified(r["near"], r["far"], S, bool(rnd), 0xABCDEF12345, 7, 0, 1000, lindisp=bool(lindisp))
     assert np.array_equal(t.cpu().numpy(), ref)
 
 
@@ -87,7 +90,7 @@ def test_samplers_config1_size(gpu, oracle):
     r = synth.blender_rays(n, width=400, height=400, num_views=1, seed=1)
     t0 = empty((n, S + 1), gpu)
     nof._lib.call("nof_kernel_sample_stratified", n, S, T(r["near"], gpu).data_ptr(), T(r["far"], gpu).data_ptr(), 1,
-                  seed, 0, 0, 0, t0.data_ptr(), None)
+                  0, seed, 0, 0, 0, t0.data_ptr(), None)
     sync()
     ref0 = oracle.sample_stratified(r["near"], r["far"], S, True, seed, 0, 0, 0)
     assert np.array_equal(t0.cpu().numpy(), ref0)
@@ -103,7 +106,9 @@ def test_samplers_config1_size(gpu, oracle):
     assert np.array_equal(t1.cpu().numpy(), rt)
 
 
-def test_cast_bitexact_and_encode(gpu, oracle):
+@pytest.mark.parametrize("ray_shape", [0, 1])
+def test_cast_bitexact_and_encode(gpu, oracle, ray_shape):
+    """conical frustums (MH:391-402) and, RayShape.Cylindrical, cylinders (MH:403-409): bit-exact Gaussians"""
     import nof
 
     n, S = 19, 128
@@ -111,12 +116,12 @@ def test_cast_bitexact_and_encode(gpu, oracle):
     t = oracle.sample_stratified(r["near"], r["far"], S, True, 9, 2, 0, 0)
     mean, cov = empty((n, S, 3), gpu), empty((n, S, 3), gpu)
     nof._lib.call("nof_kernel_cast", n, S, T(t, gpu).data_ptr(), T(r["o"], gpu).data_ptr(), T(r["d"], gpu).data_ptr(),
-                  T(r["radius"], gpu).data_ptr(), mean.data_ptr(), cov.data_ptr(), None)
+                  T(r["radius"], gpu).data_ptr(), ray_shape, mean.data_ptr(), cov.data_ptr(), None)
     ep, ed = empty((n * S, 96), gpu), empty((n, 27), gpu)
     nof._lib.call("nof_kernel_encode", n, S, mean.data_ptr(), cov.data_ptr(), T(r["d"], gpu).data_ptr(),
                   ep.data_ptr(), ed.data_ptr(), None)
     sync()
-    rm, rc = oracle.cast(t, r["o"], r["d"], r["radius"])
+    rm, rc = oracle.cast(t, r["o"], r["d"], r["radius"], ray_shape)
     assert np.array_equal(mean.cpu().numpy(), rm)
     assert np.array_equal(cov.cpu().numpy(), rc)
     spec = oracle.Spec()

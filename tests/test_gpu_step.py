@@ -40,12 +40,25 @@ PRECISIONS = [0, 1, 2, 3, 4]
 @pytest.mark.parametrize("kind,n,samples", [("blender", 16, (64, 64)), ("blender", 8, (128, 128)),
                                             ("blender", 6, (64, 128)), ("llff", 3, (256, 256))])
 def test_step_parity(gpu, oracle, kind, n, samples, precision):
+    _check_step(gpu, oracle, kind, n, samples, precision)
+
+
+# the spec's non-default ray options (MipNerfModel.cs:14-15): LinDisp sampling (MH:618-620) and cylinders
+# (CylinderToGaussian MH:403-409), through the fp32 / split / F16 forward kernels' fused prologues
+@pytest.mark.parametrize("precision", [0, 1, 4])
+@pytest.mark.parametrize("lindisp,ray_shape", [(1, 0), (0, 1), (1, 1)])
+def test_step_parity_ray_options(gpu, oracle, lindisp, ray_shape, precision):
+    _check_step(gpu, oracle, "blender", 8, (64, 128), precision, lindisp=lindisp, ray_shape=ray_shape)
+
+
+def _check_step(gpu, oracle, kind, n, samples, precision, lindisp=0, ray_shape=0):
     import torch
     import nof
     from nof import synth
 
     seed, step, ray_base = 0x1234, 3, 500
-    model = nof.AcceleratedMipNeRF(seed=seed, max_rays=n, num_samples=samples, precision=precision)
+    opts = dict(lindisp=lindisp, ray_shape=ray_shape)
+    model = nof.AcceleratedMipNeRF(seed=seed, max_rays=n, num_samples=samples, precision=precision, **opts)
     model.set_rng(seed, step, ray_base)
     r = synth.blender_rays(n, seed=11) if kind == "blender" else synth.llff_rays(n, seed=11)
     grads = _run_gpu(model, r, gpu)
@@ -58,7 +71,7 @@ def test_step_parity(gpu, oracle, kind, n, samples, precision):
     assert grads[0] == gptr
 
     # level-0 samples: bit-exact; level-1 resampling: bit-exact given the GPU's level-0 weights
-    t0 = oracle.sample_stratified(r["near"], r["far"], samples[0], True, seed, step, 0, ray_base)
+    t0 = oracle.sample_stratified(r["near"], r["far"], samples[0], True, seed, step, 0, ray_base, lindisp=bool(lindisp))
     assert np.array_equal(lv[0]["t"], t0)
     t1, _ = oracle.sample_pdf(lv[0]["t"], lv[0]["weights"], samples[1], 0.01, True, seed, step, 1, ray_base)
     assert np.array_equal(lv[1]["t"], t1)
@@ -67,10 +80,11 @@ def test_step_parity(gpu, oracle, kind, n, samples, precision):
     # to opposite signs in fp32 and fp64, which would shift every gradient below that unit (measure-zero tie).
     masks = {l: model.mlp.relu_masks(l).reshape(n, samples[l], -1) for l in range(len(samples))}
     ref = oracle.step(oracle.Spec(), params, r, samples=samples, seed=seed, step_idx=step, ray_base=ray_base,
-                      t_override={1: lv[1]["t"]}, relu_mask=masks, nthreads=16)
+                      t_override={1: lv[1]["t"]}, relu_mask=masks, nthreads=16, **opts)
     # forward outputs and the integrator adjoint: the oracle's own ReLU decisions (no adoption)
     free = oracle.step(oracle.Spec(), params, r, samples=samples, seed=seed, step_idx=step, ray_base=ray_base,
-                       t_override={1: lv[1]["t"]}, nthreads=16, want=("sigma", "rgb", "w", "C", "dsigma", "drgb"))
+                       t_override={1: lv[1]["t"]}, nthreads=16, want=("sigma", "rgb", "w", "C", "dsigma", "drgb"),
+                       **opts)
     tol = TOLS[precision]
     for l in range(len(samples)):
         assert rel_l2(lv[l]["density"], free["sigma"][l]) < tol, f"density level {l}"
@@ -169,7 +183,7 @@ def test_encoded_get_output_equals_fused(gpu):
     mean = torch.zeros((n, S, 3), device=gpu)
     cov = torch.zeros((n, S, 3), device=gpu)
     nof._lib.call("nof_kernel_cast", n, S, t.data_ptr(), dev["o"].data_ptr(), dev["d"].data_ptr(),
-                  dev["radius"].data_ptr(), mean.data_ptr(), cov.data_ptr(), None)
+                  dev["radius"].data_ptr(), 0, mean.data_ptr(), cov.data_ptr(), None)
     ep = torch.zeros((n * S, 96), device=gpu)
     ed = torch.zeros((n, 27), device=gpu)
     nof._lib.call("nof_kernel_encode", n, S, mean.data_ptr(), cov.data_ptr(), dev["d"].data_ptr(), ep.data_ptr(),

@@ -176,3 +176,39 @@ def test_adam_and_lr_formulas(oracle):
     ref = (0.01 + 0.99 * np.sin(0.5 * np.pi / 2500)) * np.exp(np.log(5e-4) * (1 - 1e-6) + np.log(5e-6) * 1e-6)
     assert abs(lr - ref) < 1e-9
     assert abs(oracle.lr_decay(1000000) - 5e-6) < 1e-10
+
+
+@pytest.mark.parametrize("lindisp,ray_shape", [(1, 0), (0, 1), (1, 1)])
+def test_ray_options_match_independent_restatement(oracle, lindisp, ray_shape):
+    """LinDisp sampling (MipNerfModel.cs:14, MipHelpers.cs:618-620) and cylinders (MipNerfModel.cs:15,
+    MipHelpers.cs:403-409): the oracle's t-values and Gaussians bit-exact, and its whole two-level step
+    (fp64) within 1e-9, against the independent numpy / torch-autograd restatement (tests/torch_ref.py)."""
+    from nof import synth
+
+    n, samples, seed, step, base = 3, (16, 16), 0x77, 2, 40
+    spec = oracle.Spec(D=4, W=32, skip=2)
+    r = synth.blender_rays(n, seed=5)
+    P = oracle.glorot_init(spec, 9)
+    gids = np.arange(base, base + n)
+    t_ref = TR.stratified(r["near"], r["far"], samples[0], TR.uniforms(seed, step, 0, 1, gids, samples[0] + 1),
+                          bool(lindisp))
+    t = oracle.sample_stratified(r["near"], r["far"], samples[0], True, seed, step, 0, base, lindisp=bool(lindisp))
+    assert np.array_equal(t, t_ref), "stratified t"
+    if lindisp:  # disparity-linear: the un-jittered grid's inverse is linear in s
+        g = oracle.sample_stratified(r["near"], r["far"], samples[0], False, lindisp=True)
+        inv = 1.0 / g.astype(np.float64)
+        assert np.allclose(np.diff(inv, 2, axis=1), 0, atol=1e-5 * np.abs(inv).max())
+    m, c = oracle.cast(t, r["o"], r["d"], r["radius"], ray_shape)
+    m_ref, c_ref = TR.cast(t, r["o"], r["d"], r["radius"], bool(ray_shape))
+    assert np.array_equal(m, m_ref) and np.array_equal(c, c_ref), "Gaussians"
+    net = TR.Net(D=4, W=32, skip=2)
+    ref = TR.step(P, r, samples=samples, seed=seed, step_idx=step, ray_base=base, net=net, lindisp=bool(lindisp),
+                  cylinder=bool(ray_shape))
+    got = oracle.step(spec, P, r, samples=samples, seed=seed, step_idx=step, ray_base=base, nthreads=1,
+                      lindisp=bool(lindisp), ray_shape=ray_shape)
+    for l in range(2):
+        assert np.array_equal(got["t"][l], ref["t"][l]), f"t level {l}"
+        assert np.allclose(got["w"][l], ref["w"][l], rtol=1e-9, atol=1e-12), f"weights level {l}"
+    assert abs(got["loss"] - ref["loss"]) <= 1e-9 * abs(ref["loss"])
+    e = np.linalg.norm(got["grads"] - ref["grads"]) / np.linalg.norm(ref["grads"])
+    assert e < 1e-9, f"gradients rel L2 {e:.3g}"

@@ -45,9 +45,13 @@ def uniforms(seed, step, level, stream, rays, count):
 f32 = np.float32
 
 
-def stratified(near, far, S, u):
+def stratified(near, far, S, u, lindisp=False):
+    """SampleAlongRay (MipHelpers.cs:611-631); lindisp: linear in disparity (MipHelpers.cs:618-620)"""
     tv = np.arange(S + 1, dtype=f32) / f32(S)
-    lin = near[:, None] * (f32(1) - tv)[None, :] + far[:, None] * tv[None, :]
+    if lindisp:
+        lin = f32(1) / (f32(1) / near[:, None] * (f32(1) - tv)[None, :] + f32(1) / far[:, None] * tv[None, :])
+    else:
+        lin = near[:, None] * (f32(1) - tv)[None, :] + far[:, None] * tv[None, :]
     mids = f32(0.5) * (lin[:, :-1] + lin[:, 1:])
     lower = np.concatenate([lin[:, :1], mids], 1)
     upper = np.concatenate([mids, lin[:, -1:]], 1)
@@ -81,15 +85,22 @@ def resample(t, w, S_out, padding, u_raw):
     return (b0 + tt * (b1 - b0)).astype(f32), idx.astype(np.int32)
 
 
-def cast(t, o, d, radius):
+def cast(t, o, d, radius, cylinder=False):
+    """CastRay (MipHelpers.cs:410-428): ConicalFrustumToGaussian (MipHelpers.cs:391-402) or, cylinder,
+    CylinderToGaussian (MipHelpers.cs:403-409), lifted by LiftGaussian (MipHelpers.cs:367-379)"""
     t0, t1 = t[:, :-1], t[:, 1:]
-    mu = (t0 + t1) / f32(2)
-    hw = (t1 - t0) / f32(2)
-    mu2, hw2 = mu * mu, hw * hw
-    den = f32(3) * mu2 + hw2
-    tmean = mu + (f32(2) * mu * hw2) / den
-    tvar = hw2 / f32(3) - (f32(4) / f32(15)) * (hw2 * hw2 * (f32(12) * mu2 - hw2)) / (den * den)
-    rvar = radius[:, None] * radius[:, None] * (mu2 / f32(4) + (f32(5) / f32(12)) * hw2 - (f32(4) / f32(15)) * (hw2 * hw2) / den)
+    if cylinder:
+        tmean = (t0 + t1) / f32(2)
+        rvar = np.broadcast_to(radius[:, None] * radius[:, None] / f32(4), tmean.shape)
+        tvar = (t1 - t0) * (t1 - t0) / f32(12)
+    else:
+        mu = (t0 + t1) / f32(2)
+        hw = (t1 - t0) / f32(2)
+        mu2, hw2 = mu * mu, hw * hw
+        den = f32(3) * mu2 + hw2
+        tmean = mu + (f32(2) * mu * hw2) / den
+        tvar = hw2 / f32(3) - (f32(4) / f32(15)) * (hw2 * hw2 * (f32(12) * mu2 - hw2)) / (den * den)
+        rvar = radius[:, None] * radius[:, None] * (mu2 / f32(4) + (f32(5) / f32(12)) * hw2 - (f32(4) / f32(15)) * (hw2 * hw2) / den)
     dms = np.maximum(f32(1e-10), (d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2])
     dd = d * d
     nul = f32(1) - dd / dms[:, None]
@@ -173,7 +184,7 @@ def render(sigma, rgb, t, d, white=True):
 
 
 def step(P_np, rays, samples=(128, 128), seed=0, step_idx=0, ray_base=0, padding=0.01, coarse_mult=0.1,
-         white=True, net=None, t_override=None):
+         white=True, net=None, t_override=None, lindisp=False, cylinder=False):
     """Full two-level step; returns dict with t, w, C per level, loss, grads (fp64 autograd)."""
     net = net or Net()
     n = rays["o"].shape[0]
@@ -189,14 +200,14 @@ def step(P_np, rays, samples=(128, 128), seed=0, step_idx=0, ray_base=0, padding
     NL = len(samples)
     for lv, S in enumerate(samples):
         if lv == 0:
-            t = stratified(rays["near"], rays["far"], S, uniforms(seed, step_idx, 0, 1, gids, S + 1))
+            t = stratified(rays["near"], rays["far"], S, uniforms(seed, step_idx, 0, 1, gids, S + 1), lindisp)
             idx = None
         elif t_override is not None and lv in t_override:
             t, idx = t_override[lv], None
         else:
             wprev = res["w"][-1].detach().numpy().astype(f32)
             t, idx = resample(res["t"][-1], wprev, S, padding, uniforms(seed, step_idx, lv, 2, gids, S + 1))
-        mean, cov = cast(t, o, d, rad)
+        mean, cov = cast(t, o, d, rad, cylinder)
         enc = torch.from_numpy(ipe(mean, cov))
         zs, zc = net.forward(P, enc, dirv[:, None, :].expand(n, S, dirv.shape[-1]))
         sigma = torch.nn.functional.softplus(zs - 1.0, beta=1, threshold=20)

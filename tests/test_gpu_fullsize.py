@@ -49,14 +49,14 @@ def _gpu_step(model, r, gpu, msum, lo=0, hi=None):
     torch.cuda.synchronize()
 
 
-def _check_t(oracle, lv, r, samples, seed, step, base):
-    t0 = oracle.sample_stratified(r["near"], r["far"], samples[0], True, seed, step, 0, base)
+def _check_t(oracle, lv, r, samples, seed, step, base, lindisp=0):
+    t0 = oracle.sample_stratified(r["near"], r["far"], samples[0], True, seed, step, 0, base, lindisp=bool(lindisp))
     assert np.array_equal(lv[0]["t"], t0), "level-0 t not bit-exact"
     t1, _ = oracle.sample_pdf(lv[0]["t"], lv[0]["weights"], samples[1], 0.01, True, seed, step, 1, base)
     assert np.array_equal(lv[1]["t"], t1), "level-1 t not bit-exact (given the GPU's level-0 weights)"
 
 
-def _compare_step(oracle, model, r, samples, seed, step, base, msum, precision):
+def _compare_step(oracle, model, r, samples, seed, step, base, msum, precision, lindisp=0, ray_shape=0):
     """Everything of one GPU step vs the oracle on the same samples; returns (max grad rel, flip frac).
 
     The forward outputs and the integrator adjoint (density, rgb, weights, comp_rgb, dsigma, drgb, the
@@ -67,14 +67,15 @@ def _compare_step(oracle, model, r, samples, seed, step, base, msum, precision):
 
     n = r["o"].shape[0]
     tol = TOLS[precision]
+    opts = dict(lindisp=lindisp, ray_shape=ray_shape)
     lv = [model.level_numpy(l) for l in range(len(samples))]
-    _check_t(oracle, lv, r, samples, seed, step, base)
+    _check_t(oracle, lv, r, samples, seed, step, base, lindisp)
     pptr, P = model.mlp.flat_params()
     params = nof.to_numpy(pptr, (P,))
     G = nof.to_numpy(model.mlp.flat_grads()[0], (P,))
     free = oracle.step(oracle.Spec(), params, r, samples=samples, seed=seed, step_idx=step, ray_base=base,
                        loss_mult_sum=msum, t_override={1: lv[1]["t"]}, nthreads=NTHREADS,
-                       want=tuple(ORACLE_KEY.values()))
+                       want=tuple(ORACLE_KEY.values()), **opts)
     for l in range(len(samples)):
         for k in PER_RAY:
             e = rel_l2(lv[l][k], free[ORACLE_KEY[k]][l])
@@ -84,7 +85,7 @@ def _compare_step(oracle, model, r, samples, seed, step, base, msum, precision):
     masks = {l: model.mlp.relu_masks(l).reshape(n, samples[l], -1) for l in range(len(samples))}
     ref = oracle.step(oracle.Spec(), params, r, samples=samples, seed=seed, step_idx=step, ray_base=base,
                       loss_mult_sum=msum, t_override={1: lv[1]["t"]}, relu_mask=masks, nthreads=NTHREADS,
-                      want=("grads",))
+                      want=("grads",), **opts)
     units = sum(n * s * masks[l].shape[-1] for l, s in enumerate(samples))
     flips = sum(ref["mask_flips"]) / units
     del masks
@@ -117,15 +118,26 @@ def _compare_step(oracle, model, r, samples, seed, step, base, msum, precision):
     ("config5", "llff", 512, (256, 256), 4),
 ])
 def test_fullsize_step_parity(gpu, oracle, name, kind, n, samples, precision):
+    _fullsize(gpu, oracle, name, kind, n, samples, precision)
+
+
+@pytest.mark.parametrize("precision", [0, 4])
+def test_fullsize_ray_options(gpu, oracle, precision):
+    """config 2 with the spec's non-default ray options (MipNerfModel.cs:14-15): LinDisp sampling and
+    cylindrical Gaussians, fp32 and F16"""
+    _fullsize(gpu, oracle, "config2", "blender", 1024, (128, 128), precision, lindisp=1, ray_shape=1)
+
+
+def _fullsize(gpu, oracle, name, kind, n, samples, precision, **opts):
     import nof
 
     seed, step, base = 0x5EED0000 + int(name[-1]), 5, 0
     r = _rays(kind, n, seed=21)
     msum = float(np.sum(r["lossmult"], dtype=np.float32))
-    model = nof.AcceleratedMipNeRF(seed=31, max_rays=n, num_samples=samples, precision=precision)
+    model = nof.AcceleratedMipNeRF(seed=31, max_rays=n, num_samples=samples, precision=precision, **opts)
     model.set_rng(seed, step, base)
     _gpu_step(model, r, gpu, msum)
-    _compare_step(oracle, model, r, samples, seed, step, base, msum, precision)
+    _compare_step(oracle, model, r, samples, seed, step, base, msum, precision, **opts)
     model.close()
 
 

@@ -314,10 +314,9 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int lv0, int lv1, int bucket)
   };
   auto Wg = [&](int l) { return G + woff_[l]; };
   auto Bg = [&](int l) { return G + boff_[l]; };
-  // F16 (k_wgrad_s) and F32_F16SPLIT (k_wgrad_xs): the problems that share an A operand are one problem
-  // with more output columns — delta_4 x [h3 | IPE] and delta_9x x [h7 | view PE | h9] — so each delta
-  // block is read once
-  const bool merge = precision_ == NOF_PRECISION_F16 || precision_ == NOF_PRECISION_F32_F16SPLIT;
+  // F16 (k_wgrad_s): the problems that share an A operand are one problem with more output columns —
+  // delta_4 x [h3 | IPE] and delta_9x x [h7 | view PE | h9] — so each delta block is read once
+  const bool merge = precision_ == NOF_PRECISION_F16;
   // The per-level problem list is the same for every level; problem q of level lev goes to index
   // q nlev + (lev - lv0), so a problem's items over all levels are contiguous (level order) and one
   // output spec (WgOut) reduces them all.
@@ -411,9 +410,8 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int lv0, int lv1, int bucket)
   // measured for the (8,8) / (8,3) / (5,8) / (4,1) / (1,4) problems = 160 / 96 / 124 / 47 / 37.
   std::vector<int64_t> cost(P.size());
   for (size_t i = 0; i < P.size(); ++i) {
-    if (precision_ == NOF_PRECISION_F16 || precision_ == NOF_PRECISION_F32_F16SPLIT) {
-      // k_wgrad_s / k_wgrad_xs (F32_F16SPLIT, fp32 tiles) stream T = ntr + ntc tiles per block; k_wgrad_s:
-      // 1.65 / 1.17 us per block measured for the
+    if (precision_ == NOF_PRECISION_F16) {
+      // k_wgrad_s streams T = ntr + ntc tiles per block: 1.65 / 1.17 us per block measured for the
       // 16- / 11-tile problems (tools/diag_item_time.py f16); the merged 19- / 18-tile problems run
       // the unpipelined 12-accumulator path, 2.13 / 2.08 us
       const int RB = (P[i].ntr + 1) / 2, CB = (P[i].ntc + 3) / 4;
@@ -423,7 +421,8 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int lv0, int lv1, int bucket)
     } else if (precision_ != NOF_PRECISION_F32) {
       const int WC = nof::wgrad_x3_grid_cols();  // C/2 waves per SIMD
       const int RB = (P[i].ntr + 1) / 2, CB = (P[i].ntc + WC - 1) / WC;
-      cost[i] = 10 * RB * CB + 5 * (P[i].ntr + P[i].ntc);
+      // fp16 (hi, lo) pieces: 3 MFMAs per product instead of 6 (same loads and splits)
+      cost[i] = (precision_ == NOF_PRECISION_F32_F16SPLIT ? 5 : 10) * RB * CB + 5 * (P[i].ntr + P[i].ntc);
     } else {
       cost[i] = nof::wgrad_block_cost(P[i].ntr, P[i].ntc, &P[i].shape);
     }

@@ -872,208 +872,6 @@ __global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_s(const WgProblem* __
   NOF_WG_T1(1)
 }
 
-// ---- F32_F16SPLIT mode: fp32 operand blocks streamed by LDS-DMA, split into fp16 (hi, lo) at read time ----
-// (k_wgrad_xs; replaces k_wgrad_x3<2>'s register-staged loader, which split every chunk into LDS fragment
-// images: 5.34 GB counted per config-2 step at 0.52 of HBM peak.)  A ring stage is one 16-sample k-step of
-// EVERY operand tile of the problem (T x 2 KB of fp32: 32 rows x 64 B per tile), filled by global_load_lds
-// (16 B per lane, nt) as many stages as fit 160 KB; the problems that share an operand are merged as in
-// k_wgrad_s (delta_4 x [h3 | IPE], delta_9x x [h7 | view PE | h9]) so every operand block is read once.
-// In LDS, row r's 16-B chunk q (samples 4q .. 4q + 3 of the k-step) sits at position q ^ ((x >> 2) & 3),
-// x = r & 31: the ds_read_b128 of a 16-lane group (4 x-residues x 4 values of (x >> 2) & 3) then covers the
-// 64 banks once.  Lane (x, h) reads chunks 2h, 2h + 1 of its row (the 32x32x16 fragment's k = 8h + j, the
-// same sample order as k_wgrad_x3, so the products and their order per output are unchanged), splits the
-// 8 floats into fp16 hi + lo and issues the three products (lo.hi, hi.lo, hi.hi) per tile.  The reads are
-// inline asm (through the builtin the compiler would wait for every LDS-DMA in flight before each); the
-// next row's A fragment is read under the current row's MFMAs and settled after them
-// (tests/test_lgkm_hazards.py checks the compiled code keeps those registers untouched while in flight).
-constexpr int kXsLdsBytes = 160 * 1024;
-constexpr int kXsAux = 2;  // global_load_lds cache policy: non-temporal (streamed once)
-template <int RB, int CB>
-struct XsRing {
-  // operand tiles a problem of this grid has: the merged problems are 8 x (8 + 3) and 5 x (8 + 1 + 4)
-  static constexpr int TC = (RB == 4 && CB == 3) ? 19 : ((RB == 3 && CB == 4) ? 18 : 2 * RB + kX3WC * CB);
-  static constexpr int ND = (2 * TC + 7) / 8;  // 1-KB DMA instructions per wave per stage
-  static constexpr int NS = kXsLdsBytes / (TC * 2048) < 8 ? kXsLdsBytes / (TC * 2048) : 8;  // stages
-  static_assert((NS - 1) * ND < 64 && NS >= 4, "vmcnt range / ring depth");
-};
-
-template <int RB, int CB>
-__device__ __forceinline__ void wg_item_xs(const WgItem& item, const WgProblem& P, float* lds, int tid, int wave,
-                                           float* slabs, float* bias_slabs, const int64_t* slab_off) {
-  typedef XsRing<RB, CB> R;
-  constexpr int ND = R::ND, NS = R::NS, kStageB = R::TC * 2048;
-  int tq = tid;
-  asm volatile("" : "+v"(tq));
-  const int lane = tq & 63;
-  const int h = lane >> 5, x = lane & 31;
-  const int wr = wave / kX3WC, wc = wave % kX3WC;
-  const int r0 = wr * RB, c0 = wc * CB;
-  const bool active = r0 < P.ntr && c0 < P.ntc;  // wave-uniform
-  int rowt[RB], colt[CB];
-#pragma unroll
-  for (int r = 0; r < RB; ++r) rowt[r] = min(r0 + r, P.ntr - 1);
-#pragma unroll
-  for (int c = 0; c < CB; ++c) colt[c] = min(c0 + c, P.ntc - 1);
-  const int T = P.ntr + P.ntc;  // tiles per stage
-  // this wave's DMA instructions c = 8i + wave (clamped: surplus instructions repeat the last one, an L2
-  // hit into the same LDS bytes): 16 rows each, lane L -> row 16c + L / 4, LDS position L & 3 = chunk q
-  // per instruction: the operand (wave-uniform: 16 rows never straddle a 32-row tile) as a buffer resource at
-  // block kb0, its bytes per block, and the lane's byte offset in the block at k-step 0 (k-step 1: ^ 64)
-  const float* opb[ND];
-  uint32_t str[ND];
-  uint32_t voff[ND];
-  int dst[ND];
-#pragma unroll
-  for (int i = 0; i < ND; ++i) {
-    const int c = min(i * 8 + wave, 2 * T - 1);
-    const int row = 16 * c + (lane >> 2), xr = row & 31;
-    int t = row >> 5;
-    const int q = (lane & 3) ^ ((xr >> 2) & 3);
-    const float* base;
-    int F, row0;
-    if (t < P.ntr) {
-      base = P.A; F = P.FA; row0 = P.a_row0;
-    } else if ((t -= P.ntr) < P.ntc1) {
-      base = P.B; F = P.FB; row0 = P.b_col0;
-    } else if ((t -= P.ntc1) < P.ntc2) {
-      base = P.B2; F = P.FB2; row0 = P.b2_col0;
-    } else {
-      t -= P.ntc2;
-      base = P.B3; F = P.FB3; row0 = P.b3_col0;
-    }
-    const int f = row0 + 32 * t + xr;  // feature row (row0 a multiple of 32: f & 7 = xr & 7)
-    str[i] = (uint32_t)F * kBlk * 4u;
-    opb[i] = base + (size_t)item.kb0 * F * kBlk;
-    voff[i] = (uint32_t)f * kBlk * 4u + (uint32_t)((q ^ (xr & 7)) << 4);
-    dst[i] = c * 1024;
-  }
-  const int K = 2 * (item.kb1 - item.kb0);  // k-steps of 16 samples
-  auto dma = [&](int k, int slot) {  // k-step k (clamped to K - 1: a duplicate nobody reads) into `slot`
-    k = min(k, K - 1);
-    char* stage = reinterpret_cast<char*>(lds) + slot * kStageB;
-#pragma unroll
-    for (int i = 0; i < ND; ++i) {
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(opb[i]), (short)0, 0x7fffffff, 0x00020000);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lptr_t)(stage + dst[i]), 16, voff[i] ^ ((uint32_t)(k & 1) << 6),
-                                               (int)((uint32_t)(k >> 1) * str[i]), 0, kXsAux);
-    }
-  };
-  f32x16 acc[RB][CB];
-#pragma unroll
-  for (int r = 0; r < RB; ++r)
-#pragma unroll
-    for (int c = 0; c < CB; ++c) acc[r][c] = f32x16{};
-  float bsum = 0.0f;  // bias partial of row tile rowt[wc] (wave columns wc < RB)
-  // this lane's fragment rows: chunk 2h at position 2h ^ s, chunk 2h + 1 at that ^ 1 (byte offset ^ 16)
-  const uint32_t lane_off = (uint32_t)(x * 64 + (((2 * h) ^ ((x >> 2) & 3)) << 4));
-  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
-  typedef float f32x4v __attribute__((ext_vector_type(4)));
-  struct Raw { f32x4v lo, hi; };
-  auto rd = [&](uint32_t sb, int tile, Raw& v) {  // issue only: settled by the caller
-    const uint32_t a = sb + (uint32_t)(tile * 2048) + lane_off;
-    asm volatile("ds_read_b128 %0, %1" : "=v"(v.lo) : "v"(a));
-    asm volatile("ds_read_b128 %0, %1" : "=v"(v.hi) : "v"(a ^ 16u));
-  };
-  auto settle = [&](Raw& v) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    asm volatile("" : "+v"(v.lo), "+v"(v.hi));  // defined here, after the wait
-  };
-  auto split = [&](const Raw& v, Frag<2>& f) {
-    const float e[8] = {v.lo[0], v.lo[1], v.lo[2], v.lo[3], v.hi[0], v.hi[1], v.hi[2], v.hi[3]};
-    split8<2>(e, f);
-  };
-#pragma unroll
-  for (int k = 0; k < NS - 1; ++k) dma(k, k);
-  int slot = 0, fill = NS - 1;
-  for (int k = 0; k < K; ++k) {
-    wait_vmcnt<(NS - 2) * ND>();  // k-step k landed (this wave's part); k + 1 .. k + NS - 2 in flight
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // everyone's part; slot `fill` read out
-    dma(k + NS - 1, fill);
-    const uint32_t sb = lds_base + (uint32_t)(slot * kStageB);
-    Frag<2> fb[CB];
-    Raw ra;
-    rd(sb, P.ntr + colt[0], ra);
-    settle(ra);
-#pragma unroll
-    for (int c = 0; c < CB; ++c) {  // one raw fragment live at a time: the next read under this split
-      Frag<2>& f = fb[c];
-      split(ra, f);
-      rd(sb, c + 1 < CB ? P.ntr + colt[c + 1 < CB ? c + 1 : 0] : rowt[0], ra);
-      settle(ra);
-    }
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      Frag<2> fa;
-      split(ra, fa);
-      if (wc == r) {  // bias partials: row sums of delta (fp32, the raw values)
-        bsum += ((ra.lo[0] + ra.lo[1]) + (ra.lo[2] + ra.lo[3])) + ((ra.hi[0] + ra.hi[1]) + (ra.hi[2] + ra.hi[3]));
-      }
-      if (r + 1 < RB) rd(sb, rowt[r + 1 < RB ? r + 1 : 0], ra);  // in flight under this row's MFMAs
-#pragma unroll
-      for (int c = 0; c < CB; ++c) acc[r][c] = mfma_split<2>(fa, fb[c], acc[r][c]);
-      if (r + 1 < RB) settle(ra);
-    }
-    slot = slot + 1 == NS ? 0 : slot + 1;
-    fill = fill + 1 == NS ? 0 : fill + 1;
-  }
-  wait_vmcnt<0>();  // retire the clamped tail DMAs before the ring is reused
-  if (active) {
-    float* slab = slabs + slab_off[item.slab];
-    const int ld_ = P.ntc * 32;
-#pragma unroll
-    for (int r = 0; r < RB; ++r)
-#pragma unroll
-      for (int c = 0; c < CB; ++c) {
-        if (r0 + r < P.ntr && c0 + c < P.ntc) {
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int row = rowt[r] * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-            slab[(size_t)row * ld_ + colt[c] * 32 + x] = acc[r][c][e];
-          }
-        }
-      }
-  }
-  if (wc < RB) {
-    const float v = bsum + __shfl_xor(bsum, 32, 64);
-    if (r0 + wc < P.ntr && h == 0) bias_slabs[(size_t)item.slab * 256 + (r0 + wc) * 32 + x] = v;
-  }
-  __syncthreads();  // the ring is reused by the next item
-}
-
-__global__ __launch_bounds__(kWgX3Threads, 1) void k_wgrad_xs(const WgProblem* __restrict__ probs,
-                                                              const WgItem* __restrict__ items,
-                                                              const int* __restrict__ item_ptr,
-                                                              const int64_t* __restrict__ slab_off, float* slabs,
-                                                              float* bias_slabs) {
-  extern __shared__ __attribute__((aligned(16))) float ldsx[];
-  NOF_WG_T0(1)
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int it0 = item_ptr[blockIdx.x], it1 = item_ptr[blockIdx.x + 1];
-  for (int it = it0; it < it1; ++it) {
-    NOF_IT_T0(1)
-    const WgItem item = items[it];
-    const WgProblem P = probs[item.prob];
-    NOF_DCHECK(item.kb0 < item.kb1 && P.ntr >= 1 && P.ntr <= 8 && P.ntc >= 1 && P.ntc <= 16 &&
-                   P.ntc == P.ntc1 + P.ntc2 + P.ntc3 && P.a_row0 + 32 * P.ntr <= P.FA &&
-                   P.b_col0 + 32 * P.ntc1 <= P.FB && (P.ntc2 == 0 || P.b2_col0 + 32 * P.ntc2 <= P.FB2) &&
-                   (P.ntc3 == 0 || P.b3_col0 + 32 * P.ntc3 <= P.FB3),
-               kChkWgradGeom);
-    switch (((P.ntr + 1) >> 1) * 10 + (P.ntc + kX3WC - 1) / kX3WC) {
-      case 11: wg_item_xs<1, 1>(item, P, ldsx, tid, wave, slabs, bias_slabs, slab_off); break;
-      case 21: wg_item_xs<2, 1>(item, P, ldsx, tid, wave, slabs, bias_slabs, slab_off); break;
-      case 34: wg_item_xs<3, 4>(item, P, ldsx, tid, wave, slabs, bias_slabs, slab_off); break;
-      case 41: wg_item_xs<4, 1>(item, P, ldsx, tid, wave, slabs, bias_slabs, slab_off); break;
-      case 42: wg_item_xs<4, 2>(item, P, ldsx, tid, wave, slabs, bias_slabs, slab_off); break;
-      case 43: wg_item_xs<4, 3>(item, P, ldsx, tid, wave, slabs, bias_slabs, slab_off); break;
-      default: NOF_DCHECK(false, kChkWgradGeom); break;
-    }
-    NOF_IT_T1(1)
-  }
-  NOF_WG_T1(1)
-}
-
 int wgrad_x3_grid_cols() { return kX3WC; }
 
 int wgrad_shape(int ntr, int ntc, int* cost2) {
@@ -1150,146 +948,110 @@ hipError_t launch_wgrad_x3(const WgProblem* probs, const WgItem* items, const in
                        slabs, bias_slabs);
     return hipGetLastError();
   }
-  if (precision == 3) {  // F32_F16SPLIT: fp32 operand blocks split into fp16 (hi, lo) at read time (k_wgrad_xs)
-    static bool attr_x = false;
-    if (!attr_x) {
-      const hipError_t e =
-          hipFuncSetAttribute((const void*)k_wgrad_xs, hipFuncAttributeMaxDynamicSharedMemorySize, kXsLdsBytes);
-      if (e != hipSuccess) return e;
-      attr_x = true;
-    }
-    hipLaunchKernelGGL(k_wgrad_xs, dim3(num_wg), dim3(kWgX3Threads), kXsLdsBytes, st, probs, items, item_ptr, slab_off,
-                       slabs, bias_slabs);
-    return hipGetLastError();
-  }
+  if (precision == 3)  // F32_F16SPLIT: fp32 operand blocks split into fp16 (hi, lo), 3 products
+    return launch_wgrad_split<2>(probs, items, item_ptr, num_wg, slab_off, slabs, bias_slabs, st);
   return launch_wgrad_split<1>(probs, items, item_ptr, num_wg, slab_off, slabs, bias_slabs, st);
 }
 
-// The ordered reduce: output element e (4 consecutive elements — a float4 of every slab — when the output's
-// columns come in fours, one element otherwise) is the sum of the problem's item slabs in item order, level
-// by level, each level's sum times its delta scale (f16 modes), added in level order — the arithmetic of one
-// reduce per level.  A block covers kRedE elements with kRedG waves: wave g sums the g-th contiguous quarter of
-// every level's items (kU slabs in flight per wave), and wave 0 adds the quarters in order
-// ((q0 + q1) + q2) + q3.  Four waves per element put four times the loads in flight (one thread per element
-// was bound by load latency: ~25 slabs in ~4 dependent rounds per thread).  The grouping is fixed by the item
-// count alone, so every run sums in the same order.
-constexpr int kRedE = 64, kRedG = 4;
+// Thread t sums 4 consecutive output elements (a float4 of every slab) when the output's columns come
+// in fours, element t otherwise, over the problem's item slabs in item order (the host sizes the grid:
+// wgrad_reduce_threads).  Items are grouped by level (two-level launches): each level's sum is scaled by
+// its delta scale (f16 modes) and added in level order — the arithmetic of one reduce per level.
 __host__ __device__ inline bool reduce_vec(int ncols, int col_off) { return (ncols & 3) == 0 && (col_off & 3) == 0; }
 int wgrad_reduce_threads(int nrows, int ncols, int col_off) {
   const int ne = nrows * ncols;
   return std::max(reduce_vec(ncols, col_off) ? (ne + 3) / 4 : ne, nrows);
 }
 
-__global__ __launch_bounds__(kRedE * kRedG) void k_wgrad_reduce(const WgOut* __restrict__ outs,
-                                                                 const WgItem* __restrict__ items,
-                                                                 const WgProblem* __restrict__ probs,
-                                                                 const int64_t* __restrict__ slab_off,
-                                                                 const float* __restrict__ slabs,
-                                                                 const float* __restrict__ bias_slabs, int accumulate,
-                                                                 const uint32_t* __restrict__ amax) {
+__global__ __launch_bounds__(256) void k_wgrad_reduce(const WgOut* __restrict__ outs, const WgItem* __restrict__ items,
+                                                      const WgProblem* __restrict__ probs,
+                                                      const int64_t* __restrict__ slab_off,
+                                                      const float* __restrict__ slabs,
+                                                      const float* __restrict__ bias_slabs, int accumulate,
+                                                      const uint32_t* __restrict__ amax) {
   const WgOut o = outs[blockIdx.y];
-  const int lane = threadIdx.x & (kRedE - 1);
-  const int g = threadIdx.x / kRedE;  // wave-uniform
-  const int t = blockIdx.x * kRedE + lane;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int ld = probs[o.prob].ntc * 32;
   const int ne = o.nrows * o.ncols;
-  constexpr int kU = 8;  // item slabs in flight per wave
+  constexpr int kU = 8;  // item slabs in flight per step
   const int64_t* so = slab_off + o.item0;  // item i writes slab i: no item-table indirection
   // the output's slab offsets staged in LDS once (as scalar loads inside the k loop each round of
   // partials waited for its offsets first); an output with more items reads the rest from memory
   __shared__ int64_t s_off[256];
-  __shared__ f32x4 part[kRedG][kRedE];
-  __shared__ float bpart[kRedG][kRedE];
-  for (int i = threadIdx.x; i < o.nitems && i < 256; i += blockDim.x) s_off[i] = so[i];
+  if ((int)threadIdx.x < o.nitems) s_off[threadIdx.x] = so[threadIdx.x];
   __syncthreads();
   auto slab = [&](int k) { return k < 256 ? s_off[k] : so[k]; };
   auto inv_of = [&](int lev) { return amax ? delta_scale(amax + lev, true) : 1.0f; };  // exact powers of 2
   const bool vec = reduce_vec(o.ncols, o.col_off);
-  const bool live = vec ? 4 * t < ne : t < ne;
-  const bool blive = o.bias_dst && t < o.nrows;
-  const int e = vec ? 4 * t : t;
-  const int rr = live ? e / o.ncols : 0, cc = live ? e - rr * o.ncols : 0;
-  const size_t off = (size_t)(o.row_off + rr) * ld + o.col_off + cc;  // 16-B aligned when vec (ld % 32 == 0)
-  float* dst = o.dst + (size_t)rr * o.ld + o.dst_col + cc;
-  f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-  float bacc = 0.0f;
-  int k = 0;
-  for (int lev = 0; lev < o.nlev; ++lev) {
-    const int n = o.lev_items[lev];
-    const int q0 = k + (n * g) / kRedG, q1 = k + (n * (g + 1)) / kRedG;  // this wave's quarter
-    f32x4 s = {0.0f, 0.0f, 0.0f, 0.0f};
-    float bs = 0.0f;
-    if (live) {
+  if (vec ? 4 * t < ne : t < ne) {
+    const int e = vec ? 4 * t : t;
+    const int rr = e / o.ncols, cc = e - rr * o.ncols;
+    const size_t off = (size_t)(o.row_off + rr) * ld + o.col_off + cc;  // 16-B aligned when vec (ld % 32 == 0)
+    float* dst = o.dst + (size_t)rr * o.ld + o.dst_col + cc;
+    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    int k = 0;
+    for (int lev = 0; lev < o.nlev; ++lev) {
+      const int k1 = k + o.lev_items[lev];
+      f32x4 s = {0.0f, 0.0f, 0.0f, 0.0f};
+      // kU slabs in flight, the last round guarded (uniform conditions), summed in item order
       if (vec) {
-        for (int j = q0; j < q1; j += kU) {
+        for (; k < k1; k += kU) {
           f32x4 v[kU];
 #pragma unroll
           for (int u = 0; u < kU; ++u)
-            if (j + u < q1) v[u] = *reinterpret_cast<const f32x4*>(slabs + slab(j + u) + off);
+            if (k + u < k1) v[u] = *reinterpret_cast<const f32x4*>(slabs + slab(k + u) + off);
 #pragma unroll
           for (int u = 0; u < kU; ++u)
-            if (j + u < q1) s += v[u];
+            if (k + u < k1) s += v[u];
         }
       } else {
-        for (int j = q0; j < q1; j += kU) {
+        for (; k < k1; k += kU) {
           float v[kU];
 #pragma unroll
           for (int u = 0; u < kU; ++u)
-            if (j + u < q1) v[u] = slabs[slab(j + u) + off];
+            if (k + u < k1) v[u] = slabs[slab(k + u) + off];
 #pragma unroll
           for (int u = 0; u < kU; ++u)
-            if (j + u < q1) s[0] += v[u];
+            if (k + u < k1) s[0] += v[u];
         }
       }
+      k = k1;
+      const float inv = inv_of(lev);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float v = s[j] * inv;
+        acc[j] = lev == 0 ? (accumulate ? dst[vec ? j : 0] + v : v) : acc[j] + v;
+      }
     }
-    if (blive) {  // bias partials = row sums of delta, the same quarters
-      for (int j = q0; j < q1; j += kU) {
+    if (vec) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dst[j] = acc[j];
+    } else {
+      dst[0] = acc[0];
+    }
+  }
+  if (o.bias_dst && t < o.nrows) {
+    float acc = 0.0f;
+    int k = 0;
+    for (int lev = 0; lev < o.nlev; ++lev) {
+      float s = 0.0f;
+      const int k1 = k + o.lev_items[lev];
+      // kU partials in flight, summed in item order (as one at a time, the same bits): a single load per
+      // step made this chain — one HBM/MALL latency per item of the output — the reduce's critical path
+      for (; k < k1; k += kU) {
         float v[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u)
-          if (j + u < q1) v[u] = bias_slabs[(size_t)(o.item0 + j + u) * 256 + o.row_off + t];
+          if (k + u < k1) v[u] = bias_slabs[(size_t)(o.item0 + k + u) * 256 + o.row_off + t];
 #pragma unroll
         for (int u = 0; u < kU; ++u)
-          if (j + u < q1) bs += v[u];
+          if (k + u < k1) s += v[u];
       }
+      k = k1;
+      const float v = s * inv_of(lev);
+      acc = lev == 0 ? (accumulate ? o.bias_dst[t] + v : v) : acc + v;
     }
-    part[g][lane] = s;
-    bpart[g][lane] = bs;
-    __syncthreads();
-    if (g == 0) {
-      f32x4 q = part[0][lane];
-      float bq = bpart[0][lane];
-#pragma unroll
-      for (int w = 1; w < kRedG; ++w) {
-        q += part[w][lane];
-        bq += bpart[w][lane];
-      }
-      const float inv = inv_of(lev);
-      if (live) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float v = q[j] * inv;
-          acc[j] = lev == 0 ? (accumulate ? dst[vec ? j : 0] + v : v) : acc[j] + v;
-        }
-      }
-      if (blive) {
-        const float v = bq * inv;
-        bacc = lev == 0 ? (accumulate ? o.bias_dst[t] + v : v) : bacc + v;
-      }
-    }
-    __syncthreads();  // the partials are rewritten by the next level
-    k += n;
-  }
-  if (g == 0) {
-    if (live) {
-      if (vec) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) dst[j] = acc[j];
-      } else {
-        dst[0] = acc[0];
-      }
-    }
-    if (blive) o.bias_dst[t] = bacc;
+    o.bias_dst[t] = acc;
   }
 }
 
@@ -1312,8 +1074,8 @@ hipError_t launch_wgrad_reduce(const WgOut* outs, int nouts, int max_elems, cons
                                const WgProblem* probs, const int64_t* slab_off, const float* slabs,
                                const float* bias_slabs, int accumulate, const uint32_t* amax, hipStream_t st) {
   if (nouts <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3((max_elems + kRedE - 1) / kRedE, nouts), dim3(kRedE * kRedG), 0, st, outs,
-                     items, probs, slab_off, slabs, bias_slabs, accumulate, amax);
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((max_elems + 255) / 256, nouts), dim3(256), 0, st, outs, items, probs,
+                     slab_off, slabs, bias_slabs, accumulate, amax);
   return hipGetLastError();
 }
 

@@ -378,6 +378,10 @@ typedef struct nof_mlp_debug {
   const float* zhead;     /* [M][4]: z_density, z_rgb[3] (pre-activation heads) */
   const float* delta;     /* 8 consecutive [256]-feature dL/dz tensors (last get_gradient) */
   const float* delta9x;   /* [160]-feature blocks: dL/dz9 | dz_density | dz_rgb | 0 */
+  /* any-shape networks (generic != 0: every field above but M and zhead is NULL): row-major activations */
+  int32_t generic;
+  const float* gen_h;     /* net_depth consecutive [M][net_width] trunk activations */
+  const float* gen_hc;    /* net_depth_condition consecutive [M][net_width_condition] (view layer first) */
 } nof_mlp_debug;
 nof_status nof_mlp_debug_view(nof_mlp* m, int32_t level, nof_mlp_debug* out);
 

@@ -96,13 +96,27 @@ static void check_cfg(const nof_config& c) {
     if (!(S == 64 || S == 128 || S == 256 || S == 512))
       throw Error(NOF_ERR_UNSUPPORTED, "GPU path supports 64/128/256/512 samples per level");
   }
-  if (c.net_depth != 8 || c.net_width != 256 || c.net_depth_condition != 1 || c.net_width_condition != 128 ||
-      c.skip_layer != 4 || c.min_deg_point != 0 || c.max_deg_point != 16 || c.deg_view != 4)
-    throw Error(NOF_ERR_UNSUPPORTED, "GPU path implements the reference network (8x256, 1x128, skip 4, PE 16/4)");
+  // the network (MLP.cs:64-86): any depth / width / skip / PE degrees within the checkpoint's 16 layers
+  NOF_REQUIRE(c.net_depth >= 1 && c.net_depth_condition >= 1 &&
+                  c.net_depth + c.net_depth_condition + 2 <= AcceleratedMLP::kMaxLayers,
+              "net_depth >= 1, net_depth_condition >= 1, net_depth + net_depth_condition <= 14");
+  NOF_REQUIRE(c.net_width >= 1 && c.net_width <= 4096 && c.net_width_condition >= 1 && c.net_width_condition <= 4096,
+              "network widths must be in [1, 4096]");
+  NOF_REQUIRE(c.skip_layer >= 1, "skip_layer must be >= 1");
+  NOF_REQUIRE(c.min_deg_point >= 0 && c.max_deg_point > c.min_deg_point && c.max_deg_point <= 24,
+              "point PE degrees: 0 <= min_deg_point < max_deg_point <= 24");
+  NOF_REQUIRE(c.deg_view >= 0 && c.deg_view <= 24, "deg_view must be in [0, 24]");
   NOF_REQUIRE(c.precision == NOF_PRECISION_F32 || c.precision == NOF_PRECISION_F32_SPLIT ||
                   c.precision == NOF_PRECISION_F16X2 || c.precision == NOF_PRECISION_F32_F16SPLIT ||
                   c.precision == NOF_PRECISION_F16,
               "unknown precision mode");
+  const bool reference_net = c.net_depth == 8 && c.net_width == 256 && c.net_depth_condition == 1 &&
+                             c.net_width_condition == 128 && c.skip_layer == 4 && c.min_deg_point == 0 &&
+                             c.max_deg_point == 16 && c.deg_view == 4;
+  if (!reference_net && c.precision != NOF_PRECISION_F32)
+    throw Error(NOF_ERR_UNSUPPORTED,
+                "networks other than the reference's 8x256 / 1x128 / skip 4 / PE 16, 4 run in NOF_PRECISION_F32 "
+                "only (the any-shape path, generic.hip)");
   NOF_REQUIRE(c.grad_buckets == 0 || c.grad_buckets == 1, "grad_buckets must be 0 or 1");
   NOF_REQUIRE(c.lindisp == 0 || c.lindisp == 1, "lindisp must be 0 or 1");
   NOF_REQUIRE(c.ray_shape == NOF_RAY_CONICAL || c.ray_shape == NOF_RAY_CYLINDRICAL, "unknown ray_shape");
@@ -122,27 +136,44 @@ AcceleratedMLP::AcceleratedMLP(int deg_point, int deg_view, const nof_config& cf
   num_cu_ = prop.multiProcessorCount;
   aligned_ = cfg.grad_buckets != 0;
 
-  // layer dims (get_layer_sizes MLPcpp:131-154)
-  const int W = 256, Wc = 128, pos = 96, dir = 27;
-  for (int l = 0; l < 8; ++l) { out_[l] = W; in_[l] = l == 0 ? pos : (l == 4 ? W + pos : W); }
-  out_[8] = 1; in_[8] = W;
-  out_[9] = Wc; in_[9] = W + dir;
-  out_[10] = 3; in_[10] = Wc;
+  // layer dims (get_layer_sizes MLPcpp:131-154, generalised as MLP.cs:64-86): trunk 0..D-1 (the IPE
+  // concatenated into every skip-th layer after the first), density D, view D+1 ([h | view PE]),
+  // condition layers D+2..D+Dc, rgb D+Dc+1
+  const int D = cfg.net_depth, W = cfg.net_width, Dc = cfg.net_depth_condition, Wc = cfg.net_width_condition;
+  const int pos = 6 * (cfg.max_deg_point - cfg.min_deg_point), dir = 3 * (2 * cfg.deg_view + 1);
+  const int L = D + Dc + 2;
+  out_.resize(L); in_.resize(L); woff_.resize(L); boff_.resize(L);
+  for (int l = 0; l < D; ++l) { out_[l] = W; in_[l] = l == 0 ? pos : (l % cfg.skip_layer == 0 ? W + pos : W); }
+  out_[D] = 1; in_[D] = W;
+  out_[D + 1] = Wc; in_[D + 1] = W + dir;
+  for (int i = 1; i < Dc; ++i) { out_[D + 1 + i] = Wc; in_[D + 1 + i] = Wc; }
+  out_[D + 1 + Dc] = 3; in_[D + 1 + Dc] = Wc;
   size_t o = 0;
-  for (int l = 0; l < kLayers; ++l) { woff_[l] = (int)o; o += (size_t)out_[l] * in_[l]; }
-  for (int l = 0; l < kLayers; ++l) { boff_[l] = (int)o; o += out_[l]; }
+  for (int l = 0; l < L; ++l) { woff_[l] = (int)o; o += (size_t)out_[l] * in_[l]; }
+  for (int l = 0; l < L; ++l) { boff_[l] = (int)o; o += out_[l]; }
+  NOF_REQUIRE(o < (size_t)1 << 31, "network too large");
   P_ = o;
+  generic_ = !(D == 8 && W == 256 && Dc == 1 && Wc == 128 && cfg.skip_layer == 4 && cfg.min_deg_point == 0 &&
+               cfg.max_deg_point == 16 && cfg.deg_view == 4);
 
   params_.alloc(P_);
   grads_.alloc(P_);
   NOF_HIP(hipMemset(grads_.p, 0, P_ * sizeof(float)));
   std::vector<float> h(P_, 0.0f);
-  glorot_host(h.data(), out_.data(), in_.data(), woff_.data(), kLayers, cfg.seed);
+  glorot_host(h.data(), out_.data(), in_.data(), woff_.data(), L, cfg.seed);
   NOF_HIP(hipMemcpy(params_.p, h.data(), P_ * sizeof(float), hipMemcpyHostToDevice));
-  for (int l = 0; l < kLayers; ++l) { param_views_.push_back(params_.p + woff_[l]); grad_views_.push_back(grads_.p + woff_[l]); }
-  for (int l = 0; l < kLayers; ++l) { param_views_.push_back(params_.p + boff_[l]); grad_views_.push_back(grads_.p + boff_[l]); }
+  for (int l = 0; l < L; ++l) { param_views_.push_back(params_.p + woff_[l]); grad_views_.push_back(grads_.p + woff_[l]); }
+  for (int l = 0; l < L; ++l) { param_views_.push_back(params_.p + boff_[l]); grad_views_.push_back(grads_.p + boff_[l]); }
 
   precision_ = cfg.precision;
+  numeric_.alloc(2);
+  NOF_HIP(hipMemset(numeric_.p, 0, 2 * sizeof(uint32_t)));
+  if (generic_) {
+    gD_ = D; gW_ = W; gDc_ = Dc; gWc_ = Wc; gskip_ = cfg.skip_layer; gmin_deg_ = cfg.min_deg_point;
+    gP_ = pos; gVd_ = dir;
+    gen_alloc();
+    return;
+  }
   if (precision_ == NOF_PRECISION_F32_SPLIT) {  // bf16 (hi, mid, lo) slices + the fp32 tails (mlp_common.h)
     wimg_f_.alloc(nof::fwd_image_split_floats<1>() + nof::kFwdTail);
     wimg_b_.alloc(nof::bwd_image_split_floats<1>() + nof::kBwdTail);
@@ -176,20 +207,20 @@ AcceleratedMLP::AcceleratedMLP(int deg_point, int deg_view, const nof_config& cf
     NOF_HIP(hipMemset(L.delta9x.p, 0, L.delta9x.n * sizeof(float)));  // rows 132..159 stay zero
     max_M_ = std::max(max_M_, L.cap);
   }
-  numeric_.alloc(2);
-  NOF_HIP(hipMemset(numeric_.p, 0, 2 * sizeof(uint32_t)));
   slab_cap_ = (size_t)(num_cu_ + 64) * 65536;
   slabs_.alloc(slab_cap_);
   bias_slabs_.alloc((size_t)(num_cu_ + 64) * 256);
 }
 
 std::vector<int> AcceleratedMLP::get_layer_sizes() const {
-  std::vector<int> s(2 * kLayers);
-  for (int l = 0; l < kLayers; ++l) { s[l] = out_[l] * in_[l]; s[kLayers + l] = out_[l]; }
+  const int L = num_layers();
+  std::vector<int> s(2 * L);
+  for (int l = 0; l < L; ++l) { s[l] = out_[l] * in_[l]; s[L + l] = out_[l]; }
   return s;
 }
 
 void AcceleratedMLP::pack_weights() {
+  if (generic_) return;  // the any-shape path reads the canonical arena directly
   nof::PackArgs pa;
   for (int l = 0; l < kLayers; ++l) { pa.woff[l] = woff_[l]; pa.boff[l] = boff_[l]; }
   if (f16_pieces()) {  // the step's delta-scale maxima start at 0 (no memset launch per level)
@@ -237,6 +268,16 @@ void AcceleratedMLP::forward_fused(int level, int n, int samples, const float* t
   const int M = n * samples;
   NOF_REQUIRE(n > 0 && samples % kBlk == 0 && M <= lv_[level].cap, "batch exceeds the level's capacity");
   lv_[level].M = M; lv_[level].n = n; lv_[level].S = samples;
+  if (generic_) {  // cast + encode, then the layer GEMMs
+    GenLevel& G = gl_[level];
+    tb(kTMlpFwd);
+    NOF_HIP(nof::launch_cast(n, samples, t, origins, dirs, radii, G.mean.p, G.cov.p, st_, cfg_.ray_shape));
+    NOF_HIP(nof::launch_encode_g(n, samples, G.mean.p, G.cov.p, dirs, gmin_deg_, gP_, gVd_, G.enc_pos.p, G.enc_dir.p,
+                                 st_));
+    te(kTMlpFwd);
+    gen_forward(level, G.enc_pos.p, G.enc_dir.p);
+    return;
+  }
   nof::FwdArgs a{};
   a.M = M; a.S = samples; a.encoded = 0;
   a.no_store = inference ? 1 : 0;
@@ -254,6 +295,10 @@ std::pair<float*, float*> AcceleratedMLP::get_output(const float* enc_pos, const
               "n_rays * samples must be a multiple of 32 within the level's capacity");
   pack_weights();
   lv_[level].M = M; lv_[level].n = n_rays; lv_[level].S = samples;
+  if (generic_) {
+    gen_forward(level, enc_pos, enc_dir);
+    return {lv_[level].sigma.p, lv_[level].rgb.p};
+  }
   nof::FwdArgs a{};
   a.M = M; a.S = samples; a.encoded = 1;
   a.enc_pos = enc_pos; a.enc_dir = enc_dir;
@@ -264,16 +309,23 @@ std::pair<float*, float*> AcceleratedMLP::get_output(const float* enc_pos, const
 nof_mlp_debug AcceleratedMLP::debug_view(int level) const {
   NOF_REQUIRE(level >= 0 && level < (int)lv_.size(), "level out of range");
   const Level& L = lv_[level];
-  nof_mlp_debug d;
+  nof_mlp_debug d{};
   d.M = L.M;
+  if (generic_) {
+    const GenLevel& G = gl_[level];
+    d.generic = 1;
+    d.gen_h = G.h.p; d.gen_hc = G.hc.p; d.zhead = G.z.p;
+    return d;
+  }
   d.act_in = L.act_in.p; d.act_h = L.act_h.p; d.act_h9 = L.act_h9.p; d.masks = L.masks.p; d.zhead = L.zhead.p;
   d.delta = L.delta.p; d.delta9x = L.delta9x.p;
   return d;
 }
 
 int grad_bucket_spans(const int* sizes, int num_layers, int b, int64_t* off, int64_t* cnt) {
-  // arena [W0..W(L-1), b0..b(L-1)] (MLPcpp:131-154); bucket 0 = W5..W(L-1), bucket 1 = the rest
-  NOF_REQUIRE(sizes && num_layers > 5 && b >= 0 && b < AcceleratedMLP::kBuckets, "bad bucket query");
+  // arena [W0..W(L-1), b0..b(L-1)] (MLPcpp:131-154); bucket 0 = W5..W(L-1) (empty for L <= 5), bucket 1 =
+  // the rest
+  NOF_REQUIRE(sizes && num_layers >= 1 && b >= 0 && b < AcceleratedMLP::kBuckets, "bad bucket query");
   int64_t w5 = 0, wend = 0, total = 0;
   for (int l = 0; l < num_layers; ++l) {
     if (l < 5) w5 += sizes[l];
@@ -291,7 +343,7 @@ int grad_bucket_spans(const int* sizes, int num_layers, int b, int64_t* off, int
 
 int AcceleratedMLP::bucket_spans(int b, int64_t* off, int64_t* cnt) const {
   const std::vector<int> s = get_layer_sizes();
-  return grad_bucket_spans(s.data(), kLayers, b, off, cnt);
+  return grad_bucket_spans(s.data(), num_layers(), b, off, cnt);
 }
 
 AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int lv0, int lv1, int bucket) {
@@ -632,6 +684,10 @@ float* const* AcceleratedMLP::get_gradient(const float* color_grad, const float*
   NOF_REQUIRE(color_grad && density_grad, "null output gradients");
   NOF_REQUIRE((flags & ~(uint32_t)(NOF_GRAD_ACCUMULATE | NOF_GRAD_PUBLISH)) == 0, "unknown gradient flags");
   const bool buckets = (flags & NOF_GRAD_PUBLISH) && hook_;
+  if (generic_) {
+    gen_backward(level, color_grad, density_grad, (level > 0 || (flags & NOF_GRAD_ACCUMULATE)) ? 1 : 0);
+    return gen_publish(buckets);
+  }
   // build every schedule this call needs before the first launch (a schedule may grow the slabs,
   // which synchronises the stream)
   if (!buckets) (void)schedule(level, level + 1);
@@ -651,6 +707,11 @@ float* const* AcceleratedMLP::get_gradient_levels(const float* const* color_grad
   }
   NOF_REQUIRE((flags & ~(uint32_t)(NOF_GRAD_ACCUMULATE | NOF_GRAD_PUBLISH)) == 0, "unknown gradient flags");
   const bool buckets = (flags & NOF_GRAD_PUBLISH) && hook_;
+  if (generic_) {
+    for (int l = 0; l < nl; ++l)
+      gen_backward(l, color_grads[l], density_grads[l], (l > 0 || (flags & NOF_GRAD_ACCUMULATE)) ? 1 : 0);
+    return gen_publish(buckets);
+  }
   if (!buckets) (void)schedule(0, nl);
   else
     for (int b = 0; b < kBuckets; ++b) (void)schedule(0, nl, b);
@@ -659,6 +720,233 @@ float* const* AcceleratedMLP::get_gradient_levels(const float* const* color_grad
     for (; l + 1 < nl; l += 2) run_backward2(l, color_grads + l, density_grads + l);
   for (; l < nl; ++l) run_backward(l, color_grads[l], density_grads[l]);
   return wgrad_levels(0, nl, (flags & NOF_GRAD_ACCUMULATE) ? 1 : 0, buckets);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Any-shape fp32 path (generic.hip).  Per level: trunk activations h_l [M][W] (l < D), condition
+// activations [M][Wc] (Dc of them), heads z [M][4]; the backward walks the layers in reverse (as
+// mlp_backward_sample / MLPcpp:256-321), one dX GEMM (ReLU mask = the stored activation > 0) and one
+// split-K weight-gradient GEMM + ordered slab sum per layer and input block.
+// ------------------------------------------------------------------------------------------------
+static nof::GemmSrc gsrc(const float* p, int64_t si, int64_t sk, int idiv = 1, int kdiv = 1) {
+  nof::GemmSrc s;
+  s.p = p; s.si = si; s.sk = sk; s.idiv = idiv; s.kdiv = kdiv;
+  return s;
+}
+
+static void gemm1(nof::GemmArgs a, hipStream_t st) {  // no split: one k chunk
+  a.kchunk = (a.K1 + a.K2 + 15) / 16 * 16;
+  a.slab_stride = 0;
+  NOF_HIP(nof::launch_gemm(a, 1, st));
+}
+
+// split-K of a weight gradient (k = the level's M samples): about 2048 workgroups over the output tiles,
+// chunks of at least 256 samples, a multiple of 16
+void AcceleratedMLP::gen_split(int nout, int ncols, int M, int* ksplit, int* kchunk) {
+  const int tiles = ((nout + 63) / 64) * ((ncols + 63) / 64);
+  int ks = std::max(1, std::min((2048 + tiles - 1) / tiles, M / 256));
+  const int kc = ((M + ks - 1) / ks + 15) / 16 * 16;
+  *kchunk = kc;
+  *ksplit = (M + kc - 1) / kc;
+}
+
+void AcceleratedMLP::gen_alloc() {
+  const int NL = cfg_.num_levels;
+  lv_.resize(NL);
+  gl_.resize(NL);
+  for (int l = 0; l < NL; ++l) {
+    Level& L = lv_[l];
+    GenLevel& G = gl_[l];
+    L.cap = cfg_.max_rays * cfg_.num_samples[l];
+    const size_t M = L.cap;
+    G.mean.alloc(3 * M); G.cov.alloc(3 * M);
+    G.enc_pos.alloc(M * gP_);
+    G.enc_dir.alloc((size_t)cfg_.max_rays * gVd_);
+    G.h.alloc((size_t)gD_ * M * gW_);
+    G.hc.alloc((size_t)gDc_ * M * gWc_);
+    G.z.alloc(4 * M);
+    L.sigma.alloc(M);
+    L.rgb.alloc(3 * M);
+    max_M_ = std::max(max_M_, L.cap);
+  }
+  const size_t Wm = std::max(gW_, gWc_);
+  gd0_.alloc((size_t)max_M_ * Wm);
+  gd1_.alloc((size_t)max_M_ * Wm);
+  gdz_.alloc((size_t)max_M_ * 4);
+  gones_.alloc(1);
+  const float one = 1.0f;
+  NOF_HIP(hipMemcpy(gones_.p, &one, sizeof(float), hipMemcpyHostToDevice));
+  // split-K slabs: the largest (output rows x columns) block over every level's sample count (the split
+  // grows with M up to its tile-count cap, so each level's capacity bounds its launches)
+  const int shapes[][2] = {{gW_, gW_}, {gW_, gP_}, {1, gW_}, {gWc_, gW_}, {gWc_, gVd_}, {gWc_, gWc_},
+                           {3, gWc_}, {gW_, 1}, {gWc_, 1}, {3, 1}, {1, 1}};
+  size_t slab = 0;
+  for (int l = 0; l < NL; ++l)
+    for (const auto& s : shapes) {
+      int ks, kc;
+      gen_split(s[0], s[1], lv_[l].cap, &ks, &kc);
+      slab = std::max(slab, (size_t)ks * s[0] * s[1]);
+    }
+  gslab_.alloc(slab);
+}
+
+void AcceleratedMLP::gen_wgrad(float* dst, int64_t ld, const float* dz, int64_t ldz, int nout, nof::GemmSrc x,
+                               int ncols, int M, int accumulate) {
+  int ks, kc;
+  gen_split(nout, ncols, M, &ks, &kc);
+  NOF_REQUIRE((size_t)ks * nout * ncols <= gslab_.n, "split-K slabs too small");
+  nof::GemmArgs a;
+  a.M = nout; a.N = ncols; a.K1 = M;
+  a.A1 = gsrc(dz, 1, ldz);  // A(o, m) = dZ[m][o]
+  a.B1 = x;                 // B(j, m) = X[m][j]
+  a.C = gslab_.p; a.ci = ncols; a.cj = 1;
+  a.kchunk = kc; a.slab_stride = (int64_t)nout * ncols;
+  NOF_HIP(nof::launch_gemm(a, ks, st_));
+  NOF_HIP(nof::launch_slab_sum(nout, ncols, ks, gslab_.p, a.slab_stride, dst, ld, accumulate, st_));
+}
+
+void AcceleratedMLP::gen_forward(int level, const float* ep, const float* ed) {
+  Level& L = lv_[level];
+  GenLevel& G = gl_[level];
+  const int M = L.M, S = L.S, D = gD_, W = gW_, Dc = gDc_, Wc = gWc_, P = gP_, Vd = gVd_, lr = D + 1 + Dc;
+  G.ep = ep; G.ed = ed;
+  const float* prm = params_.p;
+  auto H = [&](int l) { return G.h.p + (size_t)l * M * W; };
+  auto Hc = [&](int i) { return G.hc.p + (size_t)i * M * Wc; };
+  tb(kTMlpFwd);
+  for (int l = 0; l < D; ++l) {  // trunk (MLPcs:90-100): [h | IPE] into every skip-th layer after the first
+    nof::GemmArgs a;
+    a.M = M; a.N = W;
+    if (l == 0) {
+      a.K1 = P; a.A1 = gsrc(ep, P, 1);
+    } else {
+      a.K1 = W; a.A1 = gsrc(H(l - 1), W, 1);
+      if (l % gskip_ == 0) { a.K2 = P; a.A2 = gsrc(ep, P, 1); }
+    }
+    a.B1 = gsrc(prm + woff_[l], in_[l], 1);
+    a.B2 = gsrc(prm + woff_[l] + a.K1, in_[l], 1);
+    a.bias = prm + boff_[l]; a.relu = 1;
+    a.C = H(l); a.ci = W; a.cj = 1;
+    gemm1(a, st_);
+  }
+  {  // density head (MLPcs:101): z[:, 0]
+    nof::GemmArgs a;
+    a.M = M; a.N = 1; a.K1 = W;
+    a.A1 = gsrc(H(D - 1), W, 1);
+    a.B1 = gsrc(prm + woff_[D], W, 1);
+    a.bias = prm + boff_[D];
+    a.C = G.z.p; a.ci = 4; a.cj = 1;
+    gemm1(a, st_);
+  }
+  for (int i = 0; i < Dc; ++i) {  // view layer [h | view PE of the ray] (MLPcs:102-106), condition layers
+    const int l = D + 1 + i;
+    nof::GemmArgs a;
+    a.M = M; a.N = Wc;
+    if (i == 0) {
+      a.K1 = W; a.A1 = gsrc(H(D - 1), W, 1);
+      a.K2 = Vd; a.A2 = gsrc(ed, Vd, 1, S);
+    } else {
+      a.K1 = Wc; a.A1 = gsrc(Hc(i - 1), Wc, 1);
+    }
+    a.B1 = gsrc(prm + woff_[l], in_[l], 1);
+    a.B2 = gsrc(prm + woff_[l] + a.K1, in_[l], 1);
+    a.bias = prm + boff_[l]; a.relu = 1;
+    a.C = Hc(i); a.ci = Wc; a.cj = 1;
+    gemm1(a, st_);
+  }
+  {  // rgb head (MLPcs:107): z[:, 1..3]
+    nof::GemmArgs a;
+    a.M = M; a.N = 3; a.K1 = Wc;
+    a.A1 = gsrc(Hc(Dc - 1), Wc, 1);
+    a.B1 = gsrc(prm + woff_[lr], Wc, 1);
+    a.bias = prm + boff_[lr];
+    a.C = G.z.p + 1; a.ci = 4; a.cj = 1;
+    gemm1(a, st_);
+  }
+  NOF_HIP(nof::launch_heads_fwd(M, G.z.p, L.sigma.p, L.rgb.p, st_));
+  te(kTMlpFwd);
+}
+
+void AcceleratedMLP::gen_backward(int level, const float* color_grad, const float* density_grad, int acc) {
+  Level& L = lv_[level];
+  GenLevel& G = gl_[level];
+  NOF_REQUIRE(G.ep && G.ed, "get_gradient before get_output for this level");
+  const int M = L.M, S = L.S, D = gD_, W = gW_, Dc = gDc_, Wc = gWc_, P = gP_, Vd = gVd_, lr = D + 1 + Dc;
+  const float* prm = params_.p;
+  float* gr = grads_.p;
+  auto H = [&](int l) { return G.h.p + (size_t)l * M * W; };
+  auto Hc = [&](int i) { return G.hc.p + (size_t)i * M * Wc; };
+  const nof::GemmSrc ones = gsrc(gones_.p, 0, 0);
+  float* dz = gdz_.p;
+  float *cur = gd0_.p, *nxt = gd1_.p;
+  // dX of layer l into C, masked by the activation `mask` > 0: C[m][j] = sum_o dZ[m][o] W_l[o][j]
+  auto dx = [&](const float* dzp, int64_t ldz, int nout, int l, const float* mask, int width, float* C) {
+    nof::GemmArgs a;
+    a.M = M; a.N = width; a.K1 = nout;
+    a.A1 = gsrc(dzp, ldz, 1);
+    a.B1 = gsrc(prm + woff_[l], 1, in_[l]);
+    a.G = mask; a.gi = width; a.gj = 1;
+    a.C = C; a.ci = width; a.cj = 1;
+    gemm1(a, st_);
+  };
+  tb(kTMlpBwd);
+  NOF_HIP(nof::launch_heads_bwd(M, density_grad, color_grad, G.z.p, dz, st_));  // MNcs:23-28, 184-189
+  // rgb head: dW, db from dz[:, 1..3]; its dX into the last condition layer
+  gen_wgrad(gr + woff_[lr], Wc, dz + 1, 4, 3, gsrc(Hc(Dc - 1), 1, Wc), Wc, M, acc);
+  gen_wgrad(gr + boff_[lr], 1, dz + 1, 4, 3, ones, 1, M, acc);
+  dx(dz + 1, 4, 3, lr, Hc(Dc - 1), Wc, cur);
+  for (int i = Dc - 1; i >= 1; --i) {  // condition layers
+    const int l = D + 1 + i;
+    gen_wgrad(gr + woff_[l], Wc, cur, Wc, Wc, gsrc(Hc(i - 1), 1, Wc), Wc, M, acc);
+    gen_wgrad(gr + boff_[l], 1, cur, Wc, Wc, ones, 1, M, acc);
+    dx(cur, Wc, Wc, l, Hc(i - 1), Wc, nxt);
+    std::swap(cur, nxt);
+  }
+  // view layer: columns [0, W) against h_{D-1}, [W, W + Vd) against the ray's view PE
+  gen_wgrad(gr + woff_[D + 1], W + Vd, cur, Wc, Wc, gsrc(H(D - 1), 1, W), W, M, acc);
+  gen_wgrad(gr + woff_[D + 1] + W, W + Vd, cur, Wc, Wc, gsrc(G.ed, 1, Vd, 1, S), Vd, M, acc);
+  gen_wgrad(gr + boff_[D + 1], 1, cur, Wc, Wc, ones, 1, M, acc);
+  // density head
+  gen_wgrad(gr + woff_[D], W, dz, 4, 1, gsrc(H(D - 1), 1, W), W, M, acc);
+  gen_wgrad(gr + boff_[D], 1, dz, 4, 1, ones, 1, M, acc);
+  {  // dh_{D-1} = dZ_view W_view[:, :W] + dz_density w_D (MLPcs:148-153, D11), masked
+    nof::GemmArgs a;
+    a.M = M; a.N = W; a.K1 = Wc; a.K2 = 1;
+    a.A1 = gsrc(cur, Wc, 1);
+    a.A2 = gsrc(dz, 4, 1);
+    a.B1 = gsrc(prm + woff_[D + 1], 1, W + Vd);
+    a.B2 = gsrc(prm + woff_[D], 1, 0);
+    a.G = H(D - 1); a.gi = W; a.gj = 1;
+    a.C = nxt; a.ci = W; a.cj = 1;
+    gemm1(a, st_);
+    std::swap(cur, nxt);
+  }
+  for (int l = D - 1; l >= 0; --l) {  // trunk
+    float* gw = gr + woff_[l];
+    if (l > 0) {
+      gen_wgrad(gw, in_[l], cur, W, W, gsrc(H(l - 1), 1, W), W, M, acc);
+      if (l % gskip_ == 0) gen_wgrad(gw + W, in_[l], cur, W, W, gsrc(G.ep, 1, P), P, M, acc);
+    } else {
+      gen_wgrad(gw, P, cur, W, W, gsrc(G.ep, 1, P), P, M, acc);
+    }
+    gen_wgrad(gr + boff_[l], 1, cur, W, W, ones, 1, M, acc);
+    if (l > 0) {
+      dx(cur, W, W, l, H(l - 1), W, nxt);
+      std::swap(cur, nxt);
+    }
+  }
+  te(kTMlpBwd);
+}
+
+float* const* AcceleratedMLP::gen_publish(bool buckets) {
+  if (buckets)
+    for (int bk = 0; bk < kBuckets; ++bk) {
+      int64_t off[2], cnt[2];
+      const int ns = bucket_spans(bk, off, cnt);
+      TraceRange hr("nof:gradient_bucket_hook");
+      hook_(hook_user_, bk, ns, off, cnt);
+    }
+  return grad_views_.data();
 }
 
 // ------------------------------------------------------------------------------------------------

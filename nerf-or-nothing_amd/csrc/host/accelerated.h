@@ -96,8 +96,13 @@ enum TimerId { kTPack = 0, kTSample, kTMlpFwd, kTRenderFwd, kTRenderBwd, kTMlpBw
 // ---------------------------------------------------------------------------------------------
 class AcceleratedMLP {
  public:
-  static constexpr int kLayers = 11;   // net_depth + net_depth_condition + 2
+  static constexpr int kLayers = 11;   // the reference network's net_depth + net_depth_condition + 2
   static constexpr int kTensors = 22;  // [W0..W10, b0..b10]
+  static constexpr int kMaxLayers = 16;  // any-shape networks: D + Dc + 2 layers (2L <= 32 checkpoint sizes)
+  int num_layers() const { return (int)out_.size(); }
+  // the network is not the reference's 8x256 / 1x128 / skip 4 / PE (0, 16), 4: the any-shape fp32 path
+  // (generic.hip) runs it
+  bool generic() const { return generic_; }
 
   AcceleratedMLP(int deg_point, int deg_view, const nof_config& cfg);  // MLPcpp:168-213
   ~AcceleratedMLP() = default;
@@ -195,7 +200,26 @@ class AcceleratedMLP {
   // fp16 activation / delta blocks and the k_wgrad_h weight gradients (F16X2, F16)
   bool f16_blocks() const { return precision_ == NOF_PRECISION_F16X2 || precision_ == NOF_PRECISION_F16; }
   size_t P_ = 0;
-  std::array<int, kLayers> out_{}, in_{}, woff_{}, boff_{};
+  std::vector<int> out_, in_, woff_, boff_;  // per layer (MLPcpp:131-154 / the oracle's Spec order)
+
+  // ---- any-shape fp32 path (generic.hip): one MFMA GEMM launch per layer and level ----------------
+  bool generic_ = false;
+  int gD_ = 0, gW_ = 0, gDc_ = 0, gWc_ = 0, gskip_ = 0, gmin_deg_ = 0, gP_ = 0, gVd_ = 0;
+  struct GenLevel {
+    DevBuf<float> mean, cov, enc_pos, enc_dir;  // the fused path's encodings ([M][P], [n][Vd])
+    DevBuf<float> h, hc, z;                     // trunk [D][M][W], condition [Dc][M][Wc], heads [M][4]
+    const float *ep = nullptr, *ed = nullptr;   // the encodings the last forward read (API path: the caller's)
+  };
+  std::vector<GenLevel> gl_;
+  DevBuf<float> gd0_, gd1_, gdz_, gslab_, gones_;  // dZ ping-pong [M][max(W, Wc)], heads dz [M][4], split-K
+  void gen_alloc();
+  void gen_forward(int level, const float* enc_pos, const float* enc_dir);
+  void gen_backward(int level, const float* color_grad, const float* density_grad, int accumulate);
+  // columns [col0, col0 + ncols) of layer l's weight gradient: sum_m dZ(m, o) X(m, j) (+ bias when X = ones)
+  void gen_wgrad(float* dst, int64_t ld, const float* dz, int64_t ldz, int nout, nof::GemmSrc x, int ncols, int M,
+                 int accumulate);
+  static void gen_split(int nout, int ncols, int M, int* ksplit, int* kchunk);
+  float* const* gen_publish(bool buckets);  // the bucket hook once per bucket (every gradient is final)
   DevBuf<float> params_, grads_, wimg_f_, wimg_b_;
   std::vector<float*> param_views_, grad_views_;
   std::vector<Level> lv_;

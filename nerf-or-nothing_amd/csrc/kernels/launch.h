@@ -155,6 +155,36 @@ hipError_t launch_wgrad_reduce(const WgOut* outs, int nouts, int max_elems, cons
                                const float* bias_slabs, int accumulate, const uint32_t* amax, hipStream_t st);
 // (amax != null: sums are multiplied by the inverse f16x2 delta scale, mlp_common.h)
 
+// ---- generic.hip: the any-shape fp32 MLP, one MFMA GEMM launch per layer ----------------------
+// element (i, k) of a source = p[(i / idiv) si + (k / kdiv) sk] (idiv, kdiv: 1 or a per-ray divisor)
+struct GemmSrc {
+  const float* p = nullptr;
+  int64_t si = 0, sk = 0;
+  int idiv = 1, kdiv = 1;
+};
+// C(i, j) = epilogue(sum_{k < K1 + K2} A(i, k) B(j, k)), i < M, j < N; A(i, k) = A1(i, k) for k < K1, else
+// A2(i, k - K1) (B alike).  Epilogue: + bias[j], ReLU, then 0 where !(G(i, j) > 0) — each optional.
+// Split-K: blockIdx.z = chunk of kchunk (a multiple of 16) k values, its raw sums at C + z slab_stride.
+struct GemmArgs {
+  int M = 0, N = 0, K1 = 0, K2 = 0;
+  GemmSrc A1, A2, B1, B2;
+  const float* bias = nullptr;
+  int relu = 0;
+  const float* G = nullptr; int64_t gi = 0, gj = 0;
+  float* C = nullptr; int64_t ci = 0, cj = 0;
+  int kchunk = 0; int64_t slab_stride = 0;
+};
+hipError_t launch_gemm(const GemmArgs& a, int ksplit, hipStream_t st);
+// dst[r ld + c] (+)= sum_{z < nz} slabs[z stride + r cols + c] (z order), r < rows, c < cols
+hipError_t launch_slab_sum(int rows, int cols, int nz, const float* slabs, int64_t stride, float* dst, int64_t ld,
+                           int accumulate, hipStream_t st);
+// IPE at degrees [min_deg, min_deg + P / 6) per sample, view PE (Vd = 3 + 6 deg_view features) per ray
+hipError_t launch_encode_g(int n, int S, const float* mean, const float* cov, const float* d, int min_deg, int P,
+                           int Vd, float* enc_pos, float* enc_dir, hipStream_t st);
+// z [M][4] (density, rgb pre-activations) -> sigma [M], rgb [M][3]; backward: dz [M][4]
+hipError_t launch_heads_fwd(int M, const float* z, float* sigma, float* rgb, hipStream_t st);
+hipError_t launch_heads_bwd(int M, const float* dsigma, const float* drgb, const float* z, float* dz, hipStream_t st);
+
 // ---- adam.hip ----------------------------------------------------------------------------------
 // ---- dataset.hip: device-resident record set -> SoA batch gather (+ optional loss-mult sum) ----
 hipError_t launch_gather_batch(const float* records, int64_t count, int n, uint64_t seed, uint32_t step,

@@ -48,7 +48,8 @@ class nof_level_view(C.Structure):
 
 class nof_mlp_debug(C.Structure):
     _fields_ = [("M", C.c_int32)] + [(k, C.c_void_p) for k in
-                                     ("act_in", "act_h", "act_h9", "masks", "zhead", "delta", "delta9x")]
+                                     ("act_in", "act_h", "act_h9", "masks", "zhead", "delta", "delta9x")] + \
+        [("generic", C.c_int32), ("gen_h", C.c_void_p), ("gen_hc", C.c_void_p)]
 
 
 class nof_render_out(C.Structure):

@@ -57,11 +57,12 @@ def _ptr_list(pp, count) -> list[int]:
 class AcceleratedMLP:
     """Borrowed view of the MLP owned by an AcceleratedMipNeRF (AcceleratedMLP.h:7-45)."""
 
-    NUM_TENSORS = 22
+    NUM_TENSORS = 22  # the reference network's [W0..W10, b0..b10]; any-shape networks: 2 (D + Dc + 2)
 
     def __init__(self, handle, owner):
         self._h = handle
         self._owner = owner  # keeps the owning AcceleratedMipNeRF alive
+        self.num_tensors = len(self.get_layer_sizes())
 
     def get_layer_sizes(self) -> list[int]:
         out = (C.c_int32 * 64)()
@@ -77,36 +78,44 @@ class AcceleratedMLP:
         return d.value, r.value
 
     def get_gradient(self, color_gradient, density_gradient, level: int, flags: int | None = None) -> list[int]:
-        """MLPcpp:256-321 -> 22 device gradient pointers (flags: NOF_GRAD_* bits)."""
+        """MLPcpp:256-321 -> 2L device gradient pointers (22 for the reference network; flags: NOF_GRAD_* bits)."""
         pp = L.PP()
         if flags is None:
             call("nof_mlp_get_gradient", self._h, _ptr(color_gradient), _ptr(density_gradient), level, C.byref(pp))
         else:
             call("nof_mlp_get_gradient_ex", self._h, _ptr(color_gradient), _ptr(density_gradient), level, flags,
                  C.byref(pp))
-        return _ptr_list(pp, self.NUM_TENSORS)
+        return _ptr_list(pp, self.num_tensors)
 
     @property
     def allParams(self) -> list[int]:
         pp = L.PP()
         call("nof_mlp_params", self._h, C.byref(pp))
-        return _ptr_list(pp, self.NUM_TENSORS)
+        return _ptr_list(pp, self.num_tensors)
 
     @property
     def allGradients(self) -> list[int]:
         pp = L.PP()
         call("nof_mlp_grads", self._h, C.byref(pp))
-        return _ptr_list(pp, self.NUM_TENSORS)
+        return _ptr_list(pp, self.num_tensors)
 
     def debug_view(self, level: int) -> dict:
         d = L.nof_mlp_debug()
         call("nof_mlp_debug_view", self._h, level, C.byref(d))
-        return {k: getattr(d, k) for k in ("M", "act_in", "act_h", "act_h9", "masks", "zhead", "delta", "delta9x")}
+        return {k: getattr(d, k) for k in ("M", "act_in", "act_h", "act_h9", "masks", "zhead", "delta", "delta9x",
+                                           "generic", "gen_h", "gen_hc")}
 
     def relu_masks(self, level: int) -> np.ndarray:
-        """Decode the forward's packed ReLU bits -> uint8 [M, 8*256 + 128] (h0..h7, h9)."""
+        """Decode the forward's packed ReLU bits -> uint8 [M, 8*256 + 128] (h0..h7, h9); any-shape
+        networks: the stored activations > 0 -> [M, D*W + Dc*Wc] (the oracle's relu_mask order)."""
         dv = self.debug_view(level)
         M = dv["M"]
+        if dv["generic"]:
+            c = self._owner.config
+            D, W, Dc, Wc = c.net_depth, c.net_width, c.net_depth_condition, c.net_width_condition
+            h = to_numpy(dv["gen_h"], (D, M, W)).transpose(1, 0, 2).reshape(M, D * W)
+            hc = to_numpy(dv["gen_hc"], (Dc, M, Wc)).transpose(1, 0, 2).reshape(M, Dc * Wc)
+            return (np.concatenate([h, hc], axis=1) > 0).astype(np.uint8)
         nb = M // 32
         out = np.zeros((M, 8 * 256 + 128), np.uint8)
         if self._owner.config.precision == 4:  # F16 (mlp_h32.h): [lane][4 words], two 16-bit shift registers
@@ -205,7 +214,7 @@ class AcceleratedMipNeRF:
         if err:
             raise err[0]
         L.check(st, "nof_mipnerf_get_gradient")
-        return _ptr_list(pp, AcceleratedMLP.NUM_TENSORS)
+        return _ptr_list(pp, self.mlp.num_tensors)
 
     def get_gradient_device(self, n, origins, directions, radii, nears, fars, loss_mults, pixels, loss_mult_sum,
                             accumulate: bool = False, publish: bool = True):
@@ -224,7 +233,7 @@ class AcceleratedMipNeRF:
         if self._hook_errors:
             raise self._hook_errors[0]
         L.check(st, "nof_mipnerf_get_gradient_device")
-        return _ptr_list(pp, AcceleratedMLP.NUM_TENSORS)
+        return _ptr_list(pp, self.mlp.num_tensors)
 
     def set_grad_buckets(self, fn):
         """fn(bucket, [(offset, count), ...]) is called during every publishing get_gradient call once

@@ -46,15 +46,20 @@ def test_lr_decay_matches_oracle_bitwise(oracle):
         assert nof.learning_rate_decay(s) == oracle.lr_decay(s)
 
 
-@pytest.mark.parametrize("field,value,status", [
-    ("num_samples", (100, 128), 5),        # GPU path needs 64/128/256/512 samples per level
-    ("net_width", 128, 5),                 # only the reference network is implemented on the GPU
-    ("max_rays", 0, 1),
+@pytest.mark.parametrize("fields,status", [
+    ({"num_samples": (100, 128)}, 5),          # GPU path needs 64/128/256/512 samples per level
+    ({"net_width": 128, "precision": 4}, 5),   # other networks: the any-shape path, fp32 only
+    ({"net_depth": 0}, 1),
+    ({"net_depth": 14, "net_depth_condition": 1}, 1),  # D + Dc + 2 > 16 layers (checkpoint layout)
+    ({"min_deg_point": 4, "max_deg_point": 4}, 1),
+    ({"skip_layer": 0}, 1),
+    ({"max_rays": 0}, 1),
 ])
-def test_invalid_config_returns_status(field, value, status):
+def test_invalid_config_returns_status(fields, status):
+    """Rejected before any device call (no GPU here)."""
     import nof
 
-    cfg = nof.default_config(**{field: value})
+    cfg = nof.default_config(**fields)
     h = C.c_void_p()
     st = nof.lib().nof_mipnerf_create(C.byref(cfg), C.byref(h))
     assert st == status

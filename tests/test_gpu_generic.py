@@ -1,0 +1,168 @@
+"""GPU parity of the any-shape fp32 network path (generic.hip) vs the fp64 oracle.
+
+The reference's network is configurable (MLP.cs:64-86: depth, width, skip, the view branch's depth and
+width, PE degrees); BASELINE configs[0] uses a 4x128 net.  Networks other than the fused kernels' 8x256
+run layer by layer on MFMA GEMMs (accelerated.cpp gen_forward / gen_backward).  Same contract as
+test_gpu_step.py: t bit-exact, outputs / integrator adjoint within 1e-5 with the oracle's own ReLU
+decisions, the 2L gradient tensors within 1e-5 with the GPU's decisions adopted.
+"""
+import numpy as np
+import pytest
+
+from conftest import rel_l2
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+# (D, W, Dc, Wc, skip, min_deg, max_deg, deg_view)
+SPECS = {
+    "configs0_4x128": (4, 128, 1, 128, 4, 0, 16, 4),
+    # widths off the 64-wide tiles, three condition layers, a skip every second layer, other PE degrees
+    "odd_5x96_3x40": (5, 96, 3, 40, 2, 2, 10, 2),
+    # skip into every layer, one-degree view PE
+    "tiny_2x32_skip1": (2, 32, 1, 16, 1, 0, 4, 1),
+    # deeper than the reference, two skips, no view PE harmonics
+    "deep_10x64": (10, 64, 2, 32, 3, 0, 12, 0),
+}
+
+
+def _cfg(spec):
+    D, W, Dc, Wc, skip, lo, hi, dv = spec
+    return dict(net_depth=D, net_width=W, net_depth_condition=Dc, net_width_condition=Wc, skip_layer=skip,
+                min_deg_point=lo, max_deg_point=hi, deg_view=dv)
+
+
+def _ospec(oracle, spec):
+    D, W, Dc, Wc, skip, lo, hi, dv = spec
+    return oracle.Spec(D=D, W=W, Dc=Dc, Wc=Wc, skip=skip, min_deg=lo, max_deg=hi, deg_view=dv)
+
+
+def _run(model, r, dev):
+    import torch
+
+    d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in r.items()}
+    n = r["o"].shape[0]
+    msum = float(np.sum(r["lossmult"], dtype=np.float32))
+    return model.get_gradient_device(n, d["o"], d["d"], d["radius"], d["near"], d["far"], d["lossmult"], d["pix"],
+                                     msum)
+
+
+def _check(gpu, oracle, spec, kind, n, samples, lindisp=0, ray_shape=0, nthreads=16):
+    import torch
+    import nof
+    from nof import synth
+
+    seed, step, ray_base = 0x77, 2, 40
+    opts = dict(lindisp=lindisp, ray_shape=ray_shape)
+    model = nof.AcceleratedMipNeRF(seed=seed, max_rays=n, num_samples=samples, num_levels=len(samples), precision=0,
+                                   **opts, **_cfg(spec))
+    model.set_rng(seed, step, ray_base)
+    sp = _ospec(oracle, spec)
+    sizes = oracle.layer_sizes(sp)
+    assert model.GetLayerSizes() == list(sizes)
+    r = synth.blender_rays(n, seed=23) if kind == "blender" else synth.llff_rays(n, seed=23)
+    grads = _run(model, r, gpu)
+    torch.cuda.synchronize()
+    assert len(grads) == len(sizes)
+    lv = [model.level_numpy(l) for l in range(len(samples))]
+    pptr, P = model.mlp.flat_params()
+    assert P == int(np.sum(sizes))
+    params = nof.to_numpy(pptr, (P,))
+    gptr, _ = model.mlp.flat_grads()
+    G = nof.to_numpy(gptr, (P,))
+    assert grads[0] == gptr
+
+    t0 = oracle.sample_stratified(r["near"], r["far"], samples[0], True, seed, step, 0, ray_base, lindisp=bool(lindisp))
+    assert np.array_equal(lv[0]["t"], t0)
+    tov = {}
+    for l in range(1, len(samples)):
+        tl, _ = oracle.sample_pdf(lv[l - 1]["t"], lv[l - 1]["weights"], samples[l], 0.01, True, seed, step, l, ray_base)
+        assert np.array_equal(lv[l]["t"], tl)
+        tov[l] = lv[l]["t"]
+
+    masks = {l: model.mlp.relu_masks(l).reshape(n, samples[l], -1) for l in range(len(samples))}
+    kw = dict(samples=samples, seed=seed, step_idx=step, ray_base=ray_base, t_override=tov, nthreads=nthreads, **opts)
+    ref = oracle.step(sp, params, r, relu_mask=masks, want=("grads",), **kw)
+    free = oracle.step(sp, params, r, want=("sigma", "rgb", "w", "C", "dsigma", "drgb"), **kw)
+    for l in range(len(samples)):
+        for key, fk in (("density", "sigma"), ("rgb", "rgb"), ("weights", "w"), ("comp_rgb", "C"),
+                        ("density_grad", "dsigma"), ("rgb_grad", "drgb")):
+            e = rel_l2(lv[l][key], free[fk][l])
+            assert e < TOL, f"{key} level {l}: rel L2 {e:.3g}"
+    off, errs = 0, []
+    for i, s in enumerate(sizes):
+        e = rel_l2(G[off:off + s], ref["grads"][off:off + s])
+        errs.append(e)
+        assert e < TOL, f"gradient tensor {i} (size {s}): rel L2 {e:.3g}"
+        off += s
+    print(f"{spec}: gradient rel L2 max {max(errs):.2e} median {np.median(errs):.2e}")
+    assert abs(model.loss() - free["loss"]) <= TOL * abs(free["loss"])
+    model.close()
+
+
+@pytest.mark.parametrize("name", list(SPECS))
+def test_generic_step_parity(gpu, oracle, name):
+    _check(gpu, oracle, SPECS[name], "blender", 8, (64, 128))
+
+
+def test_generic_step_parity_llff_options(gpu, oracle):
+    """NDC forward-facing rays, LinDisp sampling and cylinders through the any-shape path."""
+    _check(gpu, oracle, SPECS["odd_5x96_3x40"], "llff", 4, (64, 64), lindisp=1, ray_shape=1)
+
+
+def test_generic_single_and_three_levels(gpu, oracle):
+    _check(gpu, oracle, SPECS["configs0_4x128"], "blender", 6, (64,))
+    _check(gpu, oracle, SPECS["tiny_2x32_skip1"], "blender", 4, (64, 64, 128))
+
+
+def test_generic_configs0_fullsize(gpu, oracle):
+    """BASELINE configs[0] at its size: 4096 rays x 64 (+64 resampled) samples, 4x128 MLP."""
+    _check(gpu, oracle, SPECS["configs0_4x128"], "blender", 4096, (64, 64), nthreads=16)
+
+
+def test_generic_per_level_and_deterministic(gpu):
+    """get_gradient per level (MLPcpp:256-321: level 0 overwrites, level 1 accumulates) == the step's
+    gradient, and two runs are bitwise equal (ordered split-K sums, no atomics)."""
+    import torch
+    import nof
+    from nof import synth
+
+    n = 32
+    r = synth.blender_rays(n, seed=3)
+    outs = []
+    for _ in range(2):
+        m = nof.AcceleratedMipNeRF(seed=4, max_rays=n, num_samples=(64, 128), **_cfg(SPECS["odd_5x96_3x40"]))
+        _run(m, r, gpu)
+        torch.cuda.synchronize()
+        gp, P = m.mlp.flat_grads()
+        outs.append(nof.to_numpy(gp, (P,)).copy())
+        views = [m.level_view(l) for l in range(2)]
+        for l in range(2):
+            m.mlp.get_gradient(views[l]["rgb_grad"][0], views[l]["density_grad"][0], l)
+        torch.cuda.synchronize()
+        assert np.array_equal(nof.to_numpy(gp, (P,)), outs[-1])
+        m.close()
+    assert np.array_equal(outs[0], outs[1])
+
+
+def test_generic_adam_training_lowers_loss(gpu):
+    """A few steps of the training loop on the 4x128 net: Adam over the 2L-tensor arena, loss decreases."""
+    import torch
+    import nof
+    from nof import synth
+
+    n = 256
+    r = synth.blender_rays(n, seed=8)
+    m = nof.AcceleratedMipNeRF(seed=1, max_rays=n, num_samples=(64, 64), **_cfg(SPECS["configs0_4x128"]))
+    adam = nof.AcceleratedAdamOptimizer(m.GetLayerSizes(), m.config)
+    losses = []
+    for s in range(30):
+        m.set_rng(5, s, 0)
+        g = _run(m, r, gpu)
+        losses.append(m.loss())
+        adam.step(m.mlp.allParams, g, 5e-3)
+    torch.cuda.synchronize()
+    assert np.all(np.isfinite(losses))
+    assert losses[-1] < 0.7 * losses[0], losses
+    adam.close()
+    m.close()

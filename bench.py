@@ -63,6 +63,20 @@ WGRAD_BYTES_PER_VALUE = {"f32": 4, "split": 4, "f16x2": 2, "f16split": 4, "f16":
 #   rgb 16 = 4928; backward writes delta 8 x 256 x 2 + delta9x 132 x 2 = 4360 and reads the masks 288,
 #   zhead 16, dsigma / drgb 16 = 4680; weight gradients read every stored operand once (WGRAD_VALUES x 2)
 KERNEL_BYTES_PER_SAMPLE = {"f16": {"mlp_fwd": 4928, "mlp_bwd": 4680, "wgrad": WGRAD_VALUES * 2}}
+# BASELINE configs[0]'s network (4x128, one 128-wide view layer, PE 16 / 4): the any-shape fp32 path
+CONFIG0_NET = dict(net_depth=4, net_width=128, net_depth_condition=1, net_width_condition=128, skip_layer=4,
+                   min_deg_point=0, max_deg_point=16, deg_view=4)
+
+
+def net_macs(net):
+    """(forward, dX, dW) MACs per sample of a network (the layer list of accelerated.cpp / MLPcpp:131-154):
+    forward and dW = every weight; dX = every weight row block that multiplies a hidden activation."""
+    D, W, Dc, Wc = net["net_depth"], net["net_width"], net["net_depth_condition"], net["net_width_condition"]
+    pos, dirs, skip = 6 * (net["max_deg_point"] - net["min_deg_point"]), 3 * (2 * net["deg_view"] + 1), net["skip_layer"]
+    w = pos * W + sum(W * (W + (pos if l % skip == 0 else 0)) for l in range(1, D)) + W + Wc * (W + dirs) \
+        + (Dc - 1) * Wc * Wc + 3 * Wc
+    dx = (D - 1) * W * W + W + Wc * W + (Dc - 1) * Wc * Wc + 3 * Wc
+    return w, dx, w
 INTEGRATOR_FWD_B = lambda S: S * (12 + 4 + 4) + (S + 1) * 4 + 12 + 12  # rgb, sigma, w | t | d | C  (3100 @128)
 INTEGRATOR_BWD_B = lambda S: 12 + S * (12 + 4) + (S + 1) * 4 + 12 + S * (12 + 4)  # 4636 @128
 
@@ -128,7 +142,7 @@ def host_cpus():
     return os.cpu_count() or 1, aff, quota, model
 
 
-def cpu_baseline(samples, target_s):
+def cpu_baseline(samples, target_s, net=None):
     """Oracle = faithful scalar C++ restatement of MipNerfModel.GetGradient (MNcs:99-200) + the Adam
     step (TrainState.cs:25-37 / AF:403-416), float, on a bounded sample of the same workload (BASELINE.md
     §2): once single-threaded (the C# path is single-threaded) and once OpenMP over rays on every host
@@ -138,7 +152,10 @@ def cpu_baseline(samples, target_s):
     from nof import synth
 
     nproc, aff, quota, model = host_cpus()
-    spec = O.Spec()
+    spec = O.Spec() if net is None else O.Spec(D=net["net_depth"], W=net["net_width"], Dc=net["net_depth_condition"],
+                                               Wc=net["net_width_condition"], skip=net["skip_layer"],
+                                               min_deg=net["min_deg_point"], max_deg=net["max_deg_point"],
+                                               deg_view=net["deg_view"])
     P0 = O.glorot_init(spec, 0x5EED0002)
 
     def timed(n, threads, seed):
@@ -423,7 +440,7 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         native = [NativeDP.init_rank(obj[0], world, rank, dev_idx)]
 
-    def measure(prec, B_run=None, steps=None, warmup=None, timers_on=True, scene=None, smp=None):
+    def measure(prec, B_run=None, steps=None, warmup=None, timers_on=True, scene=None, smp=None, net=None):
         """W untimed + K timed training steps of one precision mode over the global batch (each
         rank's shard in micro-batches accumulated into one gradient, one all-reduce), then a short
         untimed pass with every kernel class event-timed (the per-kernel breakdown); returns
@@ -443,7 +460,7 @@ def main():
         for r, d in zip(ranks, devs):
             st = torch.cuda.current_stream(torch.device("cuda", d)).cuda_stream
             m = nof.AcceleratedMipNeRF(device=d, max_rays=mb, num_samples=smp, seed=seed, stream=st,
-                                       precision=PRECISIONS[prec])
+                                       precision=PRECISIONS[prec], **(net or {}))
             models.append(m)
             opts.append(nof.AcceleratedAdamOptimizer(m.GetLayerSizes(), m.config))
         if world > 1 and native is None:  # torch.distributed: bucketed, overlapped with the backward
@@ -634,6 +651,22 @@ def main():
                                   "unit": "TFLOP/s", "frac": round(c3_tf / PEAKS[a.precision], 4)},
                 "kernels": c3_kernels, "psnr_fine": round(c3_psnr, 3)}
 
+    cfg0 = None
+    if lead and world == 1 and G == 1 and a.scene == "blender" and not a.no_alt:
+        # BASELINE configs[0] (the reference's CPU-only plumbing case: 4096 rays x 64 samples, 4x128 MLP) on
+        # the HIP path: the any-shape fp32 network path (generic.hip), coarse 64 + fine 64 samples
+        z_B, z_smp = 4096, (64, 64)
+        z_dt, _, z_psnr, _ = measure("f32", B_run=z_B, steps=20, warmup=3, timers_on=False, smp=z_smp, net=CONFIG0_NET)
+        z_tf = 2 * sum(net_macs(CONFIG0_NET)) * z_B * sum(z_smp) / (z_dt / 20) / 1e12
+        cfg0 = {"workload": f"BASELINE configs[0] on the GPU: {z_B}-ray batches x 64+64 samples, 4x128 MLP "
+                            "(any-shape fp32 path: one MFMA GEMM launch per layer) fwd/bwd + Adam",
+                "value": round(z_B * 20 / z_dt, 1), "unit": "rays/s", "ms_per_step": round(z_dt * 1e3 / 20, 4),
+                "steps": 20, "warmup": 3, "dtype": "f32",
+                "roofline_step": {"bound": "mfma", "achieved": round(z_tf, 2), "peak": PEAK_F32_TFLOPS,
+                                  "unit": "TFLOP/s", "frac": round(z_tf / PEAK_F32_TFLOPS, 4),
+                                  "macs_per_sample": net_macs(CONFIG0_NET)},
+                "psnr_fine": round(z_psnr, 3)}
+
     cfg5 = None
     if a.scene == "blender" and not a.no_config5:
         # BASELINE configs[4] (north_star's "rays/sec on synthetic LLFF-shape batches at 1, 2, 4 and 8
@@ -706,6 +739,8 @@ def main():
                 result["rehearsal"] = f"{backend}: {world} ranks on {torch.cuda.device_count()} GPU(s), not a scaling run"
         if llff:
             result["llff_1gpu"] = llff
+        if cfg0:
+            result["config0"] = cfg0
         if cfg3:
             result["config3"] = cfg3
         if cfg4:
@@ -736,6 +771,8 @@ def main():
             result["roofline_integrator"] = integrator_roofline(torch, nof, dev)
         if not a.no_cpu_baseline and world == 1 and G == 1:
             result["cpu_baseline"] = cpu_baseline(samples, a.cpu_seconds)
+            if cfg0:  # configs[0]'s own case: the CPU restatement of the reference path on its 4x128 net
+                cfg0["cpu_baseline"] = cpu_baseline((64, 64), a.cpu_seconds * 0.25, net=CONFIG0_NET)
             # same leg (the oracle runs only here): the reference's float CPU path trained beside the
             # HIP path on identical batches -> the metric's "PSNR vs ref"
             result["psnr_vs_ref"] = psnr_vs_ref(torch, nof, synth, dev, a.precision, samples=samples)

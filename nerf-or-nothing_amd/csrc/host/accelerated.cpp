@@ -740,11 +740,11 @@ static void gemm1(nof::GemmArgs a, hipStream_t st) {  // no split: one k chunk
   NOF_HIP(nof::launch_gemm(a, 1, st));
 }
 
-// split-K of a weight gradient (k = the level's M samples): about 2048 workgroups over the output tiles,
-// chunks of at least 256 samples, a multiple of 16
+// split-K of a weight gradient (k = the level's M samples): about 1024 workgroups (four per CU) over the
+// output tiles, chunks of at least 512 samples, a multiple of 16
 void AcceleratedMLP::gen_split(int nout, int ncols, int M, int* ksplit, int* kchunk) {
   const int tiles = ((nout + 63) / 64) * ((ncols + 63) / 64);
-  int ks = std::max(1, std::min((2048 + tiles - 1) / tiles, M / 256));
+  int ks = std::max(1, std::min((1024 + tiles - 1) / tiles, M / 512));
   const int kc = ((M + ks - 1) / ks + 15) / 16 * 16;
   *kchunk = kc;
   *ksplit = (M + kc - 1) / kc;
@@ -773,36 +773,36 @@ void AcceleratedMLP::gen_alloc() {
   gd0_.alloc((size_t)max_M_ * Wm);
   gd1_.alloc((size_t)max_M_ * Wm);
   gdz_.alloc((size_t)max_M_ * 4);
-  gones_.alloc(1);
-  const float one = 1.0f;
-  NOF_HIP(hipMemcpy(gones_.p, &one, sizeof(float), hipMemcpyHostToDevice));
   // split-K slabs: the largest (output rows x columns) block over every level's sample count (the split
   // grows with M up to its tile-count cap, so each level's capacity bounds its launches)
-  const int shapes[][2] = {{gW_, gW_}, {gW_, gP_}, {1, gW_}, {gWc_, gW_}, {gWc_, gVd_}, {gWc_, gWc_},
-                           {3, gWc_}, {gW_, 1}, {gWc_, 1}, {3, 1}, {1, 1}};
+  const int shapes[][2] = {{gW_, gW_}, {gW_, gP_}, {1, gW_}, {gWc_, gW_}, {gWc_, gVd_}, {gWc_, gWc_}, {3, gWc_}};
   size_t slab = 0;
-  for (int l = 0; l < NL; ++l)
+  for (int l = 0; l < NL; ++l) {
     for (const auto& s : shapes) {
       int ks, kc;
       gen_split(s[0], s[1], lv_[l].cap, &ks, &kc);
-      slab = std::max(slab, (size_t)ks * s[0] * s[1]);
+      slab = std::max(slab, (size_t)ks * s[0] * (s[1] + 1));  // + the bias partials
     }
+  }
   gslab_.alloc(slab);
 }
 
 void AcceleratedMLP::gen_wgrad(float* dst, int64_t ld, const float* dz, int64_t ldz, int nout, nof::GemmSrc x,
-                               int ncols, int M, int accumulate) {
+                               int ncols, int M, int accumulate, float* bias_dst) {
   int ks, kc;
   gen_split(nout, ncols, M, &ks, &kc);
-  NOF_REQUIRE((size_t)ks * nout * ncols <= gslab_.n, "split-K slabs too small");
+  NOF_REQUIRE((size_t)ks * nout * (ncols + 1) <= gslab_.n, "split-K slabs too small");
   nof::GemmArgs a;
   a.M = nout; a.N = ncols; a.K1 = M;
   a.A1 = gsrc(dz, 1, ldz);  // A(o, m) = dZ[m][o]
   a.B1 = x;                 // B(j, m) = X[m][j]
   a.C = gslab_.p; a.ci = ncols; a.cj = 1;
   a.kchunk = kc; a.slab_stride = (int64_t)nout * ncols;
+  float* bias_part = gslab_.p + (size_t)ks * nout * ncols;  // the bias gradient's per-chunk sums [ks][nout]
+  if (bias_dst) a.rowsum = bias_part;
   NOF_HIP(nof::launch_gemm(a, ks, st_));
-  NOF_HIP(nof::launch_slab_sum(nout, ncols, ks, gslab_.p, a.slab_stride, dst, ld, accumulate, st_));
+  NOF_HIP(nof::launch_slab_sum(nout, ncols, ncols, ks, gslab_.p, a.slab_stride, dst, ld, accumulate, st_));
+  if (bias_dst) NOF_HIP(nof::launch_slab_sum(1, nout, nout, ks, bias_part, nout, bias_dst, nout, accumulate, st_));
 }
 
 void AcceleratedMLP::gen_forward(int level, const float* ep, const float* ed) {
@@ -876,7 +876,6 @@ void AcceleratedMLP::gen_backward(int level, const float* color_grad, const floa
   float* gr = grads_.p;
   auto H = [&](int l) { return G.h.p + (size_t)l * M * W; };
   auto Hc = [&](int i) { return G.hc.p + (size_t)i * M * Wc; };
-  const nof::GemmSrc ones = gsrc(gones_.p, 0, 0);
   float* dz = gdz_.p;
   float *cur = gd0_.p, *nxt = gd1_.p;
   // dX of layer l into C, masked by the activation `mask` > 0: C[m][j] = sum_o dZ[m][o] W_l[o][j]
@@ -892,23 +891,19 @@ void AcceleratedMLP::gen_backward(int level, const float* color_grad, const floa
   tb(kTMlpBwd);
   NOF_HIP(nof::launch_heads_bwd(M, density_grad, color_grad, G.z.p, dz, st_));  // MNcs:23-28, 184-189
   // rgb head: dW, db from dz[:, 1..3]; its dX into the last condition layer
-  gen_wgrad(gr + woff_[lr], Wc, dz + 1, 4, 3, gsrc(Hc(Dc - 1), 1, Wc), Wc, M, acc);
-  gen_wgrad(gr + boff_[lr], 1, dz + 1, 4, 3, ones, 1, M, acc);
+  gen_wgrad(gr + woff_[lr], Wc, dz + 1, 4, 3, gsrc(Hc(Dc - 1), 1, Wc), Wc, M, acc, gr + boff_[lr]);
   dx(dz + 1, 4, 3, lr, Hc(Dc - 1), Wc, cur);
   for (int i = Dc - 1; i >= 1; --i) {  // condition layers
     const int l = D + 1 + i;
-    gen_wgrad(gr + woff_[l], Wc, cur, Wc, Wc, gsrc(Hc(i - 1), 1, Wc), Wc, M, acc);
-    gen_wgrad(gr + boff_[l], 1, cur, Wc, Wc, ones, 1, M, acc);
+    gen_wgrad(gr + woff_[l], Wc, cur, Wc, Wc, gsrc(Hc(i - 1), 1, Wc), Wc, M, acc, gr + boff_[l]);
     dx(cur, Wc, Wc, l, Hc(i - 1), Wc, nxt);
     std::swap(cur, nxt);
   }
   // view layer: columns [0, W) against h_{D-1}, [W, W + Vd) against the ray's view PE
-  gen_wgrad(gr + woff_[D + 1], W + Vd, cur, Wc, Wc, gsrc(H(D - 1), 1, W), W, M, acc);
+  gen_wgrad(gr + woff_[D + 1], W + Vd, cur, Wc, Wc, gsrc(H(D - 1), 1, W), W, M, acc, gr + boff_[D + 1]);
   gen_wgrad(gr + woff_[D + 1] + W, W + Vd, cur, Wc, Wc, gsrc(G.ed, 1, Vd, 1, S), Vd, M, acc);
-  gen_wgrad(gr + boff_[D + 1], 1, cur, Wc, Wc, ones, 1, M, acc);
   // density head
-  gen_wgrad(gr + woff_[D], W, dz, 4, 1, gsrc(H(D - 1), 1, W), W, M, acc);
-  gen_wgrad(gr + boff_[D], 1, dz, 4, 1, ones, 1, M, acc);
+  gen_wgrad(gr + woff_[D], W, dz, 4, 1, gsrc(H(D - 1), 1, W), W, M, acc, gr + boff_[D]);
   {  // dh_{D-1} = dZ_view W_view[:, :W] + dz_density w_D (MLPcs:148-153, D11), masked
     nof::GemmArgs a;
     a.M = M; a.N = W; a.K1 = Wc; a.K2 = 1;
@@ -924,12 +919,11 @@ void AcceleratedMLP::gen_backward(int level, const float* color_grad, const floa
   for (int l = D - 1; l >= 0; --l) {  // trunk
     float* gw = gr + woff_[l];
     if (l > 0) {
-      gen_wgrad(gw, in_[l], cur, W, W, gsrc(H(l - 1), 1, W), W, M, acc);
+      gen_wgrad(gw, in_[l], cur, W, W, gsrc(H(l - 1), 1, W), W, M, acc, gr + boff_[l]);
       if (l % gskip_ == 0) gen_wgrad(gw + W, in_[l], cur, W, W, gsrc(G.ep, 1, P), P, M, acc);
     } else {
-      gen_wgrad(gw, P, cur, W, W, gsrc(G.ep, 1, P), P, M, acc);
+      gen_wgrad(gw, P, cur, W, W, gsrc(G.ep, 1, P), P, M, acc, gr + boff_[l]);
     }
-    gen_wgrad(gr + boff_[l], 1, cur, W, W, ones, 1, M, acc);
     if (l > 0) {
       dx(cur, W, W, l, H(l - 1), W, nxt);
       std::swap(cur, nxt);

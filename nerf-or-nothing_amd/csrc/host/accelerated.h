@@ -211,13 +211,14 @@ class AcceleratedMLP {
     const float *ep = nullptr, *ed = nullptr;   // the encodings the last forward read (API path: the caller's)
   };
   std::vector<GenLevel> gl_;
-  DevBuf<float> gd0_, gd1_, gdz_, gslab_, gones_;  // dZ ping-pong [M][max(W, Wc)], heads dz [M][4], split-K
+  DevBuf<float> gd0_, gd1_, gdz_, gslab_;  // dZ ping-pong [M][max(W, Wc)], heads dz [M][4], split-K partials
   void gen_alloc();
   void gen_forward(int level, const float* enc_pos, const float* enc_dir);
   void gen_backward(int level, const float* color_grad, const float* density_grad, int accumulate);
-  // columns [col0, col0 + ncols) of layer l's weight gradient: sum_m dZ(m, o) X(m, j) (+ bias when X = ones)
+  // a column block of a layer's weight gradient: dst[o ld + j] (+)= sum_m dZ(m, o) X(m, j); bias_dst: the
+  // layer's bias gradient sum_m dZ(m, o) too (row sums of the same A tiles)
   void gen_wgrad(float* dst, int64_t ld, const float* dz, int64_t ldz, int nout, nof::GemmSrc x, int ncols, int M,
-                 int accumulate);
+                 int accumulate, float* bias_dst = nullptr);
   static void gen_split(int nout, int ncols, int M, int* ksplit, int* kchunk);
   float* const* gen_publish(bool buckets);  // the bucket hook once per bucket (every gradient is final)
   DevBuf<float> params_, grads_, wimg_f_, wimg_b_;

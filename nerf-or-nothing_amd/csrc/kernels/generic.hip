@@ -4,7 +4,7 @@
 // AcceleratedMLP::get_output / get_gradient sequence the reference's kernels (MLPcpp:214-321), but each
 // layer is ONE MFMA GEMM launch over all samples instead of one thread per (neuron, ray, sample) with
 // global atomics (AF:36-182):
-//   * k_gemm: C(i, j) = sum_k A(i, k) B(j, k) on v_mfma_f32_16x16x4f32 (64 x 64 tiles, 4 waves of 32 x 32,
+//   * k_gemm: C(i, j) = sum_k A(i, k) B(j, k) on v_mfma_f32_16x16x4f32 (64 x 64 or 64 x 128 tiles, 4 waves,
 //     k-steps of 16 through LDS), where A and B may each be the concatenation of two strided sources along
 //     k ([h | IPE] skip inputs, [h | view PE] with the view PE per ray) and a source index may be divided
 //     (per-ray operands); epilogue: bias, ReLU, or the ReLU mask of another matrix (the backward's
@@ -24,68 +24,125 @@ constexpr int kGT = 64;   // tile edge
 constexpr int kGK = 16;   // k-step
 constexpr int kGThreads = 256;
 
-__device__ __forceinline__ float g_src(const GemmSrc& s, int i, int k) {
-  const int ii = s.idiv > 1 ? i / s.idiv : i;
-  const int kk = s.kdiv > 1 ? k / s.kdiv : k;
-  return s.p[(int64_t)ii * s.si + (int64_t)kk * s.sk];
-}
-// element (i, k) of a two-source operand (k < K1: source 1, else source 2 at k - K1); 0 outside
-__device__ __forceinline__ float g_elem(const GemmSrc& s1, const GemmSrc& s2, int K1, int K, int rows, int i, int k) {
-  if (i >= rows || k >= K) return 0.0f;
-  return k < K1 ? g_src(s1, i, k) : g_src(s2, i, k - K1);
-}
+// Per-thread load plan of one operand tile (T rows x 16 k per k-step, E = T / 16 elements per thread).
+// Threads run along the source's unit-stride index (coalesced): k when kfast (sk == 1), else the row
+// index.  A thread's rows are the same at every k-step, so the row offsets (with their per-ray divisions)
+// are computed once; each k-step then issues its E loads unconditionally (an element outside the operand
+// reads the source's first element and is zeroed at the LDS store), so they are in flight together and
+// the next step's loads overlap this step's MFMAs.
+template <int T>
+struct GPlan {
+  static constexpr int E = T * kGK / kGThreads;
+  const float* b1[E];  // source-1 / source-2 row bases of the thread's elements
+  const float* b2[E];
+  int r[E], kl[E];     // tile row, k within the step
+  bool ok[E];          // row inside the operand
+};
 
-// tile loader: 64 rows x 16 k of a two-source operand into lds[k][row] (padded rows); threads run along the
-// source's unit-stride index (coalesced) — k when sk == 1, else the row index
-__device__ __forceinline__ void g_load(float (*dst)[kGT + 4], const GemmSrc& s1, const GemmSrc& s2, int K1, int K,
-                                       int rows, int r0, int k0, int tid) {
+template <int T>
+__device__ __forceinline__ void g_plan(GPlan<T>& pl, const GemmSrc& s1, const GemmSrc& s2, int rows, int r0, int tid) {
   const bool kfast = s1.sk == 1;
 #pragma unroll
-  for (int e = 0; e < kGT * kGK / kGThreads; ++e) {
+  for (int e = 0; e < GPlan<T>::E; ++e) {
     const int q = e * kGThreads + tid;
-    const int r = kfast ? q / kGK : q % kGT;
-    const int k = kfast ? q % kGK : q / kGT;
-    dst[k][r] = g_elem(s1, s2, K1, K, rows, r0 + r, k0 + k);
+    pl.r[e] = kfast ? q / kGK : q % T;
+    pl.kl[e] = kfast ? q % kGK : q / T;
+    const int i = r0 + pl.r[e];
+    pl.ok[e] = i < rows;
+    const int ic = pl.ok[e] ? i : 0;
+    pl.b1[e] = s1.p + (int64_t)(ic / s1.idiv) * s1.si;
+    pl.b2[e] = s2.p ? s2.p + (int64_t)(ic / s2.idiv) * s2.si : s1.p;
   }
 }
 
+// the loads only: the element masks are applied at the LDS store (a select here would wait for the loads)
+template <bool KDIV, int T>
+__device__ __forceinline__ void g_fetch(float (&v)[GPlan<T>::E], bool (&ok)[GPlan<T>::E], const GPlan<T>& pl,
+                                        const GemmSrc& s1, const GemmSrc& s2, int K1, int ke, int k0) {
+  constexpr int E = GPlan<T>::E;
+  const float* ptr[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int k = k0 + pl.kl[e];
+    ok[e] = pl.ok[e] && k < ke;
+    const bool one = k < K1;
+    const int kk = one ? k : k - K1;
+    int64_t off;
+    if (KDIV) off = one ? (int64_t)(kk / s1.kdiv) * s1.sk : (int64_t)(kk / s2.kdiv) * s2.sk;
+    else off = one ? (int64_t)kk * s1.sk : (int64_t)kk * s2.sk;
+    ptr[e] = ok[e] ? (one ? pl.b1[e] : pl.b2[e]) + off : s1.p;
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) v[e] = *ptr[e];
+}
+
+template <int T>
+__device__ __forceinline__ void g_store(float (*dst)[T + 4], const GPlan<T>& pl, const float (&v)[GPlan<T>::E],
+                                        const bool (&ok)[GPlan<T>::E]) {
+#pragma unroll
+  for (int e = 0; e < GPlan<T>::E; ++e) dst[pl.kl[e]][pl.r[e]] = ok[e] ? v[e] : 0.0f;
+}
+
+// tile 64 (i) x TN (j), TN = 64 or 128; 4 waves in a 2 x 2 grid of 32 x TN/2 wave tiles
+template <bool KDIV, int TN>
 __global__ __launch_bounds__(kGThreads) void k_gemm(GemmArgs a) {
-  __shared__ float As[kGK][kGT + 4], Bs[kGK][kGT + 4];
+  constexpr int NQ = TN / 32;  // 16-wide MFMA tiles per wave along j
+  __shared__ float As[kGK][kGT + 4], Bs[kGK][TN + 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int i0 = blockIdx.y * kGT, j0 = blockIdx.x * kGT;
-  const int wi = (wave >> 1) * 32, wj = (wave & 1) * 32;
+  const int i0 = blockIdx.y * kGT, j0 = blockIdx.x * TN;
+  const int wi = (wave >> 1) * 32, wj = (wave & 1) * (TN / 2);
   const int K = a.K1 + a.K2;
+  // the chunk end bounds k as well (a split-K chunk reads only its own k)
   const int kb = blockIdx.z * a.kchunk, ke = min(K, kb + a.kchunk);
-  f32x4 acc[2][2];
+  GPlan<kGT> pa;
+  GPlan<TN> pb;
+  g_plan(pa, a.A1, a.A2, a.M, i0, tid);
+  g_plan(pb, a.B1, a.B2, a.N, j0, tid);
+  f32x4 acc[2][NQ];
 #pragma unroll
   for (int p = 0; p < 2; ++p)
 #pragma unroll
-    for (int q = 0; q < 2; ++q) acc[p][q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int q = 0; q < NQ; ++q) acc[p][q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  // row sums of A over this chunk's k (the bias gradient beside a weight gradient): the first column
+  // tile's wave 0, one row per lane, from the LDS tile, in k order
+  const bool rowsum = a.rowsum && blockIdx.x == 0 && wave == 0;
+  float rs = 0.0f;
+  float va[GPlan<kGT>::E], vb[GPlan<TN>::E];
+  bool oa[GPlan<kGT>::E], ob[GPlan<TN>::E];
+  g_fetch<KDIV>(va, oa, pa, a.A1, a.A2, a.K1, ke, kb);
+  g_fetch<KDIV>(vb, ob, pb, a.B1, a.B2, a.K1, ke, kb);
   for (int k0 = kb; k0 < ke; k0 += kGK) {
-    // the chunk end bounds k as well (a split-K chunk reads only its own k)
-    g_load(As, a.A1, a.A2, a.K1, ke, a.M, i0, k0, tid);
-    g_load(Bs, a.B1, a.B2, a.K1, ke, a.N, j0, k0, tid);
+    g_store(As, pa, va, oa);
+    g_store(Bs, pb, vb, ob);
     __syncthreads();
+    if (k0 + kGK < ke) {  // the next step's loads in flight under this step's MFMAs
+      g_fetch<KDIV>(va, oa, pa, a.A1, a.A2, a.K1, ke, k0 + kGK);
+      g_fetch<KDIV>(vb, ob, pb, a.B1, a.B2, a.K1, ke, k0 + kGK);
+    }
+    if (rowsum)
+#pragma unroll
+      for (int k = 0; k < kGK; ++k) rs += As[k][lane];
 #pragma unroll
     for (int kk = 0; kk < kGK / 4; ++kk) {
       const int k = 4 * kk + (lane >> 4);
-      float av[2], bv[2];
+      float av[2], bv[NQ];
 #pragma unroll
       for (int p = 0; p < 2; ++p) av[p] = As[k][wi + 16 * p + (lane & 15)];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) bv[q] = Bs[k][wj + 16 * q + (lane & 15)];
+      for (int q = 0; q < NQ; ++q) bv[q] = Bs[k][wj + 16 * q + (lane & 15)];
 #pragma unroll
       for (int p = 0; p < 2; ++p)
 #pragma unroll
-        for (int q = 0; q < 2; ++q) acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[p], bv[q], acc[p][q], 0, 0, 0);
+        for (int q = 0; q < NQ; ++q) acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[p], bv[q], acc[p][q], 0, 0, 0);
     }
     __syncthreads();
   }
+  if (rowsum && i0 + lane < a.M) a.rowsum[(int64_t)blockIdx.z * a.M + i0 + lane] = rs;
   float* C = a.C + (int64_t)blockIdx.z * a.slab_stride;
 #pragma unroll
   for (int p = 0; p < 2; ++p)
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < NQ; ++q)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = i0 + wi + 16 * p + 4 * (lane >> 4) + r, j = j0 + wj + 16 * q + (lane & 15);
@@ -98,16 +155,32 @@ __global__ __launch_bounds__(kGThreads) void k_gemm(GemmArgs a) {
       }
 }
 
-// dst[r ld + c] (+)= sum over slabs z = 0 .. nz - 1 of slabs[z][r cols + c], in z order
-__global__ void k_slab_sum(int rows, int cols, int nz, const float* __restrict__ slabs, int64_t stride,
-                           float* __restrict__ dst, int64_t ld, int accumulate) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (int64_t)rows * cols) return;
+// dst[r ld + c] (+)= sum over slabs z = 0 .. nz - 1 of slabs[z][r pitch + c] (z order within each of 4
+// interleaved partitions z = p mod 4, then the partitions 0..3 in order: a fixed order per shape).
+// A block: 64 elements x 4 partitions.
+__global__ __launch_bounds__(256) void k_slab_sum(int rows, int cols, int pitch, int nz, const float* __restrict__ slabs,
+                                                  int64_t stride, float* __restrict__ dst, int64_t ld, int accumulate) {
+  __shared__ float part[4][64];
+  const int t = threadIdx.x & 63, p = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + t;
+  const bool live = e < (int64_t)rows * cols;
+  const int64_t r = live ? e / cols : 0;
+  const int64_t off = r * pitch + (live ? e - r * cols : 0);
   float s = 0.0f;
-  for (int z = 0; z < nz; ++z) s += slabs[(int64_t)z * stride + e];
-  const int64_t r = e / cols;
-  float* o = dst + r * ld + (e - r * cols);
-  *o = accumulate ? *o + s : s;
+  int z = p;
+  for (; z + 12 < nz; z += 16) {  // four loads in flight
+    const float v0 = slabs[(int64_t)z * stride + off], v1 = slabs[(int64_t)(z + 4) * stride + off];
+    const float v2 = slabs[(int64_t)(z + 8) * stride + off], v3 = slabs[(int64_t)(z + 12) * stride + off];
+    s += v0; s += v1; s += v2; s += v3;
+  }
+  for (; z < nz; z += 4) s += slabs[(int64_t)z * stride + off];
+  part[p][t] = s;
+  __syncthreads();
+  if (p == 0 && live) {
+    const float tot = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
+    float* o = dst + r * ld + (e - r * cols);
+    *o = accumulate ? *o + tot : tot;
+  }
 }
 
 // IPE at degrees [min_deg, min_deg + P / 6) (MH:429-449: feature 6f + j, then 6f + 3 + j with the
@@ -154,18 +227,29 @@ __global__ void k_heads_bwd(int M, const float* __restrict__ dsigma, const float
 
 hipError_t launch_gemm(const GemmArgs& a, int ksplit, hipStream_t st) {
   if (a.M <= 0 || a.N <= 0) return hipSuccess;
-  if (ksplit < 1 || a.kchunk % kGK != 0) return hipErrorInvalidValue;
-  const dim3 grid((a.N + kGT - 1) / kGT, (a.M + kGT - 1) / kGT, ksplit);
-  hipLaunchKernelGGL(k_gemm, grid, dim3(kGThreads), 0, st, a);
+  if (ksplit < 1 || a.kchunk <= 0 || a.kchunk % kGK != 0 || !a.A1.p || !a.B1.p || (a.K2 > 0 && (!a.A2.p || !a.B2.p)) ||
+      a.A1.idiv < 1 || a.A2.idiv < 1 || a.B1.idiv < 1 || a.B2.idiv < 1 || a.A1.kdiv < 1 || a.A2.kdiv < 1 ||
+      a.B1.kdiv < 1 || a.B2.kdiv < 1)
+    return hipErrorInvalidValue;
+  const bool kdiv = a.A1.kdiv > 1 || a.A2.kdiv > 1 || a.B1.kdiv > 1 || a.B2.kdiv > 1;
+  // 64 x 128 tiles for split-K weight gradients wider than 64 (A read once for up to 128 columns; measured
+  // 5 % faster there, 10 % slower on the unsplit dX GEMMs)
+  const bool wide = a.N > 64 && ksplit > 1;
+  const int TN = wide ? 128 : 64;
+  const dim3 grid((a.N + TN - 1) / TN, (a.M + kGT - 1) / kGT, ksplit);
+  if (kdiv && wide) hipLaunchKernelGGL((k_gemm<true, 128>), grid, dim3(kGThreads), 0, st, a);
+  else if (kdiv) hipLaunchKernelGGL((k_gemm<true, 64>), grid, dim3(kGThreads), 0, st, a);
+  else if (wide) hipLaunchKernelGGL((k_gemm<false, 128>), grid, dim3(kGThreads), 0, st, a);
+  else hipLaunchKernelGGL((k_gemm<false, 64>), grid, dim3(kGThreads), 0, st, a);
   return hipGetLastError();
 }
-hipError_t launch_slab_sum(int rows, int cols, int nz, const float* slabs, int64_t stride, float* dst, int64_t ld,
-                           int accumulate, hipStream_t st) {
+hipError_t launch_slab_sum(int rows, int cols, int pitch, int nz, const float* slabs, int64_t stride, float* dst,
+                           int64_t ld, int accumulate, hipStream_t st) {
   const int64_t n = (int64_t)rows * cols;
   if (n <= 0) return hipSuccess;
-  if (nz < 1 || stride < n || ld < cols) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_slab_sum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rows, cols, nz, slabs, stride,
-                     dst, ld, accumulate);
+  if (nz < 1 || pitch < cols || stride < (int64_t)(rows - 1) * pitch + cols || ld < cols) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_slab_sum, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, rows, cols, pitch, nz, slabs,
+                     stride, dst, ld, accumulate);
   return hipGetLastError();
 }
 hipError_t launch_encode_g(int n, int S, const float* mean, const float* cov, const float* d, int min_deg, int P, int Vd,

@@ -173,11 +173,12 @@ struct GemmArgs {
   const float* G = nullptr; int64_t gi = 0, gj = 0;
   float* C = nullptr; int64_t ci = 0, cj = 0;
   int kchunk = 0; int64_t slab_stride = 0;
+  float* rowsum = nullptr;  // optional: rowsum[z M + i] = sum_{k in chunk z} A(i, k) (bias gradients)
 };
 hipError_t launch_gemm(const GemmArgs& a, int ksplit, hipStream_t st);
-// dst[r ld + c] (+)= sum_{z < nz} slabs[z stride + r cols + c] (z order), r < rows, c < cols
-hipError_t launch_slab_sum(int rows, int cols, int nz, const float* slabs, int64_t stride, float* dst, int64_t ld,
-                           int accumulate, hipStream_t st);
+// dst[r ld + c] (+)= sum_{z < nz} slabs[z stride + r pitch + c] (a fixed order), r < rows, c < cols
+hipError_t launch_slab_sum(int rows, int cols, int pitch, int nz, const float* slabs, int64_t stride, float* dst,
+                           int64_t ld, int accumulate, hipStream_t st);
 // IPE at degrees [min_deg, min_deg + P / 6) per sample, view PE (Vd = 3 + 6 deg_view features) per ray
 hipError_t launch_encode_g(int n, int S, const float* mean, const float* cov, const float* d, int min_deg, int P,
                            int Vd, float* enc_pos, float* enc_dir, hipStream_t st);

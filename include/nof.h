@@ -44,7 +44,10 @@ typedef struct nof_config {
   int32_t max_rays;                       /* capacity in rays per call (reference: 1024, helpers.h:18) */
   int32_t num_levels;                     /* 2 (helpers.h:16) */
   int32_t num_samples[NOF_MAX_LEVELS];    /* per level; 128, 128 (helpers.h:17); GPU: 64, 128, 256 or 512 */
-  int32_t net_depth, net_width;           /* 8, 256 */
+  int32_t net_depth, net_width;           /* 8, 256.  Any network (MLP.cs:64-86; net_depth + net_depth_condition
+                                             <= 14, widths <= 4096, 0 <= min_deg < max_deg <= 24, deg_view <= 24)
+                                             runs; shapes other than the reference's 8x256 / 1x128 / skip 4 / PE
+                                             (0, 16), 4 run on the any-shape fp32 path: NOF_PRECISION_F32 only */
   int32_t net_depth_condition, net_width_condition; /* 1, 128 */
   int32_t skip_layer;                     /* 4 */
   int32_t min_deg_point, max_deg_point;   /* 0, 16 */
@@ -124,7 +127,8 @@ nof_status nof_mipnerf_create(const nof_config* cfg, nof_mipnerf** out);
 /* dtor MNcpp:151-176 */
 nof_status nof_mipnerf_destroy(nof_mipnerf* h);
 /* GetGradient MNcpp:52-144: host ray SoA (origins/dirs [n][3]; radii, nears, fars, loss_mults [n])
- * + loss-gradient callback -> 22 borrowed device gradient pointers [W0..W10, b0..b10]. */
+ * + loss-gradient callback -> 2L borrowed device gradient pointers [W0..W(L-1), b0..b(L-1)] (L = net_depth +
+ * net_depth_condition + 2: 22 pointers [W0..W10, b0..b10] for the reference network). */
 nof_status nof_mipnerf_get_gradient(nof_mipnerf* h, int32_t n, const float* origins, const float* directions,
                                     const float* radii, const float* nears, const float* fars,
                                     const float* loss_mults, nof_output_grad_fn cb, void* cb_user,
@@ -360,7 +364,7 @@ nof_status nof_mlp_get_gradient(nof_mlp* m, const float* dev_color_grad, const f
 /* ... with NOF_GRAD_* flags (ACCUMULATE: level 0 accumulates too; PUBLISH: see above) */
 nof_status nof_mlp_get_gradient_ex(nof_mlp* m, const float* dev_color_grad, const float* dev_density_grad,
                                    int32_t level, uint32_t flags, float* const** out_dev_grads);
-/* allParams / allGradients (AcceleratedMLP.h:24-25): 22 views into one flat arena */
+/* allParams / allGradients (AcceleratedMLP.h:24-25): 2L views into one flat arena (22 for 8x256) */
 nof_status nof_mlp_params(nof_mlp* m, float* const** out);
 nof_status nof_mlp_grads(nof_mlp* m, float* const** out);
 nof_status nof_mlp_flat_params(nof_mlp* m, float** out, int64_t* count);

@@ -166,3 +166,84 @@ def test_generic_adam_training_lowers_loss(gpu):
     assert losses[-1] < 0.7 * losses[0], losses
     adam.close()
     m.close()
+
+
+def test_generic_matches_golden_fixture(gpu):
+    """The any-shape path against the committed fixture of the INDEPENDENT restatement for configs[0]'s
+    network (tests/golden/small_4x128.npz: tests/torch_ref.py fp64 autograd, 6 rays x 64+64, 4x128), not
+    through the oracle: the GPU's Glorot init reproduces the fixture's checksum, level-0 t bit-exact,
+    level-1 t within rounding, weights / composite / loss and the FULL gradient arena within 1e-5 (no ReLU
+    decisions adopted: the fixture's fp64 z > 0 decide)."""
+    import os
+    import torch
+    import nof
+    from golden.make_golden import CASES
+
+    c = CASES["small_4x128"]
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "small_4x128.npz"))
+    rays = {k: g["ray_" + k] for k in ("o", "d", "radius", "near", "far", "lossmult", "pix")}
+    n = rays["o"].shape[0]
+    net = c["net"]
+    model = nof.AcceleratedMipNeRF(seed=c["param_seed"], max_rays=n, num_samples=c["samples"], precision=0,
+                                   **_cfg((net["D"], net["W"], net["Dc"], net["Wc"], 4, 0, 16, 4)))
+    pptr, P = model.mlp.flat_params()
+    params = nof.to_numpy(pptr, (P,)).copy()
+    assert float(params.astype(np.float64).sum()) == float(g["param_checksum"]), "Glorot init differs from the fixture"
+    model.set_rng(c["seed"], c["step"], c["ray_base"])
+    _run(model, rays, gpu)
+    torch.cuda.synchronize()
+    lv = [model.level_numpy(l) for l in range(2)]
+    assert np.array_equal(lv[0]["t"], g["t0"])
+    assert np.allclose(lv[1]["t"], g["t1"], rtol=4e-7, atol=0)
+    for l in range(2):
+        assert rel_l2(lv[l]["weights"], g[f"w{l}"]) < TOL, f"weights level {l}"
+        assert rel_l2(lv[l]["comp_rgb"], g[f"C{l}"]) < TOL, f"comp_rgb level {l}"
+    assert abs(model.loss() - float(g["loss"])) <= TOL * abs(float(g["loss"]))
+    G = nof.to_numpy(model.mlp.flat_grads()[0], (P,))
+    sizes = model.GetLayerSizes()
+    for i, (a, b) in enumerate(zip(np.split(G, np.cumsum(sizes)[:-1]), np.split(g["grads"], np.cumsum(sizes)[:-1]))):
+        e = rel_l2(a, b)
+        assert e < TOL, f"gradient tensor {i}: rel L2 {e:.3g}"
+    model.close()
+
+
+def test_generic_render_and_checkpoint(gpu, tmp_path):
+    """render_device on an any-shape network == the training step's forward bitwise on the same Philox
+    state; a checkpoint of the 2L-tensor arena + Adam state round-trips into a fresh model exactly."""
+    import torch
+    import nof
+    from nof import synth
+
+    n, samples = 40, (64, 128)
+    r = synth.blender_rays(n, seed=31)
+    d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(gpu) for k, v in r.items()}
+    cfg = _cfg(SPECS["odd_5x96_3x40"])
+    m = nof.AcceleratedMipNeRF(seed=2, max_rays=n, num_samples=samples, **cfg)
+    m.set_rng(0xABC, 4, 100)
+    lv = m.render_device(n, d["o"], d["d"], d["radius"], d["near"], d["far"], randomized=True)
+    torch.cuda.synchronize()
+    out = [nof.to_numpy(*L["comp_rgb"]) for L in lv]
+    m.set_rng(0xABC, 4, 100)
+    g = _run(m, r, gpu)
+    adam = nof.AcceleratedAdamOptimizer(m.GetLayerSizes(), m.config)
+    adam.step(m.mlp.allParams, g, 1e-3)
+    torch.cuda.synchronize()
+    for l in range(2):
+        assert np.array_equal(m.level_numpy(l)["comp_rgb"], out[l]), f"level {l}"
+    path = str(tmp_path / "generic.ckpt")
+    nof.save_checkpoint(path, m, adam)
+    m2 = nof.AcceleratedMipNeRF(seed=99, max_rays=n, num_samples=samples, **cfg)
+    adam2 = nof.AcceleratedAdamOptimizer(m2.GetLayerSizes(), m2.config)
+    nof.load_checkpoint(path, m2, adam2)
+    torch.cuda.synchronize()
+    p1, P = m.mlp.flat_params()
+    p2, _ = m2.mlp.flat_params()
+    assert np.array_equal(nof.to_numpy(p1, (P,)), nof.to_numpy(p2, (P,)))
+    assert adam2.iteration == 1 and m2.get_rng() == m.get_rng()
+    ref = nof.AcceleratedMipNeRF(seed=99, max_rays=n, num_samples=samples, **_cfg(SPECS["tiny_2x32_skip1"]))
+    with pytest.raises(nof.NofError):  # a different network's layout is refused
+        nof.load_checkpoint(path, ref, nof.AcceleratedAdamOptimizer(ref.GetLayerSizes(), ref.config))
+    for o in (adam, adam2):
+        o.close()
+    for o in (m, m2, ref):
+        o.close()

@@ -36,11 +36,15 @@ def _records(n, seed):
     return synth.pack_records(r)
 
 
-def _models(k, max_rays, precision=0, grad_buckets=0):
+# the any-shape path's network (configs[0]: 4x128): its 2L-tensor arena through the same all-reduce
+NETS = {"ref": {}, "4x128": dict(net_depth=4, net_width=128)}
+
+
+def _models(k, max_rays, precision=0, grad_buckets=0, net="ref"):
     import nof
 
     ms = [nof.AcceleratedMipNeRF(seed=SEED, max_rays=max_rays, num_samples=SAMPLES, precision=precision,
-                                 grad_buckets=grad_buckets) for _ in range(k)]
+                                 grad_buckets=grad_buckets, **NETS[net]) for _ in range(k)]
     return ms, [nof.AcceleratedAdamOptimizer(m.GetLayerSizes(), m.config) for m in ms]
 
 
@@ -59,8 +63,9 @@ def _grad(m, ds, n, step, ray_base, msum, accumulate=False, publish=True):
                           accumulate=accumulate, publish=publish)
 
 
+@pytest.mark.parametrize("net", list(NETS))
 @pytest.mark.parametrize("mode", ["grouped", "attached"])
-def test_loopback_k2_equals_single_model(gpu, mode):
+def test_loopback_k2_equals_single_model(gpu, mode, net):
     import torch
     import nof
     from nof.dp import NativeDP
@@ -68,13 +73,13 @@ def test_loopback_k2_equals_single_model(gpu, mode):
     B, K, step = 256, 2, 3
     ds = nof.RayDataset(records=_records(3000, 5))
     _, msum = ds.next(B, SEED, step, 0)
-    single, sadam = _models(1, B)
+    single, sadam = _models(1, B, net=net)
     _grad(single[0], ds, B, step, 0, msum)
     torch.cuda.synchronize()
     g_full = _flat(single[0], "g")
 
     sh = B // K
-    ms, adams = _models(K, sh)
+    ms, adams = _models(K, sh, net=net)
     dps = NativeDP.init_loopback(K, 0)
     try:
         if mode == "attached":

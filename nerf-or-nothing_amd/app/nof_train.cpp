@@ -56,6 +56,9 @@ struct Args {
   long long max_resident = -1;  // >= 0: stream the record file when it holds more records than this
   bool host_api = false;
   uint64_t seed = 0x5EED0000ull;
+  // the network (MLP.cs:64-86; 0 = the reference default) and samples per level (helpers.h:17)
+  int net_depth = 0, net_width = 0, net_depth_condition = 0, net_width_condition = 0;
+  std::vector<int> samples;
   // Config (TrainState.cs:54-58)
   float lr_init = 5e-4f, lr_final = 5e-6f, lr_delay_mult = 0.01f;
   int max_steps = 1000000, lr_delay_steps = 2500;
@@ -66,7 +69,10 @@ struct Args {
                "usage: nof_train --records FILE [--steps K] [--batch N] [--precision f32|split|f16x2|f16split|f16]\n"
                "                 [--print-every P] [--save-every S --ckpt-dir DIR] [--resume CKPT] [--host-api]\n"
                "                 [--seed X] [--device D | --gpus N [--dp rccl|loopback] [--attach]] [--micro-batch M]\n"
-               "                 [--dump-params FILE] [--max-resident RECORDS]\n");
+               "                 [--dump-params FILE] [--max-resident RECORDS]\n"
+               "                 [--net-depth D] [--net-width W] [--net-depth-condition DC] [--net-width-condition WC]\n"
+               "                 [--samples S0,S1[,...]]  (e.g. BASELINE configs[0]: --net-depth 4 --net-width 128 "
+               "--samples 64,64)\n");
   std::exit(code);
 }
 
@@ -94,6 +100,21 @@ Args parse(int argc, char** argv) {
     else if (k == "--attach") a.attach = true;
     else if (k == "--micro-batch") a.micro = std::atoi(val());
     else if (k == "--max-resident") a.max_resident = std::atoll(val());
+    else if (k == "--net-depth") a.net_depth = std::atoi(val());
+    else if (k == "--net-width") a.net_width = std::atoi(val());
+    else if (k == "--net-depth-condition") a.net_depth_condition = std::atoi(val());
+    else if (k == "--net-width-condition") a.net_width_condition = std::atoi(val());
+    else if (k == "--samples") {
+      const std::string v = val();
+      a.samples.clear();
+      for (size_t p = 0; p <= v.size();) {
+        const size_t q = v.find(',', p);
+        a.samples.push_back(std::atoi(v.substr(p, q == std::string::npos ? std::string::npos : q - p).c_str()));
+        if (q == std::string::npos) break;
+        p = q + 1;
+      }
+      if (a.samples.empty() || a.samples.size() > NOF_MAX_LEVELS) usage(2);
+    }
     else if (k == "--dp") {
       const std::string d = val();
       if (d == "loopback") a.loopback = true;
@@ -210,6 +231,14 @@ int main(int argc, char** argv) {
     R.cfg.max_rays = micro;
     R.cfg.seed = a.seed;
     R.cfg.precision = a.precision;
+    if (a.net_depth) R.cfg.net_depth = a.net_depth;  // other shapes: the any-shape fp32 path
+    if (a.net_width) R.cfg.net_width = a.net_width;
+    if (a.net_depth_condition) R.cfg.net_depth_condition = a.net_depth_condition;
+    if (a.net_width_condition) R.cfg.net_width_condition = a.net_width_condition;
+    if (!a.samples.empty()) {
+      R.cfg.num_levels = (int32_t)a.samples.size();
+      for (size_t l = 0; l < a.samples.size(); ++l) R.cfg.num_samples[l] = a.samples[l];
+    }
     // data-parallel runs cut the weight-gradient items per all-reduce bucket: attached (bucketed,
     // overlapped) and grouped all-reduces then give bitwise-identical parameters
     R.cfg.grad_buckets = G > 1 ? 1 : 0;

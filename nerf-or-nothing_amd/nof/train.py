@@ -144,11 +144,23 @@ def main(argv=None):
     ap.add_argument("--resume", help="checkpoint to resume from")
     ap.add_argument("--sync-check-every", type=int, default=0,
                     help="under torch.distributed: assert bitwise-identical parameters across ranks every K steps")
+    # the network (MLP.cs:64-86) and samples per level; other shapes than 8x256 run on the any-shape fp32
+    # path (BASELINE configs[0]: --net-depth 4 --net-width 128 --samples 64 64)
+    ap.add_argument("--net-depth", type=int)
+    ap.add_argument("--net-width", type=int)
+    ap.add_argument("--net-depth-condition", type=int)
+    ap.add_argument("--net-width-condition", type=int)
+    ap.add_argument("--samples", type=int, nargs="+")
     a = ap.parse_args(argv)
+    net = {k: getattr(a, k) for k in ("net_depth", "net_width", "net_depth_condition", "net_width_condition")
+           if getattr(a, k) is not None}
+    if a.samples:
+        net["num_samples"] = tuple(a.samples)
     ds = (api.RayDataset(a.records, device=a.device) if a.records else
           api.RayDataset(records=synth.pack_records(synth.blender_rays(a.synthetic, seed=1)), device=a.device))
     tr = Trainer(ds, batch_size=a.batch, device=a.device, print_every=a.print_every, save_every=a.save_every,
-                 ckpt_dir=a.ckpt_dir, sync_check_every=a.sync_check_every, precision={"f32": 0, "split": 1, "f16x2": 2, "f16split": 3, "f16": 4}[a.precision])
+                 ckpt_dir=a.ckpt_dir, sync_check_every=a.sync_check_every,
+                 precision={"f32": 0, "split": 1, "f16x2": 2, "f16split": 3, "f16": 4}[a.precision], **net)
     if a.resume:
         tr.resume(a.resume)
     t0 = time.perf_counter()

@@ -247,3 +247,34 @@ def test_generic_render_and_checkpoint(gpu, tmp_path):
         o.close()
     for o in (m, m2, ref):
         o.close()
+
+
+def test_generic_native_and_python_drivers(gpu, tmp_path):
+    """BASELINE configs[0] through both training drivers: bin/nof_train (the C ABI alone) and
+    `python -m nof.train`, --net-depth 4 --net-width 128 --samples 64 64: both run, and the native driver's
+    parameter dump is the finite 4x128 arena."""
+    import os
+    import subprocess
+    import sys
+
+    from nof import synth
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "nerf-or-nothing_amd", "bin", "nof_train")
+    path = str(tmp_path / "rays.bin")
+    synth.pack_records(synth.blender_rays(4096, seed=4)).tofile(path)
+    dump = str(tmp_path / "params.bin")
+    cmd = [exe, "--records", path, "--batch", "512", "--steps", "4", "--print-every", "2", "--seed", "77",
+           "--net-depth", "4", "--net-width", "128", "--samples", "64,64", "--dump-params", dump]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    P = np.fromfile(dump, np.float32)
+    D, W, pos, dirs = 4, 128, 96, 27
+    expect = pos * W + (D - 1) * W * W + W + 128 * (W + dirs) + 3 * 128 + (D * W + 1 + 128 + 3)
+    assert P.size == expect and np.all(np.isfinite(P))
+    env = dict(os.environ, PYTHONPATH=os.path.join(root, "nerf-or-nothing_amd"))
+    q = subprocess.run([sys.executable, "-m", "nof.train", "--records", path, "--batch", "512", "--steps", "4",
+                        "--print-every", "2", "--net-depth", "4", "--net-width", "128", "--samples", "64", "64"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert q.returncode == 0, q.stderr[-2000:]
+    assert "rays/s" in q.stdout

@@ -233,7 +233,10 @@ hipError_t launch_gemm(const GemmArgs& a, int ksplit, hipStream_t st) {
     return hipErrorInvalidValue;
   const bool kdiv = a.A1.kdiv > 1 || a.A2.kdiv > 1 || a.B1.kdiv > 1 || a.B2.kdiv > 1;
   // 64 x 128 tiles for split-K weight gradients wider than 64 (A read once for up to 128 columns; measured
-  // 5 % faster there, 10 % slower on the unsplit dX GEMMs)
+  // 5 % faster there, 10 % slower on the unsplit dX GEMMs).  Measured and not kept: 128 x 128 tiles (two
+  // waves per SIMD) ran the trunk dX / dW GEMMs 185 -> 260 / 158 -> 230 us (the loop is latency-bound:
+  // occupancy wins), and addresses recomputed per k-step instead of per-element row pointers 6.52 -> 6.84
+  // ms per configs[0] step
   const bool wide = a.N > 64 && ksplit > 1;
   const int TN = wide ? 128 : 64;
   const dim3 grid((a.N + TN - 1) / TN, (a.M + kGT - 1) / kGT, ksplit);

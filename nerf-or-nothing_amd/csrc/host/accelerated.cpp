@@ -498,33 +498,71 @@ AcceleratedMLP::Schedule& AcceleratedMLP::schedule(int lv0, int lv1, int bucket)
     for (int i = 0; i < np; ++i) groups[0].push_back(i);
   }
   const int G_wg = num_cu_;
+  // f16split (HBM-bound k_wgrad_x3<2>): problems of one level that read the same delta rows — δ4 x h3 |
+  // δ4 x IPE and δ9x x h7 | δ9x x view PE | δ9x x h9, which F16 merges into wider problems instead — form
+  // one scheduling unit: a workgroup's k-range of the unit becomes one item per member over the SAME
+  // k-blocks, issued back to back, so the second read of the shared delta block comes from the CU's L2
+  // instead of HBM.  Measured (tools/ab_multi.sh, two boxes): weight gradients 1.124 -> 1.017 ms and
+  // 1.145 -> 1.034 ms, the reduce +11 us (more items per output), the step -1.9..-2.6 %.  Not kept for the
+  // other modes (fp32 / split MFMA-bound: unchanged, f16x2's k_wgrad_h 4 % slower), nor for operands shared
+  // as B (δ0 x IPE with δ4 x IPE: a larger reduce for no further gain).
+  std::vector<int> unit_of(np);
+  for (int i = 0; i < np; ++i) unit_of[i] = i;
+  if (precision_ == NOF_PRECISION_F32_F16SPLIT) {
+    auto root = [&](int i) {
+      while (unit_of[i] != i) i = unit_of[i] = unit_of[unit_of[i]];
+      return i;
+    };
+    for (int i = 0; i < np; ++i)
+      for (int j = i + 1; j < np; ++j) {
+        const nof::WgProblem &x = P[i], &y = P[j];
+        if (x.level != y.level || pbucket[i] != pbucket[j] || pnblk[i] != pnblk[j] || x.A != y.A) continue;
+        if (x.a_row0 < y.a_row0 + 32 * y.ntr && y.a_row0 < x.a_row0 + 32 * x.ntr) unit_of[root(j)] = root(i);
+      }
+    for (int i = 0; i < np; ++i) unit_of[i] = root(i);
+  }
   std::vector<std::vector<nof::WgItem>> wg_items(G_wg);
-  for (const std::vector<int>& grp : groups) {
+  for (const std::vector<int>& grp0 : groups) {
+    // the group's units in sequence order (a unit at its first member), each with its members
+    std::vector<int> grp;
+    std::vector<std::vector<int>> members;
+    {
+      std::vector<int> pos(np, -1);
+      for (int i : grp0) {
+        const int u = unit_of[i];
+        if (pos[u] < 0) { pos[u] = (int)grp.size(); grp.push_back(u); members.emplace_back(); }
+        members[pos[u]].push_back(i);
+      }
+    }
     const int ng = (int)grp.size();
     if (ng == 0) continue;
+    std::vector<int64_t> ucost(ng, 0);
+    for (int j = 0; j < ng; ++j)
+      for (int i : members[j]) ucost[j] += cost[i];
     std::vector<int64_t> cum(ng + 1, 0);
-    for (int j = 0; j < ng; ++j) cum[j + 1] = cum[j] + cost[grp[j]] * pnblk[grp[j]];
+    for (int j = 0; j < ng; ++j) cum[j + 1] = cum[j] + ucost[j] * pnblk[grp[j]];
     const int64_t total = cum.back();
-    auto mark = [&](int w) -> std::pair<int, int> {  // the cut before workgroup w: (group position, block)
+    auto mark = [&](int w) -> std::pair<int, int> {  // the cut before workgroup w: (unit position, block)
       if (w >= G_wg) return {ng, 0};
       const double x = (double)total * w / G_wg;
       int pj = 0;
       while (pj + 1 < ng && (double)cum[pj + 1] <= x) ++pj;
       const int nb = pnblk[grp[pj]];
-      const int kb = (int)std::min<int64_t>(nb, std::llround((x - (double)cum[pj]) / (double)cost[grp[pj]]));
+      const int kb = (int)std::min<int64_t>(nb, std::llround((x - (double)cum[pj]) / (double)ucost[pj]));
       return kb >= nb ? std::make_pair(pj + 1, 0) : std::make_pair(pj, kb);
     };
     for (int w = 0; w < G_wg; ++w) {
       std::pair<int, int> a = mark(w);
       const std::pair<int, int> b = std::max(a, mark(w + 1));
-      while (a < b) {  // split the workgroup's range at problem boundaries
+      while (a < b) {  // split the workgroup's range at unit boundaries
         const int pj = a.first, nb = pnblk[grp[pj]];
         const int kb1 = b.first == pj ? b.second : nb;
-        if (kb1 > a.second) {
-          nof::WgItem itm;
-          itm.prob = grp[pj]; itm.kb0 = a.second; itm.kb1 = kb1; itm.slab = -1;
-          wg_items[w].push_back(itm);
-        }
+        if (kb1 > a.second)
+          for (int i : members[pj]) {
+            nof::WgItem itm;
+            itm.prob = i; itm.kb0 = a.second; itm.kb1 = kb1; itm.slab = -1;
+            wg_items[w].push_back(itm);
+          }
         a = kb1 >= nb ? std::make_pair(pj + 1, 0) : std::make_pair(pj, kb1);
       }
     }

@@ -18,6 +18,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 K = "csrc/kernels/"
 
 EDITS = {
+    "h32_prio_b": [(K + "mlp_f16.hip",
+                    "  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);\n  // level 0's groups",
+                    "  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);\n  if (wave >= 4) __builtin_amdgcn_s_setprio(1);\n"
+                    "  // level 0's groups")],
+    # static s_setprio 1 for the younger half of the 8-wave F16 workgroups (cdna_hip_programming.md T5)
+    "h32_prio": [(K + "mlp_f16.hip",
+                  "  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);\n  const int nblk = a.M / kBlk;\n"
+                  "  const int ngroups = (nblk + kH32Waves - 1) / kH32Waves;  // 256 samples (8 blocks) per group",
+                  "  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);\n  if (wave >= 4) __builtin_amdgcn_s_setprio(1);\n"
+                  "  const int nblk = a.M / kBlk;\n"
+                  "  const int ngroups = (nblk + kH32Waves - 1) / kH32Waves;  // 256 samples (8 blocks) per group")],
     # F16 forward / backward (mlp_h32.h, mlp_f16.hip)
     "h32_nodma": [(K + "mlp_h32.h",
                    "    slice16_dma_step(next, lds + ((cur + kDmaAhead) & (kH32Slots - 1)) * kPeriodFloats, tid, step);",

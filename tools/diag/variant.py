@@ -18,6 +18,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 K = "csrc/kernels/"
 
 EDITS = {
+    # any-shape GEMM (generic.hip): k-steps of 32 (half the barriers per MFMA, twice the loads in flight)
+    "g_k32": [(K + "generic.hip", "constexpr int kGK = 16;   // k-step", "constexpr int kGK = 32;   // k-step"),
+              ("csrc/host/accelerated.cpp", "  a.kchunk = (a.K1 + a.K2 + 15) / 16 * 16;",
+               "  a.kchunk = (a.K1 + a.K2 + 31) / 32 * 32;"),
+              ("csrc/host/accelerated.cpp", "  const int kc = ((M + ks - 1) / ks + 15) / 16 * 16;",
+               "  const int kc = ((M + ks - 1) / ks + 31) / 32 * 32;")],
+    # any-shape GEMM: two workgroups per CU guaranteed by the register budget
+    "g_lb2": [(K + "generic.hip", "__global__ __launch_bounds__(kGThreads) void k_gemm(GemmArgs a) {",
+               "__global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {")],
     "h32_prio_b": [(K + "mlp_f16.hip",
                     "  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);\n  // level 0's groups",
                     "  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);\n  if (wave >= 4) __builtin_amdgcn_s_setprio(1);\n"

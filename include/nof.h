@@ -353,8 +353,10 @@ nof_status nof_image_metrics(const float* dev_img0, const float* dev_img1, int32
 
 /* ---- AcceleratedMLP (AcceleratedMLP.h:7-45) -------------------------------------------------- */
 /* get_output MLPcpp:214-255: encoded inputs in device memory (enc_pos [n*S][96] in the reference's
- * feature order, enc_dir [n][27] per ray, D5) -> (density [n*S], rgb [n*S][3]) borrowed.  The
- * reference returns (density, rgb) but its caller binds them swapped (D9): here they are named. */
+ * feature order, enc_dir [n][27] per ray, D5; any-shape networks: [n*S][6 (max_deg - min_deg)] and
+ * [n][3 + 6 deg_view]) -> (density [n*S], rgb [n*S][3]) borrowed.  The inputs are read during the
+ * call's stream work only (the library keeps its own copy for get_gradient).  The reference returns
+ * (density, rgb) but its caller binds them swapped (D9): here they are named. */
 nof_status nof_mlp_get_output(nof_mlp* m, const float* dev_enc_pos, const float* dev_enc_dir, int32_t level,
                               int32_t n_rays, int32_t samples, uint64_t* dev_density, uint64_t* dev_rgb);
 /* get_gradient MLPcpp:256-321: dL/d rgb [n*S][3] and dL/d density [n*S] of `level`'s last forward.

@@ -295,8 +295,12 @@ std::pair<float*, float*> AcceleratedMLP::get_output(const float* enc_pos, const
               "n_rays * samples must be a multiple of 32 within the level's capacity");
   pack_weights();
   lv_[level].M = M; lv_[level].n = n_rays; lv_[level].S = samples;
-  if (generic_) {
-    gen_forward(level, enc_pos, enc_dir);
+  if (generic_) {  // the encodings copied in: the backward reads them after the caller's buffers may be gone
+    GenLevel& G = gl_[level];
+    NOF_HIP(hipMemcpyAsync(G.enc_pos.p, enc_pos, (size_t)M * gP_ * sizeof(float), hipMemcpyDeviceToDevice, st_));
+    NOF_HIP(hipMemcpyAsync(G.enc_dir.p, enc_dir, (size_t)n_rays * gVd_ * sizeof(float), hipMemcpyDeviceToDevice,
+                           st_));
+    gen_forward(level, G.enc_pos.p, G.enc_dir.p);
     return {lv_[level].sigma.p, lv_[level].rgb.p};
   }
   nof::FwdArgs a{};

@@ -47,7 +47,7 @@ def _run(model, r, dev):
                                      msum)
 
 
-def _check(gpu, oracle, spec, kind, n, samples, lindisp=0, ray_shape=0, nthreads=16):
+def _check(gpu, oracle, spec, kind, n, samples, lindisp=0, ray_shape=0, nthreads=16, lossmult=None):
     import torch
     import nof
     from nof import synth
@@ -61,6 +61,8 @@ def _check(gpu, oracle, spec, kind, n, samples, lindisp=0, ray_shape=0, nthreads
     sizes = oracle.layer_sizes(sp)
     assert model.GetLayerSizes() == list(sizes)
     r = synth.blender_rays(n, seed=23) if kind == "blender" else synth.llff_rays(n, seed=23)
+    if lossmult is not None:
+        r["lossmult"] = np.resize(np.asarray(lossmult, np.float32), n)
     grads = _run(model, r, gpu)
     torch.cuda.synchronize()
     assert len(grads) == len(sizes)
@@ -80,6 +82,10 @@ def _check(gpu, oracle, spec, kind, n, samples, lindisp=0, ray_shape=0, nthreads
         assert np.array_equal(lv[l]["t"], tl)
         tov[l] = lv[l]["t"]
 
+    if lossmult is not None:  # masked rays: exactly zero output gradients
+        for l in range(len(samples)):
+            assert not np.any(lv[l]["density_grad"][r["lossmult"] == 0])
+            assert not np.any(lv[l]["rgb_grad"][r["lossmult"] == 0])
     masks = {l: model.mlp.relu_masks(l).reshape(n, samples[l], -1) for l in range(len(samples))}
     kw = dict(samples=samples, seed=seed, step_idx=step, ray_base=ray_base, t_override=tov, nthreads=nthreads, **opts)
     ref = oracle.step(sp, params, r, relu_mask=masks, want=("grads",), **kw)
@@ -113,6 +119,14 @@ def test_generic_step_parity_llff_options(gpu, oracle):
 def test_generic_single_and_three_levels(gpu, oracle):
     _check(gpu, oracle, SPECS["configs0_4x128"], "blender", 6, (64,))
     _check(gpu, oracle, SPECS["tiny_2x32_skip1"], "blender", 4, (64, 64, 128))
+
+
+# the edge cases of test_gpu_edges.py on the any-shape path: one ray, one ray at 512 + 512 samples, the fine
+# level smaller than the coarse one, masked rays (lossmult = 0)
+@pytest.mark.parametrize("n,samples,lossmult", [(1, (64, 64), None), (1, (512, 512), None), (5, (128, 64), None),
+                                                (12, (64, 128), [1.0, 0.0, 2.0, 0.0])])
+def test_generic_edges(gpu, oracle, n, samples, lossmult):
+    _check(gpu, oracle, SPECS["odd_5x96_3x40"], "blender", n, samples, lossmult=lossmult)
 
 
 def test_generic_configs0_fullsize(gpu, oracle):

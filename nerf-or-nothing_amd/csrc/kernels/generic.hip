@@ -91,7 +91,10 @@ __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
   constexpr int NQ = TN / 32;  // 16-wide MFMA tiles per wave along j
   __shared__ float As[kGK][kGT + 4], Bs[kGK][TN + 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int i0 = blockIdx.y * kGT, j0 = blockIdx.x * TN;
+  // output tiles linear in blockIdx.x, columns fastest (a grid's y is capped at 65535 row tiles)
+  const int ntc = (a.N + TN - 1) / TN;
+  const int tcol = blockIdx.x % ntc;
+  const int i0 = (blockIdx.x / ntc) * kGT, j0 = tcol * TN;
   const int wi = (wave >> 1) * 32, wj = (wave & 1) * (TN / 2);
   const int K = a.K1 + a.K2;
   // the chunk end bounds k as well (a split-K chunk reads only its own k)
@@ -107,7 +110,7 @@ __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
     for (int q = 0; q < NQ; ++q) acc[p][q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
   // row sums of A over this chunk's k (the bias gradient beside a weight gradient): the first column
   // tile's wave 0, one row per lane, from the LDS tile, in k order
-  const bool rowsum = a.rowsum && blockIdx.x == 0 && wave == 0;
+  const bool rowsum = a.rowsum && tcol == 0 && wave == 0;
   float rs = 0.0f;
   float va[GPlan<kGT>::E], vb[GPlan<TN>::E];
   bool oa[GPlan<kGT>::E], ob[GPlan<TN>::E];
@@ -241,7 +244,9 @@ hipError_t launch_gemm(const GemmArgs& a, int ksplit, hipStream_t st) {
   // ms per configs[0] step
   const bool wide = a.N > 64 && ksplit > 1;
   const int TN = wide ? 128 : 64;
-  const dim3 grid((a.N + TN - 1) / TN, (a.M + kGT - 1) / kGT, ksplit);
+  const int64_t tiles = (int64_t)((a.N + TN - 1) / TN) * ((a.M + kGT - 1) / kGT);
+  if (tiles > 0x7fffffff || ksplit > 65535) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)tiles, 1, ksplit);
   if (kdiv && wide) hipLaunchKernelGGL((k_gemm<true, 128>), grid, dim3(kGThreads), 0, st, a);
   else if (kdiv) hipLaunchKernelGGL((k_gemm<true, 64>), grid, dim3(kGThreads), 0, st, a);
   else if (wide) hipLaunchKernelGGL((k_gemm<false, 128>), grid, dim3(kGThreads), 0, st, a);

@@ -338,3 +338,37 @@ def test_generic_encoded_api_path(gpu, oracle):
         assert rel_l2(x, y) < TOL, f"gradient tensor {i}"
     a.close()
     b.close()
+
+
+def test_generic_more_than_65535_row_tiles(gpu):
+    """8192 rays x 512 + 512 samples: 4.19 M samples per level = 65 536 GEMM row tiles, past a launch grid's
+    y limit (the tiles are linear in x).  The step equals its two accumulated 4096-ray halves (global ray
+    ids, the global loss-multiplier sum) within 1e-5."""
+    import torch
+    import nof
+    from nof import synth
+
+    n, samples = 8192, (512, 512)
+    cfg = _cfg(SPECS["tiny_2x32_skip1"])
+    r = synth.blender_rays(n, seed=12)
+    d = {k: torch.from_numpy(np.ascontiguousarray(v)).to(gpu) for k, v in r.items()}
+    msum = float(n)
+    m = nof.AcceleratedMipNeRF(seed=3, max_rays=n, num_samples=samples, **cfg)
+    m.set_rng(5, 1, 0)
+    m.get_gradient_device(n, d["o"], d["d"], d["radius"], d["near"], d["far"], d["lossmult"], d["pix"], msum)
+    torch.cuda.synchronize()
+    gp, P = m.mlp.flat_grads()
+    g_full = nof.to_numpy(gp, (P,)).copy()
+    assert np.all(np.isfinite(g_full)) and np.any(g_full != 0)
+    m.close()
+    h = n // 2
+    m = nof.AcceleratedMipNeRF(seed=3, max_rays=h, num_samples=samples, **cfg)
+    for i in range(2):
+        sl = slice(i * h, (i + 1) * h)
+        m.set_rng(5, 1, i * h)
+        m.get_gradient_device(h, d["o"][sl], d["d"][sl], d["radius"][sl], d["near"][sl], d["far"][sl],
+                              d["lossmult"][sl], d["pix"][sl], msum, accumulate=i > 0, publish=i == 1)
+    torch.cuda.synchronize()
+    g_acc = nof.to_numpy(m.mlp.flat_grads()[0], (P,))
+    assert rel_l2(g_acc, g_full) < TOL
+    m.close()

@@ -112,17 +112,22 @@ __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
   // tile's wave 0, one row per lane, from the LDS tile, in k order
   const bool rowsum = a.rowsum && tcol == 0 && wave == 0;
   float rs = 0.0f;
-  float va[GPlan<kGT>::E], vb[GPlan<TN>::E];
-  bool oa[GPlan<kGT>::E], ob[GPlan<TN>::E];
-  g_fetch<KDIV>(va, oa, pa, a.A1, a.A2, a.K1, ke, kb);
-  g_fetch<KDIV>(vb, ob, pb, a.B1, a.B2, a.K1, ke, kb);
-  for (int k0 = kb; k0 < ke; k0 += kGK) {
-    g_store(As, pa, va, oa);
-    g_store(Bs, pb, vb, ob);
+  // two k-steps of loads in flight: set 0 holds the even steps, set 1 the odd ones; a step's loads are
+  // issued two steps ahead of their LDS store (one step ahead left the global-load latency exposed: the
+  // loop is latency-bound, not MFMA- or HBM-bound)
+  float va[2][GPlan<kGT>::E], vb[2][GPlan<TN>::E];
+  bool oa[2][GPlan<kGT>::E], ob[2][GPlan<TN>::E];
+  g_fetch<KDIV>(va[0], oa[0], pa, a.A1, a.A2, a.K1, ke, kb);
+  g_fetch<KDIV>(vb[0], ob[0], pb, a.B1, a.B2, a.K1, ke, kb);
+  g_fetch<KDIV>(va[1], oa[1], pa, a.A1, a.A2, a.K1, ke, kb + kGK);
+  g_fetch<KDIV>(vb[1], ob[1], pb, a.B1, a.B2, a.K1, ke, kb + kGK);
+  auto step = [&](int k0, int s) {
+    g_store(As, pa, va[s], oa[s]);
+    g_store(Bs, pb, vb[s], ob[s]);
     __syncthreads();
-    if (k0 + kGK < ke) {  // the next step's loads in flight under this step's MFMAs
-      g_fetch<KDIV>(va, oa, pa, a.A1, a.A2, a.K1, ke, k0 + kGK);
-      g_fetch<KDIV>(vb, ob, pb, a.B1, a.B2, a.K1, ke, k0 + kGK);
+    if (k0 + 2 * kGK < ke) {
+      g_fetch<KDIV>(va[s], oa[s], pa, a.A1, a.A2, a.K1, ke, k0 + 2 * kGK);
+      g_fetch<KDIV>(vb[s], ob[s], pb, a.B1, a.B2, a.K1, ke, k0 + 2 * kGK);
     }
     if (rowsum)
 #pragma unroll
@@ -141,6 +146,10 @@ __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
         for (int q = 0; q < NQ; ++q) acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[p], bv[q], acc[p][q], 0, 0, 0);
     }
     __syncthreads();
+  };
+  for (int k0 = kb; k0 < ke; k0 += 2 * kGK) {
+    step(k0, 0);
+    if (k0 + kGK < ke) step(k0 + kGK, 1);
   }
   if (rowsum && i0 + lane < a.M) a.rowsum[(int64_t)blockIdx.z * a.M + i0 + lane] = rs;
   float* C = a.C + (int64_t)blockIdx.z * a.slab_stride;

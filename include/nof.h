@@ -69,8 +69,12 @@ typedef struct nof_config {
                                              MNcs:14, SampleAlongRay MH:618-620); default 0 */
   int32_t ray_shape;                      /* NOF_RAY_CONICAL (MNcs:15, MH:391-402) or NOF_RAY_CYLINDRICAL
                                              (CylinderToGaussian MH:403-409); default conical */
+  float density_bias;                     /* MipNerfModel.DensityBias (MNcs:20): sigma = softplus(z + bias); -1 */
+  float rgb_padding;                      /* MipNerfModel.RgbPadding (MNcs:22): rgb = sigmoid(z) (1 + 2 p) - p;
+                                             0.001, in [0, 0.5).  The activations themselves are the
+                                             reference's fixed softplus / sigmoid (MNcs:19,21) */
 } nof_config;
-/* The struct grows at its end only (grad_buckets, then lindisp / ray_shape were appended): a binding
+/* The struct grows at its end only (grad_buckets, then lindisp / ray_shape, then density_bias / rgb_padding): a binding
  * compiled against an older header passes a shorter struct.  nof_config_size() is sizeof(nof_config) of
  * this library; a binding checks it against its own struct size before passing one. */
 size_t nof_config_size(void);

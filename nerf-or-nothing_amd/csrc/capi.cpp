@@ -99,6 +99,8 @@ void nof_config_default(nof_config* c) {
   c->grad_buckets = 0;
   c->lindisp = 0;
   c->ray_shape = NOF_RAY_CONICAL;
+  c->density_bias = -1.0f;  // MNcs:20
+  c->rgb_padding = 0.001f;  // MNcs:22
 }
 
 size_t nof_config_size(void) { return sizeof(nof_config); }

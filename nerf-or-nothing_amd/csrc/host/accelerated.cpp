@@ -120,6 +120,9 @@ static void check_cfg(const nof_config& c) {
   NOF_REQUIRE(c.grad_buckets == 0 || c.grad_buckets == 1, "grad_buckets must be 0 or 1");
   NOF_REQUIRE(c.lindisp == 0 || c.lindisp == 1, "lindisp must be 0 or 1");
   NOF_REQUIRE(c.ray_shape == NOF_RAY_CONICAL || c.ray_shape == NOF_RAY_CYLINDRICAL, "unknown ray_shape");
+  NOF_REQUIRE(std::isfinite(c.density_bias) && std::isfinite(c.rgb_padding) && c.rgb_padding >= 0.0f &&
+                  c.rgb_padding < 0.5f,
+              "density_bias must be finite, rgb_padding in [0, 0.5)");
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -249,6 +252,9 @@ void AcceleratedMLP::run_forward(int level, const nof::FwdArgs& a0) {
   Level& L = lv_[level];
   nof::FwdArgs a = a0;
   a.split = precision_;
+  a.dbias = cfg_.density_bias;  // MipNerfModel.DensityBias / RgbPadding (MNcs:20-22)
+  a.rgb_pad = cfg_.rgb_padding;
+  a.rgb_scale = rgb_scale();
   a.wimg = wimg_f_.p;
   a.act_in = L.act_in.p;
   a.act_h = L.act_h.p;
@@ -664,6 +670,8 @@ nof::BwdArgs AcceleratedMLP::bwd_args(int level, const float* color_grad, const 
   nof::BwdArgs b{};
   b.M = L.M;
   b.split = precision_;
+  b.dbias = cfg_.density_bias;
+  b.rgb_scale = rgb_scale();
   if (f16_pieces()) {  // the level's power-of-two delta scale
     if ((amax_given_ >> level) & 1u) {  // filled by the integrator adjoint (claim_delta_amax)
       amax_given_ &= ~(1u << level);
@@ -905,7 +913,7 @@ void AcceleratedMLP::gen_forward(int level, const float* ep, const float* ed) {
     a.C = G.z.p + 1; a.ci = 4; a.cj = 1;
     gemm1(a, st_);
   }
-  NOF_HIP(nof::launch_heads_fwd(M, G.z.p, L.sigma.p, L.rgb.p, st_));
+  NOF_HIP(nof::launch_heads_fwd(M, G.z.p, L.sigma.p, L.rgb.p, cfg_.density_bias, rgb_scale(), cfg_.rgb_padding, st_));
   te(kTMlpFwd);
 }
 
@@ -931,7 +939,7 @@ void AcceleratedMLP::gen_backward(int level, const float* color_grad, const floa
     gemm1(a, st_);
   };
   tb(kTMlpBwd);
-  NOF_HIP(nof::launch_heads_bwd(M, density_grad, color_grad, G.z.p, dz, st_));  // MNcs:23-28, 184-189
+  NOF_HIP(nof::launch_heads_bwd(M, density_grad, color_grad, G.z.p, dz, cfg_.density_bias, rgb_scale(), st_));  // MNcs:23-28,184-189
   // rgb head: dW, db from dz[:, 1..3]; its dX into the last condition layer
   gen_wgrad(gr + woff_[lr], Wc, dz + 1, 4, 3, gsrc(Hc(Dc - 1), 1, Wc), Wc, M, acc, gr + boff_[lr]);
   dx(dz + 1, 4, 3, lr, Hc(Dc - 1), Wc, cur);

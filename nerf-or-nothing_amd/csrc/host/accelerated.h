@@ -199,6 +199,8 @@ class AcceleratedMLP {
   }
   // fp16 activation / delta blocks and the k_wgrad_h weight gradients (F16X2, F16)
   bool f16_blocks() const { return precision_ == NOF_PRECISION_F16X2 || precision_ == NOF_PRECISION_F16; }
+  // RGB head scale (1 + 2 RgbPadding) formed in fp32 as the C# expression is (MNcs:22,151)
+  float rgb_scale() const { return 1.0f + 2.0f * cfg_.rgb_padding; }
   size_t P_ = 0;
   std::vector<int> out_, in_, woff_, boff_;  // per layer (MLPcpp:131-154 / the oracle's Spec order)
 

@@ -123,6 +123,8 @@ static __device__ uint32_t g_nof_checks[32];  // one copy per translation unit (
 __device__ inline float softplus_f(float x) { return x > 20.0f ? x : log1pf(expf(x)); }  // D28
 __device__ inline float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// the heads' reference constants (MNcs:20-22); the kernels take the configured values (nof_config
+// density_bias / rgb_padding, FwdArgs / BwdArgs), these are the defaults
 constexpr float kRgbPadding = 0.001f;
 constexpr float kRgbScale = 1.0f + 2.0f * 0.001f;  // (1 + 2*RgbPadding), MNcs:22,151
 constexpr float kDensityBias = -1.0f;              // MNcs:20

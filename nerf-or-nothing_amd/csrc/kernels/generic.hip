@@ -219,23 +219,24 @@ __global__ void k_encode_g(int n, int S, const float* __restrict__ mean, const f
 }
 
 // z = [z_sigma, z_rgb] [M][4] -> sigma = softplus(z_sigma - 1), rgb = sigmoid(z_rgb) 1.002 - 0.001 (MNcs:19-22,151-152)
-__global__ void k_heads_fwd(int M, const float* __restrict__ z, float* __restrict__ sigma, float* __restrict__ rgb) {
+__global__ void k_heads_fwd(int M, const float* __restrict__ z, float* __restrict__ sigma, float* __restrict__ rgb,
+                            float dbias, float rgb_scale, float rgb_pad) {
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= M) return;
-  sigma[m] = softplus_f(z[4 * m] + kDensityBias);
+  sigma[m] = softplus_f(z[4 * m] + dbias);
 #pragma unroll
-  for (int c = 0; c < 3; ++c) rgb[3 * m + c] = sigmoid_f(z[4 * m + 1 + c]) * kRgbScale - kRgbPadding;
+  for (int c = 0; c < 3; ++c) rgb[3 * m + c] = sigmoid_f(z[4 * m + 1 + c]) * rgb_scale - rgb_pad;
 }
 // dz = [dsigma sigmoid(z_sigma - 1), drgb s (1 - s) 1.002] (MNcs:23-28,184-189; s(1 - s): D28)
 __global__ void k_heads_bwd(int M, const float* __restrict__ dsigma, const float* __restrict__ drgb,
-                            const float* __restrict__ z, float* __restrict__ dz) {
+                            const float* __restrict__ z, float* __restrict__ dz, float dbias, float rgb_scale) {
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= M) return;
-  dz[4 * m] = dsigma[m] * sigmoid_f(z[4 * m] + kDensityBias);
+  dz[4 * m] = dsigma[m] * sigmoid_f(z[4 * m] + dbias);
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const float s = sigmoid_f(z[4 * m + 1 + c]);
-    dz[4 * m + 1 + c] = drgb[3 * m + c] * (s * (1.0f - s)) * kRgbScale;
+    dz[4 * m + 1 + c] = drgb[3 * m + c] * (s * (1.0f - s)) * rgb_scale;
   }
 }
 
@@ -279,14 +280,16 @@ hipError_t launch_encode_g(int n, int S, const float* mean, const float* cov, co
                      P, Vd, enc_pos, enc_dir);
   return hipGetLastError();
 }
-hipError_t launch_heads_fwd(int M, const float* z, float* sigma, float* rgb, hipStream_t st) {
+hipError_t launch_heads_fwd(int M, const float* z, float* sigma, float* rgb, float dbias, float rgb_scale,
+                            float rgb_pad, hipStream_t st) {
   if (M <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_heads_fwd, dim3((M + 255) / 256), dim3(256), 0, st, M, z, sigma, rgb);
+  hipLaunchKernelGGL(k_heads_fwd, dim3((M + 255) / 256), dim3(256), 0, st, M, z, sigma, rgb, dbias, rgb_scale, rgb_pad);
   return hipGetLastError();
 }
-hipError_t launch_heads_bwd(int M, const float* dsigma, const float* drgb, const float* z, float* dz, hipStream_t st) {
+hipError_t launch_heads_bwd(int M, const float* dsigma, const float* drgb, const float* z, float* dz, float dbias,
+                            float rgb_scale, hipStream_t st) {
   if (M <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_heads_bwd, dim3((M + 255) / 256), dim3(256), 0, st, M, dsigma, drgb, z, dz);
+  hipLaunchKernelGGL(k_heads_bwd, dim3((M + 255) / 256), dim3(256), 0, st, M, dsigma, drgb, z, dz, dbias, rgb_scale);
   return hipGetLastError();
 }
 

@@ -69,6 +69,9 @@ struct FwdArgs {
   int no_store;                            // 1: inference only, skip the backward's side outputs
   int split;                               // MLP precision: 0 fp32, 1 bf16x3 split, 2 f16x2 (mlp_common.h)
   int cylinder;                            // fused encoding: cylinders (MH:403-409) instead of conical frustums
+  // heads (MNcs:19-22,151-152): sigma = softplus(z_s + dbias), rgb = sigmoid(z_c) rgb_scale - rgb_pad with
+  // rgb_scale = fp32(1 + 2 rgb_pad); MipNerfModel.DensityBias / RgbPadding, the reference values by default
+  float dbias = -1.0f, rgb_scale = 1.002f, rgb_pad = 0.001f;
   const float *t, *origins, *dirs, *radii;  // fused-encoding inputs
   const float *enc_pos, *enc_dir;          // encoded inputs (API path): [M][96], [n][27]
   const float* wimg;                       // packed forward image (slices + tail)
@@ -87,6 +90,7 @@ struct BwdArgs {
   int split;                               // as FwdArgs::split
   const float *dsigma, *drgb, *zhead;
   const uint32_t* amax;                    // split == 2: max |dsigma|, |drgb| bits (launch_delta_amax)
+  float dbias = -1.0f, rgb_scale = 1.002f; // the heads' derivatives (MNcs:23-28,184-189), as FwdArgs
   const uint32_t* masks;
   const float* wimg_b;                     // packed backward image (slices + tail)
   float* delta;    // [8][M/32][256][32]
@@ -183,8 +187,10 @@ hipError_t launch_slab_sum(int rows, int cols, int pitch, int nz, const float* s
 hipError_t launch_encode_g(int n, int S, const float* mean, const float* cov, const float* d, int min_deg, int P,
                            int Vd, float* enc_pos, float* enc_dir, hipStream_t st);
 // z [M][4] (density, rgb pre-activations) -> sigma [M], rgb [M][3]; backward: dz [M][4]
-hipError_t launch_heads_fwd(int M, const float* z, float* sigma, float* rgb, hipStream_t st);
-hipError_t launch_heads_bwd(int M, const float* dsigma, const float* drgb, const float* z, float* dz, hipStream_t st);
+hipError_t launch_heads_fwd(int M, const float* z, float* sigma, float* rgb, float dbias, float rgb_scale,
+                            float rgb_pad, hipStream_t st);
+hipError_t launch_heads_bwd(int M, const float* dsigma, const float* drgb, const float* z, float* dz, float dbias,
+                            float rgb_scale, hipStream_t st);
 
 // ---- adam.hip ----------------------------------------------------------------------------------
 // ---- dataset.hip: device-resident record set -> SoA batch gather (+ optional loss-mult sum) ----

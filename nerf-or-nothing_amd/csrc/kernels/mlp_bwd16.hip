@@ -90,12 +90,12 @@ __global__ __launch_bounds__(kMlp16Threads, 1) void k_mlp_bwd16(BwdArgs a) {
 
   // ---- heads (MNcs:23-28,184-189) ------------------------------------------------------------
   const f32x4 zh = reinterpret_cast<const f32x4*>(a.zhead)[m];
-  float dzs = a.dsigma[m] * sigmoid_f(zh[0] + kDensityBias);
+  float dzs = a.dsigma[m] * sigmoid_f(zh[0] + a.dbias);
   float dzc[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const float s = sigmoid_f(zh[1 + c]);
-    dzc[c] = a.drgb[(size_t)m * 3 + c] * (s * (1.0f - s)) * kRgbScale;
+    dzc[c] = a.drgb[(size_t)m * 3 + c] * (s * (1.0f - s)) * a.rgb_scale;
   }
   if constexpr (P >= 2) {  // f16 pieces: deltas enter them scaled by a power of two
     const float sc = delta_scale(a.amax, false);

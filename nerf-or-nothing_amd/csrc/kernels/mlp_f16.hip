@@ -496,9 +496,9 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
 #pragma unroll
   for (int c = 0; c < 3; ++c) zc[c] = eV.zc[c] + __shfl_xor(eV.zc[c], 32, 64) + hb[1 + c];
   if (h == 0) {
-    a.sigma[m] = softplus_f(zs + kDensityBias);
+    a.sigma[m] = softplus_f(zs + a.dbias);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) a.rgb[(size_t)m * 3 + c] = sigmoid_f(zc[c]) * kRgbScale - kRgbPadding;
+    for (int c = 0; c < 3; ++c) a.rgb[(size_t)m * 3 + c] = sigmoid_f(zc[c]) * a.rgb_scale - a.rgb_pad;
     if constexpr (kStore) reinterpret_cast<f32x4*>(a.zhead)[m] = f32x4{zs, zc[0], zc[1], zc[2]};
   }
   // the inference forward (no side outputs: the evaluation render) runs one group per workgroup — as a
@@ -670,12 +670,12 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   const uint4 mk9 = {mk9v[0], mk9v[1], mk9v[2], mk9v[3]};
   const uint4 mk7 = {mk7v[0], mk7v[1], mk7v[2], mk7v[3]};
   uint4 mk_next = mask_of(6);  // every later layer's mask words are loaded one layer before its begin()
-  const float dzs = ds_m * sigmoid_f(zh[0] + kDensityBias) * sc;
+  const float dzs = ds_m * sigmoid_f(zh[0] + a.dbias) * sc;
   float dzc[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const float s = sigmoid_f(zh[1 + c]);
-    dzc[c] = dr[c] * (s * (1.0f - s)) * kRgbScale * sc;
+    dzc[c] = dr[c] * (s * (1.0f - s)) * a.rgb_scale * sc;
   }
   // ---- delta9 = (W10^T dz_rgb) * relu'(layer 9) -> the B fragments of dh7, and delta9x ------------------
   uint32_t X[16][4], Y[16][4];

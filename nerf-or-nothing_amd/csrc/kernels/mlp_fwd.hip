@@ -270,9 +270,9 @@ __global__ __launch_bounds__(kMlpThreads, 1) void k_mlp_fwd(FwdArgs a) {
   }
 
   if (h == 0) {
-    a.sigma[m] = softplus_f(zs + kDensityBias);
+    a.sigma[m] = softplus_f(zs + a.dbias);
 #pragma unroll
-    for (int c = 0; c < 3; ++c) a.rgb[(size_t)m * 3 + c] = sigmoid_f(zc[c]) * kRgbScale - kRgbPadding;
+    for (int c = 0; c < 3; ++c) a.rgb[(size_t)m * 3 + c] = sigmoid_f(zc[c]) * a.rgb_scale - a.rgb_pad;
     f32x4 zh;
     zh[0] = zs; zh[1] = zc[0]; zh[2] = zc[1]; zh[3] = zc[2];
     if constexpr (store) reinterpret_cast<f32x4*>(a.zhead)[m] = zh;

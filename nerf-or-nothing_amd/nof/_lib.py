@@ -38,6 +38,7 @@ class nof_config(C.Structure):
         ("resample_padding", C.c_float), ("coarse_loss_mult", C.c_float),
         ("seed", C.c_uint64), ("stream", C.c_void_p), ("precision", C.c_int32), ("grad_buckets", C.c_int32),
         ("lindisp", C.c_int32), ("ray_shape", C.c_int32),
+        ("density_bias", C.c_float), ("rgb_padding", C.c_float),
     ]
 
 
@@ -196,7 +197,7 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = _RESTYPE.get(name, C.c_int32)
-        if diag and not hasattr(L, "nof_config_size"):
+        if diag and (not hasattr(L, "nof_config_size") or L.nof_config_size() < C.sizeof(nof_config)):
             pass  # an older build reads its own (shorter, prefix-identical) nof_config
         elif L.nof_config_size() != C.sizeof(nof_config):  # the struct this binding passes must be the library's
             raise RuntimeError(f"nof_config: the library expects {L.nof_config_size()} bytes, this binding "

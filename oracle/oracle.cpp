@@ -105,9 +105,11 @@ struct Spec {
 };
 
 // Config constants the reference hard-codes as float (MNcs:19-22, TrainState.cs:69).
+// Defaults of MipNerfModel.RgbPadding / DensityBias (MNcs:20,22), settable per step (StepIO); the RGB
+// scale (1 + 2 RgbPadding) is formed in fp32 as the C# expression is (MNcs:22,151).
 static const float kRgbPadding = 0.001f;
-static const float kRgbScale = 1.0f + 2.0f * 0.001f;  // (1 + 2*RgbPadding) in fp32 (MNcs:22,151)
 static const float kDensityBias = -1.0f;
+static inline float rgb_scale(float pad) { return 1.0f + 2.0f * pad; }
 static const float kHalfPi = 3.14159274f * 0.5f;      // MathF.PI * 0.5f (MH:446)
 
 template <class T> static inline T softplus(T x) { return x > T(20) ? x : std::log1p(std::exp(x)); }  // D28
@@ -445,6 +447,7 @@ struct StepIO {
   int nthreads;
   int64_t* mask_flips;     // [level] adopted ReLU decisions != the oracle's own (optional)
   bool lindisp, cylinder;  // LinDisp / RayShape.Cylindrical (MNcs:14-15; default false / conical)
+  float density_bias = kDensityBias, rgb_padding = kRgbPadding;  // MipNerfModel.DensityBias / RgbPadding (MNcs:20,22)
 };
 
 template <class T>
@@ -500,10 +503,10 @@ static void step(const Spec& sp, const float* P, const StepIO& io) {
         mlp_forward_sample<T>(sp, P, enc.data(), dpe.data(), c, mk);
         flipsp[tid][lv] += c.flips;
         zs[lv][k] = c.zs;
-        sig[lv][k] = softplus<T>(c.zs + (T)kDensityBias);                       // MNcs:19-20,152
+        sig[lv][k] = softplus<T>(c.zs + (T)io.density_bias);                     // MNcs:19-20,152
         for (int j = 0; j < 3; ++j) {
           zc[lv][3 * k + j] = c.zc[j];
-          rgb[lv][3 * k + j] = sigm<T>(c.zc[j]) * (T)kRgbScale - (T)kRgbPadding;    // MNcs:21-22,151
+          rgb[lv][3 * k + j] = sigm<T>(c.zc[j]) * (T)rgb_scale(io.rgb_padding) - (T)io.rgb_padding;  // MNcs:21-22,151
         }
       }
       render_ray<T>(S, sig[lv].data(), rgb[lv].data(), tl[lv].data(), d, io.white, Cl[lv].data(), w[lv].data(), al[lv].data(), tr[lv].data());
@@ -531,11 +534,11 @@ static void step(const Spec& sp, const float* P, const StepIO& io) {
       if (io.grads) {
         for (int k = 0; k < S; ++k) {
           // activation gradients MNcs:23-28,184-189 (sigmoid' written as s(1-s), D28-style overflow safety)
-          const T dzs = ds[k] * sigm<T>(zs[lv][k] + (T)kDensityBias);
+          const T dzs = ds[k] * sigm<T>(zs[lv][k] + (T)io.density_bias);
           T dzc[3];
           for (int j = 0; j < 3; ++j) {
             const T s = sigm<T>(zc[lv][3 * k + j]);
-            dzc[j] = dc[3 * k + j] * (s * (T(1) - s)) * (T)kRgbScale;
+            dzc[j] = dc[3 * k + j] * (s * (T(1) - s)) * (T)rgb_scale(io.rgb_padding);
           }
           mlp_backward_sample<T>(sp, P, cache[lv][k], dzs, dzc, Gp[tid].data());
         }
@@ -668,6 +671,7 @@ struct orc_step_args {
   int32_t nthreads;
   int64_t* mask_flips;
   int32_t lindisp, ray_shape;  // appended (0, 0 = the reference defaults)
+  float density_bias, rgb_padding;  // appended (MNcs:20,22: -1, 0.001)
 };
 
 static StepIO cvt(const orc_step_args* a) {
@@ -682,6 +686,8 @@ static StepIO cvt(const orc_step_args* a) {
   io.mask_flips = a->mask_flips;
   io.lindisp = a->lindisp != 0;
   io.cylinder = a->ray_shape == 1;
+  io.density_bias = a->density_bias;
+  io.rgb_padding = a->rgb_padding;
   return io;
 }
 

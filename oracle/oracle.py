@@ -42,6 +42,7 @@ class OrcStepArgs(C.Structure):
         ("grads", C.c_void_p), ("loss", C.c_void_p), ("nthreads", C.c_int32),
         ("mask_flips", C.c_void_p),
         ("lindisp", C.c_int32), ("ray_shape", C.c_int32),
+        ("density_bias", C.c_float), ("rgb_padding", C.c_float),
     ]
 
 
@@ -240,7 +241,8 @@ def render_grad(g, sigma, rgb, t, d, white=True):
 def step(spec: Spec, P, rays: dict, samples=(128, 128), seed=0, step_idx=0, ray_base=0, randomized=True,
          white=True, padding=0.01, coarse_mult=0.1, loss_mult_sum=0.0, t_override=None, relu_mask=None,
          dtype=np.float64,
-         nthreads=None, want=("t", "w", "C", "sigma", "rgb", "dsigma", "drgb", "grads"), lindisp=False, ray_shape=0):
+         nthreads=None, want=("t", "w", "C", "sigma", "rgb", "dsigma", "drgb", "grads"), lindisp=False, ray_shape=0,
+         density_bias=-1.0, rgb_padding=0.001):
     """Oracle training step (MipNerfModel.GetGradient, MNcs:99-200).
 
     ``rays``: dict of float32 arrays o[n,3], d[n,3], radius[n], near[n], far[n], lossmult[n], pix[n,3].
@@ -275,6 +277,7 @@ def step(spec: Spec, P, rays: dict, samples=(128, 128), seed=0, step_idx=0, ray_
     args.padding, args.coarse_mult, args.loss_mult_sum = padding, coarse_mult, loss_mult_sum
     args.seed, args.step, args.ray_base = seed, step_idx, ray_base
     args.lindisp, args.ray_shape = int(lindisp), int(ray_shape)
+    args.density_bias, args.rgb_padding = float(density_bias), float(rgb_padding)  # MNcs:20,22
     args.o, args.d = inputs["o"].ctypes.data, inputs["d"].ctypes.data
     args.radius, args.near_, args.far_ = inputs["radius"].ctypes.data, inputs["near"].ctypes.data, inputs["far"].ctypes.data
     args.lossmult, args.pix = inputs["lossmult"].ctypes.data, inputs["pix"].ctypes.data

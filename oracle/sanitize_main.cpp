@@ -21,6 +21,7 @@ struct orc_step_args {
   int32_t nthreads;
   int64_t* mask_flips;
   int32_t lindisp, ray_shape;
+  float density_bias, rgb_padding;
 };
 extern "C" {
 int64_t orc_param_count(const orc_spec* s);
@@ -79,7 +80,7 @@ static void run_step(const orc_spec& sp, int n, int S0, int S1, bool masked, boo
   int64_t flips[2] = {0, 0};  // per level
   orc_step_args a{n, 2, S, 1, 1, 0.01f, 0.1f, msum, 42, 3, 5, o.data(), d.data(), r.data(), nr.data(), fr.data(),
                   lm.data(), pix.data(), nullptr, nullptr, t_out, w_out, C_out, s_out, rgb_out, ds_out, dr_out,
-                  G.data(), &loss, 1, flips, lindisp, ray_shape};
+                  G.data(), &loss, 1, flips, lindisp, ray_shape, -1.0f, 0.001f};
   if (f64) orc_step_f64(&sp, params.data(), &a);
   else orc_step_f32(&sp, params.data(), &a);
   check(finite(G) && finite(C1) && finite(ds1) && finite(dr0) && std::isfinite((double)loss), "step outputs finite");

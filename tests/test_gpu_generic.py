@@ -47,13 +47,13 @@ def _run(model, r, dev):
                                      msum)
 
 
-def _check(gpu, oracle, spec, kind, n, samples, lindisp=0, ray_shape=0, nthreads=16, lossmult=None):
+def _check(gpu, oracle, spec, kind, n, samples, lindisp=0, ray_shape=0, nthreads=16, lossmult=None, heads=None):
     import torch
     import nof
     from nof import synth
 
     seed, step, ray_base = 0x77, 2, 40
-    opts = dict(lindisp=lindisp, ray_shape=ray_shape)
+    opts = dict(lindisp=lindisp, ray_shape=ray_shape, **(heads or {}))
     model = nof.AcceleratedMipNeRF(seed=seed, max_rays=n, num_samples=samples, num_levels=len(samples), precision=0,
                                    **opts, **_cfg(spec))
     model.set_rng(seed, step, ray_base)
@@ -112,8 +112,10 @@ def test_generic_step_parity(gpu, oracle, name):
 
 
 def test_generic_step_parity_llff_options(gpu, oracle):
-    """NDC forward-facing rays, LinDisp sampling and cylinders through the any-shape path."""
-    _check(gpu, oracle, SPECS["odd_5x96_3x40"], "llff", 4, (64, 64), lindisp=1, ray_shape=1)
+    """NDC forward-facing rays, LinDisp sampling, cylinders and non-default heads (DensityBias / RgbPadding,
+    MipNerfModel.cs:20,22) through the any-shape path."""
+    _check(gpu, oracle, SPECS["odd_5x96_3x40"], "llff", 4, (64, 64), lindisp=1, ray_shape=1,
+           heads=dict(density_bias=0.25, rgb_padding=0.01))
 
 
 def test_generic_single_and_three_levels(gpu, oracle):

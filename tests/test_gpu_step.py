@@ -51,13 +51,19 @@ def test_step_parity_ray_options(gpu, oracle, lindisp, ray_shape, precision):
     _check_step(gpu, oracle, "blender", 8, (64, 128), precision, lindisp=lindisp, ray_shape=ray_shape)
 
 
-def _check_step(gpu, oracle, kind, n, samples, precision, lindisp=0, ray_shape=0):
+# MipNerfModel.DensityBias / RgbPadding (MipNerfModel.cs:20,22) away from their defaults, every precision mode
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_step_parity_head_options(gpu, oracle, precision):
+    _check_step(gpu, oracle, "blender", 8, (64, 128), precision, heads=dict(density_bias=0.5, rgb_padding=0.02))
+
+
+def _check_step(gpu, oracle, kind, n, samples, precision, lindisp=0, ray_shape=0, heads=None):
     import torch
     import nof
     from nof import synth
 
     seed, step, ray_base = 0x1234, 3, 500
-    opts = dict(lindisp=lindisp, ray_shape=ray_shape)
+    opts = dict(lindisp=lindisp, ray_shape=ray_shape, **(heads or {}))
     model = nof.AcceleratedMipNeRF(seed=seed, max_rays=n, num_samples=samples, precision=precision, **opts)
     model.set_rng(seed, step, ray_base)
     r = synth.blender_rays(n, seed=11) if kind == "blender" else synth.llff_rays(n, seed=11)

@@ -212,3 +212,21 @@ def test_ray_options_match_independent_restatement(oracle, lindisp, ray_shape):
     assert abs(got["loss"] - ref["loss"]) <= 1e-9 * abs(ref["loss"])
     e = np.linalg.norm(got["grads"] - ref["grads"]) / np.linalg.norm(ref["grads"])
     assert e < 1e-9, f"gradients rel L2 {e:.3g}"
+
+
+@pytest.mark.parametrize("density_bias,rgb_padding", [(-1.0, 0.001), (0.5, 0.02), (-3.0, 0.0)])
+def test_head_options_match_independent_restatement(oracle, density_bias, rgb_padding):
+    """MipNerfModel.DensityBias / RgbPadding (MipNerfModel.cs:20,22; the heads MNcs:19-28,151-152,184-189)
+    as settable step options: the oracle's fp64 step within 1e-9 of the torch-autograd restatement."""
+    from nof import synth
+
+    spec = oracle.Spec(D=4, W=32, skip=2)
+    r = synth.blender_rays(3, seed=5)
+    P = oracle.glorot_init(spec, 9)
+    ref = TR.step(P, r, samples=(16, 16), seed=0x77, step_idx=2, ray_base=40, net=TR.Net(D=4, W=32, skip=2),
+                  density_bias=density_bias, rgb_padding=rgb_padding)
+    got = oracle.step(spec, P, r, samples=(16, 16), seed=0x77, step_idx=2, ray_base=40, nthreads=1,
+                      density_bias=density_bias, rgb_padding=rgb_padding)
+    assert abs(got["loss"] - ref["loss"]) <= 1e-9 * abs(ref["loss"])
+    e = np.linalg.norm(got["grads"] - ref["grads"]) / np.linalg.norm(ref["grads"])
+    assert e < 1e-9, f"gradients rel L2 {e:.3g}"

@@ -184,7 +184,7 @@ def render(sigma, rgb, t, d, white=True):
 
 
 def step(P_np, rays, samples=(128, 128), seed=0, step_idx=0, ray_base=0, padding=0.01, coarse_mult=0.1,
-         white=True, net=None, t_override=None, lindisp=False, cylinder=False):
+         white=True, net=None, t_override=None, lindisp=False, cylinder=False, density_bias=-1.0, rgb_padding=0.001):
     """Full two-level step; returns dict with t, w, C per level, loss, grads (fp64 autograd)."""
     net = net or Net()
     n = rays["o"].shape[0]
@@ -210,8 +210,10 @@ def step(P_np, rays, samples=(128, 128), seed=0, step_idx=0, ray_base=0, padding
         mean, cov = cast(t, o, d, rad, cylinder)
         enc = torch.from_numpy(ipe(mean, cov))
         zs, zc = net.forward(P, enc, dirv[:, None, :].expand(n, S, dirv.shape[-1]))
-        sigma = torch.nn.functional.softplus(zs - 1.0, beta=1, threshold=20)
-        rgb = torch.sigmoid(zc) * float(np.float32(1.002)) - float(np.float32(0.001))
+        # MipNerfModel.DensityBias / RgbPadding (MNcs:20-22), the scale (1 + 2 pad) formed in fp32 as in C#
+        pad = np.float32(rgb_padding)
+        sigma = torch.nn.functional.softplus(zs + float(np.float32(density_bias)), beta=1, threshold=20)
+        rgb = torch.sigmoid(zc) * float(np.float32(1) + np.float32(2) * pad) - float(pad)
         C, w = render(sigma, rgb, t, d, white)
         lam = float(np.float32(coarse_mult)) if lv < NL - 1 else 1.0
         loss = loss + lam * (lm[:, None] * (C - pix) ** 2).sum() / msum

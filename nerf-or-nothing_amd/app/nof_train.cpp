@@ -59,6 +59,9 @@ struct Args {
   // the network (MLP.cs:64-86; 0 = the reference default) and samples per level (helpers.h:17)
   int net_depth = 0, net_width = 0, net_depth_condition = 0, net_width_condition = 0;
   std::vector<int> samples;
+  // MipNerfModel options (MipNerfModel.cs:14-15,20,22): LinDisp, RayShape, DensityBias, RgbPadding
+  bool lindisp = false, cylinder = false;
+  float density_bias = -1.0f, rgb_padding = 0.001f;
   // Config (TrainState.cs:54-58)
   float lr_init = 5e-4f, lr_final = 5e-6f, lr_delay_mult = 0.01f;
   int max_steps = 1000000, lr_delay_steps = 2500;
@@ -72,7 +75,8 @@ struct Args {
                "                 [--dump-params FILE] [--max-resident RECORDS]\n"
                "                 [--net-depth D] [--net-width W] [--net-depth-condition DC] [--net-width-condition WC]\n"
                "                 [--samples S0,S1[,...]]  (e.g. BASELINE configs[0]: --net-depth 4 --net-width 128 "
-               "--samples 64,64)\n");
+               "--samples 64,64)\n"
+               "                 [--lindisp] [--cylinder] [--density-bias B] [--rgb-padding P]\n");
   std::exit(code);
 }
 
@@ -100,6 +104,10 @@ Args parse(int argc, char** argv) {
     else if (k == "--attach") a.attach = true;
     else if (k == "--micro-batch") a.micro = std::atoi(val());
     else if (k == "--max-resident") a.max_resident = std::atoll(val());
+    else if (k == "--lindisp") a.lindisp = true;
+    else if (k == "--cylinder") a.cylinder = true;
+    else if (k == "--density-bias") a.density_bias = std::strtof(val(), nullptr);
+    else if (k == "--rgb-padding") a.rgb_padding = std::strtof(val(), nullptr);
     else if (k == "--net-depth") a.net_depth = std::atoi(val());
     else if (k == "--net-width") a.net_width = std::atoi(val());
     else if (k == "--net-depth-condition") a.net_depth_condition = std::atoi(val());
@@ -231,6 +239,10 @@ int main(int argc, char** argv) {
     R.cfg.max_rays = micro;
     R.cfg.seed = a.seed;
     R.cfg.precision = a.precision;
+    R.cfg.lindisp = a.lindisp ? 1 : 0;
+    R.cfg.ray_shape = a.cylinder ? NOF_RAY_CYLINDRICAL : NOF_RAY_CONICAL;
+    R.cfg.density_bias = a.density_bias;
+    R.cfg.rgb_padding = a.rgb_padding;
     if (a.net_depth) R.cfg.net_depth = a.net_depth;  // other shapes: the any-shape fp32 path
     if (a.net_width) R.cfg.net_width = a.net_width;
     if (a.net_depth_condition) R.cfg.net_depth_condition = a.net_depth_condition;

@@ -151,11 +151,18 @@ def main(argv=None):
     ap.add_argument("--net-depth-condition", type=int)
     ap.add_argument("--net-width-condition", type=int)
     ap.add_argument("--samples", type=int, nargs="+")
+    # MipNerfModel options (MipNerfModel.cs:14-15,20,22)
+    ap.add_argument("--lindisp", action="store_true")
+    ap.add_argument("--cylinder", action="store_true")
+    ap.add_argument("--density-bias", type=float, default=-1.0)
+    ap.add_argument("--rgb-padding", type=float, default=0.001)
     a = ap.parse_args(argv)
     net = {k: getattr(a, k) for k in ("net_depth", "net_width", "net_depth_condition", "net_width_condition")
            if getattr(a, k) is not None}
     if a.samples:
         net["num_samples"] = tuple(a.samples)
+    net.update(lindisp=int(a.lindisp), ray_shape=int(a.cylinder), density_bias=a.density_bias,
+               rgb_padding=a.rgb_padding)
     ds = (api.RayDataset(a.records, device=a.device) if a.records else
           api.RayDataset(records=synth.pack_records(synth.blender_rays(a.synthetic, seed=1)), device=a.device))
     tr = Trainer(ds, batch_size=a.batch, device=a.device, print_every=a.print_every, save_every=a.save_every,

@@ -281,7 +281,8 @@ def test_generic_native_and_python_drivers(gpu, tmp_path):
     synth.pack_records(synth.blender_rays(4096, seed=4)).tofile(path)
     dump = str(tmp_path / "params.bin")
     cmd = [exe, "--records", path, "--batch", "512", "--steps", "4", "--print-every", "2", "--seed", "77",
-           "--net-depth", "4", "--net-width", "128", "--samples", "64,64", "--dump-params", dump]
+           "--net-depth", "4", "--net-width", "128", "--samples", "64,64", "--dump-params", dump,
+           "--lindisp", "--cylinder", "--density-bias", "-0.5", "--rgb-padding", "0.002"]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stderr[-2000:]
     P = np.fromfile(dump, np.float32)
@@ -290,7 +291,8 @@ def test_generic_native_and_python_drivers(gpu, tmp_path):
     assert P.size == expect and np.all(np.isfinite(P))
     env = dict(os.environ, PYTHONPATH=os.path.join(root, "nerf-or-nothing_amd"))
     q = subprocess.run([sys.executable, "-m", "nof.train", "--records", path, "--batch", "512", "--steps", "4",
-                        "--print-every", "2", "--net-depth", "4", "--net-width", "128", "--samples", "64", "64"],
+                        "--print-every", "2", "--net-depth", "4", "--net-width", "128", "--samples", "64", "64",
+                        "--lindisp", "--cylinder", "--density-bias", "-0.5", "--rgb-padding", "0.002"],
                        capture_output=True, text=True, timeout=300, env=env)
     assert q.returncode == 0, q.stderr[-2000:]
     assert "rays/s" in q.stdout

@@ -85,7 +85,8 @@ __device__ __forceinline__ void g_store(float (*dst)[T + 4], const GPlan<T>& pl,
 
 // tile 64 (i) x TN (j), TN = 64 or 128; 4 waves in a 2 x 2 grid of 32 x TN/2 wave tiles.  Launch bounds
 // (256, 2): at least two waves per SIMD, so the accumulators live in VGPRs, not AGPRs (no accvgpr copies;
-// measured configs[0] step 6.52 -> 6.41 ms; k-steps of 32 instead of 16: 7.42 ms)
+// measured configs[0] step 6.52 -> 6.41 ms; k-steps of 32 instead of 16: 7.42 ms, and 9.59 ms against
+// 6.32 ms once the loads run two k-steps ahead: 256 VGPRs, so the occupancy falls to two waves per SIMD)
 template <bool KDIV, int TN>
 __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
   constexpr int NQ = TN / 32;  // 16-wide MFMA tiles per wave along j

@@ -22,44 +22,67 @@ namespace nof {
 
 constexpr int kGT = 64;   // tile edge
 constexpr int kGK = 16;   // k-step
+constexpr int kGS = 24;   // LDS row stride of a [row][k] tile (floats): conflict-free 16-byte operand reads
 constexpr int kGThreads = 256;
 
 // Per-thread load plan of one operand tile (T rows x 16 k per k-step, E = T / 16 elements per thread).
 // Threads run along the source's unit-stride index (coalesced): k when kfast (sk == 1), else the row
-// index.  A thread's rows are the same at every k-step, so the row offsets (with their per-ray divisions)
-// are computed once; each k-step then issues its E loads unconditionally (an element outside the operand
-// reads the source's first element and is zeroed at the LDS store), so they are in flight together and
-// the next step's loads overlap this step's MFMAs.
+// index — then a thread holds 4 consecutive k of one row (one 16-byte LDS store per 4 elements).  A
+// thread's rows and k-within-step are the same at every k-step, so its element pointers at k-step 0
+// (with the per-ray row divisions) are computed once; a k-step whose 16 k lie inside one source and
+// inside the chunk (every step of a plain layer) then moves them by one wave-uniform offset, k0 sk: one
+// 64-bit add per element, no masks (a row outside the operand re-reads row 0 and feeds only outputs that
+// are never stored).  Other steps (a source boundary or the chunk's tail inside the step, per-element k
+// divisions) compute each element's address and mask it at the LDS store.  Either way the E loads of a
+// step are issued unconditionally, so they are in flight together and overlap the previous step's MFMAs.
 template <int T>
 struct GPlan {
   static constexpr int E = T * kGK / kGThreads;
-  const float* b1[E];  // source-1 / source-2 row bases of the thread's elements
+  const float* b1[E];  // source-1 / source-2 element pointers at k = 0 (row base + kl sk)
   const float* b2[E];
   int r[E], kl[E];     // tile row, k within the step
   bool ok[E];          // row inside the operand
+  bool kfast;
 };
 
 template <int T>
-__device__ __forceinline__ void g_plan(GPlan<T>& pl, const GemmSrc& s1, const GemmSrc& s2, int rows, int r0, int tid) {
+__device__ __forceinline__ void g_plan(GPlan<T>& pl, const GemmSrc& s1, const GemmSrc& s2, int rows, int r0, int tid,
+                                       bool kdiv) {
+  static_assert(GPlan<T>::E % 4 == 0, "row-fast plans store 4 k per thread");
   const bool kfast = s1.sk == 1;
+  pl.kfast = kfast;
 #pragma unroll
   for (int e = 0; e < GPlan<T>::E; ++e) {
     const int q = e * kGThreads + tid;
-    pl.r[e] = kfast ? q / kGK : q % T;
-    pl.kl[e] = kfast ? q % kGK : q / T;
+    pl.r[e] = kfast ? q / kGK : tid % T;
+    pl.kl[e] = kfast ? q % kGK : (tid / T) * GPlan<T>::E + e;
     const int i = r0 + pl.r[e];
     pl.ok[e] = i < rows;
     const int ic = pl.ok[e] ? i : 0;
-    pl.b1[e] = s1.p + (int64_t)(ic / s1.idiv) * s1.si;
-    pl.b2[e] = s2.p ? s2.p + (int64_t)(ic / s2.idiv) * s2.si : s1.p;
+    const int64_t kl = kdiv ? 0 : pl.kl[e];  // per-element k divisions: plain row bases
+    pl.b1[e] = s1.p + (int64_t)(ic / s1.idiv) * s1.si + kl * s1.sk;
+    pl.b2[e] = s2.p ? s2.p + (int64_t)(ic / s2.idiv) * s2.si + kl * s2.sk : s1.p;
   }
 }
 
-// the loads only: the element masks are applied at the LDS store (a select here would wait for the loads)
+// the loads only: the element masks are applied at the LDS store (a select here would wait for the
+// loads).  Returns whether the step took the uniform-offset path (no masks).
 template <bool KDIV, int T>
-__device__ __forceinline__ void g_fetch(float (&v)[GPlan<T>::E], bool (&ok)[GPlan<T>::E], const GPlan<T>& pl,
+__device__ __forceinline__ bool g_fetch(float (&v)[GPlan<T>::E], bool (&ok)[GPlan<T>::E], const GPlan<T>& pl,
                                         const GemmSrc& s1, const GemmSrc& s2, int K1, int ke, int k0) {
   constexpr int E = GPlan<T>::E;
+  if (!KDIV && k0 + kGK <= ke && (k0 + kGK <= K1 || k0 >= K1)) {
+    if (k0 < K1) {  // separate loops: a select between the two pointer arrays would put them in scratch
+      const int64_t koff = (int64_t)k0 * s1.sk;
+#pragma unroll
+      for (int e = 0; e < E; ++e) v[e] = pl.b1[e][koff];
+    } else {
+      const int64_t koff = (int64_t)(k0 - K1) * s2.sk;
+#pragma unroll
+      for (int e = 0; e < E; ++e) v[e] = pl.b2[e][koff];
+    }
+    return true;
+  }
   const float* ptr[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
@@ -67,20 +90,33 @@ __device__ __forceinline__ void g_fetch(float (&v)[GPlan<T>::E], bool (&ok)[GPla
     ok[e] = pl.ok[e] && k < ke;
     const bool one = k < K1;
     const int kk = one ? k : k - K1;
-    int64_t off;
+    int64_t off;  // from the element's k = 0 pointer
     if (KDIV) off = one ? (int64_t)(kk / s1.kdiv) * s1.sk : (int64_t)(kk / s2.kdiv) * s2.sk;
-    else off = one ? (int64_t)kk * s1.sk : (int64_t)kk * s2.sk;
+    else off = one ? (int64_t)(kk - pl.kl[e]) * s1.sk : (int64_t)(kk - pl.kl[e]) * s2.sk;
     ptr[e] = ok[e] ? (one ? pl.b1[e] : pl.b2[e]) + off : s1.p;
   }
 #pragma unroll
   for (int e = 0; e < E; ++e) v[e] = *ptr[e];
+  return false;
 }
 
+// tile layout [row][k] (row stride kGS): k-fast plans store one dword per element (lanes along k, 2-way
+// bank sharing, free for ds_write_b32), row-fast plans 4 consecutive k per ds_write_b128
 template <int T>
-__device__ __forceinline__ void g_store(float (*dst)[T + 4], const GPlan<T>& pl, const float (&v)[GPlan<T>::E],
-                                        const bool (&ok)[GPlan<T>::E]) {
+__device__ __forceinline__ void g_store(float (*dst)[kGS], const GPlan<T>& pl, const float (&v)[GPlan<T>::E],
+                                        const bool (&ok)[GPlan<T>::E], bool nomask) {
+  if (pl.kfast) {
 #pragma unroll
-  for (int e = 0; e < GPlan<T>::E; ++e) dst[pl.kl[e]][pl.r[e]] = ok[e] ? v[e] : 0.0f;
+    for (int e = 0; e < GPlan<T>::E; ++e) dst[pl.r[e]][pl.kl[e]] = nomask || ok[e] ? v[e] : 0.0f;
+  } else {
+#pragma unroll
+    for (int e = 0; e < GPlan<T>::E; e += 4) {
+      f32x4 w;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) w[u] = nomask || ok[e + u] ? v[e + u] : 0.0f;
+      *reinterpret_cast<f32x4*>(&dst[pl.r[e]][pl.kl[e]]) = w;
+    }
+  }
 }
 
 // tile 64 (i) x TN (j), TN = 64 or 128; 4 waves in a 2 x 2 grid of 32 x TN/2 wave tiles.  Launch bounds
@@ -90,7 +126,10 @@ __device__ __forceinline__ void g_store(float (*dst)[T + 4], const GPlan<T>& pl,
 template <bool KDIV, int TN>
 __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
   constexpr int NQ = TN / 32;  // 16-wide MFMA tiles per wave along j
-  __shared__ float As[kGK][kGT + 4], Bs[kGK][TN + 4];
+  // k-steps of loads in flight: 3 or 4 at TN 64 (116 / 124 VGPRs, occupancy unchanged) ran the configs[0]
+  // step 6.23 -> 6.40 / 6.44 ms; 3 at TN 128 takes 175 VGPRs (two waves per SIMD)
+  constexpr int kGD = 2;
+  __shared__ __attribute__((aligned(16))) float As[kGT][kGS], Bs[TN][kGS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // output tiles linear in blockIdx.x, columns fastest (a grid's y is capped at 65535 row tiles)
   const int ntc = (a.N + TN - 1) / TN;
@@ -102,8 +141,8 @@ __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
   const int kb = blockIdx.z * a.kchunk, ke = min(K, kb + a.kchunk);
   GPlan<kGT> pa;
   GPlan<TN> pb;
-  g_plan(pa, a.A1, a.A2, a.M, i0, tid);
-  g_plan(pb, a.B1, a.B2, a.N, j0, tid);
+  g_plan(pa, a.A1, a.A2, a.M, i0, tid, KDIV);
+  g_plan(pb, a.B1, a.B2, a.N, j0, tid, KDIV);
   f32x4 acc[2][NQ];
 #pragma unroll
   for (int p = 0; p < 2; ++p)
@@ -113,45 +152,52 @@ __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
   // tile's wave 0, one row per lane, from the LDS tile, in k order
   const bool rowsum = a.rowsum && tcol == 0 && wave == 0;
   float rs = 0.0f;
-  // two k-steps of loads in flight: set 0 holds the even steps, set 1 the odd ones; a step's loads are
-  // issued two steps ahead of their LDS store (one step ahead left the global-load latency exposed: the
-  // loop is latency-bound, not MFMA- or HBM-bound)
-  float va[2][GPlan<kGT>::E], vb[2][GPlan<TN>::E];
-  bool oa[2][GPlan<kGT>::E], ob[2][GPlan<TN>::E];
-  g_fetch<KDIV>(va[0], oa[0], pa, a.A1, a.A2, a.K1, ke, kb);
-  g_fetch<KDIV>(vb[0], ob[0], pb, a.B1, a.B2, a.K1, ke, kb);
-  g_fetch<KDIV>(va[1], oa[1], pa, a.A1, a.A2, a.K1, ke, kb + kGK);
-  g_fetch<KDIV>(vb[1], ob[1], pb, a.B1, a.B2, a.K1, ke, kb + kGK);
+  // kGD k-steps of loads in flight: set s holds the steps = s mod kGD; a step's loads are issued kGD steps
+  // ahead of their LDS store (one step ahead left the global-load latency exposed: the loop is
+  // latency-bound, not MFMA- or HBM-bound)
+  float va[kGD][GPlan<kGT>::E], vb[kGD][GPlan<TN>::E];
+  bool oa[kGD][GPlan<kGT>::E], ob[kGD][GPlan<TN>::E];
+  bool fa[kGD], fb[kGD];  // the set's step took the uniform-offset path (wave-uniform)
+#pragma unroll
+  for (int s = 0; s < kGD; ++s) {
+    fa[s] = g_fetch<KDIV>(va[s], oa[s], pa, a.A1, a.A2, a.K1, ke, kb + s * kGK);
+    fb[s] = g_fetch<KDIV>(vb[s], ob[s], pb, a.B1, a.B2, a.K1, ke, kb + s * kGK);
+  }
   auto step = [&](int k0, int s) {
-    g_store(As, pa, va[s], oa[s]);
-    g_store(Bs, pb, vb[s], ob[s]);
+    g_store(As, pa, va[s], oa[s], fa[s]);
+    g_store(Bs, pb, vb[s], ob[s], fb[s]);
     __syncthreads();
-    if (k0 + 2 * kGK < ke) {
-      g_fetch<KDIV>(va[s], oa[s], pa, a.A1, a.A2, a.K1, ke, k0 + 2 * kGK);
-      g_fetch<KDIV>(vb[s], ob[s], pb, a.B1, a.B2, a.K1, ke, k0 + 2 * kGK);
+    if (k0 + kGD * kGK < ke) {
+      fa[s] = g_fetch<KDIV>(va[s], oa[s], pa, a.A1, a.A2, a.K1, ke, k0 + kGD * kGK);
+      fb[s] = g_fetch<KDIV>(vb[s], ob[s], pb, a.B1, a.B2, a.K1, ke, k0 + kGD * kGK);
     }
     if (rowsum)
 #pragma unroll
-      for (int k = 0; k < kGK; ++k) rs += As[k][lane];
+      for (int u = 0; u < kGK / 4; ++u) {
+        const f32x4 w = *reinterpret_cast<const f32x4*>(&As[lane][4 * u]);
+        rs += w[0]; rs += w[1]; rs += w[2]; rs += w[3];
+      }
+    // lane group g = lane / 16 reads k = 4g .. 4g + 3 of its row as one 16-byte LDS read; MFMA kk takes
+    // k = 4g + kk, so within a step the products are summed in the order k = 0, 4, 8, 12, 1, 5, ...
+    // (the same order for every element and every run)
+    f32x4 av[2], bv[NQ];
 #pragma unroll
-    for (int kk = 0; kk < kGK / 4; ++kk) {
-      const int k = 4 * kk + (lane >> 4);
-      float av[2], bv[NQ];
+    for (int p = 0; p < 2; ++p) av[p] = *reinterpret_cast<const f32x4*>(&As[wi + 16 * p + (lane & 15)][4 * (lane >> 4)]);
 #pragma unroll
-      for (int p = 0; p < 2; ++p) av[p] = As[k][wi + 16 * p + (lane & 15)];
+    for (int q = 0; q < NQ; ++q) bv[q] = *reinterpret_cast<const f32x4*>(&Bs[wj + 16 * q + (lane & 15)][4 * (lane >> 4)]);
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) bv[q] = Bs[k][wj + 16 * q + (lane & 15)];
+    for (int kk = 0; kk < kGK / 4; ++kk)
 #pragma unroll
       for (int p = 0; p < 2; ++p)
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[p], bv[q], acc[p][q], 0, 0, 0);
-    }
+        for (int q = 0; q < NQ; ++q)
+          acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[p][kk], bv[q][kk], acc[p][q], 0, 0, 0);
     __syncthreads();
   };
-  for (int k0 = kb; k0 < ke; k0 += 2 * kGK) {
-    step(k0, 0);
-    if (k0 + kGK < ke) step(k0 + kGK, 1);
-  }
+  for (int k0 = kb; k0 < ke; k0 += kGD * kGK)
+#pragma unroll
+    for (int s = 0; s < kGD; ++s)
+      if (k0 + s * kGK < ke) step(k0 + s * kGK, s);
   if (rowsum && i0 + lane < a.M) a.rowsum[(int64_t)blockIdx.z * a.M + i0 + lane] = rs;
   float* C = a.C + (int64_t)blockIdx.z * a.slab_stride;
 #pragma unroll

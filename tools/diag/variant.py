@@ -18,6 +18,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 K = "csrc/kernels/"
 
 EDITS = {
+    # any-shape GEMM: four k-steps of loads in flight for the 64 x 64 tiles
+    "g_d4": [(K + "generic.hip", "constexpr int kGD = TN == 64 ? 3 : 2;", "constexpr int kGD = TN == 64 ? 4 : 2;")],
     # any-shape GEMM (generic.hip): k-steps of 32 (half the barriers per MFMA, twice the loads in flight)
     "g_k32": [(K + "generic.hip", "constexpr int kGK = 16;   // k-step", "constexpr int kGK = 32;   // k-step"),
               ("csrc/host/accelerated.cpp", "  a.kchunk = (a.K1 + a.K2 + 15) / 16 * 16;",

@@ -823,6 +823,7 @@ void AcceleratedMLP::gen_alloc() {
   gd0_.alloc((size_t)max_M_ * Wm);
   gd1_.alloc((size_t)max_M_ * Wm);
   gdz_.alloc((size_t)max_M_ * 4);
+  gray_.alloc((size_t)cfg_.max_rays * gWc_);
   // split-K slabs: the largest (output rows x columns) block over every level's sample count (the split
   // grows with M up to its tile-count cap, so each level's capacity bounds its launches)
   const int shapes[][2] = {{gW_, gW_}, {gW_, gP_}, {1, gW_}, {gWc_, gW_}, {gWc_, gVd_}, {gWc_, gWc_}, {3, gWc_}};
@@ -951,7 +952,9 @@ void AcceleratedMLP::gen_backward(int level, const float* color_grad, const floa
   }
   // view layer: columns [0, W) against h_{D-1}, [W, W + Vd) against the ray's view PE
   gen_wgrad(gr + woff_[D + 1], W + Vd, cur, Wc, Wc, gsrc(H(D - 1), 1, W), W, M, acc, gr + boff_[D + 1]);
-  gen_wgrad(gr + woff_[D + 1] + W, W + Vd, cur, Wc, Wc, gsrc(G.ed, 1, Vd, 1, S), Vd, M, acc);
+  // (the view PE is per ray: dW_pe = sum over rays of (sum over the ray's samples of dZ) PE(ray))
+  NOF_HIP(nof::launch_ray_sum(M / S, S, Wc, cur, Wc, gray_.p, st_));
+  gen_wgrad(gr + woff_[D + 1] + W, W + Vd, gray_.p, Wc, Wc, gsrc(G.ed, 1, Vd), Vd, M / S, acc);
   // density head
   gen_wgrad(gr + woff_[D], W, dz, 4, 1, gsrc(H(D - 1), 1, W), W, M, acc, gr + boff_[D]);
   {  // dh_{D-1} = dZ_view W_view[:, :W] + dz_density w_D (MLPcs:148-153, D11), masked

@@ -214,6 +214,7 @@ class AcceleratedMLP {
   };
   std::vector<GenLevel> gl_;
   DevBuf<float> gd0_, gd1_, gdz_, gslab_;  // dZ ping-pong [M][max(W, Wc)], heads dz [M][4], split-K partials
+  DevBuf<float> gray_;                    // per-ray sums of the view layer's dZ [rays][Wc]
   void gen_alloc();
   void gen_forward(int level, const float* enc_pos, const float* enc_dir);
   void gen_backward(int level, const float* color_grad, const float* density_grad, int accumulate);

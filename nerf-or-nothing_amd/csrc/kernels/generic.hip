@@ -45,7 +45,7 @@ struct GPlan {
   bool kfast;
 };
 
-template <int T>
+template <bool TWO, int T>  // TWO: a second source along k (K2 > 0)
 __device__ __forceinline__ void g_plan(GPlan<T>& pl, const GemmSrc& s1, const GemmSrc& s2, int rows, int r0, int tid,
                                        bool kdiv) {
   static_assert(GPlan<T>::E % 4 == 0, "row-fast plans store 4 k per thread");
@@ -60,19 +60,23 @@ __device__ __forceinline__ void g_plan(GPlan<T>& pl, const GemmSrc& s1, const Ge
     pl.ok[e] = i < rows;
     const int ic = pl.ok[e] ? i : 0;
     const int64_t kl = kdiv ? 0 : pl.kl[e];  // per-element k divisions: plain row bases
-    pl.b1[e] = s1.p + (int64_t)(ic / s1.idiv) * s1.si + kl * s1.sk;
-    pl.b2[e] = s2.p ? s2.p + (int64_t)(ic / s2.idiv) * s2.si + kl * s2.sk : s1.p;
+    const int i1 = s1.idiv == 1 ? ic : ic / s1.idiv;  // wave-uniform test: no integer division for plain rows
+    pl.b1[e] = s1.p + (int64_t)i1 * s1.si + kl * s1.sk;
+    if (TWO) {
+      const int i2 = s2.idiv == 1 ? ic : ic / s2.idiv;
+      pl.b2[e] = s2.p + (int64_t)i2 * s2.si + kl * s2.sk;
+    }
   }
 }
 
 // the loads only: the element masks are applied at the LDS store (a select here would wait for the
 // loads).  Returns whether the step took the uniform-offset path (no masks).
-template <bool KDIV, int T>
+template <bool KDIV, bool TWO, int T>
 __device__ __forceinline__ bool g_fetch(float (&v)[GPlan<T>::E], bool (&ok)[GPlan<T>::E], const GPlan<T>& pl,
                                         const GemmSrc& s1, const GemmSrc& s2, int K1, int ke, int k0) {
   constexpr int E = GPlan<T>::E;
   if (!KDIV && k0 + kGK <= ke && (k0 + kGK <= K1 || k0 >= K1)) {
-    if (k0 < K1) {  // separate loops: a select between the two pointer arrays would put them in scratch
+    if (!TWO || k0 < K1) {  // separate loops: a select between the two pointer arrays would put them in scratch
       const int64_t koff = (int64_t)k0 * s1.sk;
 #pragma unroll
       for (int e = 0; e < E; ++e) v[e] = pl.b1[e][koff];
@@ -88,12 +92,12 @@ __device__ __forceinline__ bool g_fetch(float (&v)[GPlan<T>::E], bool (&ok)[GPla
   for (int e = 0; e < E; ++e) {
     const int k = k0 + pl.kl[e];
     ok[e] = pl.ok[e] && k < ke;
-    const bool one = k < K1;
+    const bool one = !TWO || k < K1;
     const int kk = one ? k : k - K1;
     int64_t off;  // from the element's k = 0 pointer
     if (KDIV) off = one ? (int64_t)(kk / s1.kdiv) * s1.sk : (int64_t)(kk / s2.kdiv) * s2.sk;
     else off = one ? (int64_t)(kk - pl.kl[e]) * s1.sk : (int64_t)(kk - pl.kl[e]) * s2.sk;
-    ptr[e] = ok[e] ? (one ? pl.b1[e] : pl.b2[e]) + off : s1.p;
+    ptr[e] = ok[e] ? (TWO && !one ? pl.b2[e] : pl.b1[e]) + off : s1.p;
   }
 #pragma unroll
   for (int e = 0; e < E; ++e) v[e] = *ptr[e];
@@ -123,7 +127,7 @@ __device__ __forceinline__ void g_store(float (*dst)[kGS], const GPlan<T>& pl, c
 // (256, 2): at least two waves per SIMD, so the accumulators live in VGPRs, not AGPRs (no accvgpr copies;
 // measured configs[0] step 6.52 -> 6.41 ms; k-steps of 32 instead of 16: 7.42 ms, and 9.59 ms against
 // 6.32 ms once the loads run two k-steps ahead: 256 VGPRs, so the occupancy falls to two waves per SIMD)
-template <bool KDIV, int TN>
+template <bool KDIV, int TN, bool TWO>
 __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
   constexpr int NQ = TN / 32;  // 16-wide MFMA tiles per wave along j
   // k-steps of loads in flight: 3 or 4 at TN 64 (116 / 124 VGPRs, occupancy unchanged) ran the configs[0]
@@ -141,8 +145,8 @@ __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
   const int kb = blockIdx.z * a.kchunk, ke = min(K, kb + a.kchunk);
   GPlan<kGT> pa;
   GPlan<TN> pb;
-  g_plan(pa, a.A1, a.A2, a.M, i0, tid, KDIV);
-  g_plan(pb, a.B1, a.B2, a.N, j0, tid, KDIV);
+  g_plan<TWO>(pa, a.A1, a.A2, a.M, i0, tid, KDIV);
+  g_plan<TWO>(pb, a.B1, a.B2, a.N, j0, tid, KDIV);
   f32x4 acc[2][NQ];
 #pragma unroll
   for (int p = 0; p < 2; ++p)
@@ -160,16 +164,16 @@ __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
   bool fa[kGD], fb[kGD];  // the set's step took the uniform-offset path (wave-uniform)
 #pragma unroll
   for (int s = 0; s < kGD; ++s) {
-    fa[s] = g_fetch<KDIV>(va[s], oa[s], pa, a.A1, a.A2, a.K1, ke, kb + s * kGK);
-    fb[s] = g_fetch<KDIV>(vb[s], ob[s], pb, a.B1, a.B2, a.K1, ke, kb + s * kGK);
+    fa[s] = g_fetch<KDIV, TWO>(va[s], oa[s], pa, a.A1, a.A2, a.K1, ke, kb + s * kGK);
+    fb[s] = g_fetch<KDIV, TWO>(vb[s], ob[s], pb, a.B1, a.B2, a.K1, ke, kb + s * kGK);
   }
   auto step = [&](int k0, int s) {
     g_store(As, pa, va[s], oa[s], fa[s]);
     g_store(Bs, pb, vb[s], ob[s], fb[s]);
     __syncthreads();
     if (k0 + kGD * kGK < ke) {
-      fa[s] = g_fetch<KDIV>(va[s], oa[s], pa, a.A1, a.A2, a.K1, ke, k0 + kGD * kGK);
-      fb[s] = g_fetch<KDIV>(vb[s], ob[s], pb, a.B1, a.B2, a.K1, ke, k0 + kGD * kGK);
+      fa[s] = g_fetch<KDIV, TWO>(va[s], oa[s], pa, a.A1, a.A2, a.K1, ke, k0 + kGD * kGK);
+      fb[s] = g_fetch<KDIV, TWO>(vb[s], ob[s], pb, a.B1, a.B2, a.K1, ke, k0 + kGD * kGK);
     }
     if (rowsum)
 #pragma unroll
@@ -200,20 +204,29 @@ __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
       if (k0 + s * kGK < ke) step(k0 + s * kGK, s);
   if (rowsum && i0 + lane < a.M) a.rowsum[(int64_t)blockIdx.z * a.M + i0 + lane] = rs;
   float* C = a.C + (int64_t)blockIdx.z * a.slab_stride;
+  // lane rows i = ib + 16 p + r, columns j = jb + 16 q: one 64-bit row offset per lane, wave-uniform steps
+  const int ib = i0 + wi + 4 * (lane >> 4), jb = j0 + wj + (lane & 15);
+  const int64_t crow = (int64_t)ib * a.ci, grow = (int64_t)ib * a.gi;
+  float bj[NQ];
 #pragma unroll
-  for (int p = 0; p < 2; ++p)
+  for (int q = 0; q < NQ; ++q) bj[q] = a.bias && jb + 16 * q < a.N ? a.bias[jb + 16 * q] : 0.0f;
 #pragma unroll
-    for (int q = 0; q < NQ; ++q)
+  for (int q = 0; q < NQ; ++q) {
+    const int j = jb + 16 * q;
+    if (j >= a.N) continue;
+    const int64_t cj = (int64_t)j * a.cj, gj = (int64_t)j * a.gj;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int i = i0 + wi + 16 * p + 4 * (lane >> 4) + r, j = j0 + wj + 16 * q + (lane & 15);
-        if (i >= a.M || j >= a.N) continue;
+        if (ib + 16 * p + r >= a.M) continue;
         float v = acc[p][q][r];
-        if (a.bias) v += a.bias[j];
+        if (a.bias) v += bj[q];
         if (a.relu) v = fmaxf(v, 0.0f);
-        if (a.G && !(a.G[(int64_t)i * a.gi + (int64_t)j * a.gj] > 0.0f)) v = 0.0f;
-        C[(int64_t)i * a.ci + (int64_t)j * a.cj] = v;
+        if (a.G && !(a.G[grow + (int64_t)(16 * p + r) * a.gi + gj] > 0.0f)) v = 0.0f;
+        C[crow + (int64_t)(16 * p + r) * a.ci + cj] = v;
       }
+  }
 }
 
 // dst[r ld + c] (+)= sum over slabs z = 0 .. nz - 1 of slabs[z][r pitch + c] (z order within each of 4
@@ -242,6 +255,21 @@ __global__ __launch_bounds__(256) void k_slab_sum(int rows, int cols, int pitch,
     float* o = dst + r * ld + (e - r * cols);
     *o = accumulate ? *o + tot : tot;
   }
+}
+
+// out[r][c] = sum over s = 0 .. S - 1 (in s order) of in[(r S + s) ld + c].  The view PE is constant over a
+// ray's samples, so the view layer's PE weight gradient sum_m dZ[m][o] PE[ray(m)][j] is a GEMM over rays
+// of these per-ray sums (S times fewer k than over samples).
+__global__ __launch_bounds__(256) void k_ray_sum(int R, int S, int cols, const float* __restrict__ in, int64_t ld,
+                                                 float* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)R * cols) return;
+  const int r = (int)(e / cols), c = (int)(e - (int64_t)r * cols);
+  const float* p = in + (int64_t)r * S * ld + c;
+  float acc = 0.0f;
+#pragma unroll 8
+  for (int s = 0; s < S; ++s) acc += p[(int64_t)s * ld];
+  out[e] = acc;
 }
 
 // IPE at degrees [min_deg, min_deg + P / 6) (MH:429-449: feature 6f + j, then 6f + 3 + j with the
@@ -304,10 +332,19 @@ hipError_t launch_gemm(const GemmArgs& a, int ksplit, hipStream_t st) {
   const int64_t tiles = (int64_t)((a.N + TN - 1) / TN) * ((a.M + kGT - 1) / kGT);
   if (tiles > 0x7fffffff || ksplit > 65535) return hipErrorInvalidValue;
   const dim3 grid((unsigned)tiles, 1, ksplit);
-  if (kdiv && wide) hipLaunchKernelGGL((k_gemm<true, 128>), grid, dim3(kGThreads), 0, st, a);
-  else if (kdiv) hipLaunchKernelGGL((k_gemm<true, 64>), grid, dim3(kGThreads), 0, st, a);
-  else if (wide) hipLaunchKernelGGL((k_gemm<false, 128>), grid, dim3(kGThreads), 0, st, a);
-  else hipLaunchKernelGGL((k_gemm<false, 64>), grid, dim3(kGThreads), 0, st, a);
+  const bool two = a.K2 > 0;
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(kGThreads), 0, st, a); };
+  if (two) {
+    if (kdiv && wide) go(k_gemm<true, 128, true>);
+    else if (kdiv) go(k_gemm<true, 64, true>);
+    else if (wide) go(k_gemm<false, 128, true>);
+    else go(k_gemm<false, 64, true>);
+  } else {
+    if (kdiv && wide) go(k_gemm<true, 128, false>);
+    else if (kdiv) go(k_gemm<true, 64, false>);
+    else if (wide) go(k_gemm<false, 128, false>);
+    else go(k_gemm<false, 64, false>);
+  }
   return hipGetLastError();
 }
 hipError_t launch_slab_sum(int rows, int cols, int pitch, int nz, const float* slabs, int64_t stride, float* dst,
@@ -317,6 +354,13 @@ hipError_t launch_slab_sum(int rows, int cols, int pitch, int nz, const float* s
   if (nz < 1 || pitch < cols || stride < (int64_t)(rows - 1) * pitch + cols || ld < cols) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_slab_sum, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, rows, cols, pitch, nz, slabs,
                      stride, dst, ld, accumulate);
+  return hipGetLastError();
+}
+hipError_t launch_ray_sum(int R, int S, int cols, const float* in, int64_t ld, float* out, hipStream_t st) {
+  const int64_t n = (int64_t)R * cols;
+  if (n <= 0) return hipSuccess;
+  if (S < 1 || ld < cols || n > 0x7fffffffLL * 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_ray_sum, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, R, S, cols, in, ld, out);
   return hipGetLastError();
 }
 hipError_t launch_encode_g(int n, int S, const float* mean, const float* cov, const float* d, int min_deg, int P, int Vd,

@@ -184,6 +184,8 @@ hipError_t launch_gemm(const GemmArgs& a, int ksplit, hipStream_t st);
 hipError_t launch_slab_sum(int rows, int cols, int pitch, int nz, const float* slabs, int64_t stride, float* dst,
                            int64_t ld, int accumulate, hipStream_t st);
 // IPE at degrees [min_deg, min_deg + P / 6) per sample, view PE (Vd = 3 + 6 deg_view features) per ray
+// out[r][c] = sum over a ray's S sample rows of in (the per-ray operand's weight gradient over rays)
+hipError_t launch_ray_sum(int R, int S, int cols, const float* in, int64_t ld, float* out, hipStream_t st);
 hipError_t launch_encode_g(int n, int S, const float* mean, const float* cov, const float* d, int min_deg, int P,
                            int Vd, float* enc_pos, float* enc_dir, hipStream_t st);
 // z [M][4] (density, rgb pre-activations) -> sigma [M], rgb [M][3]; backward: dz [M][4]

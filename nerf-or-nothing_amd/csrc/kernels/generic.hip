@@ -11,6 +11,7 @@
 //     relu'(z) as activation > 0), or a raw split-K partial (weight gradients: k = samples);
 //   * k_slab_sum: the split-K partials summed in fixed order (deterministic, no atomics), added to or
 //     overwriting the gradient arena;
+//   * k_ray_sum: dZ summed over each ray's samples, for the per-ray view PE's weight gradient;
 //   * k_encode_g / k_heads_fwd / k_heads_bwd: the encodings at any degree range (MH:337-356, 429-449) and
 //     the heads (MNcs:19-28, 151-152, 184-189).
 // Numerics: fp32 products in k order (the MFMA's fmaf chain) — the fp32 mode's 1e-5 contract.

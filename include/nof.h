@@ -434,14 +434,22 @@ nof_status nof_stream_sync(void* stream);
  * encode_input_data AF:187-221, volumetric_rendering AF:318-344, volumetric_rendering_gradient
  * AF:362-402 (g = dL/dC given, or fused from pixels when dev_g == NULL). */
 nof_status nof_kernel_sample_stratified(int32_t n, int32_t samples, const float* nears, const float* fars,
-                                        int32_t randomized, int32_t lindisp, uint64_t seed, uint32_t step,
-                                        uint32_t level, uint32_t ray_base, float* t_out, void* stream);
+                                        int32_t randomized, uint64_t seed, uint32_t step, uint32_t level,
+                                        uint32_t ray_base, float* t_out, void* stream);
+/* ABI 2: the ray options as trailing arguments of _ex entry points (the round-4 signatures above are
+ * unchanged, so a binding built against them keeps working): lindisp 1 = SampleAlongRay's disparity branch
+ * (MipHelpers.cs:618-620); ray_shape NOF_RAY_CYLINDRICAL = CylinderToGaussian (MipHelpers.cs:403-409). */
+nof_status nof_kernel_sample_stratified_ex(int32_t n, int32_t samples, const float* nears, const float* fars,
+                                           int32_t randomized, uint64_t seed, uint32_t step, uint32_t level,
+                                           uint32_t ray_base, float* t_out, void* stream, int32_t lindisp);
 nof_status nof_kernel_sample_pdf(int32_t n, int32_t samples_in, const float* t_in, const float* weights,
                                  int32_t samples_out, float padding, int32_t randomized, uint64_t seed,
                                  uint32_t step, uint32_t level, uint32_t ray_base, float* t_out, int32_t* idx_out,
                                  void* stream);
 nof_status nof_kernel_cast(int32_t n, int32_t samples, const float* t, const float* origins, const float* dirs,
-                           const float* radii, int32_t ray_shape, float* means, float* covs, void* stream);
+                           const float* radii, float* means, float* covs, void* stream);
+nof_status nof_kernel_cast_ex(int32_t n, int32_t samples, const float* t, const float* origins, const float* dirs,
+                              const float* radii, float* means, float* covs, void* stream, int32_t ray_shape);
 nof_status nof_kernel_encode(int32_t n, int32_t samples, const float* means, const float* covs, const float* dirs,
                              float* enc_pos, float* enc_dir, void* stream);
 nof_status nof_kernel_render(int32_t n, int32_t samples, const float* density, const float* rgb, const float* t,

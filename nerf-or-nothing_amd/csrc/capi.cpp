@@ -106,7 +106,7 @@ void nof_config_default(nof_config* c) {
 size_t nof_config_size(void) { return sizeof(nof_config); }
 
 const char* nof_last_error(void) { return g_err.c_str(); }
-const char* nof_version(void) { return "nerf-or-nothing_amd 0.1 (gfx950)"; }
+const char* nof_version(void) { return "nerf-or-nothing_amd 0.2 (gfx950; C ABI 2)"; }
 
 // ---- AcceleratedMipNeRF ---------------------------------------------------------------------
 nof_status nof_mipnerf_create(const nof_config* cfg, nof_mipnerf** out) {
@@ -555,14 +555,19 @@ nof_status nof_memset(void* dst, int value, size_t bytes) { return guard([&] { N
 nof_status nof_stream_sync(void* stream) { return guard([&] { NOF_HIP(hipStreamSynchronize((hipStream_t)stream)); }); }
 
 // ---- individual kernels ---------------------------------------------------------------------
-nof_status nof_kernel_sample_stratified(int32_t n, int32_t S, const float* nears, const float* fars, int32_t rnd,
-                                        int32_t lindisp, uint64_t seed, uint32_t step, uint32_t level,
-                                        uint32_t ray_base, float* t, void* stream) {
+nof_status nof_kernel_sample_stratified_ex(int32_t n, int32_t S, const float* nears, const float* fars,
+                                           int32_t rnd, uint64_t seed, uint32_t step, uint32_t level,
+                                           uint32_t ray_base, float* t, void* stream, int32_t lindisp) {
   return guard([&] {
     ARG(n >= 0 && S > 0 && nears && fars && t && (lindisp == 0 || lindisp == 1));
     NOF_HIP(nof::launch_sample_stratified(n, S, nears, fars, rnd, seed, step, level, ray_base, t, (hipStream_t)stream,
                                           lindisp));
   });
+}
+nof_status nof_kernel_sample_stratified(int32_t n, int32_t S, const float* nears, const float* fars, int32_t rnd,
+                                        uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base, float* t,
+                                        void* stream) {
+  return nof_kernel_sample_stratified_ex(n, S, nears, fars, rnd, seed, step, level, ray_base, t, stream, 0);
 }
 nof_status nof_kernel_sample_pdf(int32_t n, int32_t S_in, const float* t_in, const float* w, int32_t S_out,
                                  float padding, int32_t rnd, uint64_t seed, uint32_t step, uint32_t level,
@@ -573,13 +578,17 @@ nof_status nof_kernel_sample_pdf(int32_t n, int32_t S_in, const float* t_in, con
                                    (hipStream_t)stream));
   });
 }
-nof_status nof_kernel_cast(int32_t n, int32_t S, const float* t, const float* o, const float* d, const float* r,
-                           int32_t ray_shape, float* mean, float* cov, void* stream) {
+nof_status nof_kernel_cast_ex(int32_t n, int32_t S, const float* t, const float* o, const float* d, const float* r,
+                              float* mean, float* cov, void* stream, int32_t ray_shape) {
   return guard([&] {
     ARG(n >= 0 && S > 0 && t && o && d && r && mean && cov &&
         (ray_shape == NOF_RAY_CONICAL || ray_shape == NOF_RAY_CYLINDRICAL));
     NOF_HIP(nof::launch_cast(n, S, t, o, d, r, mean, cov, (hipStream_t)stream, ray_shape));
   });
+}
+nof_status nof_kernel_cast(int32_t n, int32_t S, const float* t, const float* o, const float* d, const float* r,
+                           float* mean, float* cov, void* stream) {
+  return nof_kernel_cast_ex(n, S, t, o, d, r, mean, cov, stream, NOF_RAY_CONICAL);
 }
 nof_status nof_kernel_encode(int32_t n, int32_t S, const float* mean, const float* cov, const float* d, float* ep,
                              float* ed, void* stream) {

@@ -275,6 +275,8 @@ void AcceleratedMLP::forward_fused(int level, int n, int samples, const float* t
   NOF_REQUIRE(n > 0 && samples % kBlk == 0 && M <= lv_[level].cap, "batch exceeds the level's capacity");
   lv_[level].M = M; lv_[level].n = n; lv_[level].S = samples;
   if (generic_) {  // cast + encode, then the layer GEMMs
+    // (per-ray buffers — the view encodings, the ray sums of the view-layer gradient — hold max_rays rays)
+    NOF_REQUIRE(n <= cfg_.max_rays, "n_rays exceeds max_rays");
     GenLevel& G = gl_[level];
     tb(kTMlpFwd);
     NOF_HIP(nof::launch_cast(n, samples, t, origins, dirs, radii, G.mean.p, G.cov.p, st_, cfg_.ray_shape));
@@ -302,6 +304,7 @@ std::pair<float*, float*> AcceleratedMLP::get_output(const float* enc_pos, const
   pack_weights();
   lv_[level].M = M; lv_[level].n = n_rays; lv_[level].S = samples;
   if (generic_) {  // the encodings copied in: the backward reads them after the caller's buffers may be gone
+    NOF_REQUIRE(n_rays <= cfg_.max_rays, "n_rays exceeds max_rays");  // enc_dir / the ray sums: max_rays rays
     GenLevel& G = gl_[level];
     NOF_HIP(hipMemcpyAsync(G.enc_pos.p, enc_pos, (size_t)M * gP_ * sizeof(float), hipMemcpyDeviceToDevice, st_));
     NOF_HIP(hipMemcpyAsync(G.enc_dir.p, enc_dir, (size_t)n_rays * gVd_ * sizeof(float), hipMemcpyDeviceToDevice,
@@ -778,9 +781,9 @@ float* const* AcceleratedMLP::get_gradient_levels(const float* const* color_grad
 // mlp_backward_sample / MLPcpp:256-321), one dX GEMM (ReLU mask = the stored activation > 0) and one
 // split-K weight-gradient GEMM + ordered slab sum per layer and input block.
 // ------------------------------------------------------------------------------------------------
-static nof::GemmSrc gsrc(const float* p, int64_t si, int64_t sk, int idiv = 1, int kdiv = 1) {
+static nof::GemmSrc gsrc(const float* p, int64_t si, int64_t sk, int idiv = 1) {
   nof::GemmSrc s;
-  s.p = p; s.si = si; s.sk = sk; s.idiv = idiv; s.kdiv = kdiv;
+  s.p = p; s.si = si; s.sk = sk; s.idiv = idiv;
   return s;
 }
 
@@ -825,25 +828,31 @@ void AcceleratedMLP::gen_alloc() {
   gd1_.alloc((size_t)max_M_ * Wm);
   gdz_.alloc((size_t)max_M_ * 4);
   gray_.alloc((size_t)cfg_.max_rays * gWc_);
-  // split-K slabs: the largest (output rows x columns) block over every level's sample count (the split
-  // grows with M up to its tile-count cap, so each level's capacity bounds its launches)
-  const int shapes[][2] = {{gW_, gW_}, {gW_, gP_}, {1, gW_}, {gWc_, gW_}, {gWc_, gVd_}, {gWc_, gWc_}, {3, gWc_}};
+  // split-K slabs: the largest block any weight-gradient launch needs, from a dry run of gen_backward at
+  // every level's capacity (the split grows with M up to its tile-count cap, so the capacity bounds every
+  // call): the same call sequence as a step, so a new layer shape cannot outgrow the slab mid-step
   size_t slab = 0;
+  wg_need_ = &slab;
   for (int l = 0; l < NL; ++l) {
-    for (const auto& s : shapes) {
-      int ks, kc;
-      gen_split(s[0], s[1], lv_[l].cap, &ks, &kc);
-      slab = std::max(slab, (size_t)ks * s[0] * (s[1] + 1));  // + the bias partials
-    }
+    Level& L = lv_[l];
+    L.M = L.cap; L.n = cfg_.max_rays; L.S = cfg_.num_samples[l];
+    gen_backward(l, nullptr, nullptr, 0);
+    L.M = L.n = L.S = 0;
   }
-  gslab_.alloc(slab);
+  wg_need_ = nullptr;
+  gslab_.alloc(std::max<size_t>(slab, 1));
 }
 
 void AcceleratedMLP::gen_wgrad(float* dst, int64_t ld, const float* dz, int64_t ldz, int nout, nof::GemmSrc x,
                                int ncols, int M, int accumulate, float* bias_dst) {
   int ks, kc;
   gen_split(nout, ncols, M, &ks, &kc);
-  NOF_REQUIRE((size_t)ks * nout * (ncols + 1) <= gslab_.n, "split-K slabs too small");
+  const size_t need = (size_t)ks * nout * (ncols + 1);  // + the bias partials
+  if (wg_need_) {  // construction's dry run
+    *wg_need_ = std::max(*wg_need_, need);
+    return;
+  }
+  NOF_REQUIRE(need <= gslab_.n, "split-K slabs too small");
   nof::GemmArgs a;
   a.M = nout; a.N = ncols; a.K1 = M;
   a.A1 = gsrc(dz, 1, ldz);  // A(o, m) = dZ[m][o]
@@ -922,7 +931,8 @@ void AcceleratedMLP::gen_forward(int level, const float* ep, const float* ed) {
 void AcceleratedMLP::gen_backward(int level, const float* color_grad, const float* density_grad, int acc) {
   Level& L = lv_[level];
   GenLevel& G = gl_[level];
-  NOF_REQUIRE(G.ep && G.ed, "get_gradient before get_output for this level");
+  const bool dry = wg_need_ != nullptr;  // slab sizing (gen_alloc): only gen_wgrad's records, no launches
+  NOF_REQUIRE(dry || (G.ep && G.ed), "get_gradient before get_output for this level");
   const int M = L.M, S = L.S, D = gD_, W = gW_, Dc = gDc_, Wc = gWc_, P = gP_, Vd = gVd_, lr = D + 1 + Dc;
   const float* prm = params_.p;
   float* gr = grads_.p;
@@ -932,6 +942,7 @@ void AcceleratedMLP::gen_backward(int level, const float* color_grad, const floa
   float *cur = gd0_.p, *nxt = gd1_.p;
   // dX of layer l into C, masked by the activation `mask` > 0: C[m][j] = sum_o dZ[m][o] W_l[o][j]
   auto dx = [&](const float* dzp, int64_t ldz, int nout, int l, const float* mask, int width, float* C) {
+    if (dry) return;
     nof::GemmArgs a;
     a.M = M; a.N = width; a.K1 = nout;
     a.A1 = gsrc(dzp, ldz, 1);
@@ -940,8 +951,10 @@ void AcceleratedMLP::gen_backward(int level, const float* color_grad, const floa
     a.C = C; a.ci = width; a.cj = 1;
     gemm1(a, st_);
   };
-  tb(kTMlpBwd);
-  NOF_HIP(nof::launch_heads_bwd(M, density_grad, color_grad, G.z.p, dz, cfg_.density_bias, rgb_scale(), st_));  // MNcs:23-28,184-189
+  if (!dry) {
+    tb(kTMlpBwd);
+    NOF_HIP(nof::launch_heads_bwd(M, density_grad, color_grad, G.z.p, dz, cfg_.density_bias, rgb_scale(), st_));  // MNcs:23-28,184-189
+  }
   // rgb head: dW, db from dz[:, 1..3]; its dX into the last condition layer
   gen_wgrad(gr + woff_[lr], Wc, dz + 1, 4, 3, gsrc(Hc(Dc - 1), 1, Wc), Wc, M, acc, gr + boff_[lr]);
   dx(dz + 1, 4, 3, lr, Hc(Dc - 1), Wc, cur);
@@ -954,11 +967,11 @@ void AcceleratedMLP::gen_backward(int level, const float* color_grad, const floa
   // view layer: columns [0, W) against h_{D-1}, [W, W + Vd) against the ray's view PE
   gen_wgrad(gr + woff_[D + 1], W + Vd, cur, Wc, Wc, gsrc(H(D - 1), 1, W), W, M, acc, gr + boff_[D + 1]);
   // (the view PE is per ray: dW_pe = sum over rays of (sum over the ray's samples of dZ) PE(ray))
-  NOF_HIP(nof::launch_ray_sum(M / S, S, Wc, cur, Wc, gray_.p, st_));
+  if (!dry) NOF_HIP(nof::launch_ray_sum(M / S, S, Wc, cur, Wc, gray_.p, st_));
   gen_wgrad(gr + woff_[D + 1] + W, W + Vd, gray_.p, Wc, Wc, gsrc(G.ed, 1, Vd), Vd, M / S, acc);
   // density head
   gen_wgrad(gr + woff_[D], W, dz, 4, 1, gsrc(H(D - 1), 1, W), W, M, acc, gr + boff_[D]);
-  {  // dh_{D-1} = dZ_view W_view[:, :W] + dz_density w_D (MLPcs:148-153, D11), masked
+  if (!dry) {  // dh_{D-1} = dZ_view W_view[:, :W] + dz_density w_D (MLPcs:148-153, D11), masked
     nof::GemmArgs a;
     a.M = M; a.N = W; a.K1 = Wc; a.K2 = 1;
     a.A1 = gsrc(cur, Wc, 1);
@@ -983,7 +996,7 @@ void AcceleratedMLP::gen_backward(int level, const float* color_grad, const floa
       std::swap(cur, nxt);
     }
   }
-  te(kTMlpBwd);
+  if (!dry) te(kTMlpBwd);
 }
 
 float* const* AcceleratedMLP::gen_publish(bool buckets) {

@@ -218,6 +218,9 @@ class AcceleratedMLP {
   void gen_alloc();
   void gen_forward(int level, const float* enc_pos, const float* enc_dir);
   void gen_backward(int level, const float* color_grad, const float* density_grad, int accumulate);
+  // non-null: gen_backward launches nothing and gen_wgrad records its split-K slab need here instead (the
+  // slab is sized at construction by a dry run of the same call sequence a step makes)
+  size_t* wg_need_ = nullptr;
   // a column block of a layer's weight gradient: dst[o ld + j] (+)= sum_m dZ(m, o) X(m, j); bias_dst: the
   // layer's bias gradient sum_m dZ(m, o) too (row sums of the same A tiles)
   void gen_wgrad(float* dst, int64_t ld, const float* dz, int64_t ldz, int nout, nof::GemmSrc x, int ncols, int M,

@@ -47,8 +47,7 @@ struct GPlan {
 };
 
 template <bool TWO, int T>  // TWO: a second source along k (K2 > 0)
-__device__ __forceinline__ void g_plan(GPlan<T>& pl, const GemmSrc& s1, const GemmSrc& s2, int rows, int r0, int tid,
-                                       bool kdiv) {
+__device__ __forceinline__ void g_plan(GPlan<T>& pl, const GemmSrc& s1, const GemmSrc& s2, int rows, int r0, int tid) {
   static_assert(GPlan<T>::E % 4 == 0, "row-fast plans store 4 k per thread");
   const bool kfast = s1.sk == 1;
   pl.kfast = kfast;
@@ -60,7 +59,7 @@ __device__ __forceinline__ void g_plan(GPlan<T>& pl, const GemmSrc& s1, const Ge
     const int i = r0 + pl.r[e];
     pl.ok[e] = i < rows;
     const int ic = pl.ok[e] ? i : 0;
-    const int64_t kl = kdiv ? 0 : pl.kl[e];  // per-element k divisions: plain row bases
+    const int64_t kl = pl.kl[e];
     const int i1 = s1.idiv == 1 ? ic : ic / s1.idiv;  // wave-uniform test: no integer division for plain rows
     pl.b1[e] = s1.p + (int64_t)i1 * s1.si + kl * s1.sk;
     if (TWO) {
@@ -72,11 +71,11 @@ __device__ __forceinline__ void g_plan(GPlan<T>& pl, const GemmSrc& s1, const Ge
 
 // the loads only: the element masks are applied at the LDS store (a select here would wait for the
 // loads).  Returns whether the step took the uniform-offset path (no masks).
-template <bool KDIV, bool TWO, int T>
+template <bool TWO, int T>
 __device__ __forceinline__ bool g_fetch(float (&v)[GPlan<T>::E], bool (&ok)[GPlan<T>::E], const GPlan<T>& pl,
                                         const GemmSrc& s1, const GemmSrc& s2, int K1, int ke, int k0) {
   constexpr int E = GPlan<T>::E;
-  if (!KDIV && k0 + kGK <= ke && (k0 + kGK <= K1 || k0 >= K1)) {
+  if (k0 + kGK <= ke && (k0 + kGK <= K1 || k0 >= K1)) {
     if (!TWO || k0 < K1) {  // separate loops: a select between the two pointer arrays would put them in scratch
       const int64_t koff = (int64_t)k0 * s1.sk;
 #pragma unroll
@@ -95,9 +94,8 @@ __device__ __forceinline__ bool g_fetch(float (&v)[GPlan<T>::E], bool (&ok)[GPla
     ok[e] = pl.ok[e] && k < ke;
     const bool one = !TWO || k < K1;
     const int kk = one ? k : k - K1;
-    int64_t off;  // from the element's k = 0 pointer
-    if (KDIV) off = one ? (int64_t)(kk / s1.kdiv) * s1.sk : (int64_t)(kk / s2.kdiv) * s2.sk;
-    else off = one ? (int64_t)(kk - pl.kl[e]) * s1.sk : (int64_t)(kk - pl.kl[e]) * s2.sk;
+    // from the element's k = 0 pointer
+    const int64_t off = one ? (int64_t)(kk - pl.kl[e]) * s1.sk : (int64_t)(kk - pl.kl[e]) * s2.sk;
     ptr[e] = ok[e] ? (TWO && !one ? pl.b2[e] : pl.b1[e]) + off : s1.p;
   }
 #pragma unroll
@@ -128,7 +126,7 @@ __device__ __forceinline__ void g_store(float (*dst)[kGS], const GPlan<T>& pl, c
 // (256, 2): at least two waves per SIMD, so the accumulators live in VGPRs, not AGPRs (no accvgpr copies;
 // measured configs[0] step 6.52 -> 6.41 ms; k-steps of 32 instead of 16: 7.42 ms, and 9.59 ms against
 // 6.32 ms once the loads run two k-steps ahead: 256 VGPRs, so the occupancy falls to two waves per SIMD)
-template <bool KDIV, int TN, bool TWO>
+template <int TN, bool TWO>
 __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
   constexpr int NQ = TN / 32;  // 16-wide MFMA tiles per wave along j
   // k-steps of loads in flight: 3 or 4 at TN 64 (116 / 124 VGPRs, occupancy unchanged) ran the configs[0]
@@ -146,8 +144,8 @@ __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
   const int kb = blockIdx.z * a.kchunk, ke = min(K, kb + a.kchunk);
   GPlan<kGT> pa;
   GPlan<TN> pb;
-  g_plan<TWO>(pa, a.A1, a.A2, a.M, i0, tid, KDIV);
-  g_plan<TWO>(pb, a.B1, a.B2, a.N, j0, tid, KDIV);
+  g_plan<TWO>(pa, a.A1, a.A2, a.M, i0, tid);
+  g_plan<TWO>(pb, a.B1, a.B2, a.N, j0, tid);
   f32x4 acc[2][NQ];
 #pragma unroll
   for (int p = 0; p < 2; ++p)
@@ -165,16 +163,16 @@ __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
   bool fa[kGD], fb[kGD];  // the set's step took the uniform-offset path (wave-uniform)
 #pragma unroll
   for (int s = 0; s < kGD; ++s) {
-    fa[s] = g_fetch<KDIV, TWO>(va[s], oa[s], pa, a.A1, a.A2, a.K1, ke, kb + s * kGK);
-    fb[s] = g_fetch<KDIV, TWO>(vb[s], ob[s], pb, a.B1, a.B2, a.K1, ke, kb + s * kGK);
+    fa[s] = g_fetch<TWO>(va[s], oa[s], pa, a.A1, a.A2, a.K1, ke, kb + s * kGK);
+    fb[s] = g_fetch<TWO>(vb[s], ob[s], pb, a.B1, a.B2, a.K1, ke, kb + s * kGK);
   }
   auto step = [&](int k0, int s) {
     g_store(As, pa, va[s], oa[s], fa[s]);
     g_store(Bs, pb, vb[s], ob[s], fb[s]);
     __syncthreads();
     if (k0 + kGD * kGK < ke) {
-      fa[s] = g_fetch<KDIV, TWO>(va[s], oa[s], pa, a.A1, a.A2, a.K1, ke, k0 + kGD * kGK);
-      fb[s] = g_fetch<KDIV, TWO>(vb[s], ob[s], pb, a.B1, a.B2, a.K1, ke, k0 + kGD * kGK);
+      fa[s] = g_fetch<TWO>(va[s], oa[s], pa, a.A1, a.A2, a.K1, ke, k0 + kGD * kGK);
+      fb[s] = g_fetch<TWO>(vb[s], ob[s], pb, a.B1, a.B2, a.K1, ke, k0 + kGD * kGK);
     }
     if (rowsum)
 #pragma unroll
@@ -319,10 +317,8 @@ __global__ void k_heads_bwd(int M, const float* __restrict__ dsigma, const float
 hipError_t launch_gemm(const GemmArgs& a, int ksplit, hipStream_t st) {
   if (a.M <= 0 || a.N <= 0) return hipSuccess;
   if (ksplit < 1 || a.kchunk <= 0 || a.kchunk % kGK != 0 || !a.A1.p || !a.B1.p || (a.K2 > 0 && (!a.A2.p || !a.B2.p)) ||
-      a.A1.idiv < 1 || a.A2.idiv < 1 || a.B1.idiv < 1 || a.B2.idiv < 1 || a.A1.kdiv < 1 || a.A2.kdiv < 1 ||
-      a.B1.kdiv < 1 || a.B2.kdiv < 1)
+      a.A1.idiv < 1 || a.A2.idiv < 1 || a.B1.idiv < 1 || a.B2.idiv < 1)
     return hipErrorInvalidValue;
-  const bool kdiv = a.A1.kdiv > 1 || a.A2.kdiv > 1 || a.B1.kdiv > 1 || a.B2.kdiv > 1;
   // 64 x 128 tiles for split-K weight gradients wider than 64 (A read once for up to 128 columns; measured
   // 5 % faster there, 10 % slower on the unsplit dX GEMMs).  Measured and not kept: 128 x 128 tiles (two
   // waves per SIMD) ran the trunk dX / dW GEMMs 185 -> 260 / 158 -> 230 us (the loop is latency-bound:
@@ -336,15 +332,11 @@ hipError_t launch_gemm(const GemmArgs& a, int ksplit, hipStream_t st) {
   const bool two = a.K2 > 0;
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(kGThreads), 0, st, a); };
   if (two) {
-    if (kdiv && wide) go(k_gemm<true, 128, true>);
-    else if (kdiv) go(k_gemm<true, 64, true>);
-    else if (wide) go(k_gemm<false, 128, true>);
-    else go(k_gemm<false, 64, true>);
+    if (wide) go(k_gemm<128, true>);
+    else go(k_gemm<64, true>);
   } else {
-    if (kdiv && wide) go(k_gemm<true, 128, false>);
-    else if (kdiv) go(k_gemm<true, 64, false>);
-    else if (wide) go(k_gemm<false, 128, false>);
-    else go(k_gemm<false, 64, false>);
+    if (wide) go(k_gemm<128, false>);
+    else go(k_gemm<64, false>);
   }
   return hipGetLastError();
 }

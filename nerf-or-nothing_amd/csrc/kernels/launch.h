@@ -160,11 +160,12 @@ hipError_t launch_wgrad_reduce(const WgOut* outs, int nouts, int max_elems, cons
 // (amax != null: sums are multiplied by the inverse f16x2 delta scale, mlp_common.h)
 
 // ---- generic.hip: the any-shape fp32 MLP, one MFMA GEMM launch per layer ----------------------
-// element (i, k) of a source = p[(i / idiv) si + (k / kdiv) sk] (idiv, kdiv: 1 or a per-ray divisor)
+// element (i, k) of a source = p[(i / idiv) si + k sk] (idiv: 1 or a per-ray divisor, the view encodings
+// read per sample without a per-sample copy)
 struct GemmSrc {
   const float* p = nullptr;
   int64_t si = 0, sk = 0;
-  int idiv = 1, kdiv = 1;
+  int idiv = 1;
 };
 // C(i, j) = epilogue(sum_{k < K1 + K2} A(i, k) B(j, k)), i < M, j < N; A(i, k) = A1(i, k) for k < K1, else
 // A2(i, k - K1) (B alike).  Epilogue: + bias[j], ReLU, then 0 where !(G(i, j) > 0) — each optional.

@@ -157,9 +157,11 @@ SIGNATURES = {
     "nof_memcpy_d2d": [P, P, C.c_size_t, P],
     "nof_memset": [P, C.c_int, C.c_size_t],
     "nof_stream_sync": [P],
-    "nof_kernel_sample_stratified": [I32, I32, P, P, I32, I32, U64, U32, U32, U32, P, P],
+    "nof_kernel_sample_stratified": [I32, I32, P, P, I32, U64, U32, U32, U32, P, P],
+    "nof_kernel_sample_stratified_ex": [I32, I32, P, P, I32, U64, U32, U32, U32, P, P, I32],
     "nof_kernel_sample_pdf": [I32, I32, P, P, I32, F, I32, U64, U32, U32, U32, P, P, P],
-    "nof_kernel_cast": [I32, I32, P, P, P, P, I32, P, P, P],
+    "nof_kernel_cast": [I32, I32, P, P, P, P, P, P, P],
+    "nof_kernel_cast_ex": [I32, I32, P, P, P, P, P, P, P, I32],
     "nof_kernel_encode": [I32, I32, P, P, P, P, P, P],
     "nof_kernel_render": [I32, I32, P, P, P, P, I32, P, P, P],
     "nof_kernel_render_grad": [I32, I32, P, P, P, P, I32, P, P, P, P, F, F, P, P, P],

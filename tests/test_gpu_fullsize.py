@@ -20,7 +20,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import F16_GRAD_TOL, rel_l2
+from conftest import f16_grad_tol, rel_l2
 
 pytestmark = pytest.mark.gpu
 TOLS = {0: 1e-5, 1: 1e-5, 2: 2e-3, 3: 1e-5, 4: 2e-3}
@@ -148,8 +148,8 @@ def _fullsize(gpu, oracle, name, kind, n, samples, precision, **opts):
 def test_f16_gradients_mask_free(gpu, oracle, name, kind, n, samples):
     """All 22 F16 gradient tensors vs an fp64 oracle run that makes its own fp64 z > 0 decisions.  The F16
     pre-activations are rounded to fp16 before the ReLU, so a unit with |z| within fp16 rounding of 0 may
-    gate the other way; no decision is adopted here, so the bound (F16_GRAD_TOL, conftest.py) covers those
-    flips as well: every tensor within it, the whole arena within 2e-3."""
+    gate the other way; no decision is adopted here, so the per-tensor bound (f16_grad_tol, conftest.py: W0
+    6e-3, every other tensor 2e-3) covers those flips as well; the whole arena within 2e-3."""
     import nof
 
     seed, step, base = 0x5EED0000 + int(name[-1]), 5, 0
@@ -170,8 +170,9 @@ def test_f16_gradients_mask_free(gpu, oracle, name, kind, n, samples):
         off += s
     whole = rel_l2(G, ref["grads"])
     print(f"{name} F16 mask-free gradients: per tensor max {max(errs):.2e} (tensor {int(np.argmax(errs))}) "
-          f"median {np.median(errs):.2e}; whole arena {whole:.2e}")
-    assert max(errs) < F16_GRAD_TOL, f"tensor {int(np.argmax(errs))}: rel L2 {max(errs):.3g}"
+          f"median {np.median(errs):.2e}; whole arena {whole:.2e}; all: {' '.join(f'{e:.1e}' for e in errs)}")
+    for i, e in enumerate(errs):
+        assert e < f16_grad_tol(i), f"tensor {i}: rel L2 {e:.3g} (bound {f16_grad_tol(i):.0e})"
     assert whole < 2e-3, f"whole gradient arena: rel L2 {whole:.3g}"
     model.close()
 

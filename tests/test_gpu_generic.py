@@ -344,6 +344,27 @@ def test_generic_encoded_api_path(gpu, oracle):
     b.close()
 
 
+def test_generic_get_output_refuses_more_rays_than_max_rays(gpu):
+    """a call with fewer samples per ray than the level was built for fits the level's
+    sample capacity with more rays than max_rays, but the per-ray buffers (view encodings, the view-layer
+    gradient's ray sums) hold max_rays rays: refused with a status, and the object stays usable."""
+    import torch
+    import nof
+
+    n, samples = 8, (64, 64)
+    m = nof.AcceleratedMipNeRF(seed=6, max_rays=n, num_samples=samples, **_cfg(SPECS["odd_5x96_3x40"]))
+    P, V = 2 * 3 * (10 - 2), 3 + 3 * 2 * 2  # IPE of degrees 2..9, view PE of degree 2 (the spec above)
+    big = 2 * n  # 2n rays x 32 samples = the level's n x 64 capacity
+    ep = torch.zeros(big * 32, P, device=gpu)
+    ed = torch.zeros(big, V, device=gpu)
+    with pytest.raises(nof.NofError):
+        m.mlp.get_output(ep, ed, 0, big, 32)
+    dptr, _ = m.mlp.get_output(ep[: n * 32], ed[:n], 0, n, 32)  # within max_rays: accepted
+    torch.cuda.synchronize()
+    assert np.all(np.isfinite(nof.to_numpy(dptr, (n, 32))))
+    m.close()
+
+
 def test_generic_more_than_65535_row_tiles(gpu):
     """8192 rays x 512 + 512 samples: 4.19 M samples per level = 65 536 GEMM row tiles, past a launch grid's
     y limit (the tiles are linear in x).  The step equals its two accumulated 4096-ray halves (global ray

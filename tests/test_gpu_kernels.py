@@ -51,8 +51,8 @@ def test_sample_stratified_bitexact(gpu, oracle, S, lindisp, rnd):
 
     r = rays(37, seed=1)
     t = empty((37, S + 1), gpu)
-    nof._lib.call("nof_kernel_sample_stratified", 37, S, T(r["near"], gpu).data_ptr(), T(r["far"], gpu).data_ptr(), rnd,
-                  lindisp, 0xABCDEF12345, 7, 0, 1000, t.data_ptr(), None)
+    nof._lib.call("nof_kernel_sample_stratified_ex", 37, S, T(r["near"], gpu).data_ptr(), T(r["far"], gpu).data_ptr(),
+                  rnd, 0xABCDEF12345, 7, 0, 1000, t.data_ptr(), None, lindisp)
     sync()
     ref = oracle.sample_stratified(r["near"], r["far"], S, bool(rnd), 0xABCDEF12345, 7, 0, 1000, lindisp=bool(lindisp))
     assert np.array_equal(t.cpu().numpy(), ref)
@@ -90,7 +90,7 @@ def test_samplers_config1_size(gpu, oracle):
     r = synth.blender_rays(n, width=400, height=400, num_views=1, seed=1)
     t0 = empty((n, S + 1), gpu)
     nof._lib.call("nof_kernel_sample_stratified", n, S, T(r["near"], gpu).data_ptr(), T(r["far"], gpu).data_ptr(), 1,
-                  0, seed, 0, 0, 0, t0.data_ptr(), None)
+                  seed, 0, 0, 0, t0.data_ptr(), None)
     sync()
     ref0 = oracle.sample_stratified(r["near"], r["far"], S, True, seed, 0, 0, 0)
     assert np.array_equal(t0.cpu().numpy(), ref0)
@@ -115,8 +115,9 @@ def test_cast_bitexact_and_encode(gpu, oracle, ray_shape):
     r = rays(n, seed=4)
     t = oracle.sample_stratified(r["near"], r["far"], S, True, 9, 2, 0, 0)
     mean, cov = empty((n, S, 3), gpu), empty((n, S, 3), gpu)
-    nof._lib.call("nof_kernel_cast", n, S, T(t, gpu).data_ptr(), T(r["o"], gpu).data_ptr(), T(r["d"], gpu).data_ptr(),
-                  T(r["radius"], gpu).data_ptr(), ray_shape, mean.data_ptr(), cov.data_ptr(), None)
+    nof._lib.call("nof_kernel_cast_ex", n, S, T(t, gpu).data_ptr(), T(r["o"], gpu).data_ptr(),
+                  T(r["d"], gpu).data_ptr(), T(r["radius"], gpu).data_ptr(), mean.data_ptr(), cov.data_ptr(), None,
+                  ray_shape)
     ep, ed = empty((n * S, 96), gpu), empty((n, 27), gpu)
     nof._lib.call("nof_kernel_encode", n, S, mean.data_ptr(), cov.data_ptr(), T(r["d"], gpu).data_ptr(),
                   ep.data_ptr(), ed.data_ptr(), None)

@@ -189,7 +189,7 @@ def test_encoded_get_output_equals_fused(gpu):
     mean = torch.zeros((n, S, 3), device=gpu)
     cov = torch.zeros((n, S, 3), device=gpu)
     nof._lib.call("nof_kernel_cast", n, S, t.data_ptr(), dev["o"].data_ptr(), dev["d"].data_ptr(),
-                  dev["radius"].data_ptr(), 0, mean.data_ptr(), cov.data_ptr(), None)
+                  dev["radius"].data_ptr(), mean.data_ptr(), cov.data_ptr(), None)
     ep = torch.zeros((n * S, 96), device=gpu)
     ed = torch.zeros((n, 27), device=gpu)
     nof._lib.call("nof_kernel_encode", n, S, mean.data_ptr(), cov.data_ptr(), dev["d"].data_ptr(), ep.data_ptr(),

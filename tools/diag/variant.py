@@ -98,6 +98,43 @@ EDITS = {
         (K + "mlp_f16.hip", "  }  // groups\n  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n}",
          "  H32_ST(5)\n  H32_FLUSH(1)\n  }  // groups\n  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n}"),
     ],
+    # barrier-count probes (timing only: without the barrier the ring slots race, results garbage): no
+    # workgroup barrier at the period ends (the vmcnt waits stay), or one every other period
+    "h32_nobar": [(K + "mlp_h32.h", "\"s_waitcnt vmcnt(\" #N \")\\n\\ts_waitcnt lgkmcnt(0)\\n\\ts_barrier\"",
+                   "\"s_waitcnt vmcnt(\" #N \")\\n\\ts_waitcnt lgkmcnt(0)\""),
+                  (K + "mlp_h32.h", "\"s_waitcnt vmcnt(47)\\n\\ts_waitcnt lgkmcnt(0)\\n\\ts_barrier\"",
+                   "\"s_waitcnt vmcnt(47)\\n\\ts_waitcnt lgkmcnt(0)\"")],
+    "h32_halfbar": [(K + "mlp_h32.h", "\"s_waitcnt vmcnt(\" #N \")\\n\\ts_waitcnt lgkmcnt(0)\\n\\ts_barrier\"",
+                     "\"s_waitcnt vmcnt(\" #N \")\\n\\ts_waitcnt lgkmcnt(0)\""),
+                    (K + "mlp_h32.h", "\"s_waitcnt vmcnt(47)\\n\\ts_waitcnt lgkmcnt(0)\\n\\ts_barrier\"",
+                     "\"s_waitcnt vmcnt(47)\\n\\ts_waitcnt lgkmcnt(0)\""),
+                    (K + "mlp_h32.h", "    h32_barrier(2 * (kDmaAhead - 1) + now + h0 + h1 + h2 + h3);\n",
+                     "    h32_barrier(2 * (kDmaAhead - 1) + now + h0 + h1 + h2 + h3);\n    if (cur & 1) __builtin_amdgcn_s_barrier();\n")],
+    # the mask bits' two VALU ops in ONE asm statement (two statements get an s_nop 0 between them)
+    "h32_mask1": [(K + "mlp_h32.h",
+                   "  asm(\"v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]\" : \"=v\"(b) : \"v\"(relu));\n"
+                   "  asm(\"v_pk_mad_u16 %0, %1, 2, %2 op_sel_hi:[1,0,1]\" : \"=v\"(r) : \"v\"(w), \"v\"(b));",
+                   "  asm(\"v_pk_min_u16 %1, %2, 1 op_sel_hi:[1,0]\\n\\tv_pk_mad_u16 %0, %3, 2, %1 op_sel_hi:[1,0,1]\"\n"
+                   "      : \"=v\"(r), \"=&v\"(b) : \"v\"(relu), \"v\"(w));")],
+    # the weight ring's LDS-DMA as global_load_lds_dwordx4 (per-lane address) instead of buffer_load ... lds
+    "h32_glds": [(K + "mlp_h32.h", "template <int kLate>\nstruct H32Ring {",
+                  "__device__ __forceinline__ void h32_dma_step(const float* src, float* dst, int tid, int i) {\n"
+                  "  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);\n"
+                  "  __builtin_amdgcn_global_load_lds((gptr_t)(src + (kH32Threads * i + tid) * 4),\n"
+                  "                                   (lptr_t)(dst + (kH32Threads * i + 64 * wave) * 4), 16, 0, 0);\n}\n"
+                  "template <int kLate>\nstruct H32Ring {"),
+                 (K + "mlp_h32.h", "      slice16_dma_step(stream + p * kPeriodFloats, lds + p * kPeriodFloats, tid, 0);\n"
+                  "      slice16_dma_step(stream + p * kPeriodFloats, lds + p * kPeriodFloats, tid, 1);",
+                  "      h32_dma_step(stream + p * kPeriodFloats, lds + p * kPeriodFloats, tid, 0);\n"
+                  "      h32_dma_step(stream + p * kPeriodFloats, lds + p * kPeriodFloats, tid, 1);"),
+                 (K + "mlp_h32.h",
+                  "    slice16_dma_step(next, lds + ((cur + kDmaAhead) & (kH32Slots - 1)) * kPeriodFloats, tid, step);",
+                  "    h32_dma_step(next, lds + ((cur + kDmaAhead) & (kH32Slots - 1)) * kPeriodFloats, tid, step);")],
+    # A fragments not re-read from LDS (the layer's first R fragments reused; timing only, results garbage)
+    "h32_noread": [(K + "mlp_h32.h", "  for (int i = 0; i < kReadAhead; ++i) fr[i] = ring.frag(i, lane);  // (cur: already this period's slot)",
+                    "  for (int i = 0; i < R; ++i) fr[i] = ring.frag(i, lane);"),
+                   (K + "mlp_h32.h", "    if constexpr (i + kReadAhead < N) fr[(i + kReadAhead) % R] = ring.frag((pos + kReadAhead) % kPeriod, lane);",
+                    "    if constexpr (i + kReadAhead < N) asm volatile(\"\" : \"+v\"(fr[(i + kReadAhead) % R]));")],
     "h32_nomask": [(K + "mlp_h32.h", "__device__ __forceinline__ uint32_t mask_shift(uint32_t w, uint32_t relu) {\n  uint32_t b, r;",
                     "__device__ __forceinline__ uint32_t mask_shift(uint32_t w, uint32_t relu) {\n  return w ^ relu;\n  uint32_t b, r;")],
     "h32_prio": [(K + "mlp_f16.hip", "  ring.prologue(a.wimg, kFwdFrags * kFragFloats, tid);",

@@ -214,8 +214,11 @@ hipError_t launch_pack_weights_x3(const float* params, const PackArgs& pa, float
 // F16-mode (h32) images (mlp_h32.h): the forward / backward k-step fragment streams in fp16 (RNE) plus the
 // fp32 tails.  One thread per 16-B fragment chunk (lane l = (x, h) of fragment g: 8 halves) or tail float.
 // Forward segment (layer l, chunk c, k-step kk): A[row 32c + x][column kfeat(kk, h, j)] = W_l[row][col]
-// (layer 4's k-steps 16..21: its IPE columns 256 + kfeat(kk - 16, h, j)).  Backward segment: A[i][o] =
-// W_l[o][i], i = 32c + x (a feature of h_{l-1}), o = kfeat(kk, h, j) (a feature of delta_l).
+// (layer 4's k-steps 16..21: its IPE columns 256 + kfeat(kk - 16, h, j)); the view layer's chunk 4 is the
+// density head (row 0 = W8, MNcs:19-20 on h7), the RGB segment W10 in rows 0..2; rows past a layer's
+// outputs are zero.  Backward segment: A[i][o] =
+// W_l[o][i], i = 32c + x (a feature of h_{l-1}), o = kfeat(kk, h, j) (a feature of delta_l); layer 9's
+// k-step 8 holds w8 at o = 128 (the feature the kernel sets to dz_s), k-step 9 is zero padding.
 __global__ void k_pack_weights_h32(const float* __restrict__ P, PackArgs pa, float* __restrict__ wf,
                                    float* __restrict__ wb) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -242,9 +245,13 @@ __global__ void k_pack_weights_h32(const float* __restrict__ P, PackArgs pa, flo
         float w;
         if (fwd) {
           const int col = kk < 16 ? kfeat(kk, h, j) : 256 + kfeat(kk - 16, h, j);
-          w = P[pa.woff[l] + (int64_t)(32 * c + x) * in + col];
-        } else {
+          const bool dens = l == 9 && c == 4;  // the density head as the view layer's fifth chunk
+          const int ll = dens ? 8 : l, row = dens ? x : 32 * c + x;
+          w = row < layer_out(ll) ? P[pa.woff[ll] + (int64_t)row * layer_in(ll) + col] : 0.0f;
+        } else if (kk < 16 && (l != 9 || kk < 8)) {
           w = P[pa.woff[l] + (int64_t)kfeat(kk, h, j) * in + 32 * c + x];
+        } else {  // layer 9's k-step 8: feature 128 = dz_s, A = w8 (the density head, MNcs:23-24, D11); 9: padding
+          w = (kk == 8 && kfeat(0, h, j) == 0) ? P[pa.woff[8] + 32 * c + x] : 0.0f;
         }
         out[j] = (_Float16)w;
       }

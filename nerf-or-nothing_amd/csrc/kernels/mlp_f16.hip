@@ -66,9 +66,6 @@ __device__ __forceinline__ float sload_f32(const float* p) {
   asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
   return v;
 }
-__device__ __forceinline__ float dot2(uint32_t a, uint32_t b, float c) {
-  return __builtin_amdgcn_fdot2(__builtin_bit_cast(h16x2, a), __builtin_bit_cast(h16x2, b), c, false);
-}
 
 // ---- IPE of the F16 mode -----------------------------------------------------------------------------
 // sin(arg) = v_sin_f32(frac(arg / 2pi)) with arg / 2pi in double-float (exact product residual by FMA),
@@ -95,32 +92,26 @@ __device__ __forceinline__ float ipe_h32(int c, const float (&mu_h)[3], const fl
 }
 
 // ---- forward epilogues ----------------------------------------------------------------------------------
-// trunk: tile T of acc -> packed fp16 ReLU into dst (the next layer's B fragments), mask bits, the act
-// block stores; the density head's dot product (layer 7: z_s = w8 . h7, fp16 operands, fp32 sum)
-template <bool kStore>
+// tile T of acc -> packed fp16 ReLU into dst (the next layer's B fragments), mask bits, the act block
+// stores.  kNC = the layer's chunks with an epilogue: 8 (trunk) or 4 (the view layer, whose fifth chunk is
+// the density head, taken by the caller; its output h9 builds the RGB head's B fragments).
+template <bool kStore, int NCE = 8>
 struct FwdEpiH {
-  static constexpr int kNC = 8;
+  static constexpr int kNC = NCE;
   const f32x16 (&acc)[2];
   uint32_t (&dst)[16][4];
   uint32_t (&mw)[4];  // mask words (a kernel-local array: a member array is left in scratch memory)
   __amdgpu_buffer_rsrc_t blk, mrs;
   uint32_t voff, moff;
   int mimm;
-  const uint32_t* w8;  // LDS, packed w8 pairs of this lane half: [T][2][8] + 8h
-  float zs;
-  bool dens;
   __device__ __forceinline__ FwdEpiH(const f32x16 (&a)[2], uint32_t (&d)[16][4], uint32_t (&mw_)[4], uint32_t voff_,
                                      uint32_t moff_)
       : acc(a), dst(d), mw(mw_), voff(voff_), moff(moff_) {}
-  __device__ __forceinline__ void begin(const void* blk_, const void* masks_blk, int slot, const uint32_t* w8_,
-                                        bool dens_) {
+  __device__ __forceinline__ void begin(const void* blk_, const void* masks_blk, int slot) {
     blk = h32_rsrc(blk_);
     mrs = h32_rsrc(masks_blk);
     mimm = slot * 1024;
     mw[0] = mw[1] = mw[2] = mw[3] = 0u;
-    w8 = w8_;
-    zs = 0.0f;
-    dens = dens_;
   }
   __device__ __forceinline__ int piece(int T, int kk, int NK) {
     int n = 0;
@@ -130,7 +121,6 @@ struct FwdEpiH {
         const uint32_t p = relu_pk(pk_h(acc[T & 1][2 * d], acc[T & 1][2 * d + 1]));
         mw[T >> 1] = mask_shift(mw[T >> 1], p);
         dst[2 * T + (d >> 2)][d & 3] = p;
-        if (dens) zs = dot2(p, w8[T * 16 + d], zs);
       }
     if constexpr (kStore) {
 #pragma unroll
@@ -149,59 +139,13 @@ struct FwdEpiH {
   }
 };
 
-// view layer 9: tile T -> ReLU fp16, mask bits, act_h9 stores, and the RGB head's three dot products
-template <bool kStore>
-struct ViewEpiH {
-  static constexpr int kNC = 4;
-  const f32x16 (&acc)[2];
-  uint32_t (&mw)[4];
-  uint32_t (&p8)[8];
-  __amdgpu_buffer_rsrc_t blk, mrs;
-  uint32_t voff, moff;
-  const uint32_t* w10;  // LDS, packed W10 pairs: [3][T][2][8] + 8h
-  float zc[3];
-  __device__ __forceinline__ ViewEpiH(const f32x16 (&a)[2], uint32_t (&mw_)[4], uint32_t (&p8_)[8], uint32_t voff_,
-                                      uint32_t moff_, const void* blk_, const void* masks_blk, const uint32_t* w10_)
-      : acc(a), mw(mw_), p8(p8_), voff(voff_), moff(moff_), w10(w10_) {
-    blk = h32_rsrc(blk_);
-    mrs = h32_rsrc(masks_blk);
-    mw[0] = mw[1] = mw[2] = mw[3] = 0u;
-    zc[0] = zc[1] = zc[2] = 0.0f;
-  }
-  __device__ __forceinline__ int piece(int T, int kk, int NK) {
-    int n = 0;
-#pragma unroll
-    for (int d = 0; d < 8; ++d)
-      if (kk == epi_valu_pos(d, NK)) {
-        const uint32_t p = relu_pk(pk_h(acc[T & 1][2 * d], acc[T & 1][2 * d + 1]));
-        mw[T >> 1] = mask_shift(mw[T >> 1], p);
-        p8[d] = p;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) zc[c] = dot2(p, w10[(c * 4 + T) * 16 + d], zc[c]);
-      }
-    if constexpr (kStore) {
-#pragma unroll
-      for (int sh = 0; sh < 2; ++sh)
-        if (kk == epi_half_pos(sh, NK)) {
-          store_half<kFwdAux>(blk, voff, T, sh, p8[4 * sh], p8[4 * sh + 1], p8[4 * sh + 2], p8[4 * sh + 3]);
-          ++n;
-        }
-      if (T == kNC - 1 && kk == epi_mask_pos(NK)) {
-        store_b128<kFwdAux>(mrs, moff, 8 * 1024, u32x4{mw[0], mw[1], mw[2], mw[3]});
-        ++n;
-      }
-    }
-    return n;
-  }
-};
-
 template <bool kStore>
 __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   constexpr int kBias = kH32RingFloats;           // fp32 trunk biases [8][256]
-  constexpr int kDirb = kBias + 8 * 256;          // per-wave view-direction bias [8][128]
-  constexpr int kW8 = kDirb + kH32Waves * 128;    // packed w8 [8][2][8]
-  constexpr int kW10 = kW8 + 128;                 // packed W10 [3][4][2][8]
-  constexpr int kW9d = kW10 + 192;                // W9[:, 256:283] transposed [27][128], then b9 [128]
+  // per-wave C operands of the view layer [8][160]: the view-direction bias of its 128 rows, then zeros for
+  // the density-head chunk (its bias b8 is added with the heads)
+  constexpr int kDirb = kBias + 8 * 256;
+  constexpr int kW9d = kDirb + kH32Waves * 160;   // W9[:, 256:283] transposed [27][128], then b9 [128]
   constexpr int kTin = kW9d + (kDirIn + 1) * 128;  // per-wave group inputs [8][64] (in_dma)
   __shared__ __attribute__((aligned(16))) float lds[kTin + kH32Waves * 64];
   const int tid = threadIdx.x, lane = tid & 63, x = lane & 31, h = lane >> 5;
@@ -215,17 +159,10 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   ring.lds = lds;
   ring.prologue(a.wimg, kFwdFrags * kFragFloats, tid);  // the first periods land while the encodings run
 
-  // ---- LDS tables, the same for every group: trunk biases, packed w8 / W10 -------------------------
+  // ---- LDS tables, the same for every group: trunk biases, the density chunk's zero C operand ---------
   for (int i = tid; i < 2048 / 4; i += kH32Threads)
     *reinterpret_cast<f32x4*>(lds + kBias + 4 * i) = *reinterpret_cast<const f32x4*>(tail + kFwdTailBias + 4 * i);
-  if (tid < 128 + 192) {  // packed pairs of features 32T + 8(d >> 1) + 4hh + 2(d & 1) + {0, 1}
-    const bool is8 = tid < 128;  // w8 [T][hh][d] | W10 [c][T][hh][d]
-    const int i = is8 ? tid : tid - 128;
-    const int d = i & 7, hh = (i >> 3) & 1, T = (i >> 4) & (is8 ? 7 : 3), c = is8 ? 0 : i >> 6;
-    const int f = 32 * T + 8 * (d >> 1) + 4 * hh + 2 * (d & 1);
-    const float* src = is8 ? tail + kFwdTailW8 : tail + kFwdTailW10 + c * 128;
-    reinterpret_cast<uint32_t*>(lds + (is8 ? kW8 : kW10))[i] = pk_h(src[f], src[f + 1]);
-  }
+  if (tid < kH32Waves * 32) lds[kDirb + (tid >> 5) * 160 + 128 + (tid & 31)] = 0.0f;
   // the view layer's direction columns, feature-major so that the 64 lanes of a wave (64 outputs) read 64
   // consecutive words: every group's direction bias from LDS, not from global memory (a global load would
   // wait, in vmcnt order, for the weight DMA in flight)
@@ -237,12 +174,11 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   const uint32_t moff = (uint32_t)lane * 16u;
   const size_t lstride = (size_t)nblk * kBlk * kWidth;  // halves per act_h layer
   const float* bias_h = lds + kBias + 4 * h;
-  const uint32_t* w8h = reinterpret_cast<const uint32_t*>(lds + kW8) + 8 * h;
   // VMEM instructions a group issues outside the layers (ring.add_ops: a lower bound): the act_in tiles (8)
-  // and, after the first group, its predecessor's last view tile (two halves and the mask) and heads (sigma,
-  // rgb — perhaps one store —, zhead)
+  // and, after the first group, its predecessor's heads (sigma, rgb — perhaps one store —, zhead); the last
+  // view tile's stores run inside the density chunk, counted by the layer
   constexpr int kFirstOps = kStore ? 8 : 0;
-  constexpr int kGroupOps = kStore ? 8 + 3 + 3 : 2;
+  constexpr int kGroupOps = kStore ? 8 + 3 : 2;
 
   // A group's inputs — the 33 t of each wave's 32 samples and its ray's direction, origin and radius — go
   // into the wave's LDS slot by LDS-DMA (in_dma: [0, 33) t, [40, 43) direction, [44, 47) origin, 48 radius)
@@ -337,7 +273,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
     // values would stay live across every group and spill)
     if (first) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the W9 / b9 table written
     else asm volatile("" ::: "memory");
-    float* dirb = lds + kDirb + wave * 128;  // b9 + W9[:, 256:283] . PE(d) (LDS; read by this wave only)
+    float* dirb = lds + kDirb + wave * 160;  // b9 + W9[:, 256:283] . PE(d) (LDS; read by this wave only)
 #pragma unroll
     for (int rep = 0; rep < 2; ++rep) {
       const int o = lane + 64 * rep;
@@ -441,7 +377,7 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
   f32x16 acc[2];
   uint32_t X[16][4], Y[16][4];
   const _Float16* act_h = reinterpret_cast<const _Float16*>(a.act_h) + (size_t)m0 * kWidth;
-  uint32_t mwX[4], mwY[4], mwV[4], p8[8];
+  uint32_t mwX[4], mwY[4], mwV[4];
   FwdEpiH<kStore> eX(acc, X, mwX, vrow, moff), eY(acc, Y, mwY, vrow, moff);
   NoEpiH none;
   auto srcI = [&](int kk, uint32_t (&b)[4]) {
@@ -460,41 +396,42 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) b[e] = kk < 16 ? Y[kk < 16 ? kk : 0][e] : ipe[kk >= 16 ? kk - 16 : 0][e];
   };
-  eX.begin(act_h, masks_blk, 0, w8h, false);
+  eX.begin(act_h, masks_blk, 0);
   ring.add_ops(first ? kFirstOps : kGroupOps);
   h32_layer<6, 8, true>(srcI, acc, ring, eX, none, bias_h, tid, lane);
   for (int it = 0; it < 2; ++it) {  // layers 1..3, (4), 5..7
     const int la = 1 + 4 * it;
-    eY.begin(act_h + la * lstride, masks_blk, la, w8h, false);
+    eY.begin(act_h + la * lstride, masks_blk, la);
     h32_layer<16, 8, true>(srcX, acc, ring, eY, eX, bias_h + la * 256, tid, lane);
-    eX.begin(act_h + (la + 1) * lstride, masks_blk, la + 1, w8h, false);
+    eX.begin(act_h + (la + 1) * lstride, masks_blk, la + 1);
     h32_layer<16, 8, true>(srcY, acc, ring, eX, eY, bias_h + (la + 1) * 256, tid, lane);
-    eY.begin(act_h + (la + 2) * lstride, masks_blk, la + 2, w8h, la + 2 == kDepth - 1);  // + density (layer 8)
+    eY.begin(act_h + (la + 2) * lstride, masks_blk, la + 2);
     if (kStore && it == 1 && !a.encoded && g + (int)gridDim.x < ngroups) {  // 12 periods ahead of read_in
       in_dma(g + gridDim.x);
       ring.add_ops(kInOps);
     }
     h32_layer<16, 8, true>(srcX, acc, ring, eY, eX, bias_h + (la + 2) * 256, tid, lane);
     if (it == 0) {
-      eX.begin(act_h + kSkip * lstride, masks_blk, kSkip, w8h, false);
+      eX.begin(act_h + kSkip * lstride, masks_blk, kSkip);
       h32_layer<22, 8, true>(srcYI, acc, ring, eX, eY, bias_h + kSkip * 256, tid, lane);
     }
   }
   static_assert(kDepth == 8 && kSkip == 4, "the trunk schedule assumes 8 layers, skip into layer 4");
-  // ---- view layer 9: relu(W9[:, :256] h7 + dirbias), the RGB head (layer 10) in its epilogue ----------
-  ViewEpiH<kStore> eV(acc, mwV, p8, vrow, moff, reinterpret_cast<const _Float16*>(a.act_h9) + (size_t)m0 * kWidthCond,
-                      masks_blk, reinterpret_cast<const uint32_t*>(lds + kW10) + 8 * h);
-  h32_layer<16, 4, true>(srcY, acc, ring, eV, eY, lds + kDirb + wave * 128 + 4 * h, tid, lane);
-#pragma unroll
-  for (int kk = 0; kk < 16; ++kk) eV.piece(3, kk, 16);  // the last view tile: nothing left to hide it under
+  // ---- view layer 9: relu(W9[:, :256] h7 + dirbias); its fifth chunk is the density head z_s = w8 . h7
+  // (layer 8, MNcs:19-20), whose row 0 lands in register 0 of the lanes h = 0; the view tiles' epilogue builds
+  // h9 as the RGB head's B fragments in X (free: the view layer reads h7 from Y) ---------------------------
+  FwdEpiH<kStore, 4> eV(acc, X, mwV, vrow, moff);
+  eV.begin(reinterpret_cast<const _Float16*>(a.act_h9) + (size_t)m0 * kWidthCond, masks_blk, 8);
+  h32_layer<16, 5, true>(srcY, acc, ring, eV, eY, lds + kDirb + wave * 160 + 4 * h, tid, lane);
+  const float zs = acc[0][0] + hb[0];
+  // ---- RGB head (layer 10): z_c = W10 h9, rows 0..2 of one chunk over 8 k-steps (the second chunk is ring
+  // padding: no MFMA) -------------------------------------------------------------------------------------
+  h32_layer<8, 2, false, 1>(srcX, acc, ring, none, none, nullptr, tid, lane);
 
   // ---- heads: sigma = softplus(z_s - 1), rgb = sigmoid(z_c) 1.002 - 0.001 (MNcs:19-22,151-152) -------------
-  float zs = eY.zs;
-  zs += __shfl_xor(zs, 32, 64);
-  zs += hb[0];
   float zc[3];
 #pragma unroll
-  for (int c = 0; c < 3; ++c) zc[c] = eV.zc[c] + __shfl_xor(eV.zc[c], 32, 64) + hb[1 + c];
+  for (int c = 0; c < 3; ++c) zc[c] = acc[0][c] + hb[1 + c];
   if (h == 0) {
     a.sigma[m] = softplus_f(zs + a.dbias);
 #pragma unroll
@@ -509,8 +446,8 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_fwd_h32(FwdArgs a) {
 }
 
 // ---- backward ---------------------------------------------------------------------------------------
-// delta = mask ? acc (+ w8 dz_s at layer 7) : 0, as packed fp16 (the deltas carry the level's power-of-
-// two scale), into dst (the next layer's B fragments) and the delta block
+// delta = mask ? acc : 0, as packed fp16 (the deltas carry the level's power-of-two scale), into dst (the
+// next layer's B fragments) and the delta block.  (Layer 7's w8 dz_s term is the dh7 layer's k-step 8.)
 struct BwdEpiH {
   static constexpr int kNC = 8;
   const f32x16 (&acc)[2];
@@ -518,34 +455,20 @@ struct BwdEpiH {
   __amdgpu_buffer_rsrc_t blk;
   uint32_t voff;
   uint4 mk;
-  const float* w8;  // LDS fp32 [T][2][16] + 16h, or null
-  float dzs;
   __device__ __forceinline__ BwdEpiH(const f32x16 (&a)[2], uint32_t (&d)[16][4], uint32_t voff_)
       : acc(a), dst(d), voff(voff_) {}
   // mask: the layer's ReLU mask words, loaded one layer ahead by the caller (a load issued here would
   // be waited for one chunk later together with every store issued before it: vmcnt retires in order)
-  __device__ __forceinline__ void begin(const void* blk_, const uint4& mask, const float* w8_, float dzs_) {
+  __device__ __forceinline__ void begin(const void* blk_, const uint4& mask) {
     blk = h32_rsrc(blk_);
     mk = mask;
-    w8 = w8_;
-    dzs = dzs_;
   }
   __device__ __forceinline__ int piece(int T, int kk, int NK) {
     int n = 0;
 #pragma unroll
     for (int d = 0; d < 8; ++d)
       if (kk == epi_valu_pos(d, NK)) {
-        float v0 = acc[T & 1][2 * d], v1 = acc[T & 1][2 * d + 1];
-        if (w8) {
-          // an opaque read that waits for itself: as a plain LDS load the compiler cannot tell it from
-          // the ring's LDS-DMA destination and puts a full s_waitcnt vmcnt(0) before it — draining every
-          // store and weight DMA in flight, twice per tile of the layer
-          const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)w8;
-          f32x2 w;
-          asm volatile("ds_read_b64 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)" : "=v"(w) : "v"(la), "i"(4 * (T * 32 + 2 * d)));
-          v0 = __builtin_fmaf(w[0], dzs, v0);
-          v1 = __builtin_fmaf(w[1], dzs, v1);
-        }
+        const float v0 = acc[T & 1][2 * d], v1 = acc[T & 1][2 * d + 1];
         const uint32_t word = (T >> 1) == 0 ? mk.x : ((T >> 1) == 1 ? mk.y : ((T >> 1) == 2 ? mk.z : mk.w));
         dst[2 * T + (d >> 2)][d & 3] = pk_h(v0, v1) & mask_expand(word, 8 * (T & 1) + d);
       }
@@ -561,8 +484,7 @@ struct BwdEpiH {
 };
 
 __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
-  constexpr int kW8 = kH32RingFloats;  // fp32 w8 in D-register order [8][2][16]
-  constexpr int kW10 = kW8 + 256;      // fp32 W10 [3][128]
+  constexpr int kW10 = kH32RingFloats;  // fp32 W10 [3][128]
   // per-wave group inputs (bwd_in_dma): masks of layers 8 and 7 [64 lanes][4], zhead [32][4], drgb [32][3],
   // dsigma [32]
   constexpr int kIn = kW10 + 3 * 128, kInFloats = 256 + 256 + 128 + 96 + 32;
@@ -600,11 +522,8 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   H32Ring<kBwdDmaLate> ring;
   ring.lds = lds;
   ring.prologue(a.wimg_b, kBwdFrags * kFragFloats, tid);
-  if (tid < 256) {  // the tables, the same for every group
-    const int T = tid >> 5, hh = (tid >> 4) & 1, r = tid & 15;
-    lds[kW8 + tid] = tail[kBwdTailW8 + 32 * T + 8 * (r >> 2) + 4 * hh + (r & 3)];
-  }
-  if (tid < 96) *reinterpret_cast<f32x4*>(lds + kW10 + 4 * tid) = *reinterpret_cast<const f32x4*>(tail + kBwdTailW10 + 4 * tid);
+  if (tid < 96)  // the W10 table, the same for every group
+    *reinterpret_cast<f32x4*>(lds + kW10 + 4 * tid) = *reinterpret_cast<const f32x4*>(tail + kBwdTailW10 + 4 * tid);
   const uint32_t vrow = slot_off(x, h);
   const float sc0 = delta_scale(a.amax, false), sc1 = a.M1 > 0 ? delta_scale(a.amax1, false) : 1.0f;
   // VMEM instructions a group issues outside the layers (ring.add_ops: a lower bound): the delta9x tiles
@@ -660,12 +579,17 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
   float dr[3], ds_m;
   {
     const auto la = [](const float* p) { return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)p; };
+    // (the lane's offsets from an opaque lane id, as in in_dma: hoisted out of the group loop they are spilled,
+    // and a scratch reload waits with a full vmcnt drain)
+    uint32_t id;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(id));
     asm volatile(
         "ds_read_b128 %0, %7\n\tds_read_b128 %1, %7 offset:1024\n\tds_read_b128 %2, %8 offset:2048\n\t"
         "ds_read_b32 %3, %9 offset:2560\n\tds_read_b32 %4, %9 offset:2564\n\tds_read_b32 %5, %9 offset:2568\n\t"
         "ds_read_b32 %6, %10 offset:2944\n\ts_waitcnt lgkmcnt(0)"
         : "=&v"(mk9v), "=&v"(mk7v), "=&v"(zh), "=&v"(dr[0]), "=&v"(dr[1]), "=&v"(dr[2]), "=&v"(ds_m)
-        : "v"(la(in_slot + lane * 4)), "v"(la(in_slot + x * 4)), "v"(la(in_slot + x * 3)), "v"(la(in_slot + x)));
+        : "v"(la(in_slot) + 16u * id), "v"(la(in_slot) + 16u * (id & 31u)), "v"(la(in_slot) + 12u * (id & 31u)),
+          "v"(la(in_slot) + 4u * (id & 31u)));
   }
   const uint4 mk9 = {mk9v[0], mk9v[1], mk9v[2], mk9v[3]};
   const uint4 mk7 = {mk7v[0], mk7v[1], mk7v[2], mk7v[3]};
@@ -705,9 +629,15 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
       }
       store_tile<kBwdAux>(d9, vrow, T, p);
     }
-    if (h == 0) store_b64<kBwdAux>(d9, vrow, 4 * 2048, pk_h(dzs, dzc[0]), pk_h(dzc[1], dzc[2]));  // features 128..131
+    const uint32_t dzs_h = pk_h(dzs, dzc[0]);
+    if (h == 0) store_b64<kBwdAux>(d9, vrow, 4 * 2048, dzs_h, pk_h(dzc[1], dzc[2]));  // features 128..131
+    // k-step 8 of the dh7 layer: feature 128 (element 0 of the lane half h = 0) = dz_s, the rest zero — the
+    // density head's term w8 dz_s (MNcs:23-24) as one more fp16 product on MFMA, with the same fp16 dz_s the
+    // weight gradients read from delta9x
+    X[8][0] = h == 0 ? (dzs_h & 0xffffu) : 0u;
+    X[8][1] = X[8][2] = X[8][3] = 0u;
   }
-  if (first) h32_prologue_barrier();  // w8 table written, the first periods landed
+  if (first) h32_prologue_barrier();  // the first periods landed
 
   f32x16 acc[2];
   const _Float16* delta = reinterpret_cast<const _Float16*>(lv.delta) + (size_t)m0 * kWidth;
@@ -721,21 +651,21 @@ __global__ __launch_bounds__(kH32Threads, 1) void k_mlp_bwd_h32(BwdArgs a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) b[e] = Y[kk][e];
   };
-  // dh7 = W9[:, :256]^T delta9 + w8 dz_s ; delta7
-  eY.begin(delta + 7 * lstride, mk7, lds + kW8 + 16 * h, dzs);
+  // dh7 = [W9[:, :256]^T | w8] [delta9 | dz_s] (k-steps 0..8; 9 is ring padding) ; delta7
+  eY.begin(delta + 7 * lstride, mk7);
   ring.add_ops(first ? kFirstOps : kGroupOps);
-  h32_layer<8, 8, false>(srcX, acc, ring, eY, none, nullptr, tid, lane);
+  h32_layer<10, 8, false, 8, 9>(srcX, acc, ring, eY, none, nullptr, tid, lane);
   // dh_{l-1} = W_l[:, :256]^T delta_l ; delta_{l-1}, l = 7..2 in pairs, then l = 1
   for (int it = 0; it < 3; ++it) {
     const int l = kDepth - 1 - 2 * it;
-    eX.begin(delta + (l - 1) * lstride, mk_next, nullptr, 0.0f);
+    eX.begin(delta + (l - 1) * lstride, mk_next);
     mk_next = mask_of(l - 2);
     h32_layer<16, 8, false>(srcY, acc, ring, eX, eY, nullptr, tid, lane);
-    eY.begin(delta + (l - 2) * lstride, mk_next, nullptr, 0.0f);
+    eY.begin(delta + (l - 2) * lstride, mk_next);
     mk_next = mask_of(l - 3);
     h32_layer<16, 8, false>(srcX, acc, ring, eY, eX, nullptr, tid, lane);
   }
-  eX.begin(delta, mk_next, nullptr, 0.0f);
+  eX.begin(delta, mk_next);
   if (g + (int)gridDim.x < ngroups) {
     in_dma(g + gridDim.x);
     ring.add_ops(kInOps);

@@ -60,15 +60,23 @@ constexpr int kH32RingFloats = kH32Slots * kPeriodFloats;  // 128 KB
 struct H32Seg {
   int layer, nk, nc;
 };
-constexpr int kFwdSegs = 9, kBwdSegs = 8;
+// Forward: layers 0..7, the view layer 9 with the density head (layer 8, one row on h7) as its fifth chunk,
+// then the RGB head (layer 10, three rows on h9) as a chunk of 8 k-steps plus a padding chunk (no MFMAs: a
+// layer is a whole number of periods).  Both heads run on MFMA instead of per-dword v_dot2 in the epilogues
+// (round 6: 160 dot2 + a wave-uniform branch per epilogue dword per wave and group).
+constexpr int kFwdSegs = 10, kBwdSegs = 8;
 __host__ __device__ constexpr H32Seg fwd_seg(int i) {
-  return i == 0 ? H32Seg{0, 6, 8} : (i == 4 ? H32Seg{4, 22, 8} : (i == 8 ? H32Seg{9, 16, 4} : H32Seg{i, 16, 8}));
+  return i == 0 ? H32Seg{0, 6, 8}
+                : (i == 4 ? H32Seg{4, 22, 8}
+                          : (i == 8 ? H32Seg{9, 16, 5} : (i == 9 ? H32Seg{10, 8, 2} : H32Seg{i, 16, 8})));
 }
-__host__ __device__ constexpr H32Seg bwd_seg(int i) {  // L9 (dh7 <- delta9), then L7 .. L1 (dh_{l-1} <- delta_l)
-  return i == 0 ? H32Seg{9, 8, 8} : H32Seg{8 - i, 16, 8};
+// Backward: L9 (dh7 <- [delta9 | dz_s]: the density head's w8 dz_s term as k-step 8, a padding k-step 9 so
+// the layer is whole periods), then L7 .. L1 (dh_{l-1} <- delta_l)
+__host__ __device__ constexpr H32Seg bwd_seg(int i) {
+  return i == 0 ? H32Seg{9, 10, 8} : H32Seg{8 - i, 16, 8};
 }
-constexpr int kFwdFrags = 8 * 6 + 6 * 8 * 16 + 8 * 22 + 4 * 16;  // 1056
-constexpr int kBwdFrags = 8 * 8 + 7 * 8 * 16;                     // 960
+constexpr int kFwdFrags = 8 * 6 + 6 * 8 * 16 + 8 * 22 + 5 * 16 + 2 * 8;  // 1088
+constexpr int kBwdFrags = 8 * 10 + 7 * 8 * 16;                    // 976
 static_assert(kFwdFrags % kPeriod == 0 && kBwdFrags % kPeriod == 0, "streams are whole periods");
 constexpr int kStreamPad = kDmaAhead * kPeriod;  // the DMA runs kDmaAhead periods past the end: zero padding
 // images (floats): fragments (+ pad), then the fp32 tail of mlp_common.h (kFwdTail / kBwdTail layout)
@@ -249,7 +257,10 @@ constexpr int kBarrierPos = kPeriod - 1 - kReadAhead;
 // One layer: NC chunks of 32 output rows x NK k-steps.  bsrc(kk) gives k-step kk's B fragment (4
 // packed dwords); chunk c accumulates into acc[c & 1]; epi.piece(T, kk, NK) runs the epilogue of
 // this layer's tile T = c - 1 at k-step kk of chunk c, prev.piece the previous layer's last tile in
-// chunk 0 (its tile index NCp - 1 is odd: acc[1]).  cv: the layer's C-operand vector (LDS, + 4h;
+// chunk 0 (its tile index NCp - 1 is odd: acc[1]; a layer with an odd NC leaves its last tile in acc[0],
+// which the caller takes before the next layer).  Chunks NCC .. NC - 1 and k-steps NKC .. NK - 1 of every
+// chunk are ring padding: their positions keep the period schedule (DMA, barriers) but read no fragment and
+// issue no MFMA.  cv: the layer's C-operand vector (LDS, + 4h;
 // kBias false: C = 0).  Returns with the last tile's epilogue pending (the caller's next layer or a
 // drain).  Every loop is unrolled: all positions and store counts are constants.  The layer starts at
 // a period boundary, one barrier past the point where its first kReadAhead fragments may be read.
@@ -263,11 +274,14 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-template <int NK, int NC, bool kBias, class BSrc, class Ring, class Epi, class Prev>
+template <int NK, int NC, bool kBias, int NCC = NC, int NKC = NK, class BSrc, class Ring, class Epi, class Prev>
 __device__ __forceinline__ void h32_layer(const BSrc& bsrc, f32x16 (&acc)[2], Ring& ring, Epi& epi, Prev& prev,
                                           const float* cv, int tid, int lane) {
   static_assert((NK * NC) % kPeriod == 0, "a layer is a whole number of ring periods");
-  static_assert(NC % 2 == 0 && Prev::kNC % 2 == 0, "the pending last tile of a layer sits in acc[1]");
+  static_assert(Prev::kNC % 2 == 0, "the pending last tile of the previous layer sits in acc[1]");
+  static_assert(NCC >= 1 && NCC <= NC && NKC >= kReadAhead && NKC <= NK, "computed chunks and k-steps");
+  // a position whose fragment is read and multiplied
+  constexpr auto live = [](int p) { return p / NK < NCC && p % NK < NKC; };
   constexpr int N = NK * NC;
   constexpr int R = kReadAhead + 1;
   if constexpr (kBias) acc[0] = cinit_load(cv, 0);
@@ -277,20 +291,23 @@ __device__ __forceinline__ void h32_layer(const BSrc& bsrc, f32x16 (&acc)[2], Ri
   for (int i = 0; i < kReadAhead; ++i) fr[i] = ring.frag(i, lane);  // (cur: already this period's slot)
   static_for<0, N>([&](auto ic) {
     constexpr int i = decltype(ic)::value, c = i / NK, kk = i % NK, pos = i % kPeriod;
-    asm volatile("" ::"v"(fr[i % R]));  // fragment i has landed before more reads issue
+    if constexpr (live(i)) asm volatile("" ::"v"(fr[i % R]));  // fragment i has landed before more reads issue
     constexpr int kLate = Ring::kLatePos;
     if constexpr (pos < 2 || (pos >= kLate && pos < kLate + 2)) {
       // a wave-uniform branch when staggered: the partner's MFMAs keep the pipe busy while one wave issues
       if (kLate == 0 || (pos < 2) == ring.early) ring.dma(pos & 1, tid);
     }
-    if constexpr (i + kReadAhead < N) fr[(i + kReadAhead) % R] = ring.frag((pos + kReadAhead) % kPeriod, lane);
+    if constexpr (i + kReadAhead < N && live(i + kReadAhead))
+      fr[(i + kReadAhead) % R] = ring.frag((pos + kReadAhead) % kPeriod, lane);
     __builtin_amdgcn_sched_barrier(0);
-    uint32_t b[4];
-    bsrc(kk, b);
-    acc[c & 1] = mfma_h32(fr[i % R], b, (kk == 0 && !kBias) ? f32x16{} : acc[c & 1]);
+    if constexpr (live(i)) {
+      uint32_t b[4];
+      bsrc(kk, b);
+      acc[c & 1] = mfma_h32(fr[i % R], b, (kk == 0 && !kBias) ? f32x16{} : acc[c & 1]);
+    }
     if constexpr (c == 0) nst += prev.piece(Prev::kNC - 1, kk, NK);  // the previous layer's last tile (acc[1])
     else nst += epi.piece(c - 1, kk, NK);
-    if constexpr (kBias && c + 1 < NC && kk == cinit_pos(NK)) acc[(c + 1) & 1] = cinit_load(cv, c + 1);
+    if constexpr (kBias && c + 1 < NCC && kk == cinit_pos(NK)) acc[(c + 1) & 1] = cinit_load(cv, c + 1);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (pos == kBarrierPos) {  // the next period's reads start at the next position
       ring.end_period(nst);

@@ -148,8 +148,8 @@ def _fullsize(gpu, oracle, name, kind, n, samples, precision, **opts):
 def test_f16_gradients_mask_free(gpu, oracle, name, kind, n, samples):
     """All 22 F16 gradient tensors vs an fp64 oracle run that makes its own fp64 z > 0 decisions.  The F16
     pre-activations are rounded to fp16 before the ReLU, so a unit with |z| within fp16 rounding of 0 may
-    gate the other way; no decision is adopted here, so the per-tensor bound (f16_grad_tol, conftest.py: W0
-    6e-3, every other tensor 2e-3) covers those flips as well; the whole arena within 2e-3."""
+    gate the other way; no decision is adopted here, so the per-tensor bound (f16_grad_tol, conftest.py: W0 and
+    b0 6e-3, every other tensor 2e-3) covers those flips as well; the whole arena within 2e-3."""
     import nof
 
     seed, step, base = 0x5EED0000 + int(name[-1]), 5, 0

@@ -19,7 +19,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import f16_grad_tol, rel_l2
+from conftest import F16_L0_TENSORS, f16_grad_tol, rel_l2
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -66,7 +66,7 @@ def test_hip_step_matches_golden_fixture(gpu, precision):
     assert abs(model.loss() - float(g["loss"])) <= tol * abs(float(g["loss"]))
     G = nof.to_numpy(model.mlp.flat_grads()[0], (P,))
     sizes = model.GetLayerSizes()
-    # per tensor: the F16 mode's W0 bound apart (f16_grad_tol), every other tensor at the mode's tolerance
+    # per tensor: the F16 mode's layer-0 bound apart (f16_grad_tol), every other tensor at the mode's tolerance
     tol_of = (lambda i: f16_grad_tol(i)) if precision == 4 else (lambda i: GRAD_TOLS[precision])
     idx = g["grad_idx"]
     owner = np.searchsorted(np.cumsum(sizes), idx, side="right")  # the tensor of each sampled entry
@@ -75,12 +75,14 @@ def test_hip_step_matches_golden_fixture(gpu, precision):
     print(f"precision {precision}: per-tensor norm differences {' '.join(f'{x:.1e}' for x in rel)}")
     for i, e in enumerate(rel):
         assert e < tol_of(i), f"gradient tensor {i} norm: relative difference {e:.3g}"
-    # the sampled entries: W0's apart in the F16 mode — on two rays a single fp16 ReLU flip moves a few of its
-    # sampled entries by O(1) relative (measured 3.2e-2 over its ~180 entries; its norm is bounded above)
+    # the 4 096 sampled entries, elementwise: on two rays a single fp16 ReLU flip moves individual entries by
+    # O(1) relative, most of all layer 0's (W0's ~180 sampled entries: 3.2e-2), so in the F16 mode the
+    # per-tensor bound applies to the norms above and the entries outside layer 0 are bounded at 5e-3
+    # (measured 3.0e-3); every other mode holds its tolerance elementwise
     e = rel_l2(G[idx], g["grad_vals"])
-    rest = owner != 0 if precision == 4 else np.ones(idx.shape, bool)
+    rest = ~np.isin(owner, F16_L0_TENSORS) if precision == 4 else np.ones(idx.shape, bool)
     e_rest = rel_l2(G[idx[rest]], g["grad_vals"][rest])
-    print(f"precision {precision}: sampled gradients rel L2 {e:.2e}, without W0's {e_rest:.2e}; norms worst "
+    print(f"precision {precision}: sampled gradients rel L2 {e:.2e}, outside layer 0 {e_rest:.2e}; norms worst "
           f"{float(np.max(rel)):.2e}")
-    assert e_rest < GRAD_TOLS[precision], f"sampled gradient entries: rel L2 {e_rest:.3g}"
+    assert e_rest < (5e-3 if precision == 4 else GRAD_TOLS[precision]), f"sampled gradient entries: rel L2 {e_rest:.3g}"
     model.close()

@@ -126,8 +126,9 @@ __device__ __forceinline__ void g_store(float (*dst)[kGS], const GPlan<T>& pl, c
 // (256, 2): at least two waves per SIMD, so the accumulators live in VGPRs, not AGPRs (no accvgpr copies;
 // measured configs[0] step 6.52 -> 6.41 ms; k-steps of 32 instead of 16: 7.42 ms, and 9.59 ms against
 // 6.32 ms once the loads run two k-steps ahead: 256 VGPRs, so the occupancy falls to two waves per SIMD)
-template <int TN, bool TWO>
+template <int TN, bool TWO, bool MASK>  // MASK: the dX GEMMs' ReLU-mask epilogue (a.G), 64-column tiles only
 __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
+  static_assert(!MASK || TN == 64, "the mask epilogue is the 64-column tiles'");
   constexpr int NQ = TN / 32;  // 16-wide MFMA tiles per wave along j
   // k-steps of loads in flight: 3 or 4 at TN 64 (116 / 124 VGPRs, occupancy unchanged) ran the configs[0]
   // step 6.23 -> 6.40 / 6.44 ms; 3 at TN 128 takes 175 VGPRs (two waves per SIMD)
@@ -151,6 +152,8 @@ __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
   for (int p = 0; p < 2; ++p)
 #pragma unroll
     for (int q = 0; q < NQ; ++q) acc[p][q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  // lane rows i = ib + 16 p + r, columns j = jb + 16 q (the epilogue's)
+  const int ib = i0 + wi + 4 * (lane >> 4), jb = j0 + wj + (lane & 15);
   // row sums of A over this chunk's k (the bias gradient beside a weight gradient): the first column
   // tile's wave 0, one row per lane, from the LDS tile, in k order
   const bool rowsum = a.rowsum && tcol == 0 && wave == 0;
@@ -201,11 +204,26 @@ __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
 #pragma unroll
     for (int s = 0; s < kGD; ++s)
       if (k0 + s * kGK < ke) step(k0 + s * kGK, s);
+  // the dX GEMMs' ReLU mask (G > 0: the forward activation): all 16 loads issued together before the
+  // epilogue uses any (per element, beside its use, they were dependent loads one after another: the dX
+  // GEMMs 200 us against 136 us for forward GEMMs of the same shape; configs[0] step 5.16 -> 4.72 ms).
+  // Issued before the k loop instead they held 16 more registers through it: a wave per SIMD less, 10 % slower
+  float gv[MASK ? NQ : 1][2][4];
+  if constexpr (MASK) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t i = min(ib + 16 * p + r, a.M - 1), j = min(jb + 16 * q, a.N - 1);
+          gv[q][p][r] = a.G[i * a.gi + j * a.gj];
+        }
+  }
   if (rowsum && i0 + lane < a.M) a.rowsum[(int64_t)blockIdx.z * a.M + i0 + lane] = rs;
   float* C = a.C + (int64_t)blockIdx.z * a.slab_stride;
-  // lane rows i = ib + 16 p + r, columns j = jb + 16 q: one 64-bit row offset per lane, wave-uniform steps
-  const int ib = i0 + wi + 4 * (lane >> 4), jb = j0 + wj + (lane & 15);
-  const int64_t crow = (int64_t)ib * a.ci, grow = (int64_t)ib * a.gi;
+  // one 64-bit row offset per lane, wave-uniform steps
+  const int64_t crow = (int64_t)ib * a.ci;
   float bj[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) bj[q] = a.bias && jb + 16 * q < a.N ? a.bias[jb + 16 * q] : 0.0f;
@@ -213,7 +231,7 @@ __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
   for (int q = 0; q < NQ; ++q) {
     const int j = jb + 16 * q;
     if (j >= a.N) continue;
-    const int64_t cj = (int64_t)j * a.cj, gj = (int64_t)j * a.gj;
+    const int64_t cj = (int64_t)j * a.cj;
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -222,7 +240,8 @@ __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
         float v = acc[p][q][r];
         if (a.bias) v += bj[q];
         if (a.relu) v = fmaxf(v, 0.0f);
-        if (a.G && !(a.G[grow + (int64_t)(16 * p + r) * a.gi + gj] > 0.0f)) v = 0.0f;
+        if constexpr (MASK)
+          if (!(gv[q][p][r] > 0.0f)) v = 0.0f;
         C[crow + (int64_t)(16 * p + r) * a.ci + cj] = v;
       }
   }
@@ -325,18 +344,22 @@ hipError_t launch_gemm(const GemmArgs& a, int ksplit, hipStream_t st) {
   // occupancy wins), and addresses recomputed per k-step instead of per-element row pointers 6.52 -> 6.84
   // ms per configs[0] step
   const bool wide = a.N > 64 && ksplit > 1;
+  if (wide && a.G) return hipErrorInvalidValue;  // the mask epilogue is the 64-column tiles' (k_gemm)
   const int TN = wide ? 128 : 64;
   const int64_t tiles = (int64_t)((a.N + TN - 1) / TN) * ((a.M + kGT - 1) / kGT);
   if (tiles > 0x7fffffff || ksplit > 65535) return hipErrorInvalidValue;
   const dim3 grid((unsigned)tiles, 1, ksplit);
   const bool two = a.K2 > 0;
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(kGThreads), 0, st, a); };
+  const bool mask = a.G != nullptr;
   if (two) {
-    if (wide) go(k_gemm<128, true>);
-    else go(k_gemm<64, true>);
+    if (wide) go(k_gemm<128, true, false>);
+    else if (mask) go(k_gemm<64, true, true>);
+    else go(k_gemm<64, true, false>);
   } else {
-    if (wide) go(k_gemm<128, false>);
-    else go(k_gemm<64, false>);
+    if (wide) go(k_gemm<128, false, false>);
+    else if (mask) go(k_gemm<64, false, true>);
+    else go(k_gemm<64, false, false>);
   }
   return hipGetLastError();
 }

@@ -135,6 +135,8 @@ EDITS = {
                     "  for (int i = 0; i < R; ++i) fr[i] = ring.frag(i, lane);"),
                    (K + "mlp_h32.h", "    if constexpr (i + kReadAhead < N) fr[(i + kReadAhead) % R] = ring.frag((pos + kReadAhead) % kPeriod, lane);",
                     "    if constexpr (i + kReadAhead < N) asm volatile(\"\" : \"+v\"(fr[(i + kReadAhead) % R]));")],
+    # any-shape GEMM: the mask-epilogue GEMM at the plain launch bounds (131 VGPRs, three waves per SIMD)
+    "g_mask_lb2": [(K + "generic.hip", "__launch_bounds__(kGThreads, MASK && !TWO ? 4 : 2)", "__launch_bounds__(kGThreads, 2)")],
     "h32_nomask": [(K + "mlp_h32.h", "__device__ __forceinline__ uint32_t mask_shift(uint32_t w, uint32_t relu) {\n  uint32_t b, r;",
                     "__device__ __forceinline__ uint32_t mask_shift(uint32_t w, uint32_t relu) {\n  return w ^ relu;\n  uint32_t b, r;")],
     "h32_prio": [(K + "mlp_f16.hip", "  ring.prologue(a.wimg, kFwdFrags * kFragFloats, tid);",

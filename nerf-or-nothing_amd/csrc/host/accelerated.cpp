@@ -819,6 +819,8 @@ void AcceleratedMLP::gen_alloc() {
     G.h.alloc((size_t)gD_ * M * gW_);
     G.hc.alloc((size_t)gDc_ * M * gWc_);
     G.z.alloc(4 * M);
+    G.mbits.alloc((size_t)(gD_ + gDc_) * M * 4);
+    G.mb_ok.assign(gD_ + gDc_, 0);
     L.sigma.alloc(M);
     L.rgb.alloc(3 * M);
     max_M_ = std::max(max_M_, L.cap);
@@ -866,6 +868,17 @@ void AcceleratedMLP::gen_wgrad(float* dst, int64_t ld, const float* dz, int64_t 
   if (bias_dst) NOF_HIP(nof::launch_slab_sum(1, nout, nout, ks, bias_part, nout, bias_dst, nout, accumulate, st_));
 }
 
+bool AcceleratedMLP::gen_gemm(nof::GemmArgs a) {
+  if (nof::gemm_ws_fits(a)) {
+    NOF_HIP(nof::launch_gemm_ws(a, st_));
+    return true;
+  }
+  NOF_REQUIRE(!a.mask_in, "a ReLU-bit mask needs the weight-stationary kernel");
+  a.mask_out = nullptr;
+  gemm1(a, st_);
+  return false;
+}
+
 void AcceleratedMLP::gen_forward(int level, const float* ep, const float* ed) {
   Level& L = lv_[level];
   GenLevel& G = gl_[level];
@@ -874,6 +887,7 @@ void AcceleratedMLP::gen_forward(int level, const float* ep, const float* ed) {
   const float* prm = params_.p;
   auto H = [&](int l) { return G.h.p + (size_t)l * M * W; };
   auto Hc = [&](int i) { return G.hc.p + (size_t)i * M * Wc; };
+  auto MB = [&](int l) { return G.mbits.p + (size_t)l * M * 4; };  // trunk l, then condition D + i
   tb(kTMlpFwd);
   for (int l = 0; l < D; ++l) {  // trunk (MLPcs:90-100): [h | IPE] into every skip-th layer after the first
     nof::GemmArgs a;
@@ -888,7 +902,8 @@ void AcceleratedMLP::gen_forward(int level, const float* ep, const float* ed) {
     a.B2 = gsrc(prm + woff_[l] + a.K1, in_[l], 1);
     a.bias = prm + boff_[l]; a.relu = 1;
     a.C = H(l); a.ci = W; a.cj = 1;
-    gemm1(a, st_);
+    a.mask_out = MB(l);
+    G.mb_ok[l] = gen_gemm(a);
   }
   {  // density head (MLPcs:101): z[:, 0]
     nof::GemmArgs a;
@@ -897,7 +912,7 @@ void AcceleratedMLP::gen_forward(int level, const float* ep, const float* ed) {
     a.B1 = gsrc(prm + woff_[D], W, 1);
     a.bias = prm + boff_[D];
     a.C = G.z.p; a.ci = 4; a.cj = 1;
-    gemm1(a, st_);
+    gen_gemm(a);
   }
   for (int i = 0; i < Dc; ++i) {  // view layer [h | view PE of the ray] (MLPcs:102-106), condition layers
     const int l = D + 1 + i;
@@ -913,7 +928,8 @@ void AcceleratedMLP::gen_forward(int level, const float* ep, const float* ed) {
     a.B2 = gsrc(prm + woff_[l] + a.K1, in_[l], 1);
     a.bias = prm + boff_[l]; a.relu = 1;
     a.C = Hc(i); a.ci = Wc; a.cj = 1;
-    gemm1(a, st_);
+    a.mask_out = MB(D + i);
+    G.mb_ok[D + i] = gen_gemm(a);
   }
   {  // rgb head (MLPcs:107): z[:, 1..3]
     nof::GemmArgs a;
@@ -922,7 +938,7 @@ void AcceleratedMLP::gen_forward(int level, const float* ep, const float* ed) {
     a.B1 = gsrc(prm + woff_[lr], Wc, 1);
     a.bias = prm + boff_[lr];
     a.C = G.z.p + 1; a.ci = 4; a.cj = 1;
-    gemm1(a, st_);
+    gen_gemm(a);
   }
   NOF_HIP(nof::launch_heads_fwd(M, G.z.p, L.sigma.p, L.rgb.p, cfg_.density_bias, rgb_scale(), cfg_.rgb_padding, st_));
   te(kTMlpFwd);
@@ -940,16 +956,28 @@ void AcceleratedMLP::gen_backward(int level, const float* color_grad, const floa
   auto Hc = [&](int i) { return G.hc.p + (size_t)i * M * Wc; };
   float* dz = gdz_.p;
   float *cur = gd0_.p, *nxt = gd1_.p;
+  auto MB = [&](int l) -> const uint32_t* { return G.mbits.p + (size_t)l * M * 4; };
+  // the masking layer's ReLU: its bits where the forward wrote them (mlay: trunk l, condition D + i) and the
+  // weight-stationary kernel fits the product, else the activation `mask` > 0 (k_gemm)
+  auto masked = [&](nof::GemmArgs a, int mlay, const float* mask, int width) {
+    a.mask_in = MB(mlay);
+    if (G.mb_ok[mlay] && nof::gemm_ws_fits(a)) {
+      NOF_HIP(nof::launch_gemm_ws(a, st_));
+      return;
+    }
+    a.mask_in = nullptr;
+    a.G = mask; a.gi = width; a.gj = 1;
+    gemm1(a, st_);
+  };
   // dX of layer l into C, masked by the activation `mask` > 0: C[m][j] = sum_o dZ[m][o] W_l[o][j]
-  auto dx = [&](const float* dzp, int64_t ldz, int nout, int l, const float* mask, int width, float* C) {
+  auto dx = [&](const float* dzp, int64_t ldz, int nout, int l, int mlay, const float* mask, int width, float* C) {
     if (dry) return;
     nof::GemmArgs a;
     a.M = M; a.N = width; a.K1 = nout;
     a.A1 = gsrc(dzp, ldz, 1);
     a.B1 = gsrc(prm + woff_[l], 1, in_[l]);
-    a.G = mask; a.gi = width; a.gj = 1;
     a.C = C; a.ci = width; a.cj = 1;
-    gemm1(a, st_);
+    masked(a, mlay, mask, width);
   };
   if (!dry) {
     tb(kTMlpBwd);
@@ -957,11 +985,11 @@ void AcceleratedMLP::gen_backward(int level, const float* color_grad, const floa
   }
   // rgb head: dW, db from dz[:, 1..3]; its dX into the last condition layer
   gen_wgrad(gr + woff_[lr], Wc, dz + 1, 4, 3, gsrc(Hc(Dc - 1), 1, Wc), Wc, M, acc, gr + boff_[lr]);
-  dx(dz + 1, 4, 3, lr, Hc(Dc - 1), Wc, cur);
+  dx(dz + 1, 4, 3, lr, D + Dc - 1, Hc(Dc - 1), Wc, cur);
   for (int i = Dc - 1; i >= 1; --i) {  // condition layers
     const int l = D + 1 + i;
     gen_wgrad(gr + woff_[l], Wc, cur, Wc, Wc, gsrc(Hc(i - 1), 1, Wc), Wc, M, acc, gr + boff_[l]);
-    dx(cur, Wc, Wc, l, Hc(i - 1), Wc, nxt);
+    dx(cur, Wc, Wc, l, D + i - 1, Hc(i - 1), Wc, nxt);
     std::swap(cur, nxt);
   }
   // view layer: columns [0, W) against h_{D-1}, [W, W + Vd) against the ray's view PE
@@ -978,9 +1006,8 @@ void AcceleratedMLP::gen_backward(int level, const float* color_grad, const floa
     a.A2 = gsrc(dz, 4, 1);
     a.B1 = gsrc(prm + woff_[D + 1], 1, W + Vd);
     a.B2 = gsrc(prm + woff_[D], 1, 0);
-    a.G = H(D - 1); a.gi = W; a.gj = 1;
     a.C = nxt; a.ci = W; a.cj = 1;
-    gemm1(a, st_);
+    masked(a, D - 1, H(D - 1), W);
     std::swap(cur, nxt);
   }
   for (int l = D - 1; l >= 0; --l) {  // trunk
@@ -992,7 +1019,7 @@ void AcceleratedMLP::gen_backward(int level, const float* color_grad, const floa
       gen_wgrad(gw, P, cur, W, W, gsrc(G.ep, 1, P), P, M, acc, gr + boff_[l]);
     }
     if (l > 0) {
-      dx(cur, W, W, l, H(l - 1), W, nxt);
+      dx(cur, W, W, l, l - 1, H(l - 1), W, nxt);
       std::swap(cur, nxt);
     }
   }

@@ -211,7 +211,14 @@ class AcceleratedMLP {
     DevBuf<float> mean, cov, enc_pos, enc_dir;  // the fused path's encodings ([M][P], [n][Vd])
     DevBuf<float> h, hc, z;                     // trunk [D][M][W], condition [Dc][M][Wc], heads [M][4]
     const float *ep = nullptr, *ed = nullptr;   // the encodings the last forward read (API path: the caller's)
+    // ReLU mask bits of the trunk layers then the condition layers [D + Dc][M][4] (gemm_ws.hip), and which
+    // layers' the last forward wrote (a layer on k_gemm has none: its dX reads the activation instead)
+    DevBuf<uint32_t> mbits;
+    std::vector<char> mb_ok;
   };
+  // an unsplit product: the weight-stationary kernel where the shape fits it (gemm_ws.hip), else k_gemm;
+  // returns whether the weight-stationary kernel ran
+  bool gen_gemm(nof::GemmArgs a);
   std::vector<GenLevel> gl_;
   DevBuf<float> gd0_, gd1_, gdz_, gslab_;  // dZ ping-pong [M][max(W, Wc)], heads dz [M][4], split-K partials
   DevBuf<float> gray_;                    // per-ray sums of the view layer's dZ [rays][Wc]

@@ -179,8 +179,16 @@ struct GemmArgs {
   float* C = nullptr; int64_t ci = 0, cj = 0;
   int kchunk = 0; int64_t slab_stride = 0;
   float* rowsum = nullptr;  // optional: rowsum[z M + i] = sum_{k in chunk z} A(i, k) (bias gradients)
+  // gemm_ws.hip only: the ReLU mask as bits, 4 words per row (word (i, g) bit 4t + r = column 16t + 4g + r):
+  // written by a ReLU product (mask_out), applied by a dX product (mask_in) in place of G
+  const uint32_t* mask_in = nullptr;
+  uint32_t* mask_out = nullptr;
 };
 hipError_t launch_gemm(const GemmArgs& a, int ksplit, hipStream_t st);
+// gemm_ws.hip: the weight-stationary form for N <= 128, 16-padded K1 + K2 <= 160, no split, no G / rowsum
+constexpr int kWsMaxN = 128, kWsMaxK = 160;
+bool gemm_ws_fits(const GemmArgs& a);
+hipError_t launch_gemm_ws(const GemmArgs& a, hipStream_t st);
 // dst[r ld + c] (+)= sum_{z < nz} slabs[z stride + r pitch + c] (a fixed order), r < rows, c < cols
 hipError_t launch_slab_sum(int rows, int cols, int pitch, int nz, const float* slabs, int64_t stride, float* dst,
                            int64_t ld, int accumulate, hipStream_t st);

@@ -137,6 +137,9 @@ EDITS = {
                     "    if constexpr (i + kReadAhead < N) asm volatile(\"\" : \"+v\"(fr[(i + kReadAhead) % R]));")],
     # any-shape GEMM: the mask-epilogue GEMM at the plain launch bounds (131 VGPRs, three waves per SIMD)
     "g_mask_lb2": [(K + "generic.hip", "__launch_bounds__(kGThreads, MASK && !TWO ? 4 : 2)", "__launch_bounds__(kGThreads, 2)")],
+    # weight-stationary GEMM: three / four chunks of activation loads in flight instead of two
+    "ws_pd3": [(K + "gemm_ws.hip", "constexpr int PD = 2;  // chunks of loads in flight", "constexpr int PD = 3;  // chunks of loads in flight")],
+    "ws_pd4": [(K + "gemm_ws.hip", "constexpr int PD = 2;  // chunks of loads in flight", "constexpr int PD = 4;  // chunks of loads in flight")],
     "h32_nomask": [(K + "mlp_h32.h", "__device__ __forceinline__ uint32_t mask_shift(uint32_t w, uint32_t relu) {\n  uint32_t b, r;",
                     "__device__ __forceinline__ uint32_t mask_shift(uint32_t w, uint32_t relu) {\n  return w ^ relu;\n  uint32_t b, r;")],
     "h32_prio": [(K + "mlp_f16.hip", "  ring.prologue(a.wimg, kFwdFrags * kFragFloats, tid);",

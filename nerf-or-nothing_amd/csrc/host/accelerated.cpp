@@ -983,9 +983,9 @@ void AcceleratedMLP::gen_backward(int level, const float* color_grad, const floa
     tb(kTMlpBwd);
     NOF_HIP(nof::launch_heads_bwd(M, density_grad, color_grad, G.z.p, dz, cfg_.density_bias, rgb_scale(), st_));  // MNcs:23-28,184-189
   }
-  // rgb head: dW, db from dz[:, 1..3]; its dX into the last condition layer
-  gen_wgrad(gr + woff_[lr], Wc, dz + 1, 4, 3, gsrc(Hc(Dc - 1), 1, Wc), Wc, M, acc, gr + boff_[lr]);
-  dx(dz + 1, 4, 3, lr, D + Dc - 1, Hc(Dc - 1), Wc, cur);
+  // rgb head: dW, db from dz[:, 0..2] (k_heads_bwd: [dz_rgb, dz_sigma]); its dX into the last condition layer
+  gen_wgrad(gr + woff_[lr], Wc, dz, 4, 3, gsrc(Hc(Dc - 1), 1, Wc), Wc, M, acc, gr + boff_[lr]);
+  dx(dz, 4, 3, lr, D + Dc - 1, Hc(Dc - 1), Wc, cur);
   for (int i = Dc - 1; i >= 1; --i) {  // condition layers
     const int l = D + 1 + i;
     gen_wgrad(gr + woff_[l], Wc, cur, Wc, Wc, gsrc(Hc(i - 1), 1, Wc), Wc, M, acc, gr + boff_[l]);
@@ -998,12 +998,12 @@ void AcceleratedMLP::gen_backward(int level, const float* color_grad, const floa
   if (!dry) NOF_HIP(nof::launch_ray_sum(M / S, S, Wc, cur, Wc, gray_.p, st_));
   gen_wgrad(gr + woff_[D + 1] + W, W + Vd, gray_.p, Wc, Wc, gsrc(G.ed, 1, Vd), Vd, M / S, acc);
   // density head
-  gen_wgrad(gr + woff_[D], W, dz, 4, 1, gsrc(H(D - 1), 1, W), W, M, acc, gr + boff_[D]);
+  gen_wgrad(gr + woff_[D], W, dz + 3, 4, 1, gsrc(H(D - 1), 1, W), W, M, acc, gr + boff_[D]);
   if (!dry) {  // dh_{D-1} = dZ_view W_view[:, :W] + dz_density w_D (MLPcs:148-153, D11), masked
     nof::GemmArgs a;
     a.M = M; a.N = W; a.K1 = Wc; a.K2 = 1;
     a.A1 = gsrc(cur, Wc, 1);
-    a.A2 = gsrc(dz, 4, 1);
+    a.A2 = gsrc(dz + 3, 4, 1);
     a.B1 = gsrc(prm + woff_[D + 1], 1, W + Vd);
     a.B2 = gsrc(prm + woff_[D], 1, 0);
     a.C = nxt; a.ci = W; a.cj = 1;

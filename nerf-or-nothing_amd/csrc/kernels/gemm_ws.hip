@@ -31,10 +31,11 @@ constexpr int kWsRowsPerWave = 32;
 constexpr int kWsRows = 8 * kWsRowsPerWave;  // rows per workgroup iteration
 constexpr int kWsMaxChunks = kWsMaxK / 16;   // 16-wide k-chunks
 
-// 16-byte source: A1 always (sk == 1, si % 4 == 0, K % 4 == 0, 16-byte aligned: gemm_ws_fits), A2 when it
-// satisfies the same; else A2 (sk == 1) by dword loads (the view layer's per-ray PE: 27 features)
-__host__ __device__ inline bool ws_vec(const GemmSrc& s, int K) {
-  return s.sk == 1 && s.si % 4 == 0 && K % 4 == 0 && ((uintptr_t)s.p & 15) == 0;
+// 16-byte source: A1 always (sk == 1, si % 4 == 0, rows of at least K rounded up to 4, 16-byte aligned:
+// gemm_ws_fits; the k past K are zeroed in use), A2 when it satisfies the same; else A2 (sk == 1) by dword loads
+// (the view layer's per-ray PE: 27 features)
+__host__ __device__ inline bool ws_vec(const GemmSrc& s, int K) {  // (a row holds its K rounded up to 4)
+  return s.sk == 1 && s.si % 4 == 0 && s.si >= (K + 3) / 4 * 4 && ((uintptr_t)s.p & 15) == 0;
 }
 
 // NT: n-tiles of 16 columns (N <= 16 NT).  SC1 >= 0: a static chunk shape — K1 = 16 SC1 exactly (no k mask on

@@ -311,6 +311,31 @@ __global__ void k_encode_g(int n, int S, const float* __restrict__ mean, const f
   }
 }
 
+// k_encode_g with four consecutive IPE features per thread (P % 4 == 0): one 16-byte store each, the
+// sample's mean / cov loaded by P / 4 threads instead of P (56 -> __ us per configs[0] level)
+__global__ void k_encode_g4(int n, int S, const float* __restrict__ mean, const float* __restrict__ cov,
+                            const float* __restrict__ d, int min_deg, int P, int Vd, float* __restrict__ enc_pos,
+                            float* __restrict__ enc_dir) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int Q = P / 4;
+  if (gid < (int64_t)n * S * Q) {
+    const int64_t m = gid / Q;
+    const int F = 4 * (int)(gid - m * Q);
+    const float mu[3] = {mean[3 * m], mean[3 * m + 1], mean[3 * m + 2]};
+    const float cv[3] = {cov[3 * m], cov[3 * m + 1], cov[3 * m + 2]};
+    f32x4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = ipe_feature(6 * min_deg + F + r, mu, cv);
+    *reinterpret_cast<f32x4*>(enc_pos + m * P + F) = v;
+  }
+  if (gid < (int64_t)n * Vd) {
+    const int r = (int)(gid / Vd);
+    const int k = (int)(gid - (int64_t)r * Vd);
+    const float dd[3] = {d[3 * r], d[3 * r + 1], d[3 * r + 2]};
+    enc_dir[gid] = dir_feature(k, dd);
+  }
+}
+
 // z = [z_sigma, z_rgb] [M][4] -> sigma = softplus(z_sigma - 1), rgb = sigmoid(z_rgb) 1.002 - 0.001 (MNcs:19-22,151-152)
 __global__ void k_heads_fwd(int M, const float* __restrict__ z, float* __restrict__ sigma, float* __restrict__ rgb,
                             float dbias, float rgb_scale, float rgb_pad) {
@@ -320,16 +345,17 @@ __global__ void k_heads_fwd(int M, const float* __restrict__ z, float* __restric
 #pragma unroll
   for (int c = 0; c < 3; ++c) rgb[3 * m + c] = sigmoid_f(z[4 * m + 1 + c]) * rgb_scale - rgb_pad;
 }
-// dz = [dsigma sigmoid(z_sigma - 1), drgb s (1 - s) 1.002] (MNcs:23-28,184-189; s(1 - s): D28)
+// dz = [drgb s (1 - s) 1.002, dsigma sigmoid(z_sigma - 1)] (MNcs:23-28,184-189; s(1 - s): D28) — the colour
+// terms first, so the RGB head's dX product reads dz rows 16-byte aligned (gemm_ws.hip)
 __global__ void k_heads_bwd(int M, const float* __restrict__ dsigma, const float* __restrict__ drgb,
                             const float* __restrict__ z, float* __restrict__ dz, float dbias, float rgb_scale) {
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= M) return;
-  dz[4 * m] = dsigma[m] * sigmoid_f(z[4 * m] + dbias);
+  dz[4 * m + 3] = dsigma[m] * sigmoid_f(z[4 * m] + dbias);
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     const float s = sigmoid_f(z[4 * m + 1 + c]);
-    dz[4 * m + 1 + c] = drgb[3 * m + c] * (s * (1.0f - s)) * rgb_scale;
+    dz[4 * m + c] = drgb[3 * m + c] * (s * (1.0f - s)) * rgb_scale;
   }
 }
 
@@ -381,6 +407,13 @@ hipError_t launch_ray_sum(int R, int S, int cols, const float* in, int64_t ld, f
 }
 hipError_t launch_encode_g(int n, int S, const float* mean, const float* cov, const float* d, int min_deg, int P, int Vd,
                            float* enc_pos, float* enc_dir, hipStream_t st) {
+  if (P % 4 == 0 && ((uintptr_t)enc_pos & 15) == 0) {
+    const int64_t total = std::max((int64_t)n * S * (P / 4), (int64_t)n * Vd);
+    if (total <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_encode_g4, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, n, S, mean, cov, d, min_deg,
+                       P, Vd, enc_pos, enc_dir);
+    return hipGetLastError();
+  }
   const int64_t total = std::max((int64_t)n * S * P, (int64_t)n * Vd);
   if (total <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_encode_g, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, n, S, mean, cov, d, min_deg,

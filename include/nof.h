@@ -95,12 +95,12 @@ enum { NOF_RAY_CONICAL = 0, NOF_RAY_CYLINDRICAL = 1 };
  *               the weight gradients split into hi + lo again (three v_mfma_f32_32x32x16_f16 per
  *               product).  22 significand bits per operand: the same 1e-5 parity as F32, within fp16's
  *               exponent range (activations below 65504; deltas power-of-2 scaled per level).
- *   F16       : plain fp16 mixed precision (BASELINE config 5's "fp16 activations on MFMA"): the
- *               F16X2 kernels with ONE v_mfma_f32_16x16x32_f16 per product, fp16(weight) x
- *               fp16(activation or scaled delta), fp32 accumulation; fp16 blocks and single-product
- *               weight gradients as F16X2.  Parity: outputs and the integrator adjoint relative L2
- *               <= 2e-3; gradients <= 1e-2 per tensor against fp64 (fp16 pre-activations may gate a
- *               ReLU the other way; measured <= 4.9e-3, W0), <= 2e-3 with the ReLU decisions fixed. */
+ *   F16       : plain fp16 mixed precision (BASELINE config 5's "fp16 activations on MFMA"): ONE
+ *               v_mfma_f32_32x32x16_f16 per product, fp16(weight) x fp16(activation or scaled delta),
+ *               fp32 accumulation; fp16 blocks and single-product weight gradients.  Parity: outputs
+ *               and the integrator adjoint relative L2 <= 2e-3; gradients per tensor against fp64
+ *               <= 2e-3, layer 0's W0 / b0 <= 6e-3 (fp16 pre-activations may gate a ReLU the other
+ *               way; measured <= 4.9e-3, W0), all <= 2e-3 with the ReLU decisions fixed. */
 enum {
   NOF_PRECISION_F32 = 0,
   NOF_PRECISION_F32_SPLIT = 1,

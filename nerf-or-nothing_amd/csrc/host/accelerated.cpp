@@ -830,16 +830,19 @@ void AcceleratedMLP::gen_alloc() {
   gd1_.alloc((size_t)max_M_ * Wm);
   gdz_.alloc((size_t)max_M_ * 4);
   gray_.alloc((size_t)cfg_.max_rays * gWc_);
-  // split-K slabs: the largest block any weight-gradient launch needs, from a dry run of gen_backward at
-  // every level's capacity (the split grows with M up to its tile-count cap, so the capacity bounds every
-  // call): the same call sequence as a step, so a new layer shape cannot outgrow the slab mid-step
+  // split-K slabs: a level's weight gradients each take their own region (their sums run at the end of the
+  // level), sized by a dry run of gen_backward at every level's capacity (the split grows with M up to its
+  // tile-count cap, so the capacity bounds every call): the same call sequence as a step, so a new layer
+  // shape cannot outgrow the slab mid-step; the largest level's total
   size_t slab = 0;
-  wg_need_ = &slab;
   for (int l = 0; l < NL; ++l) {
     Level& L = lv_[l];
+    size_t need = 0;
+    wg_need_ = &need;
     L.M = L.cap; L.n = cfg_.max_rays; L.S = cfg_.num_samples[l];
     gen_backward(l, nullptr, nullptr, 0);
     L.M = L.n = L.S = 0;
+    slab = std::max(slab, need);
   }
   wg_need_ = nullptr;
   gslab_.alloc(std::max<size_t>(slab, 1));
@@ -851,21 +854,23 @@ void AcceleratedMLP::gen_wgrad(float* dst, int64_t ld, const float* dz, int64_t 
   gen_split(nout, ncols, M, &ks, &kc);
   const size_t need = (size_t)ks * nout * (ncols + 1);  // + the bias partials
   if (wg_need_) {  // construction's dry run
-    *wg_need_ = std::max(*wg_need_, need);
+    *wg_need_ += need;
     return;
   }
-  NOF_REQUIRE(need <= gslab_.n, "split-K slabs too small");
+  NOF_REQUIRE(wg_off_ + need <= gslab_.n, "split-K slabs too small");
+  float* slab = gslab_.p + wg_off_;
+  wg_off_ += need;
   nof::GemmArgs a;
   a.M = nout; a.N = ncols; a.K1 = M;
   a.A1 = gsrc(dz, 1, ldz);  // A(o, m) = dZ[m][o]
   a.B1 = x;                 // B(j, m) = X[m][j]
-  a.C = gslab_.p; a.ci = ncols; a.cj = 1;
+  a.C = slab; a.ci = ncols; a.cj = 1;
   a.kchunk = kc; a.slab_stride = (int64_t)nout * ncols;
-  float* bias_part = gslab_.p + (size_t)ks * nout * ncols;  // the bias gradient's per-chunk sums [ks][nout]
+  float* bias_part = slab + (size_t)ks * nout * ncols;  // the bias gradient's per-chunk sums [ks][nout]
   if (bias_dst) a.rowsum = bias_part;
   NOF_HIP(nof::launch_gemm(a, ks, st_));
-  NOF_HIP(nof::launch_slab_sum(nout, ncols, ncols, ks, gslab_.p, a.slab_stride, dst, ld, accumulate, st_));
-  if (bias_dst) NOF_HIP(nof::launch_slab_sum(1, nout, nout, ks, bias_part, nout, bias_dst, nout, accumulate, st_));
+  wg_jobs_.push_back({slab, dst, a.slab_stride, ld, nout, ncols, ncols, ks, accumulate});
+  if (bias_dst) wg_jobs_.push_back({bias_part, bias_dst, nout, nout, 1, nout, nout, ks, accumulate});
 }
 
 bool AcceleratedMLP::gen_gemm(nof::GemmArgs a) {
@@ -979,6 +984,8 @@ void AcceleratedMLP::gen_backward(int level, const float* color_grad, const floa
     a.C = C; a.ci = width; a.cj = 1;
     masked(a, mlay, mask, width);
   };
+  wg_jobs_.clear();
+  wg_off_ = 0;
   if (!dry) {
     tb(kTMlpBwd);
     NOF_HIP(nof::launch_heads_bwd(M, density_grad, color_grad, G.z.p, dz, cfg_.density_bias, rgb_scale(), st_));  // MNcs:23-28,184-189
@@ -1023,7 +1030,11 @@ void AcceleratedMLP::gen_backward(int level, const float* color_grad, const floa
       std::swap(cur, nxt);
     }
   }
-  if (!dry) te(kTMlpBwd);
+  if (!dry) {
+    NOF_HIP(nof::launch_slab_sums(wg_jobs_.data(), (int)wg_jobs_.size(), st_));
+    te(kTMlpBwd);
+  }
+  wg_jobs_.clear();
 }
 
 float* const* AcceleratedMLP::gen_publish(bool buckets) {

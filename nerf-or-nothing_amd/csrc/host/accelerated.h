@@ -228,6 +228,10 @@ class AcceleratedMLP {
   // non-null: gen_backward launches nothing and gen_wgrad records its split-K slab need here instead (the
   // slab is sized at construction by a dry run of the same call sequence a step makes)
   size_t* wg_need_ = nullptr;
+  // the level's slab sums, deferred to the end of gen_backward (one k_slab_sums launch); wg_off_ = the next
+  // weight gradient's slab region (each has its own, so their GEMMs need not wait for the sums)
+  std::vector<nof::SlabJob> wg_jobs_;
+  size_t wg_off_ = 0;
   // a column block of a layer's weight gradient: dst[o ld + j] (+)= sum_m dZ(m, o) X(m, j); bias_dst: the
   // layer's bias gradient sum_m dZ(m, o) too (row sums of the same A tiles)
   void gen_wgrad(float* dst, int64_t ld, const float* dz, int64_t ldz, int nout, nof::GemmSrc x, int ncols, int M,

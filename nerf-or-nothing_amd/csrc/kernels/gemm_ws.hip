@@ -43,7 +43,9 @@ __host__ __device__ inline bool ws_vec(const GemmSrc& s, int K) {  // (a row hol
 // loads of chunk c + PD sit in straight-line code before chunk c's use, so the compiler's vmcnt counts them
 // exactly.  With runtime shapes (SC1 = -1) the wave-uniform branches around each fetch made it wait for
 // vmcnt(0) at every chunk — no loads in flight across chunks (configs[0]'s products: 0.48 of peak).
-template <int NT, int SC1 = -1, int SC2 = 0, bool SV2 = false>
+// T1: a static shape whose last source-1 chunk is partial (K1 < 16 SC1: the RGB head's dX, K1 = 3), masked
+// by selects (no branch around a load).
+template <int NT, int SC1 = -1, int SC2 = 0, bool SV2 = false, bool T1 = false>
 __global__ __launch_bounds__(kWsThreads, 1) void k_gemm_ws(GemmArgs a) {
   __shared__ __attribute__((aligned(16))) float Bs[kWsMaxN * (kWsMaxK + 4)];
   __shared__ __attribute__((aligned(16))) float bias_s[kWsMaxN];
@@ -98,7 +100,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_gemm_ws(GemmArgs a) {
   // use: a clamped load may read anything)
   auto fetch = [&](int c, f32x4 (&v)[2]) {
     if (c < C1) {
-      const int k = 16 * c + 4 * g, kc = kStatic || k < a.K1 ? k : 0;
+      const int k = 16 * c + 4 * g, kc = (kStatic && !T1) || k < a.K1 ? k : 0;
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) v[mt] = *reinterpret_cast<const f32x4*>(a.A1.p + o1[mt] + kc);
     } else {
@@ -150,7 +152,7 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_gemm_ws(GemmArgs a) {
         f32x4 av[2];
         // a whole chunk inside the source: no k mask (static shapes: every source-1 chunk; source 2 always
         // masked, without a branch)
-        if (kStatic ? c < C1 : k0 + 16 <= K) {
+        if (kStatic ? c < C1 && !(T1 && c == C1 - 1) : k0 + 16 <= K) {
 #pragma unroll
           for (int mt = 0; mt < 2; ++mt) av[mt] = buf[c % (PD + 1)][mt];
         } else {
@@ -243,6 +245,9 @@ hipError_t launch_gemm_ws(const GemmArgs& a, hipStream_t st) {
     if (NT == 1 && C1 == 8 && C2 == 0) { hipLaunchKernelGGL((k_gemm_ws<1, 8, 0, false>), grid, dim3(kWsThreads), 0, st, a); return hipGetLastError(); }
     if (NT == 8 && C1 == 8 && C2 == 2 && !v2) { hipLaunchKernelGGL((k_gemm_ws<8, 8, 2, false>), grid, dim3(kWsThreads), 0, st, a); return hipGetLastError(); }
     if (NT == 8 && C1 == 8 && C2 == 1 && !v2) { hipLaunchKernelGGL((k_gemm_ws<8, 8, 1, false>), grid, dim3(kWsThreads), 0, st, a); return hipGetLastError(); }
+  } else if (NT == 8 && C1 == 1 && C2 == 0) {  // the RGB head's dX (K1 = 3)
+    hipLaunchKernelGGL((k_gemm_ws<8, 1, 0, false, true>), grid, dim3(kWsThreads), 0, st, a);
+    return hipGetLastError();
   }
   switch ((a.N + 15) / 16) {
     case 1: hipLaunchKernelGGL(k_gemm_ws<1>, grid, dim3(kWsThreads), 0, st, a); break;

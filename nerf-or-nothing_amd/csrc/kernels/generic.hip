@@ -9,7 +9,8 @@
 //     k ([h | IPE] skip inputs, [h | view PE] with the view PE per ray) and a source index may be divided
 //     (per-ray operands); epilogue: bias, ReLU, or the ReLU mask of another matrix (the backward's
 //     relu'(z) as activation > 0), or a raw split-K partial (weight gradients: k = samples);
-//   * k_slab_sum: the split-K partials summed in fixed order (deterministic, no atomics), added to or
+//   * k_slab_sum / k_slab_sums: the split-K partials summed in fixed order (deterministic, no atomics;
+//     k_slab_sums: a level's whole list of them in one launch), added to or
 //     overwriting the gradient arena;
 //   * k_ray_sum: dZ summed over each ray's samples, for the per-ray view PE's weight gradient;
 //   * k_encode_g / k_heads_fwd / k_heads_bwd: the encodings at any degree range (MH:337-356, 429-449) and
@@ -250,11 +251,12 @@ __global__ __launch_bounds__(kGThreads, 2) void k_gemm(GemmArgs a) {
 // dst[r ld + c] (+)= sum over slabs z = 0 .. nz - 1 of slabs[z][r pitch + c] (z order within each of 4
 // interleaved partitions z = p mod 4, then the partitions 0..3 in order: a fixed order per shape).
 // A block: 64 elements x 4 partitions.
-__global__ __launch_bounds__(256) void k_slab_sum(int rows, int cols, int pitch, int nz, const float* __restrict__ slabs,
-                                                  int64_t stride, float* __restrict__ dst, int64_t ld, int accumulate) {
+__device__ __forceinline__ void slab_sum_block(int blk, int rows, int cols, int pitch, int nz,
+                                               const float* __restrict__ slabs, int64_t stride, float* __restrict__ dst,
+                                               int64_t ld, int accumulate) {
   __shared__ float part[4][64];
   const int t = threadIdx.x & 63, p = threadIdx.x >> 6;
-  const int64_t e = (int64_t)blockIdx.x * 64 + t;
+  const int64_t e = (int64_t)blk * 64 + t;
   const bool live = e < (int64_t)rows * cols;
   const int64_t r = live ? e / cols : 0;
   const int64_t off = r * pitch + (live ? e - r * cols : 0);
@@ -273,6 +275,28 @@ __global__ __launch_bounds__(256) void k_slab_sum(int rows, int cols, int pitch,
     float* o = dst + r * ld + (e - r * cols);
     *o = accumulate ? *o + tot : tot;
   }
+}
+
+__global__ __launch_bounds__(256) void k_slab_sum(int rows, int cols, int pitch, int nz, const float* __restrict__ slabs,
+                                                  int64_t stride, float* __restrict__ dst, int64_t ld, int accumulate) {
+  slab_sum_block(blockIdx.x, rows, cols, pitch, nz, slabs, stride, dst, ld, accumulate);
+}
+
+// A level's slab sums in one launch (the any-shape backward defers them to its end: each weight gradient
+// has its own slab region, and no two jobs write the same element, so every element's order is unchanged).
+// Job j owns blocks [b.first[j], b.first[j + 1]); the selects run over static indices, so the table stays
+// in the kernel arguments (scalar loads) instead of being copied to scratch by a dynamic index.
+__global__ __launch_bounds__(256) void k_slab_sums(SlabBatch b) {
+  const int blk = blockIdx.x;
+  int j = 0;
+#pragma unroll
+  for (int i = 1; i < kSlabJobsMax; ++i) j = (i < b.n && blk >= b.first[i]) ? i : j;
+  SlabJob s = b.job[0];
+  int first = b.first[0];
+#pragma unroll
+  for (int i = 1; i < kSlabJobsMax; ++i)
+    if (i == j) { s = b.job[i]; first = b.first[i]; }
+  slab_sum_block(blk - first, s.rows, s.cols, s.pitch, s.nz, s.slabs, s.stride, s.dst, s.ld, s.accumulate);
 }
 
 // out[r][c] = sum over s = 0 .. S - 1 (in s order) of in[(r S + s) ld + c].  The view PE is constant over a
@@ -389,6 +413,33 @@ hipError_t launch_gemm(const GemmArgs& a, int ksplit, hipStream_t st) {
   }
   return hipGetLastError();
 }
+hipError_t launch_slab_sums(const SlabJob* jobs, int n, hipStream_t st) {
+  SlabBatch b{};
+  int blocks = 0;
+  for (int i = 0; i <= n; ++i) {
+    if (i == n || b.n == kSlabJobsMax) {  // flush
+      if (b.n) {
+        for (int k = b.n; k <= kSlabJobsMax; ++k) b.first[k] = blocks;
+        hipLaunchKernelGGL(k_slab_sums, dim3((unsigned)blocks), dim3(256), 0, st, b);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+      }
+      b = SlabBatch{};
+      blocks = 0;
+      if (i == n) break;
+    }
+    const SlabJob& s = jobs[i];
+    const int64_t ne = (int64_t)s.rows * s.cols;
+    if (ne <= 0) continue;
+    if (s.nz < 1 || s.pitch < s.cols || s.stride < (int64_t)(s.rows - 1) * s.pitch + s.cols || s.ld < s.cols)
+      return hipErrorInvalidValue;
+    b.job[b.n] = s;
+    b.first[b.n++] = blocks;
+    blocks += (int)((ne + 63) / 64);
+  }
+  return hipSuccess;
+}
+
 hipError_t launch_slab_sum(int rows, int cols, int pitch, int nz, const float* slabs, int64_t stride, float* dst,
                            int64_t ld, int accumulate, hipStream_t st) {
   const int64_t n = (int64_t)rows * cols;

@@ -192,6 +192,21 @@ hipError_t launch_gemm_ws(const GemmArgs& a, hipStream_t st);
 // dst[r ld + c] (+)= sum_{z < nz} slabs[z stride + r pitch + c] (a fixed order), r < rows, c < cols
 hipError_t launch_slab_sum(int rows, int cols, int pitch, int nz, const float* slabs, int64_t stride, float* dst,
                            int64_t ld, int accumulate, hipStream_t st);
+// many slab sums (disjoint destinations) in ceil(n / kSlabJobsMax) launches: the table travels in the
+// kernel arguments
+struct SlabJob {
+  const float* slabs;
+  float* dst;
+  int64_t stride, ld;
+  int rows, cols, pitch, nz, accumulate;
+};
+constexpr int kSlabJobsMax = 24;
+struct SlabBatch {
+  SlabJob job[kSlabJobsMax];
+  int first[kSlabJobsMax + 1];
+  int n;
+};
+hipError_t launch_slab_sums(const SlabJob* jobs, int n, hipStream_t st);
 // IPE at degrees [min_deg, min_deg + P / 6) per sample, view PE (Vd = 3 + 6 deg_view features) per ray
 // out[r][c] = sum over a ray's S sample rows of in (the per-ray operand's weight gradient over rays)
 hipError_t launch_ray_sum(int R, int S, int cols, const float* in, int64_t ld, float* out, hipStream_t st);

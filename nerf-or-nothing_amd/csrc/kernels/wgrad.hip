@@ -235,6 +235,10 @@ constexpr int kX3RowsPerC = kWgX3Threads / 4;      // concatenated rows one load
 template <int P> constexpr int x3_frag() { return SplitMode<P>::NP * 8 * 64 * 4; }
 template <int P> constexpr int x3_lds() { return 2 * 2 * x3_frag<P>(); }  // 96 KB (bf16x3), 64 KB (f16x2)
 
+// k-steps of fp32 operand loads in flight: three in f16split (HBM-bound: 96 KB per CU in flight instead
+// of 64), two in split (MFMA-bound, and at its register limit)
+template <int PM> constexpr int kX3Depth() { return PM == 2 ? 3 : 2; }
+
 template <int N>
 struct X3Raw {
   f32x4 v[N];  // chunk c: concatenated row kX3RowsPerC c + lrow, chunk lc of the k-step
@@ -387,26 +391,57 @@ __device__ __forceinline__ void wg_item_x3(const WgItem& item, const WgProblem& 
       fa = fn;
     }
   };
-  X3Raw<NCH> s0, s1;
-  load(0, s0);
-  load(min(1, K - 1), s1);
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) split_chunk(s0, 0, c, true);
-  load(min(2, K - 1), s0);
-  lds_barrier();
-  // at step k the sets hold k + 1 (split now, then refilled with k + 3) and k + 2
   int k = 0;
-  for (; k + 2 <= K; k += 2) {
-    step(k, s1);
-    load(min(k + 3, K - 1), s1);
+  if constexpr (kX3Depth<PM>() == 3) {
+    // three register sets: at step k they hold k + 1 (split now, then refilled with k + 4), k + 2, k + 3
+    X3Raw<NCH> s0, s1, s2;
+    load(0, s0);
+    load(min(1, K - 1), s1);
+    load(min(2, K - 1), s2);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) split_chunk(s0, 0, c, true);
+    load(min(3, K - 1), s0);
     lds_barrier();
-    step(k + 1, s0);
-    load(min(k + 4, K - 1), s0);
+    for (; k + 3 <= K; k += 3) {
+      step(k, s1);
+      load(min(k + 4, K - 1), s1);
+      lds_barrier();
+      step(k + 1, s2);
+      load(min(k + 5, K - 1), s2);
+      lds_barrier();
+      step(k + 2, s0);
+      load(min(k + 6, K - 1), s0);
+      lds_barrier();
+    }
+    if (k < K) {
+      step(k, s1);
+      lds_barrier();
+      if (k + 1 < K) {
+        step(k + 1, s2);
+        lds_barrier();
+      }
+    }
+  } else {
+    X3Raw<NCH> s0, s1;
+    load(0, s0);
+    load(min(1, K - 1), s1);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) split_chunk(s0, 0, c, true);
+    load(min(2, K - 1), s0);
     lds_barrier();
-  }
-  if (k < K) {
-    step(k, s1);
-    lds_barrier();
+    // at step k the sets hold k + 1 (split now, then refilled with k + 3) and k + 2
+    for (; k + 2 <= K; k += 2) {
+      step(k, s1);
+      load(min(k + 3, K - 1), s1);
+      lds_barrier();
+      step(k + 1, s0);
+      load(min(k + 4, K - 1), s0);
+      lds_barrier();
+    }
+    if (k < K) {
+      step(k, s1);
+      lds_barrier();
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // retire the clamped tail loads
   if (active) {

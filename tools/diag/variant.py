@@ -41,6 +41,12 @@ EDITS = {
                   "  const int nblk = a.M / kBlk;\n"
                   "  const int ngroups = (nblk + kH32Waves - 1) / kH32Waves;  // 256 samples (8 blocks) per group")],
     # F16 forward / backward (mlp_h32.h, mlp_f16.hip)
+    # F16 forward without the IPE transcendentals (the encodings' upper bound on overlapping them elsewhere)
+    "h32_noipe": [(K + "mlp_f16.hip",
+                   "        ix[kk][e] = pk_h(ipe_h32(c0, mu_h, nv_h), ipe_h32(c0 + 1, mu_h, nv_h));\n"
+                   "        iy[kk][e] = pk_h(ipe_h32(c1, mu_h, nv_h), ipe_h32(c1 + 1, mu_h, nv_h));",
+                   "        ix[kk][e] = pk_h(mu_h[e % 3], nv_h[(e + kk) % 3]);\n"
+                   "        iy[kk][e] = pk_h(nv_h[e % 3], mu_h[(e + kk) % 3]);")],
     "h32_nodma": [(K + "mlp_h32.h",
                    "    slice16_dma_step(next, lds + ((cur + kDmaAhead) & (kH32Slots - 1)) * kPeriodFloats, tid, step);",
                    "    (void)step; (void)tid;")],

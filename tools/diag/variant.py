@@ -47,6 +47,10 @@ EDITS = {
                    "        iy[kk][e] = pk_h(ipe_h32(c1, mu_h, nv_h), ipe_h32(c1 + 1, mu_h, nv_h));",
                    "        ix[kk][e] = pk_h(mu_h[e % 3], nv_h[(e + kk) % 3]);\n"
                    "        iy[kk][e] = pk_h(nv_h[e % 3], mu_h[(e + kk) % 3]);")],
+    # fp32-block weight gradients (split / f16split): the operand loads non-temporal (streamed once; F16's
+    # LDS-DMA stream runs 6.3 TB/s nt against 5.8 default)
+    "x3_nt": [(K + "wgrad.hip", "      q.v[c] = *(gf4*)((isA ? A : B) + (off[c] ^ par));",
+               "      q.v[c] = __builtin_nontemporal_load((gf4*)((isA ? A : B) + (off[c] ^ par)));")],
     "h32_nodma": [(K + "mlp_h32.h",
                    "    slice16_dma_step(next, lds + ((cur + kDmaAhead) & (kH32Slots - 1)) * kPeriodFloats, tid, step);",
                    "    (void)step; (void)tid;")],

@@ -1005,7 +1005,10 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const WgOut* __restrict__ 
                                                       const float* __restrict__ bias_slabs, int accumulate,
                                                       const uint32_t* __restrict__ amax) {
   const WgOut o = outs[blockIdx.y];
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  // the last x-block of an output sums its bias partials, the others its weight partials: the two chains
+  // run side by side (the bias chain after the weight chain in the same threads was the launch's tail)
+  const bool bias_blk = blockIdx.x == gridDim.x - 1;
+  const int t = bias_blk ? (int)threadIdx.x : blockIdx.x * blockDim.x + threadIdx.x;
   const int ld = probs[o.prob].ntc * 32;
   const int ne = o.nrows * o.ncols;
   constexpr int kU = 8;  // item slabs in flight per step
@@ -1018,7 +1021,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const WgOut* __restrict__ 
   auto slab = [&](int k) { return k < 256 ? s_off[k] : so[k]; };
   auto inv_of = [&](int lev) { return amax ? delta_scale(amax + lev, true) : 1.0f; };  // exact powers of 2
   const bool vec = reduce_vec(o.ncols, o.col_off);
-  if (vec ? 4 * t < ne : t < ne) {
+  if (!bias_blk && (vec ? 4 * t < ne : t < ne)) {
     const int e = vec ? 4 * t : t;
     const int rr = e / o.ncols, cc = e - rr * o.ncols;
     const size_t off = (size_t)(o.row_off + rr) * ld + o.col_off + cc;  // 16-B aligned when vec (ld % 32 == 0)
@@ -1065,7 +1068,7 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const WgOut* __restrict__ 
       dst[0] = acc[0];
     }
   }
-  if (o.bias_dst && t < o.nrows) {
+  if (bias_blk && o.bias_dst && t < o.nrows) {
     float acc = 0.0f;
     int k = 0;
     for (int lev = 0; lev < o.nlev; ++lev) {
@@ -1109,7 +1112,7 @@ hipError_t launch_wgrad_reduce(const WgOut* outs, int nouts, int max_elems, cons
                                const WgProblem* probs, const int64_t* slab_off, const float* slabs,
                                const float* bias_slabs, int accumulate, const uint32_t* amax, hipStream_t st) {
   if (nouts <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3((max_elems + 255) / 256, nouts), dim3(256), 0, st, outs, items, probs,
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((max_elems + 255) / 256 + 1, nouts), dim3(256), 0, st, outs, items, probs,
                      slab_off, slabs, bias_slabs, accumulate, amax);
   return hipGetLastError();
 }

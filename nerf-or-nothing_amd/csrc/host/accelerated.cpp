@@ -1117,20 +1117,25 @@ float* const* AcceleratedMipNeRF::run(int n, const float* o, const float* d, con
   for (int lv = 0; lv < L; ++lv) {  // MNcpp:85-123
     TraceRange lr(kFwd[lv & 3]);
     const int S = cfg_.num_samples[lv];
-    timer.begin(kTSample);
-    if (lv == 0) {
+    if (lv == 0) {  // (levels >= 1: resampled by the previous level's fused integrator launch)
+      timer.begin(kTSample);
       NOF_HIP(nof::launch_sample_stratified(n, S, nears, fars, cfg_.randomized, seed_, step_, 0, ray_base_,
                                             t_[0].p, st_, cfg_.lindisp));
-    } else {
-      NOF_HIP(nof::launch_sample_pdf(n, cfg_.num_samples[lv - 1], t_[lv - 1].p, w_[lv - 1].p, S,
-                                     cfg_.resample_padding, cfg_.randomized, seed_, step_, (uint32_t)lv, ray_base_,
-                                     t_[lv].p, nullptr, st_));
+      timer.end(kTSample);
     }
-    timer.end(kTSample);
     mlp->forward_fused(lv, n, S, t_[lv].p, o, d, radii);
     timer.begin(kTRenderFwd);
-    NOF_HIP(nof::launch_render_fwd(n, S, mlp->density(lv), mlp->rgb(lv), t_[lv].p, d, cfg_.white_bkgd, C_[lv].p,
-                                   w_[lv].p, st_, nullptr, nullptr, mlp->numeric_flags()));
+    if (lv + 1 < L) {  // this level's integrator and the next level's resampler (ResampleAlongRay) in one launch
+      nof::RenderPdfArgs ra{};
+      ra.n = n; ra.S = S; ra.sigma = mlp->density(lv); ra.rgb = mlp->rgb(lv); ra.t = t_[lv].p; ra.d = d;
+      ra.white = cfg_.white_bkgd; ra.C = C_[lv].p; ra.w = w_[lv].p; ra.nonfinite = mlp->numeric_flags();
+      ra.S_out = cfg_.num_samples[lv + 1]; ra.padding = cfg_.resample_padding; ra.randomized = cfg_.randomized;
+      ra.seed = seed_; ra.step = step_; ra.level = (uint32_t)(lv + 1); ra.ray_base = ray_base_; ra.t_out = t_[lv + 1].p;
+      NOF_HIP(nof::launch_render_fwd_pdf(ra, st_));
+    } else {
+      NOF_HIP(nof::launch_render_fwd(n, S, mlp->density(lv), mlp->rgb(lv), t_[lv].p, d, cfg_.white_bkgd, C_[lv].p,
+                                     w_[lv].p, st_, nullptr, nullptr, mlp->numeric_flags()));
+    }
     timer.end(kTRenderFwd);
   }
   // MNcpp:125-134: the loss gradient and the integrator adjoint of every level (with the f16 modes' delta

@@ -37,6 +37,22 @@ hipError_t launch_encode(int n, int S, const float* mean, const float* cov, cons
 hipError_t launch_render_fwd(int n, int S, const float* sigma, const float* rgb, const float* t, const float* d,
                              int white, float* C, float* w, hipStream_t st, float* acc = nullptr,
                              float* dist = nullptr, uint32_t* nonfinite = nullptr);
+// the training forward's integrator of a level (as launch_render_fwd, no acc / dist) and the resampler of
+// the next level (as launch_sample_pdf, no idx) in one launch, one ray per workgroup
+struct RenderPdfArgs {
+  int n, S;  // rays, samples of this level (the resampler's input bins)
+  const float *sigma, *rgb, *t, *d;
+  int white;
+  float *C, *w;
+  uint32_t* nonfinite;
+  int S_out;  // the next level's samples
+  float padding;
+  int randomized;
+  uint64_t seed;
+  uint32_t step, level, ray_base;  // level: the next level's index (its Philox stream)
+  float* t_out;
+};
+hipError_t launch_render_fwd_pdf(const RenderPdfArgs& a, hipStream_t st);
 // g_ext != null: dL/dC supplied by the caller (callback path); else fused loss gradient from pix.
 hipError_t launch_render_bwd(int n, int S, const float* sigma, const float* rgb, const float* t, const float* d,
                              int white, const float* C, const float* g_ext, const float* pix,

@@ -8,6 +8,7 @@
 // math per CachedVolumetricRendering / VolumetricRenderingGradient (MH:494-610).
 #include "common.h"
 #include "launch.h"
+#include "resample.h"
 
 namespace nof {
 
@@ -101,15 +102,15 @@ __device__ inline void ray_alpha_T(int S, int r, int lane, const float* __restri
   }
 }
 
+// one ray's composite by one wave; stage_w / stage_t (LDS, or null): the ray's weights and t row also
+// staged for the resampler (k_render_fwd_pdf)
 template <int PER>
-__global__ __launch_bounds__(256) void k_render_fwd(int n, int S, const float* __restrict__ sigma,
-                                                    const float* __restrict__ rgb, const float* __restrict__ t,
-                                                    const float* __restrict__ d, int white, float* __restrict__ C,
-                                                    float* __restrict__ w, float* __restrict__ acc_out,
-                                                    float* __restrict__ dist_out, uint32_t* __restrict__ nonfinite) {
-  const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= n) return;  // wave-uniform; no block barriers below
+__device__ __forceinline__ void render_fwd_ray(int r, int lane, int S, const float* __restrict__ sigma,
+                                               const float* __restrict__ rgb, const float* __restrict__ t,
+                                               const float* __restrict__ d, int white, float* __restrict__ C,
+                                               float* __restrict__ w, float* __restrict__ acc_out,
+                                               float* __restrict__ dist_out, uint32_t* __restrict__ nonfinite,
+                                               float* stage_w, float* stage_t) {
   RayState<PER> rs;
   ray_alpha_T<PER>(S, r, lane, sigma, t, d, rs);
   const int k0 = lane * PER;
@@ -126,6 +127,14 @@ __global__ __launch_bounds__(256) void k_render_fwd(int n, int S, const float* _
     if (dist_out) wd += wk[p] * (rs.tv[p] + rs.tv[p + 1]) / 2.0f;  // weighted midpoint (MH:488)
   }
   vstore<PER, PER>(w + (size_t)r * S + k0, wk);
+  if (stage_w) {
+#pragma unroll
+    for (int p = 0; p < PER; ++p) {
+      stage_w[k0 + p] = wk[p];
+      stage_t[k0 + p] = rs.tv[p];
+    }
+    if (lane == 63) stage_t[S] = rs.tv[PER];
+  }
   if (nonfinite) {  // an inf sigma (fp16 overflow upstream) gives alpha = 1 and a finite colour: check inputs
     float in = rs.sg_sum;
 #pragma unroll
@@ -146,6 +155,34 @@ __global__ __launch_bounds__(256) void k_render_fwd(int n, int S, const float* _
       dist_out[r] = fminf(fmaxf(dv, t0), tS);
     }
   }
+}
+
+template <int PER>
+__global__ __launch_bounds__(256) void k_render_fwd(int n, int S, const float* __restrict__ sigma,
+                                                    const float* __restrict__ rgb, const float* __restrict__ t,
+                                                    const float* __restrict__ d, int white, float* __restrict__ C,
+                                                    float* __restrict__ w, float* __restrict__ acc_out,
+                                                    float* __restrict__ dist_out, uint32_t* __restrict__ nonfinite) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= n) return;  // wave-uniform; no block barriers below
+  render_fwd_ray<PER>(r, lane, S, sigma, rgb, t, d, white, C, w, acc_out, dist_out, nonfinite, nullptr, nullptr);
+}
+
+// The training forward's integrator of level l and the resampler of level l + 1 in one launch (one ray per
+// 64-lane workgroup): the ray's weights and t row go to the resampler's LDS straight from the composite's
+// registers — the same values k_sample_pdf would load back, so the same t and idx (render_fwd_ray is the
+// code k_render_fwd runs: the composite's bits are unchanged too).  One launch fewer per level transition.
+template <int PER>
+__global__ __launch_bounds__(64) void k_render_fwd_pdf(RenderPdfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ float s_wsum;
+  const int r = blockIdx.x, lane = threadIdx.x, B = a.S;
+  render_fwd_ray<PER>(r, lane, B, a.sigma, a.rgb, a.t, a.d, a.white, a.C, a.w, nullptr, nullptr, a.nonfinite,
+                      smem + B, smem + 2 * B + 1);
+  __syncthreads();
+  resample_staged(r, lane, B, smem, &s_wsum, a.S_out, a.padding, a.randomized, a.seed, a.step, a.level, a.ray_base,
+                  a.t_out, nullptr);
 }
 
 // dL/dc_k = g w_k ;  dL/dsigma_k = delta_k |d| [T_{k+1} e_k - sum_{j>k} w_j e_j],  e_k = g.c_k - G
@@ -255,6 +292,13 @@ hipError_t launch_render_fwd(int n, int S, const float* sigma, const float* rgb,
   const dim3 grid((n + 3) / 4), block(256);
   NOF_RENDER_DISPATCH(S, hipLaunchKernelGGL(k_render_fwd<PER>, grid, block, 0, st, n, S, sigma, rgb, t, d, white, C, w,
                                             acc, dist, nonfinite));
+  return hipGetLastError();
+}
+
+hipError_t launch_render_fwd_pdf(const RenderPdfArgs& a, hipStream_t st) {
+  if (a.n <= 0) return hipSuccess;
+  const size_t shm = sizeof(float) * (3 * a.S + 2);
+  NOF_RENDER_DISPATCH(a.S, hipLaunchKernelGGL(k_render_fwd_pdf<PER>, dim3(a.n), dim3(64), shm, st, a));
   return hipGetLastError();
 }
 

@@ -9,6 +9,7 @@
 #include "common.h"
 #include "geometry.h"
 #include "launch.h"
+#include "resample.h"
 
 #pragma clang fp contract(off)
 
@@ -43,27 +44,14 @@ __global__ void k_sample_stratified(int n, int S, const float* __restrict__ near
   t[gid] = ti;
 }
 
-// One 64-lane workgroup per ray.  LDS: wb[B] then cdf[B+1].
-// the sequential fp32 cdf of a pdf row (lane 0).  pdf and cdf are disjoint LDS rows: restrict lets the
-// compiler issue the pdf reads ahead of the cdf writes (else each read waits for the previous write)
-__device__ __forceinline__ void cdf_chain(const float* __restrict__ pdf, float* __restrict__ cdf, int B) {
-  cdf[0] = 0.0f;
-  float run = 0.0f;
-  for (int i = 0; i < B - 1; ++i) {
-    run = run + pdf[i];
-    cdf[i + 1] = fminf(1.0f, run);
-  }
-  cdf[B] = 1.0f;
-}
-
+// One 64-lane workgroup per ray (resample.h: resample_staged).
 __global__ __launch_bounds__(64) void k_sample_pdf(int n, int B, const float* __restrict__ t_in,
                                                    const float* __restrict__ w, int S_out, float padding,
                                                    int randomized, uint64_t seed, uint32_t step, uint32_t level,
                                                    uint32_t ray_base, float* __restrict__ t_out,
                                                    int32_t* __restrict__ idx_out) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* wb = smem;           // [B]   blurred weights, then pdf
-  float* cdf = smem + B;      // [B+1] (first the input weights, staged)
+  float* cdf = smem + B;      // [B+1] (first the input weights, staged; wb[B] before it)
   float* trs = smem + 2 * B + 1;  // [B+1] the ray's input t row, staged
   __shared__ float s_wsum;
   const int r = blockIdx.x;
@@ -94,59 +82,7 @@ __global__ __launch_bounds__(64) void k_sample_pdf(int n, int B, const float* __
     }
   }
   __syncthreads();
-  // blur-pool: wmax[i] = max(pad[i], pad[i+1]); wb[i] = .5(wmax[i] + wmax[i+1]) + padding (MH:646-661)
-  for (int i = lane; i < B; i += 64) {
-    const float w0 = cdf[i];
-    const float wl = i == 0 ? w0 : cdf[i - 1];
-    const float wh = i == B - 1 ? w0 : cdf[i + 1];
-    const float m0 = fmaxf(wl, w0);
-    const float m1 = fmaxf(w0, wh);
-    wb[i] = 0.5f * (m0 + m1) + padding;
-  }
-  __syncthreads();
-  if (lane == 0) {
-    double acc = 0.0;  // LINQ Sum over float accumulates in double (MH:785)
-    for (int i = 0; i < B; ++i) acc += (double)wb[i];
-    float wsum = (float)acc;
-    const float pad = fmaxf(0.0f, 1e-5f - wsum);
-    if (pad > 0.0f) {
-      const float per = pad / (float)B;
-      for (int i = 0; i < B; ++i) wb[i] = wb[i] + per;
-      wsum = wsum + pad;
-    }
-    s_wsum = wsum;
-  }
-  __syncthreads();
-  const float wsum = s_wsum;
-  for (int i = lane; i < B; i += 64) wb[i] = wb[i] / wsum;   // pdf
-  __syncthreads();
-  if (lane == 0) {  // sequential fp32 cumsum: a parallel scan would change the rounding
-    cdf_chain(wb, cdf, B);
-  }
-  __syncthreads();
-  const int ns = S_out + 1;
-  const float s1 = 1.0f / (float)ns;
-  for (int s = lane; s < ns; s += 64) {
-    float u;
-    if (randomized) {
-      const float rr = philox_uniform(seed, step, level, kStreamPdf, ray_base + (uint32_t)r, (uint32_t)s);
-      u = fminf((float)s * s1 + rr * (s1 - 1e-7f), 1.0f - 1e-7f);
-    } else {
-      u = (float)s * ((1.0f - 1e-7f) / (float)(ns - 1));
-    }
-    int lo = 0, hi = B - 1;  // largest i in [0, B-1] with cdf[i] <= u (cdf[0] = 0 <= u)
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (cdf[mid] <= u) lo = mid; else hi = mid - 1;
-    }
-    NOF_DCHECK(lo >= 0 && lo < B, kChkSampleIdx);  // a bin of the input t row
-    const float b0 = trs[lo], b1 = trs[lo + 1], c0 = cdf[lo], c1 = cdf[lo + 1];
-    const float denom = c1 - c0;
-    float tt = denom > 0.0f ? (u - c0) / denom : 0.0f;
-    tt = fminf(fmaxf(tt, 0.0f), 1.0f);
-    t_out[(size_t)r * ns + s] = b0 + tt * (b1 - b0);
-    if (idx_out) idx_out[(size_t)r * ns + s] = lo;
-  }
+  resample_staged(r, lane, B, smem, &s_wsum, S_out, padding, randomized, seed, step, level, ray_base, t_out, idx_out);
 }
 
 // cast_rays (AF:292-317) as a standalone kernel for the encoded-input API path / parity tests.

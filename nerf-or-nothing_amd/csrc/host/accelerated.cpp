@@ -222,9 +222,10 @@ std::vector<int> AcceleratedMLP::get_layer_sizes() const {
   return s;
 }
 
-void AcceleratedMLP::pack_weights() {
-  if (generic_) return;  // the any-shape path reads the canonical arena directly
+bool AcceleratedMLP::pack_weights(const nof::StratArgs* strat) {
+  if (generic_) return false;  // the any-shape path reads the canonical arena directly
   nof::PackArgs pa;
+  if (strat) pa.strat = *strat;
   for (int l = 0; l < kLayers; ++l) { pa.woff[l] = woff_[l]; pa.boff[l] = boff_[l]; }
   if (f16_pieces()) {  // the step's delta-scale maxima start at 0 (no memset launch per level)
     pa.zero = amax_.p;
@@ -239,6 +240,7 @@ void AcceleratedMLP::pack_weights() {
     NOF_HIP(nof::launch_pack_weights_x3(params_.p, pa, wimg_f_.p, wimg_b_.p, f16_pieces() ? 2 : 1, st_));
   else NOF_HIP(nof::launch_pack_weights(params_.p, pa, wimg_f_.p, wimg_b_.p, st_));
   te(kTPack);
+  return strat != nullptr;
 }
 
 uint32_t* AcceleratedMLP::claim_delta_amax(int level) {
@@ -1113,11 +1115,14 @@ float* const* AcceleratedMipNeRF::run(int n, const float* o, const float* d, con
   static const char* const kBwd[] = {"nof:backward"};
   const int L = cfg_.num_levels;
   TraceRange step_range("nof:get_gradient");
-  mlp->pack_weights();
+  nof::StratArgs sa;  // level 0's t-values, by the pack launch's extra blocks
+  sa.n = n; sa.S = cfg_.num_samples[0]; sa.nears = nears; sa.fars = fars; sa.randomized = cfg_.randomized;
+  sa.lindisp = cfg_.lindisp; sa.seed = seed_; sa.step = step_; sa.ray_base = ray_base_; sa.t = t_[0].p;
+  const bool sampled = mlp->pack_weights(&sa);
   for (int lv = 0; lv < L; ++lv) {  // MNcpp:85-123
     TraceRange lr(kFwd[lv & 3]);
     const int S = cfg_.num_samples[lv];
-    if (lv == 0) {  // (levels >= 1: resampled by the previous level's fused integrator launch)
+    if (lv == 0 && !sampled) {  // (levels >= 1: resampled by the previous level's fused integrator launch)
       timer.begin(kTSample);
       NOF_HIP(nof::launch_sample_stratified(n, S, nears, fars, cfg_.randomized, seed_, step_, 0, ray_base_,
                                             t_[0].p, st_, cfg_.lindisp));

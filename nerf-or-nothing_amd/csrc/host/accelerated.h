@@ -142,7 +142,9 @@ class AcceleratedMLP {
   // fused path (AcceleratedMipNeRF): frustum + IPE computed inside the forward kernel
   void forward_fused(int level, int n, int samples, const float* t, const float* origins, const float* dirs,
                      const float* radii, bool inference = false);
-  void pack_weights();  // rebuild the packed weight images from the canonical arena
+  // rebuild the packed weight images from the canonical arena; strat (optional): level 0's stratified sampling
+  // run by the same launch — returns whether it did (no pack launch on the any-shape path)
+  bool pack_weights(const nof::StratArgs* strat = nullptr);
   const float* density(int level) const { return lv_[level].sigma.p; }
   const float* rgb(int level) const { return lv_[level].rgb.p; }
   KernelTimer* timer = nullptr;

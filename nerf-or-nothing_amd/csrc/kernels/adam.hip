@@ -6,12 +6,16 @@
 // result is bit-identical to oracle/oracle.cpp::orc_adam_step.
 #include "common.h"
 #include "launch.h"
+#include "resample.h"
 #include "mlp_common.h"
 #include "mlp_h32.h"
 
 #pragma clang fp contract(off)
 
 namespace nof {
+
+// 256-thread blocks the pack launch appends for PackArgs::strat (0 when it carries none)
+static int strat_blocks(const StratArgs& z) { return z.n > 0 ? (z.n * (z.S + 1) + 255) / 256 : 0; }
 
 __global__ void k_adam(int64_t n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                        float* __restrict__ v, float lr, float inv1, float inv2) {
@@ -82,6 +86,12 @@ __device__ inline void bwd_slice(int s, int& l, int& o) {
 // backward slice element (row i, col c) = W_l[o + c][i]; both stored at slice_off(r, c).
 __global__ void k_pack_weights(const float* __restrict__ P, PackArgs pa, float* __restrict__ wf,
                                float* __restrict__ wb) {
+  if ((int)blockIdx.x >= pa.pack_blocks) {  // the step's level-0 sampling (PackArgs::strat)
+    const StratArgs& z = pa.strat;
+    stratified_t(((int)blockIdx.x - pa.pack_blocks) * (int)blockDim.x + (int)threadIdx.x, z.n, z.S, z.nears, z.fars,
+                 z.randomized, z.lindisp, z.seed, z.step, 0, z.ray_base, z.t);
+    return;
+  }
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nf = (int64_t)kFwdImageFloats, nb = (int64_t)kBwdImageFloats;
   if (gid < nf) {
@@ -160,6 +170,12 @@ __device__ inline typename SplitMode<P>::V2 split_piece2(float w, int piece) {
 template <int P>
 __global__ void k_pack_weights_x3(const float* __restrict__ P_, PackArgs pa, float* __restrict__ wf,
                                   float* __restrict__ wb) {
+  if ((int)blockIdx.x >= pa.pack_blocks) {  // the step's level-0 sampling (PackArgs::strat)
+    const StratArgs& z = pa.strat;
+    stratified_t(((int)blockIdx.x - pa.pack_blocks) * (int)blockDim.x + (int)threadIdx.x, z.n, z.S, z.nears, z.fars,
+                 z.randomized, z.lindisp, z.seed, z.step, 0, z.ray_base, z.t);
+    return;
+  }
   constexpr int NP = SplitMode<P>::NP;
   constexpr int kChunks = split_slice_floats<P>() / 4;  // fragments of 16 B per slice
   const float* __restrict__ Pp = P_;
@@ -205,9 +221,11 @@ hipError_t launch_pack_weights_x3(const float* params, const PackArgs& pa, float
                                   int precision, hipStream_t st) {
   const int chunks = precision == 2 ? split_slice_floats<2>() / 4 : split_slice_floats<1>() / 4;
   const int64_t total = (int64_t)(kFwdSlices + kBwdSlices) * chunks + kFwdTail + kBwdTail;
-  const dim3 grid((unsigned)((total + 255) / 256));
-  if (precision == 2) hipLaunchKernelGGL(k_pack_weights_x3<2>, grid, dim3(256), 0, st, params, pa, wimg_f, wimg_b);
-  else hipLaunchKernelGGL(k_pack_weights_x3<1>, grid, dim3(256), 0, st, params, pa, wimg_f, wimg_b);
+  PackArgs a = pa;
+  a.pack_blocks = (int)((total + 255) / 256);
+  const dim3 grid((unsigned)(a.pack_blocks + strat_blocks(pa.strat)));
+  if (precision == 2) hipLaunchKernelGGL(k_pack_weights_x3<2>, grid, dim3(256), 0, st, params, a, wimg_f, wimg_b);
+  else hipLaunchKernelGGL(k_pack_weights_x3<1>, grid, dim3(256), 0, st, params, a, wimg_f, wimg_b);
   return hipGetLastError();
 }
 
@@ -221,6 +239,12 @@ hipError_t launch_pack_weights_x3(const float* params, const PackArgs& pa, float
 // k-step 8 holds w8 at o = 128 (the feature the kernel sets to dz_s), k-step 9 is zero padding.
 __global__ void k_pack_weights_h32(const float* __restrict__ P, PackArgs pa, float* __restrict__ wf,
                                    float* __restrict__ wb) {
+  if ((int)blockIdx.x >= pa.pack_blocks) {  // the step's level-0 sampling (PackArgs::strat)
+    const StratArgs& z = pa.strat;
+    stratified_t(((int)blockIdx.x - pa.pack_blocks) * (int)blockDim.x + (int)threadIdx.x, z.n, z.S, z.nears, z.fars,
+                 z.randomized, z.lindisp, z.seed, z.step, 0, z.ray_base, z.t);
+    return;
+  }
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid < pa.nzero) pa.zero[gid] = 0u;
   const int64_t nfc = (int64_t)(kFwdFrags + kStreamPad) * 64, nbc = (int64_t)(kBwdFrags + kStreamPad) * 64;
@@ -266,15 +290,19 @@ __global__ void k_pack_weights_h32(const float* __restrict__ P, PackArgs pa, flo
 hipError_t launch_pack_weights_h32(const float* params, const PackArgs& pa, float* wimg_f, float* wimg_b,
                                    hipStream_t st) {
   const int64_t total = (int64_t)(kFwdFrags + kBwdFrags + 2 * kStreamPad) * 64 + kFwdTail + kBwdTail;
-  hipLaunchKernelGGL(k_pack_weights_h32, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, params, pa, wimg_f,
-                     wimg_b);
+  PackArgs a = pa;
+  a.pack_blocks = (int)((total + 255) / 256);
+  hipLaunchKernelGGL(k_pack_weights_h32, dim3((unsigned)(a.pack_blocks + strat_blocks(pa.strat))), dim3(256), 0, st,
+                     params, a, wimg_f, wimg_b);
   return hipGetLastError();
 }
 
 hipError_t launch_pack_weights(const float* params, const PackArgs& pa, float* wimg_f, float* wimg_b, hipStream_t st) {
   const int64_t total = (int64_t)kFwdImageFloats + (int64_t)kBwdImageFloats;
-  hipLaunchKernelGGL(k_pack_weights, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, params, pa, wimg_f,
-                     wimg_b);
+  PackArgs a = pa;
+  a.pack_blocks = (int)((total + 255) / 256);
+  hipLaunchKernelGGL(k_pack_weights, dim3((unsigned)(a.pack_blocks + strat_blocks(pa.strat))), dim3(256), 0, st,
+                     params, a, wimg_f, wimg_b);
   return hipGetLastError();
 }
 

@@ -256,9 +256,23 @@ constexpr int kLoopMax = 8;
 hipError_t launch_loopback_sum(int k, float* const* bufs, int64_t n, hipStream_t st);
 hipError_t launch_adam(int64_t n, float* p, const float* g, float* m, float* v, float lr, float inv1, float inv2,
                        hipStream_t st);
+// level 0's stratified t-values (k_sample_stratified's arguments), computable by the pack launch's extra blocks
+struct StratArgs {
+  int n = 0, S = 0;  // rays, samples (n = 0: none)
+  const float* nears = nullptr;
+  const float* fars = nullptr;
+  int randomized = 0, lindisp = 0;
+  uint64_t seed = 0;
+  uint32_t step = 0, ray_base = 0;
+  float* t = nullptr;
+};
 struct PackArgs {
   int woff[11]; int boff[11];
   uint32_t* zero = nullptr; int nzero = 0;  // words the pack launch also clears (the f16 modes' delta-scale maxima)
+  // the training step's level-0 sampling rides the pack launch (blocks past the pack's own: one launch fewer
+  // per step; the launch wrappers set pack_blocks)
+  StratArgs strat;
+  int pack_blocks = 0;
 };
 hipError_t launch_pack_weights(const float* params, const PackArgs& pa, float* wimg_f, float* wimg_b, hipStream_t st);
 // split images: precision 1 (bf16 hi/mid/lo) or 2 (f16 hi/lo)

@@ -9,6 +9,38 @@
 
 namespace nof {
 
+// t_k linear in depth (MH:622) or, lindisp, in disparity (MH:618-620: 1 / (1/near (1 - s) + 1/far s))
+__device__ inline float lin_t(int k, int S, float nr, float fr, bool lindisp) {
+#pragma clang fp contract(off)
+  const float tv = (float)k / (float)S;
+  return lindisp ? 1.0f / (1.0f / nr * (1.0f - tv) + 1.0f / fr * tv) : nr * (1.0f - tv) + fr * tv;
+}
+
+// t-value gid = r (S + 1) + i (SampleAlongRay, MH:611-631): t_i = lower_i + (upper_i - lower_i) u_i,
+// lower = [t0, mids], upper = [mids, tS] (D3)
+__device__ __forceinline__ void stratified_t(int gid, int n, int S, const float* __restrict__ nears,
+                                             const float* __restrict__ fars, int randomized, int lindisp,
+                                             uint64_t seed, uint32_t step, uint32_t level, uint32_t ray_base,
+                                             float* __restrict__ t) {
+#pragma clang fp contract(off)
+  if (gid >= n * (S + 1)) return;
+  const int r = gid / (S + 1);
+  const int i = gid - r * (S + 1);
+  const float nr = nears[r], fr = fars[r];
+  float ti;
+  const bool ld = lindisp != 0;
+  if (!randomized) {
+    ti = lin_t(i, S, nr, fr, ld);
+  } else {
+    const float li = lin_t(i, S, nr, fr, ld);
+    const float lower = i == 0 ? li : 0.5f * (lin_t(i - 1, S, nr, fr, ld) + li);
+    const float upper = i == S ? li : 0.5f * (li + lin_t(i + 1, S, nr, fr, ld));
+    const float u = philox_uniform(seed, step, level, kStreamStratified, ray_base + (uint32_t)r, (uint32_t)i);
+    ti = lower + (upper - lower) * u;
+  }
+  t[gid] = ti;
+}
+
 // the sequential fp32 cdf of a pdf row (lane 0).  pdf and cdf are disjoint LDS rows: restrict lets the
 // compiler issue the pdf reads ahead of the cdf writes (else each read waits for the previous write)
 __device__ __forceinline__ void cdf_chain(const float* __restrict__ pdf, float* __restrict__ cdf, int B) {

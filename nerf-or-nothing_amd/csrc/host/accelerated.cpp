@@ -1137,7 +1137,7 @@ float* const* AcceleratedMipNeRF::run(int n, const float* o, const float* d, con
       ra.S_out = cfg_.num_samples[lv + 1]; ra.padding = cfg_.resample_padding; ra.randomized = cfg_.randomized;
       ra.seed = seed_; ra.step = step_; ra.level = (uint32_t)(lv + 1); ra.ray_base = ray_base_; ra.t_out = t_[lv + 1].p;
       NOF_HIP(nof::launch_render_fwd_pdf(ra, st_));
-    } else {
+    } else if (cb) {  // (without a callback the last level's integrator runs in the adjoint launch below)
       NOF_HIP(nof::launch_render_fwd(n, S, mlp->density(lv), mlp->rgb(lv), t_[lv].p, d, cfg_.white_bkgd, C_[lv].p,
                                      w_[lv].p, st_, nullptr, nullptr, mlp->numeric_flags()));
     }
@@ -1172,6 +1172,9 @@ float* const* AcceleratedMipNeRF::run(int n, const float* o, const float* d, con
       R.lam = lv < L - 1 ? cfg_.coarse_loss_mult : 1.0f;
       R.dsigma = dsig_[lv].p; R.drgb = drgb_[lv].p; R.loss_rays = cb ? nullptr : loss_rays_[lv].p;
       R.amax = mlp->claim_delta_amax(lv);
+      if (lv == L - 1 && !cb) {  // its integrator forward first, in its own blocks (k_render_bwd fwd_last)
+        ra.fwd_last = 1; ra.fwd_C = C_[lv].p; ra.fwd_w = w_[lv].p;
+      }
       if (cb) flush();
     }
     flush();

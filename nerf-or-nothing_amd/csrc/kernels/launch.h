@@ -74,6 +74,10 @@ struct RenderBwdArgs {
   float msum;
   uint32_t* nonfinite;
   RenderBwdLevel lv[kRenderMaxLevels];
+  // 1: the last entry's level has not been composited yet: its blocks run the integrator forward first
+  // (as launch_render_fwd with C = fwd_C, w = fwd_w; no acc / dist), g_ext must be null
+  int fwd_last = 0;
+  float *fwd_C = nullptr, *fwd_w = nullptr;
 };
 hipError_t launch_render_bwd(const RenderBwdArgs& a, int nlev, hipStream_t st);
 hipError_t launch_output_gradient(int n, const float* C, const float* pix, const float* lossmult,

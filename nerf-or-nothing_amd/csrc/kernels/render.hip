@@ -103,15 +103,16 @@ __device__ inline void ray_alpha_T(int S, int r, int lane, const float* __restri
 }
 
 // one ray's composite by one wave; stage_w / stage_t (LDS, or null): the ray's weights and t row also
-// staged for the resampler (k_render_fwd_pdf)
+// staged for the resampler (k_render_fwd_pdf).  rs, Cv: the ray's alpha / transmittance state and its
+// composite (in every lane: the butterfly sums are commutative pairings, the same bits everywhere), for
+// an adjoint in the same launch (k_render_bwd with fwd_last)
 template <int PER>
 __device__ __forceinline__ void render_fwd_ray(int r, int lane, int S, const float* __restrict__ sigma,
                                                const float* __restrict__ rgb, const float* __restrict__ t,
                                                const float* __restrict__ d, int white, float* __restrict__ C,
                                                float* __restrict__ w, float* __restrict__ acc_out,
                                                float* __restrict__ dist_out, uint32_t* __restrict__ nonfinite,
-                                               float* stage_w, float* stage_t) {
-  RayState<PER> rs;
+                                               float* stage_w, float* stage_t, RayState<PER>& rs, float (&Cv)[3]) {
   ray_alpha_T<PER>(S, r, lane, sigma, t, d, rs);
   const int k0 = lane * PER;
   float cr[3 * PER], wk[PER];
@@ -143,9 +144,10 @@ __device__ __forceinline__ void render_fwd_ray(int r, int lane, int S, const flo
   }
   c0 = wave_sum(c0); c1 = wave_sum(c1); c2 = wave_sum(c2); acc = wave_sum(acc);
   if (dist_out) wd = wave_sum(wd);
+  const float bg = white ? (1.0f - acc) : 0.0f;
+  Cv[0] = c0 + bg; Cv[1] = c1 + bg; Cv[2] = c2 + bg;
   if (lane == 0) {
-    const float bg = white ? (1.0f - acc) : 0.0f;
-    C[3 * r] = c0 + bg; C[3 * r + 1] = c1 + bg; C[3 * r + 2] = c2 + bg;
+    C[3 * r] = Cv[0]; C[3 * r + 1] = Cv[1]; C[3 * r + 2] = Cv[2];
     // non-finite detection (plain store of a constant: racing writers agree)
     if (nonfinite && !__builtin_isfinite(c0 + c1 + c2 + acc)) nonfinite[0] = 1u;
     if (acc_out) acc_out[r] = acc;
@@ -166,7 +168,9 @@ __global__ __launch_bounds__(256) void k_render_fwd(int n, int S, const float* _
   const int lane = threadIdx.x & 63;
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (r >= n) return;  // wave-uniform; no block barriers below
-  render_fwd_ray<PER>(r, lane, S, sigma, rgb, t, d, white, C, w, acc_out, dist_out, nonfinite, nullptr, nullptr);
+  RayState<PER> rs;
+  float Cv[3];
+  render_fwd_ray<PER>(r, lane, S, sigma, rgb, t, d, white, C, w, acc_out, dist_out, nonfinite, nullptr, nullptr, rs, Cv);
 }
 
 // The training forward's integrator of level l and the resampler of level l + 1 in one launch (one ray per
@@ -178,8 +182,10 @@ __global__ __launch_bounds__(64) void k_render_fwd_pdf(RenderPdfArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ float s_wsum;
   const int r = blockIdx.x, lane = threadIdx.x, B = a.S;
+  RayState<PER> rs;
+  float Cv[3];
   render_fwd_ray<PER>(r, lane, B, a.sigma, a.rgb, a.t, a.d, a.white, a.C, a.w, nullptr, nullptr, a.nonfinite,
-                      smem + B, smem + 2 * B + 1);
+                      smem + B, smem + 2 * B + 1, rs, Cv);
   __syncthreads();
   resample_staged(r, lane, B, smem, &s_wsum, a.S_out, a.padding, a.randomized, a.seed, a.step, a.level, a.ray_base,
                   a.t_out, nullptr);
@@ -190,7 +196,10 @@ __global__ __launch_bounds__(64) void k_render_fwd_pdf(RenderPdfArgs a) {
 // One launch covers the levels of RenderBwdArgs (blockIdx.y = level, all with S samples per ray).  With
 // lv.amax set, the level's delta-scale maximum max(|dsigma|, |drgb|) (the f16 modes' k_delta_amax,
 // mlp_bwd.hip) is taken here from the values just computed, one atomicMax of the float bits per block
-// (max is order-free: the same bits as the separate pass), *amax zero on entry.
+// (max is order-free: the same bits as the separate pass), *amax zero on entry.  fwd_last: the last
+// level's integrator forward (k_render_fwd: C, w, the input check) runs first in its own blocks, and its
+// adjoint takes the ray state and the composite from it (the values it would reload: the same bits) — the
+// training step's last forward launch folded into the adjoint launch.
 template <int PER>
 __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdArgs a) {
   const RenderBwdLevel& L = a.lv[blockIdx.y];
@@ -201,14 +210,22 @@ __global__ __launch_bounds__(256) void k_render_bwd(RenderBwdArgs a) {
   bool bad = false;
   if (live) {
     RayState<PER> rs;
-    ray_alpha_T<PER>(a.S, r, lane, L.sigma, L.t, a.d, rs);
+    float Cv[3];
+    const bool fwd = a.fwd_last && blockIdx.y == gridDim.y - 1;  // (block-uniform)
+    if (fwd) {
+      render_fwd_ray<PER>(r, lane, a.S, L.sigma, L.rgb, L.t, a.d, a.white, a.fwd_C, a.fwd_w, nullptr, nullptr,
+                          a.nonfinite, nullptr, nullptr, rs, Cv);
+    } else {
+      ray_alpha_T<PER>(a.S, r, lane, L.sigma, L.t, a.d, rs);
+    }
     float g0, g1, g2;
     if (L.g_ext) {
       g0 = L.g_ext[3 * r]; g1 = L.g_ext[3 * r + 1]; g2 = L.g_ext[3 * r + 2];
     } else {  // AF:356-358 order: 2*m/sum*(C-p)*lambda
       const float m = a.lossmult[r];
       const float s = 2.0f * m / a.msum;
-      const float e0 = L.C[3 * r] - a.pix[3 * r], e1 = L.C[3 * r + 1] - a.pix[3 * r + 1], e2 = L.C[3 * r + 2] - a.pix[3 * r + 2];
+      const float C0 = fwd ? Cv[0] : L.C[3 * r], C1 = fwd ? Cv[1] : L.C[3 * r + 1], C2 = fwd ? Cv[2] : L.C[3 * r + 2];
+      const float e0 = C0 - a.pix[3 * r], e1 = C1 - a.pix[3 * r + 1], e2 = C2 - a.pix[3 * r + 2];
       g0 = s * e0 * L.lam; g1 = s * e1 * L.lam; g2 = s * e2 * L.lam;
       if (L.loss_rays && lane == 0) L.loss_rays[r] = L.lam * m * ((e0 * e0 + e1 * e1) + e2 * e2) / a.msum;
     }
@@ -304,7 +321,8 @@ hipError_t launch_render_fwd_pdf(const RenderPdfArgs& a, hipStream_t st) {
 
 hipError_t launch_render_bwd(const RenderBwdArgs& a, int nlev, hipStream_t st) {
   if (a.n <= 0 || nlev <= 0) return hipSuccess;
-  if (nlev > kRenderMaxLevels) return hipErrorInvalidValue;
+  if (nlev > kRenderMaxLevels || (a.fwd_last && (a.lv[nlev - 1].g_ext || !a.fwd_C || !a.fwd_w)))
+    return hipErrorInvalidValue;
   const dim3 grid((a.n + 3) / 4, nlev), block(256);
   const int S = a.S;
   NOF_RENDER_DISPATCH(S, hipLaunchKernelGGL(k_render_bwd<PER>, grid, block, 0, st, a));

@@ -516,8 +516,11 @@ def main():
             timing = {}
             kb = min(5, steps) if timers_on else 0
             if kb:  # per-kernel breakdown: a few more steps with every kernel class timed (outside the clock)
+                # one untimed step first: read_timing synchronised, and the first timed class (pack) would
+                # otherwise measure the idle GPU waiting for the host's first launch
+                step(warmup + steps)
                 models[0].enable_timing(True)
-                for k in range(warmup + steps, warmup + steps + kb):
+                for k in range(warmup + steps + 1, warmup + steps + 1 + kb):
                     step(k)
                 timing = {name: (ms * steps / kb, cnt * steps // kb) for name, (ms, cnt) in models[0].read_timing().items()}
                 for name, v in live.items():  # the live (timed-region) figures where they were taken
@@ -543,7 +546,7 @@ def main():
                     allreduce(lo, op=dist.ReduceOp.MAX)
                 in_sync = bool(hi.item() == -lo.item())
             # fine-level PSNR of the last micro-batch (MseToPsnr, MipHelpers.cs:672)
-            last = pl[0][(warmup + steps + kb - 1) % 2]
+            last = pl[0][(warmup + steps + kb - (0 if kb else 1)) % 2]
             lo_, hi_ = cs[-1]
             comp = models[0].level_numpy(len(smp) - 1)["comp_rgb"]
             mse = float(np.mean((comp - last["pix"][lo_:hi_].cpu().numpy()) ** 2))

@@ -1129,7 +1129,7 @@ float* const* AcceleratedMipNeRF::run(int n, const float* o, const float* d, con
       timer.end(kTSample);
     }
     mlp->forward_fused(lv, n, S, t_[lv].p, o, d, radii);
-    timer.begin(kTRenderFwd);
+    if (lv + 1 < L || cb) timer.begin(kTRenderFwd);  // (a timer pair only around a launch)
     if (lv + 1 < L) {  // this level's integrator and the next level's resampler (ResampleAlongRay) in one launch
       nof::RenderPdfArgs ra{};
       ra.n = n; ra.S = S; ra.sigma = mlp->density(lv); ra.rgb = mlp->rgb(lv); ra.t = t_[lv].p; ra.d = d;
@@ -1141,7 +1141,7 @@ float* const* AcceleratedMipNeRF::run(int n, const float* o, const float* d, con
       NOF_HIP(nof::launch_render_fwd(n, S, mlp->density(lv), mlp->rgb(lv), t_[lv].p, d, cfg_.white_bkgd, C_[lv].p,
                                      w_[lv].p, st_, nullptr, nullptr, mlp->numeric_flags()));
     }
-    timer.end(kTRenderFwd);
+    if (lv + 1 < L || cb) timer.end(kTRenderFwd);
   }
   // MNcpp:125-134: the loss gradient and the integrator adjoint of every level (with the f16 modes' delta
   // maxima), levels of equal sample count in one launch when no callback supplies dL/dC, else one level

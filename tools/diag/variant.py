@@ -51,6 +51,11 @@ EDITS = {
     # LDS-DMA stream runs 6.3 TB/s nt against 5.8 default)
     "x3_nt": [(K + "wgrad.hip", "      q.v[c] = *(gf4*)((isA ? A : B) + (off[c] ^ par));",
                "      q.v[c] = __builtin_nontemporal_load((gf4*)((isA ? A : B) + (off[c] ^ par)));")],
+    # any-shape split-K weight gradients: about 512 / 2048 workgroups instead of 1024
+    "gsplit512": [("csrc/host/accelerated.cpp", "  int ks = std::max(1, std::min((1024 + tiles - 1) / tiles, M / 64));",
+                   "  int ks = std::max(1, std::min((512 + tiles - 1) / tiles, M / 64));")],
+    "gsplit2048": [("csrc/host/accelerated.cpp", "  int ks = std::max(1, std::min((1024 + tiles - 1) / tiles, M / 64));",
+                    "  int ks = std::max(1, std::min((2048 + tiles - 1) / tiles, M / 64));")],
     "h32_nodma": [(K + "mlp_h32.h",
                    "    slice16_dma_step(next, lds + ((cur + kDmaAhead) & (kH32Slots - 1)) * kPeriodFloats, tid, step);",
                    "    (void)step; (void)tid;")],
